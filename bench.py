@@ -1,0 +1,177 @@
+#!/usr/bin/env python3
+"""Benchmark: D-SGD round throughput (worker-iterations/s) and HBM roofline on MI355X.
+
+Workload (BASELINE.json config C3, the metric's configuration): logistic regression,
+N = 4096 workers per GPU, d = 1024 (incl. bias), m = 512 rows per worker, full-shard
+batches (b = m), random 4-regular topology with Metropolis-Hastings weights, fp32,
+objective + consensus recorded EVERY round (as trainer.py:182-191 does).
+A step = one D-SGD round over every worker (gradient, mix, step, metrics).
+
+Multi-GPU (`--gpus N` under torch.distributed.run): every rank holds its own 4096
+workers (weak scaling); see DESIGN.md for the exchange plan.
+
+Prints ONE JSON line on rank 0 (driver contract), with `roofline` for the fused
+round kernel (HIP-event timed, same timed region) and `cpu_baseline` (the oracle,
+i.e. the reference's per-worker numpy round, on a bounded sample, rank 0, N=1 only).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "distributed-optimization_amd"))
+
+METRIC = "worker-iters/sec + % HBM roofline, logistic N=4096 d=1024, 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(seconds, n_workers=64, d=1024, m=512, seed=11):
+    """The oracle (numpy restatement of the reference round, float64) on a bounded
+    sample: n_workers workers of the C3 shape, same per-round work as the reference
+    (per-worker minibatch draw + gradient, dense W @ X, objective over all sample rows,
+    consensus)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+
+    import dsgd_oracle as O
+    import topology
+
+    try:
+        from threadpoolctl import threadpool_info
+
+        threads = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
+    except Exception:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    rng = np.random.default_rng(seed)
+    wstar = rng.standard_normal(d)
+    shards = []
+    for _ in range(n_workers):
+        X = np.hstack([rng.standard_normal((m, d - 1)), np.ones((m, 1))])
+        y = np.sign(X @ wstar)
+        flip = rng.random(m) < 0.05
+        y[flip] = -y[flip]
+        shards.append((X, y))
+    Xf = np.vstack([s[0] for s in shards])
+    yf = np.concatenate([s[1] for s in shards])
+    W = topology.random_regular(n_workers, 4, seed=0).dense_W()
+    cfg = {"problem_type": "logistic", "local_batch_size": m, "learning_rate_eta0": 0.05,
+           "l2_regularization_lambda": 1e-4, "strong_convexity_mu": 1e-4}
+    t0 = time.perf_counter()
+    O.run_decentralized(shards, W, 1, cfg, Xf, yf, 0.0)
+    t1 = time.perf_counter() - t0
+    rounds = max(1, min(200, int(seconds / max(t1, 1e-3))))
+    t0 = time.perf_counter()
+    O.run_decentralized(shards, W, rounds, cfg, Xf, yf, 0.0)
+    dt = time.perf_counter() - t0
+    return {"value": n_workers * rounds / dt, "unit": "worker-iters/s", "cores": int(threads), "kind": "port",
+            "sample": f"oracle (numpy float64 restatement of trainer.py:161-193) on {n_workers} workers x "
+                      f"{m} rows x d={d}, {rounds} rounds, {dt:.1f} s, full-shard batches, metrics every round"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workers", type=int, default=4096, help="workers per GPU")
+    ap.add_argument("--d", type=int, default=1024)
+    ap.add_argument("--m", type=int, default=512)
+    ap.add_argument("--dtype", default="float32")
+    ap.add_argument("--degree", type=int, default=4)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch  # plumbing only: barrier + max-over-ranks (one HIP runtime, loaded first)
+    import torch.distributed as dist
+
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    import _dopt
+    import topology
+
+    n, d, m = args.workers, args.d, args.m
+    log(f"rank {rank}/{world}: generating {n} x {m} x {d} {args.dtype} shards on device {local}")
+    eng = _dopt.Engine(local, args.dtype)
+    eng.generate_shards("logistic", n, d, m, seed=1000 + rank, flip=0.05)
+    top = topology.random_regular(n, args.degree, seed=0)
+    eng.set_topology(top.row_ptr, top.col, top.w)
+    lam = 1e-4
+    log("warmup")
+    if args.warmup > 0:
+        eng.run_dsgd(args.warmup, 0.05, m, lam, lam, 0.0)
+    eng.set_models(__import__("numpy").zeros((n, d)))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(local)
+
+    eng.set_profiling(True)
+    barrier()
+    log(f"timing {args.steps} rounds")
+    t0 = time.perf_counter()
+    obj, cons, _ = eng.run_dsgd(args.steps, 0.05, m, lam, lam, 0.0, t0=0)
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    launches, kr_ms = eng.kernel_stats()
+    if not all(map(math.isfinite, list(obj) + list(cons))):
+        raise RuntimeError("non-finite metrics")
+
+    esz = 4 if args.dtype in ("float32", "fp32", "f32") else 8
+    bytes_per_launch = esz * n * (m * d + m + 2 * d)  # X_b + y_b + x read + x write
+    avg_s = (kr_ms / launches) * 1e-3 if launches else float("nan")
+    achieved = bytes_per_launch / avg_s / 1e9
+    value = world * n * args.steps / dt
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "worker-iters/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32" if esz == 4 else "f64",
+        "data": "synthetic (device-generated X~N(0,1)+bias, planted-w* labels, 5% flips)",
+        "config": {"workload": "C3: logistic, 4096 workers/GPU, d=1024, m=b=512, random 4-regular MH mixing, "
+                               "objective+consensus every round",
+                   "workers_per_gpu": n, "d": d, "rows_per_worker": m, "batch": m, "topology": "random_regular",
+                   "degree": args.degree, "parallelism": f"dp{world} (independent worker graphs per GPU)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "k_round<float,4,logistic,grad,metrics>", "kernel_avg_ms": avg_s * 1e3,
+                     "bytes_per_launch": bytes_per_launch},
+        "final_objective": float(obj[-1]),
+        "final_consensus": float(cons[-1]),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline")
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,302 @@
+"""ctypes binding of libdopt.so (the C ABI in include/dopt.h).
+
+This is the only place the Python host code touches the engine.  There is no
+CPU fallback: if libdopt.so is missing or no GPU is visible, device calls raise.
+
+Error mapping (so the drop-in modules raise what the reference raises):
+  DOPT_ERR_INVALID      -> ValueError
+  DOPT_ERR_UNSUPPORTED  -> NotImplementedError
+  anything else         -> RuntimeError
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DOPT_LIB", os.path.join(_HERE, "libdopt.so"))
+
+OK, ERR_INVALID, ERR_HIP, ERR_STATE, ERR_UNSUPPORTED, ERR_COMM = 0, -1, -2, -3, -4, -5
+LOGISTIC, QUADRATIC = 0, 1
+F32, F64 = 0, 1
+RUN_OBJECTIVE, RUN_CONSENSUS = 1, 2
+PROBLEMS = {"logistic": LOGISTIC, "quadratic": QUADRATIC}
+DTYPES = {"float32": F32, "fp32": F32, "f32": F32, np.float32: F32,
+          "float64": F64, "fp64": F64, "f64": F64, np.float64: F64}
+
+_lib = None
+_lock = threading.Lock()
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+_D = ctypes.c_double
+
+_SIGS = {
+    "dopt_abi_version": ([], ctypes.c_int),
+    "dopt_last_error": ([], ctypes.c_char_p),
+    "dopt_mt_choice": ([_P, _P, _I64, _I64, _P], ctypes.c_int),
+    "dopt_mt_choice_rounds": ([_P, _P, _I64, _I64, _P, _I64, _P], ctypes.c_int),
+    "dopt_device_count": ([_P], ctypes.c_int),
+    "dopt_create": ([ctypes.c_int, ctypes.c_int, _P], ctypes.c_int),
+    "dopt_destroy": ([_P], ctypes.c_int),
+    "dopt_load_shards": ([_P, ctypes.c_int, _I64, _I64, _P, _P, _P, ctypes.c_int], ctypes.c_int),
+    "dopt_generate_shards": ([_P, ctypes.c_int, _I64, _I64, _I64, ctypes.c_uint64, _D, _D], ctypes.c_int),
+    "dopt_load_objective_data": ([_P, _I64, _P, _P, ctypes.c_int], ctypes.c_int),
+    "dopt_clear_objective_data": ([_P], ctypes.c_int),
+    "dopt_get_shard": ([_P, _I64, _P, _P], ctypes.c_int),
+    "dopt_set_topology": ([_P, _I64, _P, _P, _P], ctypes.c_int),
+    "dopt_set_models": ([_P, _P], ctypes.c_int),
+    "dopt_get_models": ([_P, _P], ctypes.c_int),
+    "dopt_set_global": ([_P, _P], ctypes.c_int),
+    "dopt_get_global": ([_P, _P], ctypes.c_int),
+    "dopt_run_dsgd": ([_P, _I64, _I64, _D, _I64, _P, _D, _D, _D, ctypes.c_uint32, _P, _P, _P], ctypes.c_int),
+    "dopt_run_centralized": ([_P, _I64, _I64, _D, _I64, _P, _D, _D, _D, ctypes.c_uint32, _P, _P], ctypes.c_int),
+    "dopt_eval_gradient": ([_P, ctypes.c_int, _I64, _I64, _P, _P, _P, _D, _P], ctypes.c_int),
+    "dopt_eval_objective": ([_P, ctypes.c_int, _I64, _I64, _P, _P, _P, _D, _P], ctypes.c_int),
+    "dopt_kernel_stats": ([_P, _P, _P], ctypes.c_int),
+    "dopt_set_profiling": ([_P, ctypes.c_int], ctypes.c_int),
+}
+EXPORTED = tuple(_SIGS)
+
+
+def lib():
+    """Load libdopt.so once.  torch (when installed) is imported first so the
+    process has ONE HIP runtime: libdopt.so binds to torch's libamdhip64."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if os.environ.get("DOPT_NO_TORCH", "0") != "1":
+            try:
+                import torch  # noqa: F401
+            except Exception:  # pragma: no cover - torch is optional plumbing
+                pass
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libdopt.so not built at {LIB_PATH}: run `make -C "
+                               f"distributed-optimization_amd/csrc` or __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        if L.dopt_abi_version() != 1:
+            raise RuntimeError("libdopt.so ABI mismatch")
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc == OK:
+        return
+    msg = (lib().dopt_last_error() or b"").decode(errors="replace")
+    if rc == ERR_INVALID:
+        raise ValueError(msg)
+    if rc == ERR_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise RuntimeError(f"libdopt error {rc}: {msg}")
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    check(lib().dopt_device_count(ctypes.byref(n)))
+    return n.value
+
+
+# ---------------------------------------------------------------------------- sampler
+def _get_np_state():
+    st = np.random.get_state()
+    if st[0] != "MT19937":
+        raise RuntimeError("numpy global RNG is not the legacy MT19937")
+    return st, np.array(st[1], dtype=np.uint32, copy=True), ctypes.c_int32(int(st[2]))
+
+
+def _set_np_state(st, key, pos):
+    np.random.set_state((st[0], key, int(pos.value), st[3], st[4]))
+
+
+def mt_choice(m, b):
+    """np.random.choice(m, min(b, m), replace=False) on numpy's global state (worker.py:27)."""
+    st, key, pos = _get_np_state()
+    eb = 0 if m == 0 else min(b, m)
+    out = np.empty(max(eb, 0), dtype=np.int64)
+    check(lib().dopt_mt_choice(_ptr(key), ctypes.byref(pos), int(m), int(b), _ptr(out)))
+    _set_np_state(st, key, pos)
+    return out
+
+
+def mt_choice_rounds(T, shard_rows, b):
+    """[T, N, b] int32 index draws of T rounds x N workers, advancing numpy's global state."""
+    st, key, pos = _get_np_state()
+    rows = np.ascontiguousarray(shard_rows, dtype=np.int64)
+    out = np.empty((int(T), len(rows), int(b)), dtype=np.int32)
+    check(lib().dopt_mt_choice_rounds(_ptr(key), ctypes.byref(pos), int(T), len(rows), _ptr(rows),
+                                      int(b), _ptr(out)))
+    _set_np_state(st, key, pos)
+    return out
+
+
+# ---------------------------------------------------------------------------- device engine
+class Engine:
+    """One dopt context (one GPU): shards, topology and iterates resident in HBM."""
+
+    def __init__(self, device=0, dtype="float64"):
+        self.dtype = DTYPES[dtype] if not isinstance(dtype, int) else dtype
+        self.np_dtype = np.float32 if self.dtype == F32 else np.float64
+        self.device = int(device)
+        h = ctypes.c_void_p()
+        check(lib().dopt_create(self.device, self.dtype, ctypes.byref(h)))
+        self._h = h
+        self.n = 0
+        self.d = 0
+        self.problem = None
+        self.shard_rows = None
+        self.tag = None  # identity of the loaded data, for caching in the trainers
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().dopt_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order varies
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- data
+    def load_shards(self, problem, X, y, shard_offsets):
+        X = np.ascontiguousarray(X)
+        src_f32 = 1 if X.dtype == np.float32 else 0
+        X = np.ascontiguousarray(X, dtype=np.float32 if src_f32 else np.float64)
+        y = np.ascontiguousarray(y, dtype=X.dtype)
+        off = np.ascontiguousarray(shard_offsets, dtype=np.int64)
+        n = len(off) - 1
+        d = X.shape[1]
+        check(lib().dopt_load_shards(self._h, PROBLEMS[problem], n, d, _ptr(off), _ptr(X), _ptr(y), src_f32))
+        self.n, self.d, self.problem = n, d, problem
+        self.shard_rows = np.diff(off)
+
+    def generate_shards(self, problem, n_workers, d, rows_per_worker, seed=0, flip=0.05, noise=10.0):
+        check(lib().dopt_generate_shards(self._h, PROBLEMS[problem], int(n_workers), int(d),
+                                         int(rows_per_worker), int(seed) & (2 ** 64 - 1), float(flip),
+                                         float(noise)))
+        self.n, self.d, self.problem = int(n_workers), int(d), problem
+        self.shard_rows = np.full(int(n_workers), int(rows_per_worker), dtype=np.int64)
+
+    def load_objective_data(self, X, y):
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        check(lib().dopt_load_objective_data(self._h, X.shape[0], _ptr(X), _ptr(y), 0))
+
+    def clear_objective_data(self):
+        check(lib().dopt_clear_objective_data(self._h))
+
+    def get_shard(self, i):
+        m = int(self.shard_rows[i])
+        X = np.empty((m, self.d), dtype=np.float64)
+        y = np.empty(m, dtype=np.float64)
+        check(lib().dopt_get_shard(self._h, int(i), _ptr(X), _ptr(y)))
+        return X, y
+
+    def set_topology(self, row_ptr, col, w):
+        rp = np.ascontiguousarray(row_ptr, dtype=np.int64)
+        ci = np.ascontiguousarray(col, dtype=np.int32)
+        cw = np.ascontiguousarray(w, dtype=np.float64)
+        check(lib().dopt_set_topology(self._h, len(rp) - 1, _ptr(rp), _ptr(ci), _ptr(cw)))
+
+    def set_models(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64).reshape(self.n, self.d)
+        check(lib().dopt_set_models(self._h, _ptr(x)))
+
+    def get_models(self):
+        x = np.empty((self.n, self.d), dtype=np.float64)
+        check(lib().dopt_get_models(self._h, _ptr(x)))
+        return x
+
+    def set_global(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64).reshape(self.d)
+        check(lib().dopt_set_global(self._h, _ptr(x)))
+
+    def get_global(self):
+        x = np.empty(self.d, dtype=np.float64)
+        check(lib().dopt_get_global(self._h, _ptr(x)))
+        return x
+
+    # -- rounds
+    def run_dsgd(self, T, eta0, batch, lam_grad, lam_obj, f_opt=0.0, idx=None, t0=0,
+                 objective=True, consensus=True, want_time=True):
+        T = int(T)
+        obj = np.zeros(T) if objective else None
+        cons = np.zeros(T) if consensus else None
+        tim = np.zeros(T) if want_time else None
+        if idx is not None:
+            idx = np.ascontiguousarray(idx, dtype=np.int32)
+        flags = (RUN_OBJECTIVE if objective else 0) | (RUN_CONSENSUS if consensus else 0)
+        check(lib().dopt_run_dsgd(self._h, int(t0), T, float(eta0), int(batch), _ptr(idx), float(lam_grad),
+                                  float(lam_obj), float(f_opt), flags, _ptr(obj), _ptr(cons), _ptr(tim)))
+        return obj, cons, tim
+
+    def run_centralized(self, T, eta0, batch, lam_grad, lam_obj, f_opt=0.0, idx=None, t0=0,
+                        objective=True, want_time=True):
+        T = int(T)
+        obj = np.zeros(T) if objective else None
+        tim = np.zeros(T) if want_time else None
+        if idx is not None:
+            idx = np.ascontiguousarray(idx, dtype=np.int32)
+        flags = RUN_OBJECTIVE if objective else 0
+        check(lib().dopt_run_centralized(self._h, int(t0), T, float(eta0), int(batch), _ptr(idx),
+                                         float(lam_grad), float(lam_obj), float(f_opt), flags, _ptr(obj),
+                                         _ptr(tim)))
+        return obj, tim
+
+    # -- single evaluations (float64)
+    def eval_gradient(self, problem, w, X, y, reg):
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        X = np.ascontiguousarray(X, dtype=np.float64).reshape(-1, w.shape[0])
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        g = np.empty(w.shape[0], dtype=np.float64)
+        check(lib().dopt_eval_gradient(self._h, PROBLEMS[problem], X.shape[0], w.shape[0], _ptr(w), _ptr(X),
+                                       _ptr(y), float(reg), _ptr(g)))
+        return g
+
+    def eval_objective(self, problem, w, X, y, reg):
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        X = np.ascontiguousarray(X, dtype=np.float64).reshape(-1, w.shape[0])
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        out = np.zeros(1, dtype=np.float64)
+        check(lib().dopt_eval_objective(self._h, PROBLEMS[problem], X.shape[0], w.shape[0], _ptr(w), _ptr(X),
+                                        _ptr(y), float(reg), _ptr(out)))
+        return np.float64(out[0])
+
+    # -- profiling
+    def set_profiling(self, on):
+        check(lib().dopt_set_profiling(self._h, 1 if on else 0))
+
+    def kernel_stats(self):
+        n = ctypes.c_int64(0)
+        ms = ctypes.c_double(0.0)
+        check(lib().dopt_kernel_stats(self._h, ctypes.byref(n), ctypes.byref(ms)))
+        return n.value, ms.value
+
+
+_default = {}
+
+
+def default_engine(device=None):
+    """Float64 engine used by the obj_problems / Worker single-call API."""
+    dev = int(os.environ.get("DOPT_DEVICE", "0")) if device is None else int(device)
+    eng = _default.get(dev)
+    if eng is None:
+        eng = Engine(dev, "float64")
+        _default[dev] = eng
+    return eng

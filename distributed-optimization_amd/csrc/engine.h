@@ -1,0 +1,73 @@
+// engine.h -- internal interface between the C-ABI runtime (runtime.cpp) and
+// the gfx950 kernels (kernels.hip).  Not part of the public ABI (include/dopt.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dopt {
+
+// RoundArgs.flags
+enum : int32_t {
+  F_STEP = 1,          // fused mix + step: x_new = sum_j W_ij x_old[j] - eta * g  (trainer.py:173-175)
+  F_GOUT = 2,          // store per-worker gradient rows instead (centralized, trainer.py:47-53)
+  F_SHARED = 4,        // every worker evaluates at w_shared (centralized, trainer.py:43,48)
+  F_CONS = 8,          // consensus partial ||x_i - xbar||^2 (trainer.py:185)
+  F_LOSS = 16,         // objective partial at xbar over this workgroup's rows (trainer.py:189)
+  F_LOSS_FROM_Z = 32,  // the objective point IS the gradient point: reuse z = x.w
+};
+
+// One workgroup per worker (or per objective-row chunk).  All pointers are
+// device pointers; T-typed arrays are float or double per the launch.
+struct RoundArgs {
+  const void* X;          // [rows x ld] shard rows, back to back
+  const void* y;          // [rows]
+  const int64_t* off;     // [n+1] first row of every worker's rows
+  const int32_t* idx;     // [n x b] local row ids of this round's minibatch, or null (all rows)
+  int64_t b;              // minibatch size when idx != null
+  const void* x_old;      // [n x ld] iterates before the round (read only during the round)
+  void* x_new;            // [n x ld] iterates after the round
+  void* g_out;            // [n x ld] gradients (F_GOUT)
+  const void* w_shared;   // [ld] shared iterate (F_SHARED)
+  const void* xbar;       // [ld] metric point (F_CONS / F_LOSS)
+  const int64_t* rp;      // CSR mixing matrix, diagonal included
+  const int32_t* ci;
+  const void* cw;         // T-typed weights
+  double* slab_cons;      // [n] per-workgroup partial sums (deterministic two-stage reduction)
+  double* slab_loss;      // [n]
+  double eta;             // eta0 / sqrt(t+1)  (trainer.py:138-140)
+  double lam;             // gradient regulariser (worker.py:36-42)
+  int64_t ld;             // padded row stride in elements (multiple of the 16-byte vector)
+  int32_t nchunks;        // ld / elements-per-16B
+  int32_t flags;
+};
+
+// Kernel launchers (kernels.hip).  dtype: 0 = float, 1 = double.
+// cpl = 16-byte chunks per lane (1, 2, 4, 8, 16); grad / met select the variant.
+hipError_t launch_round(int dtype, int problem, int cpl, bool grad, bool met, const RoundArgs& a,
+                        int n_groups, hipStream_t s);
+int max_chunks_per_lane();
+
+// Column sums of an [n x ld] matrix into fp64 partials [G x ld], G = ceil(n / rpg).
+hipError_t launch_colsum_partial(int dtype, const void* x, int64_t n, int64_t ld, int32_t nchunks,
+                                 int32_t rpg, double* part, uint64_t* stamp, hipStream_t s);
+// out = sum_g part / n (mode 0, the average model, trainer.py:182), or
+// out = base - eta * (sum_g part / n) (mode 1, centralized update, trainer.py:53-57).
+hipError_t launch_colsum_final(int dtype, const double* part, int32_t groups, int64_t n, int64_t ld,
+                               int32_t nchunks, void* out, const void* base, double eta, int mode,
+                               hipStream_t s);
+// history[h] from the slabs (one workgroup, fixed reduction order).
+hipError_t launch_history(int dtype, int problem, const double* slab_cons, const double* slab_loss,
+                          int64_t n, int64_t n_loss_groups, int64_t m_obj, const void* xbar,
+                          int64_t ld, int32_t nchunks, double lam_obj, double f_opt, double* obj_out,
+                          double* cons_out, int64_t h, hipStream_t s);
+// Synthetic shards (rows_per_worker rows per worker), X ~ N(0,1) + bias column.
+hipError_t launch_generate(int dtype, int problem, void* X, void* y, int64_t rows, int64_t d,
+                           int64_t ld, uint64_t seed, double flip, double noise, hipStream_t s);
+// One thread writes the constant-rate wall clock (trainer.py:181 timestamps).
+hipError_t launch_stamp(uint64_t* out, hipStream_t s);
+// float64 host data -> T rows padded to ld (zero padding).
+hipError_t launch_convert(int dtype, const void* src, int src_f32, void* dst, int64_t rows, int64_t d,
+                          int64_t ld, hipStream_t s);
+
+}  // namespace dopt

@@ -1,0 +1,575 @@
+// kernels.hip -- gfx950 (MI355X, CDNA4) kernels of the D-SGD round.
+//
+// The round of the reference (trainer.py:161-193) per worker i:
+//   g_i   = (1/b) sum_k c_k(x_i . a_k) a_k + lam x_i      obj_problems.py:13-20 / :46-53
+//   x_i'  = sum_j W_ij x_j - eta_t g_i                     trainer.py:173-175
+// then xbar = mean_i x_i' (trainer.py:182), the consensus error (trainer.py:185)
+// and the objective at xbar over all data (trainer.py:188-191).
+//
+// Everything here is HBM-bound (two GEMVs per worker, ~1 FLOP/B at fp32), so the
+// design goal is ONE pass over the shard bytes per round:
+//
+//  k_round   one 256-thread workgroup (4 waves) per worker.  Each wave streams whole
+//            rows (16-byte loads, lane l holds columns [16B chunk l + 64j]), forms the
+//            row dot(s) by a 64-lane butterfly, turns them into the sigmoid / residual
+//            coefficient in registers and accumulates coef*row from the SAME registers
+//            (no second read of the row).  The waves' partial gradients meet in LDS;
+//            the epilogue applies 1/b and lam, reads the <= deg+1 neighbour iterates
+//            (L2 / Infinity-Cache resident) and writes x_i' -- grad, mix and step in
+//            one launch.  With metrics fused (full-shard batches) the same row pass
+//            also dots each row with xbar_t and accumulates the objective of the
+//            previous round, so logging every round costs no extra HBM bytes.
+//  k_colsum_part / k_colsum_final
+//            deterministic two-stage column mean (fp64 partials, fixed order): xbar,
+//            or the centralized gradient average + update.
+//  k_history one workgroup folds the per-worker partials into history[t].
+//
+// No atomics anywhere: every reduction has a fixed order, so runs are bitwise
+// reproducible.
+#include <math.h>
+
+#include "engine.h"
+
+namespace dopt {
+
+template <typename T>
+struct VT;
+template <>
+struct VT<float> {
+  static constexpr int n = 4;
+  typedef float v __attribute__((ext_vector_type(4)));
+};
+template <>
+struct VT<double> {
+  static constexpr int n = 2;
+  typedef double v __attribute__((ext_vector_type(2)));
+};
+
+constexpr int NW = 4;         // waves per workgroup
+constexpr int NT = NW * 64;   // threads per workgroup
+constexpr int MAX_CPL = 16;   // 16-byte chunks per lane: d <= 4096 (fp32) / 2048 (fp64)
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T, typename V>
+__device__ __forceinline__ T hsum(V v) {
+  T s = v[0];
+#pragma unroll
+  for (int e = 1; e < VT<T>::n; ++e) s += v[e];
+  return s;
+}
+
+// scipy.special.expit(x) = 1 / (1 + exp(-x)); the gradient needs expit(-y z).
+template <typename T>
+__device__ __forceinline__ T sigmoid_neg(T yz) {
+  return T(1) / (T(1) + exp(yz));
+}
+
+// obj_problems.py:5-7 (logistic, np.log(1 + exp(-|t|)) as written, not log1p)
+// and obj_problems.py:41-42 (quadratic, the 0.5 is applied once at the end).
+template <typename T, int PROB>
+__device__ __forceinline__ double row_loss(T yv, T u) {
+  if (PROB == 0) {
+    const T t = yv * u;
+    const T a = t < T(0) ? -t : t;
+    return (double)((t < T(0) ? -t : T(0)) + log(T(1) + exp(-a)));
+  } else {
+    const T e = u - yv;
+    return (double)(e * e);
+  }
+}
+
+// ---------------------------------------------------------------------------- k_round
+template <typename T, int CPL, int PROB, bool GRAD, bool MET>
+__global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
+  using V = typename VT<T>::v;
+  constexpr int VN = VT<T>::n;
+  constexpr int RB = CPL >= 8 ? 1 : 8 / CPL;  // rows in flight per wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int i = blockIdx.x;
+  const int flags = a.flags;
+  const int nch = a.nchunks;
+  const int64_t ld = a.ld;
+  const int64_t row0 = a.off[i];
+  const int64_t m = a.off[i + 1] - row0;
+  const int64_t nb = (GRAD && a.idx) ? (a.b < m ? a.b : m) : m;
+  const T* __restrict__ X = (const T*)a.X;
+  const T* __restrict__ Y = (const T*)a.y;
+  const T* wsrc = (flags & F_SHARED) ? (const T*)a.w_shared : (const T*)a.x_old + (int64_t)i * ld;
+
+  const bool loss_from_z = (flags & F_LOSS_FROM_Z) != 0;
+  const bool want_loss = MET && (flags & F_LOSS);
+  const bool want_cons = MET && (flags & F_CONS);
+  const bool compute_z = GRAD || (want_loss && loss_from_z);
+  const bool compute_u = want_loss && !loss_from_z;
+  const bool need_w = compute_z || want_cons;
+  const bool need_xb = compute_u || want_cons;
+
+  V w[CPL], xb[CPL], g[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane + 64 * j;
+    const bool in = c < nch;
+    w[j] = (need_w && in) ? *(const V*)(wsrc + (int64_t)c * VN) : V(0);
+    xb[j] = (need_xb && in) ? *(const V*)((const T*)a.xbar + (int64_t)c * VN) : V(0);
+    g[j] = V(0);
+  }
+  double loss = 0.0;
+
+  if (compute_z || compute_u) {
+    for (int64_t r0 = (int64_t)wave * RB; r0 < nb; r0 += NW * RB) {
+      V xr[RB][CPL];
+      T yv[RB];
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {
+        const int64_t rr = r0 + k;
+        const bool ok = rr < nb;
+        int64_t lr = rr;
+        if (GRAD && a.idx && ok) lr = a.idx[(int64_t)i * a.b + rr];
+        const T* xp = X + (row0 + lr) * ld;
+        yv[k] = ok ? Y[row0 + lr] : T(0);
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+          const int c = lane + 64 * j;
+          xr[k][j] = (ok && c < nch) ? *(const V*)(xp + (int64_t)c * VN) : V(0);
+        }
+      }
+      T z[RB], u[RB];
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {
+        V az = V(0), au = V(0);
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+          if (compute_z) az += xr[k][j] * w[j];
+          if (compute_u) au += xr[k][j] * xb[j];
+        }
+        z[k] = hsum<T>(az);
+        u[k] = hsum<T>(au);
+      }
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {
+        if (compute_z) z[k] = wave_sum(z[k]);
+        if (compute_u) u[k] = wave_sum(u[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {
+        if (r0 + k < nb) {
+          if (GRAD) {
+            const T coef = (PROB == 0) ? -yv[k] * sigmoid_neg(yv[k] * z[k]) : z[k] - yv[k];
+#pragma unroll
+            for (int j = 0; j < CPL; ++j) g[j] += coef * xr[k][j];
+          }
+          if (want_loss) loss += row_loss<T, PROB>(yv[k], loss_from_z ? z[k] : u[k]);
+        }
+      }
+    }
+  }
+
+  V* red = (V*)smem;  // [NW][nch]
+  double* sred = (double*)(smem + (GRAD ? (size_t)NW * nch * 16 : 0));
+  if (GRAD) {
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nch) red[wave * nch + c] = g[j];
+    }
+  }
+  if (MET) {
+    double cons = 0.0;
+    if (want_cons && wave == 0) {  // every wave holds the whole iterate: count it once
+      V dv = V(0);
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) {
+        const V t = w[j] - xb[j];
+        dv += t * t;
+      }
+      cons = wave_sum((double)hsum<T>(dv));
+    }
+    if (lane == 0) {
+      sred[wave] = cons;
+      sred[NW + wave] = loss;
+    }
+  }
+  __syncthreads();
+
+  if (GRAD) {
+    const T inv_eta = (T)a.eta;
+    const T lam = (T)a.lam;
+    const int64_t e0 = a.rp ? a.rp[i] : 0, e1 = a.rp ? a.rp[i + 1] : 0;
+    for (int c = threadIdx.x; c < nch; c += NT) {
+      V s = red[c];
+#pragma unroll
+      for (int q = 1; q < NW; ++q) s += red[q * nch + c];  // fixed order
+      const V wc = *(const V*)(wsrc + (int64_t)c * VN);
+      const V gc = (nb > 0) ? (s / (T)nb + lam * wc) : V(0);
+      if (flags & F_STEP) {
+        V acc = V(0);
+        for (int64_t e = e0; e < e1; ++e) {
+          const T wt = ((const T*)a.cw)[e];
+          acc += wt * *(const V*)((const T*)a.x_old + (int64_t)a.ci[e] * ld + (int64_t)c * VN);
+        }
+        *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = acc - inv_eta * gc;
+      } else if (flags & F_GOUT) {
+        *(V*)((T*)a.g_out + (int64_t)i * ld + (int64_t)c * VN) = gc;
+      }
+    }
+  }
+  if (MET && threadIdx.x == 0) {
+    double cs = 0.0, ls = 0.0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      cs += sred[q];
+      ls += sred[NW + q];
+    }
+    if (want_cons) a.slab_cons[i] = cs;
+    if (want_loss) a.slab_loss[i] = ls;
+  }
+}
+
+template <typename T, int CPL, int PROB, bool GRAD, bool MET>
+static hipError_t launch_round_t(const RoundArgs& a, int groups, hipStream_t s) {
+  const size_t lds = (GRAD ? (size_t)NW * a.nchunks * 16 : 0) + 2 * NW * sizeof(double);
+  static bool attr_set = false;
+  if (!attr_set) {
+    const size_t max_lds = (size_t)NW * MAX_CPL * 64 * 16 + 2 * NW * sizeof(double);
+    hipError_t e = hipFuncSetAttribute((const void*)k_round<T, CPL, PROB, GRAD, MET>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((k_round<T, CPL, PROB, GRAD, MET>), dim3(groups), dim3(NT), lds, s, a);
+  return hipGetLastError();
+}
+
+template <typename T, int CPL, int PROB>
+static hipError_t dispatch_mode(bool grad, bool met, const RoundArgs& a, int groups, hipStream_t s) {
+  if (grad && met) return launch_round_t<T, CPL, PROB, true, true>(a, groups, s);
+  if (grad) return launch_round_t<T, CPL, PROB, true, false>(a, groups, s);
+  if (met) return launch_round_t<T, CPL, PROB, false, true>(a, groups, s);
+  return hipErrorInvalidValue;
+}
+
+template <typename T, int PROB>
+static hipError_t dispatch_cpl(int cpl, bool grad, bool met, const RoundArgs& a, int groups,
+                               hipStream_t s) {
+  switch (cpl) {
+    case 1: return dispatch_mode<T, 1, PROB>(grad, met, a, groups, s);
+    case 2: return dispatch_mode<T, 2, PROB>(grad, met, a, groups, s);
+    case 4: return dispatch_mode<T, 4, PROB>(grad, met, a, groups, s);
+    case 8: return dispatch_mode<T, 8, PROB>(grad, met, a, groups, s);
+    case 16: return dispatch_mode<T, 16, PROB>(grad, met, a, groups, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_round(int dtype, int problem, int cpl, bool grad, bool met, const RoundArgs& a,
+                        int n_groups, hipStream_t s) {
+  if (n_groups <= 0) return hipSuccess;
+  if (dtype == 0)
+    return problem == 0 ? dispatch_cpl<float, 0>(cpl, grad, met, a, n_groups, s)
+                        : dispatch_cpl<float, 1>(cpl, grad, met, a, n_groups, s);
+  return problem == 0 ? dispatch_cpl<double, 0>(cpl, grad, met, a, n_groups, s)
+                      : dispatch_cpl<double, 1>(cpl, grad, met, a, n_groups, s);
+}
+
+int max_chunks_per_lane() { return MAX_CPL; }
+
+// ---------------------------------------------------------------------------- column sums
+// Stage 1: workgroup (g, cb) sums rows [g*rpg, (g+1)*rpg) of the 64-chunk column block cb;
+// lane = chunk in the block, the 4 waves split the rows and meet in LDS (fixed order).
+// Stage 2: workgroup cb sums the G partials of its block, waves split the groups.
+// Both stages are coalesced 1 KiB row segments per wave-instruction.
+template <typename T>
+__global__ __launch_bounds__(NT) void k_colsum_part(const T* __restrict__ x, int64_t n, int64_t ld,
+                                                    int nch, int rpg, double* __restrict__ part,
+                                                    uint64_t* stamp) {
+  using V = typename VT<T>::v;
+  constexpr int VN = VT<T>::n;
+  __shared__ double red[NW][64 * VN];
+  if (stamp && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *stamp = wall_clock64();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + lane;
+  const int64_t r0 = (int64_t)blockIdx.x * rpg;
+  const int64_t r1 = (r0 + rpg < n) ? r0 + rpg : n;
+  double acc[VN];
+#pragma unroll
+  for (int e = 0; e < VN; ++e) acc[e] = 0.0;
+  if (c < nch) {
+    int64_t r = r0 + wave;
+    for (; r + 3 * NW < r1; r += 4 * NW) {  // 4 rows in flight per wave
+      V v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = *(const V*)(x + (r + k * NW) * ld + (int64_t)c * VN);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int e = 0; e < VN; ++e) acc[e] += (double)v[k][e];
+    }
+    for (; r < r1; r += NW) {
+      const V v = *(const V*)(x + r * ld + (int64_t)c * VN);
+#pragma unroll
+      for (int e = 0; e < VN; ++e) acc[e] += (double)v[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < VN; ++e) red[wave][lane * VN + e] = acc[e];
+  __syncthreads();
+  if (wave == 0 && c < nch) {
+#pragma unroll
+    for (int e = 0; e < VN; ++e) {
+      double s = red[0][lane * VN + e];
+#pragma unroll
+      for (int q = 1; q < NW; ++q) s += red[q][lane * VN + e];
+      part[(int64_t)blockIdx.x * ld + (int64_t)c * VN + e] = s;
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void k_colsum_final(const double* __restrict__ part, int groups,
+                                                     int64_t n, int64_t ld, int nch, T* out,
+                                                     const T* base, double eta, int mode) {
+  constexpr int VN = VT<T>::n;
+  __shared__ double red[NW][64 * VN];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  double acc[VN];
+#pragma unroll
+  for (int e = 0; e < VN; ++e) acc[e] = 0.0;
+  if (c < nch) {
+    int q = wave;
+    for (; q + 3 * NW < groups; q += 4 * NW) {
+      double v[4][VN];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int e = 0; e < VN; ++e) v[k][e] = part[(int64_t)(q + k * NW) * ld + (int64_t)c * VN + e];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int e = 0; e < VN; ++e) acc[e] += v[k][e];
+    }
+    for (; q < groups; q += NW)
+#pragma unroll
+      for (int e = 0; e < VN; ++e) acc[e] += part[(int64_t)q * ld + (int64_t)c * VN + e];
+  }
+#pragma unroll
+  for (int e = 0; e < VN; ++e) red[wave][lane * VN + e] = acc[e];
+  __syncthreads();
+  if (wave == 0 && c < nch) {
+#pragma unroll
+    for (int e = 0; e < VN; ++e) {
+      const int64_t col = (int64_t)c * VN + e;
+      double s = red[0][lane * VN + e];
+#pragma unroll
+      for (int q = 1; q < NW; ++q) s += red[q][lane * VN + e];
+      const double mean = s / (double)n;  // np.mean: sum / count
+      if (mode == 0)
+        out[col] = (T)mean;
+      else
+        out[col] = base[col] - (T)eta * (T)mean;  // trainer.py:57
+    }
+  }
+}
+
+hipError_t launch_colsum_partial(int dtype, const void* x, int64_t n, int64_t ld, int32_t nchunks,
+                                 int32_t rpg, double* part, uint64_t* stamp, hipStream_t s) {
+  const int groups = (int)((n + rpg - 1) / rpg);
+  const dim3 grid(groups > 0 ? groups : 1, (nchunks + 63) / 64);
+  if (dtype == 0)
+    hipLaunchKernelGGL(k_colsum_part<float>, grid, dim3(NT), 0, s, (const float*)x, n, ld, nchunks,
+                       rpg, part, stamp);
+  else
+    hipLaunchKernelGGL(k_colsum_part<double>, grid, dim3(NT), 0, s, (const double*)x, n, ld, nchunks,
+                       rpg, part, stamp);
+  return hipGetLastError();
+}
+
+hipError_t launch_colsum_final(int dtype, const double* part, int32_t groups, int64_t n, int64_t ld,
+                               int32_t nchunks, void* out, const void* base, double eta, int mode,
+                               hipStream_t s) {
+  const dim3 grid((nchunks + 63) / 64);
+  if (dtype == 0)
+    hipLaunchKernelGGL(k_colsum_final<float>, grid, dim3(NT), 0, s, part, groups, n, ld, nchunks,
+                       (float*)out, (const float*)base, eta, mode);
+  else
+    hipLaunchKernelGGL(k_colsum_final<double>, grid, dim3(NT), 0, s, part, groups, n, ld, nchunks,
+                       (double*)out, (const double*)base, eta, mode);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------- history
+template <typename T>
+__global__ __launch_bounds__(NT) void k_history(const double* sc, const double* sl, int64_t n,
+                                                int64_t ng, int64_t m_obj, const T* xbar, int64_t ld,
+                                                int nch, int problem, double lam_obj, double f_opt,
+                                                double* obj_out, double* cons_out, int64_t h) {
+  constexpr int VN = VT<T>::n;
+  __shared__ double part[3][NW];
+  double a = 0.0, b = 0.0, q = 0.0;
+  if (cons_out)
+    for (int64_t k = threadIdx.x; k < n; k += NT) a += sc[k];
+  if (obj_out) {
+    for (int64_t k = threadIdx.x; k < ng; k += NT) b += sl[k];
+    for (int c = threadIdx.x; c < nch; c += NT)
+#pragma unroll
+      for (int e = 0; e < VN; ++e) {
+        const double v = (double)xbar[(int64_t)c * VN + e];
+        q += v * v;
+      }
+  }
+  a = wave_sum(a);
+  b = wave_sum(b);
+  q = wave_sum(q);
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    part[0][wave] = a;
+    part[1][wave] = b;
+    part[2][wave] = q;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double sa = 0.0, sb = 0.0, sq = 0.0;
+    for (int k = 0; k < NW; ++k) {
+      sa += part[0][k];
+      sb += part[1][k];
+      sq += part[2][k];
+    }
+    if (cons_out) cons_out[h] = sa / (double)n;  // trainer.py:185 np.mean over workers
+    if (obj_out) {
+      double obj = 0.0;  // obj_problems.py:4,40: empty data -> 0.0 (no regulariser)
+      if (m_obj > 0) {
+        const double data = (problem == 0) ? sb / (double)m_obj : 0.5 * (sb / (double)m_obj);
+        obj = data + (lam_obj / 2.0) * sq;
+      }
+      obj_out[h] = obj - f_opt;  // trainer.py:190
+    }
+  }
+}
+
+hipError_t launch_history(int dtype, int problem, const double* slab_cons, const double* slab_loss,
+                          int64_t n, int64_t n_loss_groups, int64_t m_obj, const void* xbar,
+                          int64_t ld, int32_t nchunks, double lam_obj, double f_opt, double* obj_out,
+                          double* cons_out, int64_t h, hipStream_t s) {
+  if (dtype == 0)
+    hipLaunchKernelGGL(k_history<float>, dim3(1), dim3(NT), 0, s, slab_cons, slab_loss, n,
+                       n_loss_groups, m_obj, (const float*)xbar, ld, nchunks, problem, lam_obj,
+                       f_opt, obj_out, cons_out, h);
+  else
+    hipLaunchKernelGGL(k_history<double>, dim3(1), dim3(NT), 0, s, slab_cons, slab_loss, n,
+                       n_loss_groups, m_obj, (const double*)xbar, ld, nchunks, problem, lam_obj,
+                       f_opt, obj_out, cons_out, h);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------- synthetic data
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ double unif01(uint64_t h) {  // (0, 1]
+  return ((double)(h >> 11) + 1.0) * (1.0 / 9007199254740992.0);
+}
+__device__ __forceinline__ double normal_at(uint64_t seed, uint64_t a, uint64_t b) {
+  const uint64_t h = mix64(seed ^ mix64(a * 0xD1B54A32D192ED03ull + b));
+  const double u1 = unif01(h), u2 = unif01(mix64(h));
+  return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void k_generate(T* X, T* y, int64_t rows, int64_t d, int64_t ld,
+                                                 uint64_t seed, double flip, double noise,
+                                                 int problem) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * NW + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  double dot = 0.0;
+  for (int64_t c = lane; c < ld; c += 64) {
+    double v = 0.0;
+    if (c < d - 1)
+      v = normal_at(seed, (uint64_t)r + 1, (uint64_t)c);
+    else if (c == d - 1)
+      v = 1.0;  // bias column, utils.py:28
+    X[r * ld + c] = (T)v;
+    // labels from the float64 values, so float32 and float64 engines get the same labels
+    if (c < d) dot += v * normal_at(seed ^ 0x5DEECE66Dull, 0, (uint64_t)c);  // planted w*
+  }
+  dot = wave_sum(dot);
+  if (lane == 0) {
+    if (problem == 0) {
+      T lab = dot >= 0.0 ? T(1) : T(-1);
+      if (unif01(mix64(seed ^ mix64(~(uint64_t)r))) <= flip) lab = -lab;
+      y[r] = lab;
+    } else {
+      y[r] = (T)(dot + noise * normal_at(seed ^ 0xA5A5A5A5ull, (uint64_t)r, 0xFFFFFFFFull));
+    }
+  }
+}
+
+hipError_t launch_generate(int dtype, int problem, void* X, void* y, int64_t rows, int64_t d,
+                           int64_t ld, uint64_t seed, double flip, double noise, hipStream_t s) {
+  const dim3 grid((unsigned)((rows + NW - 1) / NW));
+  if (dtype == 0)
+    hipLaunchKernelGGL(k_generate<float>, grid, dim3(NT), 0, s, (float*)X, (float*)y, rows, d, ld,
+                       seed, flip, noise, problem);
+  else
+    hipLaunchKernelGGL(k_generate<double>, grid, dim3(NT), 0, s, (double*)X, (double*)y, rows, d, ld,
+                       seed, flip, noise, problem);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------- clock stamp
+__global__ void k_stamp(uint64_t* out) { *out = wall_clock64(); }
+
+hipError_t launch_stamp(uint64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, s, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------- conversion
+template <typename T, typename S>
+__global__ __launch_bounds__(NT) void k_convert(const S* __restrict__ src, T* __restrict__ dst,
+                                                int64_t rows, int64_t d, int64_t ld) {
+  const int64_t total = rows * ld;
+  for (int64_t k = (int64_t)blockIdx.x * NT + threadIdx.x; k < total; k += (int64_t)gridDim.x * NT) {
+    const int64_t r = k / ld, c = k - r * ld;
+    dst[k] = c < d ? (T)src[r * d + c] : T(0);
+  }
+}
+
+hipError_t launch_convert(int dtype, const void* src, int src_f32, void* dst, int64_t rows, int64_t d,
+                          int64_t ld, hipStream_t s) {
+  const int64_t total = rows * ld;
+  int64_t blocks = (total + NT - 1) / NT;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  const dim3 grid((unsigned)blocks);
+  if (dtype == 0) {
+    if (src_f32)
+      hipLaunchKernelGGL((k_convert<float, float>), grid, dim3(NT), 0, s, (const float*)src,
+                         (float*)dst, rows, d, ld);
+    else
+      hipLaunchKernelGGL((k_convert<float, double>), grid, dim3(NT), 0, s, (const double*)src,
+                         (float*)dst, rows, d, ld);
+  } else {
+    if (src_f32)
+      hipLaunchKernelGGL((k_convert<double, float>), grid, dim3(NT), 0, s, (const float*)src,
+                         (double*)dst, rows, d, ld);
+    else
+      hipLaunchKernelGGL((k_convert<double, double>), grid, dim3(NT), 0, s, (const double*)src,
+                         (double*)dst, rows, d, ld);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace dopt

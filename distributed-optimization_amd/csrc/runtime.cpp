@@ -1,0 +1,804 @@
+// runtime.cpp -- the C ABI of libdopt.so (include/dopt.h): device context, data
+// layout in HBM, and the per-round launch schedule of the D-SGD / centralized
+// trainers (trainer.py:33-74, :154-197).
+//
+// HBM layout (one context = one GPU):
+//   X      [rows x ld]  T   shard rows back to back, worker i = rows [off[i], off[i+1]);
+//                           ld = d rounded up to a 16-byte multiple, zero padded
+//   y      [rows]       T
+//   xs[2]  [N x ld]     T   iterate ping-pong: round t reads xs[cur], writes xs[cur^1]
+//   xbar[2][ld]         T   average model ping-pong (xbar_t and xbar_{t+1} live together)
+//   part   [G x ld]   f64   column-sum partials, G = ceil(N / rows_per_group)
+//   slabs  [N]        f64   per-worker consensus / objective partials
+//   rp/ci/cw                CSR mixing matrix (diagonal included), cw in T
+//   G      [N x ld]     T   per-worker gradients (centralized trainer only)
+//
+// Launch schedule of one D-SGD round t (metrics fused, full-shard batches):
+//   k_round(t)       grad + mix + step for every worker, and the consensus /
+//                    objective partials of x_t at xbar_t from the same row pass
+//   k_colsum_*(t)    xbar_{t+1}
+//   k_history(t)     history[t-1]
+// plus one metrics-only pass after the last round.  With minibatches smaller than
+// the shard, the objective needs all rows, so a metrics-only pass runs every round.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "dopt.h"
+#include "engine.h"
+
+using namespace dopt;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPOK(expr)                                                                      \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess) return fail(DOPT_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+#define CHECK_ARG(cond, ...)                          \
+  do {                                                \
+    if (!(cond)) return fail(DOPT_ERR_INVALID, __VA_ARGS__); \
+  } while (0)
+
+constexpr size_t kStaging = 64ull << 20;  // host->device staging chunk
+constexpr int kRowsPerGroup = 64;         // column-sum partial group height (16 rows per wave)
+
+}  // namespace
+
+struct dopt_ctx {
+  int device = 0;
+  int dtype = DOPT_F64;
+  size_t esz = 8;
+  int vn = 2;  // elements per 16-byte vector
+  hipStream_t stream = nullptr;
+  double clock_hz = 1e8;
+
+  // problem
+  bool have_data = false;
+  int problem = DOPT_LOGISTIC;
+  int64_t n = 0, d = 0, ld = 0, nch = 0, rows = 0, max_m = 0;
+  int cpl = 1;
+  void* X = nullptr;
+  void* y = nullptr;
+  int64_t* off = nullptr;
+  std::vector<int64_t> off_h;
+
+  // separate objective dataset (X_full that is not the union of the shards)
+  bool obj_sep = false;
+  void* Xo = nullptr;
+  void* yo = nullptr;
+  int64_t* offo = nullptr;
+  int64_t rows_o = 0;
+
+  // state
+  void* xs[2] = {nullptr, nullptr};
+  int cur = 0;
+  void* xg[2] = {nullptr, nullptr};
+  int gcur = 0;
+  void* G = nullptr;
+  void* xbar[2] = {nullptr, nullptr};
+  double* part = nullptr;
+  int groups = 0;
+  double* slab_cons = nullptr;
+  double* slab_loss = nullptr;
+
+  // topology
+  bool have_topo = false;
+  int64_t* rp = nullptr;
+  int32_t* ci = nullptr;
+  void* cw = nullptr;
+
+  // per-run buffers
+  int32_t* idx = nullptr;
+  size_t idx_cap = 0;
+  double* hobj = nullptr;
+  double* hcons = nullptr;
+  uint64_t* stamps = nullptr;
+  size_t hcap = 0;
+  void* staging = nullptr;
+
+  // scratch for the single-evaluation API (float64)
+  void* sx = nullptr;
+  size_t sx_cap = 0;
+
+  // profiling of k_round
+  bool prof = false;
+  std::vector<hipEvent_t> ev;
+  int64_t kr_launches = 0;
+  double kr_ms = 0.0;
+};
+
+namespace {
+
+void dfree(void*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+template <typename P>
+void dfree_t(P*& p) {
+  void* v = (void*)p;
+  dfree(v);
+  p = nullptr;
+}
+
+int dalloc(void** p, size_t bytes) {
+  dfree(*p);
+  if (bytes == 0) bytes = 16;
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return fail(DOPT_ERR_HIP, "hipMalloc(%zu bytes): %s", bytes, hipGetErrorString(e));
+  }
+  return DOPT_OK;
+}
+template <typename P>
+int dalloc_t(P** p, size_t bytes) {
+  void* v = (void*)*p;
+  int rc = dalloc(&v, bytes);
+  *p = (P*)v;
+  return rc;
+}
+
+int cpl_for(int64_t nch) {
+  int c = 1;
+  while ((int64_t)c * 64 < nch) c *= 2;
+  return c;
+}
+
+int set_device(dopt_ctx* c) {
+  HIPOK(hipSetDevice(c->device));
+  return DOPT_OK;
+}
+
+// Upload rows x d host values (float64 or float32) into a T-typed [rows x ld]
+// device array through the staging buffer and the convert kernel.
+int upload_rows(dopt_ctx* c, int dtype, const void* src, int src_f32, void* dst, int64_t rows,
+                int64_t d, int64_t ld) {
+  if (rows == 0) return DOPT_OK;
+  const size_t src_esz = src_f32 ? 4 : 8;
+  const size_t dst_esz = dtype == DOPT_F32 ? 4 : 8;
+  if (!c->staging) {
+    int rc = dalloc(&c->staging, kStaging);
+    if (rc) return rc;
+  }
+  const int64_t row_bytes = d * (int64_t)src_esz;
+  int64_t chunk = std::max<int64_t>(1, (int64_t)kStaging / std::max<int64_t>(1, row_bytes));
+  if (row_bytes > (int64_t)kStaging) return fail(DOPT_ERR_UNSUPPORTED, "row of %lld bytes exceeds staging", (long long)row_bytes);
+  for (int64_t r0 = 0; r0 < rows; r0 += chunk) {
+    const int64_t nr = std::min(chunk, rows - r0);
+    HIPOK(hipMemcpyAsync(c->staging, (const char*)src + r0 * row_bytes, (size_t)(nr * row_bytes),
+                         hipMemcpyHostToDevice, c->stream));
+    HIPOK(launch_convert(dtype, c->staging, src_f32, (char*)dst + r0 * ld * (int64_t)dst_esz, nr, d, ld,
+                         c->stream));
+  }
+  HIPOK(hipStreamSynchronize(c->stream));
+  return DOPT_OK;
+}
+
+// Device T [rows x ld] -> host float64 [rows x d].
+int download_rows(dopt_ctx* c, const void* src, double* dst, int64_t rows, int64_t d, int64_t ld) {
+  if (rows == 0) return DOPT_OK;
+  std::vector<char> tmp((size_t)(rows * ld) * c->esz);
+  HIPOK(hipMemcpyAsync(tmp.data(), src, tmp.size(), hipMemcpyDeviceToHost, c->stream));
+  HIPOK(hipStreamSynchronize(c->stream));
+  for (int64_t r = 0; r < rows; ++r)
+    for (int64_t k = 0; k < d; ++k) {
+      const int64_t s = r * ld + k;
+      dst[r * d + k] = c->dtype == DOPT_F32 ? (double)((const float*)tmp.data())[s]
+                                            : ((const double*)tmp.data())[s];
+    }
+  return DOPT_OK;
+}
+
+int alloc_state(dopt_ctx* c) {
+  const size_t st = (size_t)std::max<int64_t>(1, c->n) * c->ld * c->esz;
+  int rc;
+  for (int k = 0; k < 2; ++k) {
+    if ((rc = dalloc(&c->xs[k], st))) return rc;
+    HIPOK(hipMemsetAsync(c->xs[k], 0, st, c->stream));  // Worker.x = zeros (worker.py:13)
+    if ((rc = dalloc(&c->xg[k], c->ld * c->esz))) return rc;
+    HIPOK(hipMemsetAsync(c->xg[k], 0, c->ld * c->esz, c->stream));  // trainer.py:11
+    if ((rc = dalloc(&c->xbar[k], c->ld * c->esz))) return rc;
+    HIPOK(hipMemsetAsync(c->xbar[k], 0, c->ld * c->esz, c->stream));
+  }
+  dfree(c->G);  // allocated on first centralized run
+  c->cur = 0;
+  c->gcur = 0;
+  c->groups = (int)((std::max<int64_t>(1, c->n) + kRowsPerGroup - 1) / kRowsPerGroup);
+  if ((rc = dalloc_t(&c->part, (size_t)c->groups * c->ld * sizeof(double)))) return rc;
+  if ((rc = dalloc_t(&c->slab_cons, (size_t)std::max<int64_t>(1, c->n) * sizeof(double)))) return rc;
+  if ((rc = dalloc_t(&c->slab_loss, (size_t)std::max<int64_t>(1, c->n) * sizeof(double)))) return rc;
+  HIPOK(hipStreamSynchronize(c->stream));
+  return DOPT_OK;
+}
+
+int set_layout(dopt_ctx* c, int problem, int64_t n, int64_t d) {
+  if (problem != DOPT_LOGISTIC && problem != DOPT_QUADRATIC)
+    return fail(DOPT_ERR_UNSUPPORTED, "unknown problem %d", problem);
+  CHECK_ARG(n >= 1 && d >= 1, "n_workers (%lld) and d (%lld) must be >= 1", (long long)n, (long long)d);
+  CHECK_ARG(n < (1LL << 31), "n_workers too large");
+  const int64_t ld = (d + c->vn - 1) / c->vn * c->vn;
+  const int64_t nch = ld / c->vn;
+  const int cpl = cpl_for(nch);
+  if (cpl > max_chunks_per_lane())
+    return fail(DOPT_ERR_UNSUPPORTED, "d = %lld exceeds the row-resident kernel limit (%d)", (long long)d,
+                max_chunks_per_lane() * 64 * c->vn);
+  c->problem = problem;
+  c->n = n;
+  c->d = d;
+  c->ld = ld;
+  c->nch = nch;
+  c->cpl = cpl;
+  c->have_topo = false;
+  c->obj_sep = false;
+  return DOPT_OK;
+}
+
+int ensure_hist(dopt_ctx* c, int64_t T) {
+  if ((size_t)T <= c->hcap && c->hobj) return DOPT_OK;
+  const size_t cap = (size_t)std::max<int64_t>(T, 16);
+  int rc;
+  if ((rc = dalloc_t(&c->hobj, cap * sizeof(double)))) return rc;
+  if ((rc = dalloc_t(&c->hcons, cap * sizeof(double)))) return rc;
+  if ((rc = dalloc_t(&c->stamps, (cap + 1) * sizeof(uint64_t)))) return rc;
+  c->hcap = cap;
+  return DOPT_OK;
+}
+
+RoundArgs base_args(dopt_ctx* c) {
+  RoundArgs a;
+  memset(&a, 0, sizeof(a));
+  a.X = c->X;
+  a.y = c->y;
+  a.off = c->off;
+  a.ld = c->ld;
+  a.nchunks = (int32_t)c->nch;
+  a.slab_cons = c->slab_cons;
+  a.slab_loss = c->slab_loss;
+  return a;
+}
+
+// Metrics-only pass over the objective rows (shards or the separate dataset).
+int metrics_pass(dopt_ctx* c, const void* x_state, const void* point, bool shared, bool cons,
+                 bool loss) {
+  RoundArgs a = base_args(c);
+  if (c->obj_sep) {
+    a.X = c->Xo;
+    a.y = c->yo;
+    a.off = c->offo;
+  }
+  a.x_old = x_state;
+  a.xbar = point;
+  a.w_shared = point;
+  a.flags = (cons ? F_CONS : 0) | (loss ? F_LOSS : 0) | (shared ? (F_SHARED | F_LOSS_FROM_Z) : 0);
+  HIPOK(launch_round(c->dtype, c->problem, c->cpl, false, true, a, (int)c->n, c->stream));
+  return DOPT_OK;
+}
+
+int64_t obj_rows(dopt_ctx* c) { return c->obj_sep ? c->rows_o : c->rows; }
+
+int upload_idx_chunk(dopt_ctx* c, const int32_t* idx, int64_t h0, int64_t nr, int64_t b) {
+  const size_t bytes = (size_t)(nr * c->n * b) * sizeof(int32_t);
+  if (bytes > c->idx_cap * sizeof(int32_t) || !c->idx) {
+    int rc = dalloc_t(&c->idx, bytes);
+    if (rc) return rc;
+    c->idx_cap = bytes / sizeof(int32_t);
+  }
+  HIPOK(hipMemcpyAsync(c->idx, idx + h0 * c->n * b, bytes, hipMemcpyHostToDevice, c->stream));
+  return DOPT_OK;
+}
+
+int prof_event(dopt_ctx* c, size_t k) {
+  while (c->ev.size() <= k) {
+    hipEvent_t e;
+    HIPOK(hipEventCreate(&e));
+    c->ev.push_back(e);
+  }
+  HIPOK(hipEventRecord(c->ev[k], c->stream));
+  return DOPT_OK;
+}
+
+int finish_run(dopt_ctx* c, int64_t T, int64_t launches, double* obj_out, double* cons_out,
+               double* time_out) {
+  HIPOK(hipStreamSynchronize(c->stream));
+  if (obj_out && T > 0) HIPOK(hipMemcpy(obj_out, c->hobj, (size_t)T * sizeof(double), hipMemcpyDeviceToHost));
+  if (cons_out && T > 0)
+    HIPOK(hipMemcpy(cons_out, c->hcons, (size_t)T * sizeof(double), hipMemcpyDeviceToHost));
+  if (time_out && T > 0) {
+    std::vector<uint64_t> st((size_t)T + 1);
+    HIPOK(hipMemcpy(st.data(), c->stamps, st.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    for (int64_t h = 0; h < T; ++h) time_out[h] = (double)(st[(size_t)h + 1] - st[0]) / c->clock_hz;
+  }
+  c->kr_launches = 0;
+  c->kr_ms = 0.0;
+  if (c->prof) {
+    for (int64_t k = 0; k < launches; ++k) {
+      float ms = 0.f;
+      HIPOK(hipEventElapsedTime(&ms, c->ev[(size_t)(2 * k)], c->ev[(size_t)(2 * k + 1)]));
+      c->kr_ms += ms;
+    }
+    c->kr_launches = launches;
+  }
+  return DOPT_OK;
+}
+
+int check_run(dopt_ctx* c, int64_t T, int64_t batch, const int32_t* idx, bool need_topo) {
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
+  if (need_topo && !c->have_topo) return fail(DOPT_ERR_STATE, "no topology set");
+  CHECK_ARG(T >= 0, "T must be >= 0");
+  CHECK_ARG(batch >= 0, "batch must be >= 0");
+  if (!idx && batch < c->max_m)
+    return fail(DOPT_ERR_INVALID, "idx == NULL needs full-shard batches (batch %lld < shard %lld)",
+                (long long)batch, (long long)c->max_m);
+  return DOPT_OK;
+}
+
+int64_t idx_chunk_rounds(dopt_ctx* c, int64_t T, int64_t b) {
+  const int64_t per = std::max<int64_t>(1, c->n * b * (int64_t)sizeof(int32_t));
+  return std::max<int64_t>(1, std::min<int64_t>(T, (int64_t)(256ll << 20) / per));
+}
+
+}  // namespace
+
+// ============================================================================ C ABI
+extern "C" {
+
+int dopt_abi_version(void) { return DOPT_ABI_VERSION; }
+const char* dopt_last_error(void) { return g_err.c_str(); }
+
+int dopt_device_count(int* count) {
+  CHECK_ARG(count, "count is NULL");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) n = 0;
+  *count = n;
+  return DOPT_OK;
+}
+
+int dopt_create(int device, int dtype, dopt_ctx** out) {
+  CHECK_ARG(out, "out is NULL");
+  CHECK_ARG(dtype == DOPT_F32 || dtype == DOPT_F64, "dtype must be DOPT_F32 or DOPT_F64");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(DOPT_ERR_HIP, "no HIP device visible");
+  CHECK_ARG(device >= 0 && device < n, "device %d out of range (%d visible)", device, n);
+  dopt_ctx* c = new dopt_ctx();
+  c->device = device;
+  c->dtype = dtype;
+  c->esz = dtype == DOPT_F32 ? 4 : 8;
+  c->vn = dtype == DOPT_F32 ? 4 : 2;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(DOPT_ERR_HIP, "context init: %s", hipGetErrorString(e));
+  }
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
+    c->clock_hz = (double)khz * 1e3;
+  *out = c;
+  return DOPT_OK;
+}
+
+int dopt_destroy(dopt_ctx* c) {
+  if (!c) return DOPT_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (void** p : {&c->X, &c->y, &c->Xo, &c->yo, &c->xs[0], &c->xs[1], &c->xg[0], &c->xg[1], &c->G,
+                   &c->xbar[0], &c->xbar[1], &c->cw, &c->staging, &c->sx})
+    dfree(*p);
+  dfree_t(c->off);
+  dfree_t(c->offo);
+  dfree_t(c->part);
+  dfree_t(c->slab_cons);
+  dfree_t(c->slab_loss);
+  dfree_t(c->rp);
+  dfree_t(c->ci);
+  dfree_t(c->idx);
+  dfree_t(c->hobj);
+  dfree_t(c->hcons);
+  dfree_t(c->stamps);
+  for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return DOPT_OK;
+}
+
+int dopt_load_shards(dopt_ctx* c, int problem, int64_t n_workers, int64_t d, const int64_t* off,
+                     const void* X, const void* y, int src_f32) {
+  CHECK_ARG(c, "ctx is NULL");
+  CHECK_ARG(off, "shard_offsets is NULL");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  c->have_data = false;
+  if ((rc = set_layout(c, problem, n_workers, d))) return rc;
+  CHECK_ARG(off[0] == 0, "shard_offsets[0] must be 0");
+  int64_t max_m = 0;
+  for (int64_t i = 0; i < n_workers; ++i) {
+    CHECK_ARG(off[i + 1] >= off[i], "shard_offsets must be non-decreasing");
+    max_m = std::max(max_m, off[i + 1] - off[i]);
+  }
+  const int64_t rows = off[n_workers];
+  CHECK_ARG(rows == 0 || (X && y), "X / y are NULL");
+  c->rows = rows;
+  c->max_m = max_m;
+  c->off_h.assign(off, off + n_workers + 1);
+  if ((rc = dalloc(&c->X, (size_t)rows * c->ld * c->esz))) return rc;
+  if ((rc = dalloc(&c->y, (size_t)rows * c->esz))) return rc;
+  if ((rc = dalloc_t(&c->off, (size_t)(n_workers + 1) * sizeof(int64_t)))) return rc;
+  HIPOK(hipMemcpy(c->off, off, (size_t)(n_workers + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  if ((rc = upload_rows(c, c->dtype, X, src_f32, c->X, rows, d, c->ld))) return rc;
+  if ((rc = upload_rows(c, c->dtype, y, src_f32, c->y, rows, 1, 1))) return rc;
+  if ((rc = alloc_state(c))) return rc;
+  c->have_data = true;
+  return DOPT_OK;
+}
+
+int dopt_generate_shards(dopt_ctx* c, int problem, int64_t n_workers, int64_t d, int64_t rpw,
+                         uint64_t seed, double flip, double noise) {
+  CHECK_ARG(c, "ctx is NULL");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  c->have_data = false;
+  if ((rc = set_layout(c, problem, n_workers, d))) return rc;
+  CHECK_ARG(rpw >= 1, "rows_per_worker must be >= 1");
+  const int64_t rows = n_workers * rpw;
+  c->rows = rows;
+  c->max_m = rpw;
+  c->off_h.resize((size_t)n_workers + 1);
+  for (int64_t i = 0; i <= n_workers; ++i) c->off_h[(size_t)i] = i * rpw;
+  if ((rc = dalloc(&c->X, (size_t)rows * c->ld * c->esz))) return rc;
+  if ((rc = dalloc(&c->y, (size_t)rows * c->esz))) return rc;
+  if ((rc = dalloc_t(&c->off, (size_t)(n_workers + 1) * sizeof(int64_t)))) return rc;
+  HIPOK(hipMemcpy(c->off, c->off_h.data(), (size_t)(n_workers + 1) * sizeof(int64_t),
+                  hipMemcpyHostToDevice));
+  HIPOK(launch_generate(c->dtype, problem, c->X, c->y, rows, d, c->ld, seed, flip, noise, c->stream));
+  HIPOK(hipStreamSynchronize(c->stream));
+  if ((rc = alloc_state(c))) return rc;
+  c->have_data = true;
+  return DOPT_OK;
+}
+
+int dopt_load_objective_data(dopt_ctx* c, int64_t n_rows, const void* X, const void* y, int src_f32) {
+  CHECK_ARG(c, "ctx is NULL");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");
+  CHECK_ARG(n_rows >= 0, "n_rows must be >= 0");
+  CHECK_ARG(n_rows == 0 || (X && y), "X / y are NULL");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  if ((rc = dalloc(&c->Xo, (size_t)n_rows * c->ld * c->esz))) return rc;
+  if ((rc = dalloc(&c->yo, (size_t)n_rows * c->esz))) return rc;
+  if ((rc = upload_rows(c, c->dtype, X, src_f32, c->Xo, n_rows, c->d, c->ld))) return rc;
+  if ((rc = upload_rows(c, c->dtype, y, src_f32, c->yo, n_rows, 1, 1))) return rc;
+  // split the objective rows over the N metric workgroups (array_split sizes)
+  std::vector<int64_t> o((size_t)c->n + 1);
+  const int64_t q = n_rows / c->n, r = n_rows % c->n;
+  o[0] = 0;
+  for (int64_t i = 0; i < c->n; ++i) o[(size_t)i + 1] = o[(size_t)i] + q + (i < r ? 1 : 0);
+  if ((rc = dalloc_t(&c->offo, o.size() * sizeof(int64_t)))) return rc;
+  HIPOK(hipMemcpy(c->offo, o.data(), o.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  c->rows_o = n_rows;
+  c->obj_sep = true;
+  return DOPT_OK;
+}
+
+int dopt_clear_objective_data(dopt_ctx* c) {
+  CHECK_ARG(c, "ctx is NULL");
+  c->obj_sep = false;
+  c->rows_o = 0;
+  return DOPT_OK;
+}
+
+int dopt_get_shard(dopt_ctx* c, int64_t worker, double* X_out, double* y_out) {
+  CHECK_ARG(c, "ctx is NULL");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
+  CHECK_ARG(worker >= 0 && worker < c->n, "worker %lld out of range", (long long)worker);
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  const int64_t r0 = c->off_h[(size_t)worker], nr = c->off_h[(size_t)worker + 1] - r0;
+  if (X_out && (rc = download_rows(c, (const char*)c->X + r0 * c->ld * (int64_t)c->esz, X_out, nr, c->d, c->ld)))
+    return rc;
+  if (y_out && (rc = download_rows(c, (const char*)c->y + r0 * (int64_t)c->esz, y_out, nr, 1, 1))) return rc;
+  return DOPT_OK;
+}
+
+int dopt_set_topology(dopt_ctx* c, int64_t n_workers, const int64_t* row_ptr, const int32_t* col,
+                      const double* w) {
+  CHECK_ARG(c, "ctx is NULL");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");
+  CHECK_ARG(n_workers == c->n, "topology has %lld workers, data has %lld", (long long)n_workers,
+            (long long)c->n);
+  CHECK_ARG(row_ptr && row_ptr[0] == 0, "row_ptr[0] must be 0");
+  for (int64_t i = 0; i < n_workers; ++i) CHECK_ARG(row_ptr[i + 1] >= row_ptr[i], "row_ptr not monotone");
+  const int64_t nnz = row_ptr[n_workers];
+  CHECK_ARG(nnz == 0 || (col && w), "col / w are NULL");
+  for (int64_t e = 0; e < nnz; ++e) CHECK_ARG(col[e] >= 0 && col[e] < n_workers, "col out of range");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  if ((rc = dalloc_t(&c->rp, (size_t)(n_workers + 1) * sizeof(int64_t)))) return rc;
+  if ((rc = dalloc_t(&c->ci, (size_t)nnz * sizeof(int32_t)))) return rc;
+  if ((rc = dalloc(&c->cw, (size_t)nnz * c->esz))) return rc;
+  HIPOK(hipMemcpy(c->rp, row_ptr, (size_t)(n_workers + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (nnz) {
+    HIPOK(hipMemcpy(c->ci, col, (size_t)nnz * sizeof(int32_t), hipMemcpyHostToDevice));
+    if (c->dtype == DOPT_F64) {
+      HIPOK(hipMemcpy(c->cw, w, (size_t)nnz * sizeof(double), hipMemcpyHostToDevice));
+    } else {
+      std::vector<float> wf((size_t)nnz);
+      for (int64_t e = 0; e < nnz; ++e) wf[(size_t)e] = (float)w[e];
+      HIPOK(hipMemcpy(c->cw, wf.data(), (size_t)nnz * sizeof(float), hipMemcpyHostToDevice));
+    }
+  }
+  c->have_topo = true;
+  return DOPT_OK;
+}
+
+int dopt_set_models(dopt_ctx* c, const double* x) {
+  CHECK_ARG(c && x, "NULL argument");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  return upload_rows(c, c->dtype, x, 0, c->xs[c->cur], c->n, c->d, c->ld);
+}
+
+int dopt_get_models(dopt_ctx* c, double* x) {
+  CHECK_ARG(c && x, "NULL argument");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  return download_rows(c, c->xs[c->cur], x, c->n, c->d, c->ld);
+}
+
+int dopt_set_global(dopt_ctx* c, const double* x) {
+  CHECK_ARG(c && x, "NULL argument");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  return upload_rows(c, c->dtype, x, 0, c->xg[c->gcur], 1, c->d, c->ld);
+}
+
+int dopt_get_global(dopt_ctx* c, double* x) {
+  CHECK_ARG(c && x, "NULL argument");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  return download_rows(c, c->xg[c->gcur], x, 1, c->d, c->ld);
+}
+
+int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch, const int32_t* idx,
+                  double lam_grad, double lam_obj, double f_opt, uint32_t flags, double* obj_out,
+                  double* cons_out, double* time_out) {
+  CHECK_ARG(c, "ctx is NULL");
+  int rc;
+  if ((rc = check_run(c, T, batch, idx, true))) return rc;
+  if ((rc = set_device(c))) return rc;
+  if ((rc = ensure_hist(c, T))) return rc;
+  const bool want_obj = flags & DOPT_RUN_OBJECTIVE, want_cons = flags & DOPT_RUN_CONSENSUS;
+  const bool metrics = want_obj || want_cons;
+  const bool fused = batch >= c->max_m && !c->obj_sep;
+  const int64_t CH = idx ? idx_chunk_rounds(c, T, batch) : 1;
+  double* hobj = want_obj ? c->hobj : nullptr;
+  double* hcons = want_cons ? c->hcons : nullptr;
+  int xb = 0;  // xbar[xb] = average of the current iterates (valid once computed)
+  HIPOK(launch_stamp(c->stamps, c->stream));
+
+  for (int64_t h = 0; h < T; ++h) {
+    const int64_t t = t0 + h;
+    if (idx && h % CH == 0) {
+      if ((rc = upload_idx_chunk(c, idx, h, std::min(CH, T - h), batch))) return rc;
+    }
+    RoundArgs a = base_args(c);
+    a.idx = idx ? c->idx + (h % CH) * c->n * batch : nullptr;
+    a.b = batch;
+    a.x_old = c->xs[c->cur];
+    a.x_new = c->xs[c->cur ^ 1];
+    a.xbar = c->xbar[xb];
+    a.rp = c->rp;
+    a.ci = c->ci;
+    a.cw = c->cw;
+    a.eta = eta0 / sqrt((double)(t + 1));  // trainer.py:138-140
+    a.lam = lam_grad;
+    const bool met = fused && metrics && h > 0;
+    a.flags = F_STEP | (met && want_cons ? F_CONS : 0) | (met && want_obj ? F_LOSS : 0);
+    if (c->prof && (rc = prof_event(c, (size_t)(2 * h)))) return rc;
+    HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, met, a, (int)c->n, c->stream));
+    if (c->prof && (rc = prof_event(c, (size_t)(2 * h + 1)))) return rc;
+    // xbar_{t+1} (trainer.py:182); the stamp marks the end of round t's update (trainer.py:181)
+    HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur ^ 1], c->n, c->ld, (int32_t)c->nch, kRowsPerGroup,
+                                c->part, c->stamps + h + 1, c->stream));
+    HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nch, c->xbar[xb ^ 1],
+                              nullptr, 0.0, 0, c->stream));
+    if (met) {
+      HIPOK(launch_history(c->dtype, c->problem, c->slab_cons, c->slab_loss, c->n, c->n, obj_rows(c),
+                           c->xbar[xb], c->ld, (int32_t)c->nch, lam_obj, f_opt, hobj, hcons, h - 1,
+                           c->stream));
+    } else if (!fused && metrics) {
+      if ((rc = metrics_pass(c, c->xs[c->cur ^ 1], c->xbar[xb ^ 1], false, want_cons, want_obj))) return rc;
+      HIPOK(launch_history(c->dtype, c->problem, c->slab_cons, c->slab_loss, c->n, c->n, obj_rows(c),
+                           c->xbar[xb ^ 1], c->ld, (int32_t)c->nch, lam_obj, f_opt, hobj, hcons, h,
+                           c->stream));
+    }
+    c->cur ^= 1;
+    xb ^= 1;
+  }
+  if (fused && metrics && T > 0) {  // history[T-1]: one metrics pass over x_T
+    if ((rc = metrics_pass(c, c->xs[c->cur], c->xbar[xb], false, want_cons, want_obj))) return rc;
+    HIPOK(launch_history(c->dtype, c->problem, c->slab_cons, c->slab_loss, c->n, c->n, obj_rows(c),
+                         c->xbar[xb], c->ld, (int32_t)c->nch, lam_obj, f_opt, hobj, hcons, T - 1,
+                         c->stream));
+  }
+  return finish_run(c, T, T, obj_out, cons_out, time_out);
+}
+
+int dopt_run_centralized(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch,
+                         const int32_t* idx, double lam_grad, double lam_obj, double f_opt,
+                         uint32_t flags, double* obj_out, double* time_out) {
+  CHECK_ARG(c, "ctx is NULL");
+  int rc;
+  if ((rc = check_run(c, T, batch, idx, false))) return rc;
+  if ((rc = set_device(c))) return rc;
+  if ((rc = ensure_hist(c, T))) return rc;
+  if (!c->G && (rc = dalloc(&c->G, (size_t)c->n * c->ld * c->esz))) return rc;
+  const bool want_obj = flags & DOPT_RUN_OBJECTIVE;
+  const bool fused = batch >= c->max_m && !c->obj_sep;
+  const int64_t CH = idx ? idx_chunk_rounds(c, T, batch) : 1;
+  HIPOK(launch_stamp(c->stamps, c->stream));
+
+  for (int64_t h = 0; h < T; ++h) {
+    const int64_t t = t0 + h;
+    if (idx && h % CH == 0) {
+      if ((rc = upload_idx_chunk(c, idx, h, std::min(CH, T - h), batch))) return rc;
+    }
+    RoundArgs a = base_args(c);
+    a.idx = idx ? c->idx + (h % CH) * c->n * batch : nullptr;
+    a.b = batch;
+    a.w_shared = c->xg[c->gcur];
+    a.g_out = c->G;
+    a.lam = lam_grad;
+    const bool met = fused && want_obj && h > 0;
+    a.flags = F_GOUT | F_SHARED | (met ? (F_LOSS | F_LOSS_FROM_Z) : 0);
+    if (c->prof && (rc = prof_event(c, (size_t)(2 * h)))) return rc;
+    HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, met, a, (int)c->n, c->stream));
+    if (c->prof && (rc = prof_event(c, (size_t)(2 * h + 1)))) return rc;
+    // mean of the worker gradients and the step (trainer.py:53-57)
+    HIPOK(launch_colsum_partial(c->dtype, c->G, c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part,
+                                c->stamps + h + 1, c->stream));
+    HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nch,
+                              c->xg[c->gcur ^ 1], c->xg[c->gcur], eta0 / sqrt((double)(t + 1)), 1,
+                              c->stream));
+    if (met) {
+      HIPOK(launch_history(c->dtype, c->problem, nullptr, c->slab_loss, c->n, c->n, obj_rows(c),
+                           c->xg[c->gcur], c->ld, (int32_t)c->nch, lam_obj, f_opt, c->hobj, nullptr,
+                           h - 1, c->stream));
+    } else if (!fused && want_obj) {
+      if ((rc = metrics_pass(c, nullptr, c->xg[c->gcur ^ 1], true, false, true))) return rc;
+      HIPOK(launch_history(c->dtype, c->problem, nullptr, c->slab_loss, c->n, c->n, obj_rows(c),
+                           c->xg[c->gcur ^ 1], c->ld, (int32_t)c->nch, lam_obj, f_opt, c->hobj, nullptr,
+                           h, c->stream));
+    }
+    c->gcur ^= 1;
+  }
+  if (fused && want_obj && T > 0) {
+    if ((rc = metrics_pass(c, nullptr, c->xg[c->gcur], true, false, true))) return rc;
+    HIPOK(launch_history(c->dtype, c->problem, nullptr, c->slab_loss, c->n, c->n, obj_rows(c),
+                         c->xg[c->gcur], c->ld, (int32_t)c->nch, lam_obj, f_opt, c->hobj, nullptr,
+                         T - 1, c->stream));
+  }
+  return finish_run(c, T, T, want_obj ? obj_out : nullptr, nullptr, time_out);
+}
+
+// ---------------------------------------------------------------------------- single evaluations
+namespace {
+int eval_common(dopt_ctx* c, int problem, int64_t rows, int64_t d, const double* w, const double* X,
+                const double* y, bool grad, double reg, double* out) {
+  CHECK_ARG(c, "ctx is NULL");
+  if (problem != DOPT_LOGISTIC && problem != DOPT_QUADRATIC)
+    return fail(DOPT_ERR_UNSUPPORTED, "unknown problem %d", problem);
+  CHECK_ARG(rows >= 0 && d >= 1, "bad shape");
+  CHECK_ARG(w && out && (rows == 0 || (X && y)), "NULL argument");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  const int vn = 2;  // float64
+  const int64_t ld = (d + vn - 1) / vn * vn, nch = ld / vn;
+  const int cpl = cpl_for(nch);
+  if (cpl > max_chunks_per_lane())
+    return fail(DOPT_ERR_UNSUPPORTED, "d = %lld exceeds the row-resident kernel limit", (long long)d);
+  // objective: split rows over workgroups; gradient: one workgroup (one worker)
+  const int64_t groups = grad ? 1 : std::max<int64_t>(1, std::min<int64_t>(4096, (rows + 255) / 256));
+  // scratch layout (bytes, 16-aligned): X | y | w | g | off | slab | out
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t bX = al((size_t)rows * ld * 8), by = al((size_t)rows * 8), bw = al((size_t)ld * 8),
+               bg = al((size_t)ld * 8), bo = al((size_t)(groups + 1) * 8), bs = al((size_t)groups * 8),
+               bout = al(8);
+  const size_t need = bX + by + bw + bg + bo + bs + bout;
+  if (need > c->sx_cap) {
+    if ((rc = dalloc(&c->sx, need))) return rc;
+    c->sx_cap = need;
+  }
+  char* base = (char*)c->sx;
+  void* dX = base;
+  void* dy = base + bX;
+  void* dw = base + bX + by;
+  void* dg = base + bX + by + bw;
+  int64_t* doff = (int64_t*)(base + bX + by + bw + bg);
+  double* dslab = (double*)(base + bX + by + bw + bg + bo);
+  double* dout = (double*)(base + bX + by + bw + bg + bo + bs);
+  if ((rc = upload_rows(c, DOPT_F64, X, 0, dX, rows, d, ld))) return rc;
+  if ((rc = upload_rows(c, DOPT_F64, y, 0, dy, rows, 1, 1))) return rc;
+  if ((rc = upload_rows(c, DOPT_F64, w, 0, dw, 1, d, ld))) return rc;
+  std::vector<int64_t> o((size_t)groups + 1);
+  for (int64_t k = 0; k <= groups; ++k) o[(size_t)k] = rows * k / groups;
+  HIPOK(hipMemcpy(doff, o.data(), o.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  RoundArgs a;
+  memset(&a, 0, sizeof(a));
+  a.X = dX;
+  a.y = dy;
+  a.off = doff;
+  a.w_shared = dw;
+  a.g_out = dg;
+  a.lam = reg;
+  a.ld = ld;
+  a.nchunks = (int32_t)nch;
+  a.slab_loss = dslab;
+  if (grad) {
+    a.flags = F_GOUT | F_SHARED;
+    HIPOK(launch_round(DOPT_F64, problem, cpl, true, false, a, 1, c->stream));
+    std::vector<double> g((size_t)ld);
+    HIPOK(hipMemcpyAsync(g.data(), dg, (size_t)ld * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPOK(hipStreamSynchronize(c->stream));
+    memcpy(out, g.data(), (size_t)d * sizeof(double));
+  } else {
+    a.flags = F_SHARED | F_LOSS | F_LOSS_FROM_Z;
+    HIPOK(launch_round(DOPT_F64, problem, cpl, false, true, a, (int)groups, c->stream));
+    HIPOK(launch_history(DOPT_F64, problem, nullptr, dslab, 1, groups, rows, dw, ld, (int32_t)nch, reg, 0.0,
+                         dout, nullptr, 0, c->stream));
+    HIPOK(hipMemcpyAsync(out, dout, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPOK(hipStreamSynchronize(c->stream));
+  }
+  return DOPT_OK;
+}
+}  // namespace
+
+int dopt_eval_gradient(dopt_ctx* c, int problem, int64_t b, int64_t d, const double* w, const double* X,
+                       const double* y, double reg, double* g_out) {
+  return eval_common(c, problem, b, d, w, X, y, true, reg, g_out);
+}
+
+int dopt_eval_objective(dopt_ctx* c, int problem, int64_t n, int64_t d, const double* w, const double* X,
+                        const double* y, double reg, double* out) {
+  return eval_common(c, problem, n, d, w, X, y, false, reg, out);
+}
+
+int dopt_set_profiling(dopt_ctx* c, int enable) {
+  CHECK_ARG(c, "ctx is NULL");
+  c->prof = enable != 0;
+  return DOPT_OK;
+}
+
+int dopt_kernel_stats(dopt_ctx* c, int64_t* launches, double* total_ms) {
+  CHECK_ARG(c && launches && total_ms, "NULL argument");
+  *launches = c->kr_launches;
+  *total_ms = c->kr_ms;
+  return DOPT_OK;
+}
+
+}  // extern "C"

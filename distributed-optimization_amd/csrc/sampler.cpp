@@ -1,0 +1,124 @@
+// sampler.cpp -- legacy-MT19937 minibatch sampler (host code).
+//
+// Worker.get_mini_batch draws idx = np.random.choice(m, b, replace=False)
+// (worker.py:27) from numpy's global RandomState.  In numpy's legacy path that is
+// permutation(m)[:b]: a full Fisher-Yates shuffle of arange(m) driven by
+// random_interval(i) (masked rejection on 32-bit MT19937 outputs), i = m-1 .. 1.
+// This file restates that algorithm so the engine can produce the same index
+// stream for T rounds x N workers in one call, reading and writing numpy's
+// state words (key[624], pos) in place.  The draw is inherently sequential
+// (one global stream, data-dependent rejection counts), so it stays on the host.
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "dopt.h"
+
+namespace {
+
+constexpr int kN = 624, kM = 397;
+constexpr uint32_t kMatrixA = 0x9908b0dfu, kUpper = 0x80000000u, kLower = 0x7fffffffu;
+
+struct MT {
+  uint32_t* key;
+  int32_t pos;
+
+  void twist() {
+    int i = 0;
+    uint32_t y;
+    for (; i < kN - kM; ++i) {
+      y = (key[i] & kUpper) | (key[i + 1] & kLower);
+      key[i] = key[i + kM] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
+    }
+    for (; i < kN - 1; ++i) {
+      y = (key[i] & kUpper) | (key[i + 1] & kLower);
+      key[i] = key[i + (kM - kN)] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
+    }
+    y = (key[kN - 1] & kUpper) | (key[0] & kLower);
+    key[kN - 1] = key[kM - 1] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
+    pos = 0;
+  }
+  uint32_t next32() {
+    if (pos >= kN) twist();
+    uint32_t y = key[pos++];
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+  }
+  uint64_t next64() {
+    const uint64_t hi = next32();
+    return (hi << 32) | next32();
+  }
+  // uniform integer in [0, max] by masked rejection
+  uint64_t interval(uint64_t max) {
+    if (max == 0) return 0;
+    uint64_t mask = max;
+    mask |= mask >> 1;
+    mask |= mask >> 2;
+    mask |= mask >> 4;
+    mask |= mask >> 8;
+    mask |= mask >> 16;
+    mask |= mask >> 32;
+    uint64_t v;
+    if (max <= 0xffffffffull) {
+      while ((v = (next32() & mask)) > max) {
+      }
+    } else {
+      while ((v = (next64() & mask)) > max) {
+      }
+    }
+    return v;
+  }
+};
+
+// permutation(m)[:eb] -> out; perm is scratch of size m.
+template <typename I>
+void choice_prefix(MT& mt, int64_t m, int64_t eb, std::vector<int64_t>& perm, I* out) {
+  perm.resize((size_t)m);
+  for (int64_t k = 0; k < m; ++k) perm[(size_t)k] = k;
+  for (int64_t k = m - 1; k >= 1; --k) {
+    const int64_t j = (int64_t)mt.interval((uint64_t)k);
+    const int64_t t = perm[(size_t)k];
+    perm[(size_t)k] = perm[(size_t)j];
+    perm[(size_t)j] = t;
+  }
+  for (int64_t k = 0; k < eb; ++k) out[k] = (I)perm[(size_t)k];
+}
+
+}  // namespace
+
+extern "C" int dopt_mt_choice(uint32_t key[624], int32_t* pos, int64_t m, int64_t b, int64_t* out) {
+  if (!key || !pos || m < 0 || b < 0 || *pos < 0 || *pos > kN) return DOPT_ERR_INVALID;
+  if (m == 0) return DOPT_OK;  // worker.py:17-18: no draw for an empty shard
+  const int64_t eb = b < m ? b : m;
+  if (eb <= 0) return DOPT_OK;  // worker.py:21-23
+  MT mt{key, *pos};
+  std::vector<int64_t> perm;
+  choice_prefix(mt, m, eb, perm, out);
+  *pos = mt.pos;
+  return DOPT_OK;
+}
+
+extern "C" int dopt_mt_choice_rounds(uint32_t key[624], int32_t* pos, int64_t T, int64_t n_workers,
+                                     const int64_t* shard_rows, int64_t b, int32_t* out) {
+  if (!key || !pos || T < 0 || n_workers < 0 || b < 0 || *pos < 0 || *pos > kN) return DOPT_ERR_INVALID;
+  if (n_workers > 0 && !shard_rows) return DOPT_ERR_INVALID;
+  for (int64_t i = 0; i < n_workers; ++i)
+    if (shard_rows[i] < 0 || shard_rows[i] > 0x7fffffffLL) return DOPT_ERR_INVALID;
+  MT mt{key, *pos};
+  std::vector<int64_t> perm;
+  for (int64_t t = 0; t < T; ++t) {
+    for (int64_t i = 0; i < n_workers; ++i) {
+      int32_t* o = out + (t * n_workers + i) * b;
+      const int64_t m = shard_rows[i];
+      const int64_t eb = (m == 0) ? 0 : (b < m ? b : m);
+      if (eb > 0) choice_prefix(mt, m, eb, perm, o);
+      for (int64_t k = eb; k < b; ++k) o[k] = -1;
+    }
+  }
+  *pos = mt.pos;
+  return DOPT_OK;
+}

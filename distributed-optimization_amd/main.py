@@ -1,0 +1,50 @@
+"""Entry point (drop-in for main.py): the report's N=25 experiment on the GPU engine.
+
+Same module constants and seed as the reference (main.py:6-24).  Run from this
+directory:  python main.py
+"""
+import numpy as np
+
+from simulator import Simulator
+
+N_WORKERS = 25
+LOCAL_BATCH_SIZE = 16
+N_ITERATIONS = 10000
+LEARNING_RATE_ETA0 = 0.05
+SUBOPTIMALITY_THRESHOLD = 0.08
+
+PROBLEM_TYPE = "quadratic"  # 'logistic', 'quadratic'
+
+N_SAMPLES = N_WORKERS * 500
+N_FEATURES = 80
+N_INFORMATIVE_FEATURES = 50
+CLASSIFICATION_SEP = 0.7
+
+L2_REGULARIZATION_LAMBDA = 1e-4
+STRONG_CONVEXITY_MU = L2_REGULARIZATION_LAMBDA
+
+
+def make_config(**overrides):
+    cfg = {
+        "n_workers": N_WORKERS,
+        "local_batch_size": LOCAL_BATCH_SIZE,
+        "n_iterations": N_ITERATIONS,
+        "learning_rate_eta0": LEARNING_RATE_ETA0,
+        "l2_regularization_lambda": L2_REGULARIZATION_LAMBDA,
+        "strong_convexity_mu": STRONG_CONVEXITY_MU,
+        "problem_type": PROBLEM_TYPE,
+        "n_samples": N_SAMPLES,
+        "n_features": N_FEATURES,
+        "n_informative_features": N_INFORMATIVE_FEATURES,
+        "classification_sep": CLASSIFICATION_SEP,
+        "suboptimality_threshold": SUBOPTIMALITY_THRESHOLD,
+    }
+    cfg.update(overrides)
+    return cfg
+
+
+if __name__ == "__main__":
+    np.random.seed(203)
+    simulator = Simulator(make_config())
+    simulator.run_all()
+    simulator.plot_results()

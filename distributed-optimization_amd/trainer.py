@@ -1,0 +1,257 @@
+"""Trainers (drop-in for trainer.py): the round loop runs on the GPU.
+
+CentralizedTrainer   trainer.py:7-74     parameter-server mini-batch SGD
+DecentralizedTrainer trainer.py:76-197   D-SGD with Metropolis-Hastings mixing
+
+Same constructor signatures, attributes (workers, W, adj, degrees, topology,
+history, total_floats_transmitted, x_global), prints, errors and return values
+as the reference.  What changes is underneath `run`: instead of a Python loop
+over workers per round, the shards live in HBM and every round is one fused
+HIP launch (gradient + mix + step, with the metrics of the previous round folded
+into the same pass over the data), driven through libdopt.so.
+
+Config keys beyond the reference's (all optional):
+  dtype      'float64' (default, trajectory parity) or 'float32' (throughput)
+  device     GPU ordinal (default: $LOCAL_RANK or $DOPT_DEVICE or 0)
+  sampling   'legacy' (default): minibatch indices are the exact numpy legacy
+             RNG stream (np.random.choice per worker per round, worker.py:27);
+             'full': with full-shard batches skip the RNG entirely
+  regular_degree / topology_seed   for topology='random_regular'
+  spectral_gap   force / skip the spectral-gap print (default: N <= 4096)
+"""
+import os
+import time
+
+import numpy as np
+
+import _dopt
+import topology as _topology
+from obj_problems import logistic_objective, quadratic_objective
+
+DENSE_LIMIT = 4096          # dense adj / W attributes up to this many workers
+IDX_CHUNK_ELEMS = 1 << 24   # host index buffer per device call (64 MiB of int32)
+
+
+# ---------------------------------------------------------------------------- shared helpers
+def _device(config):
+    return int(config.get("device", os.environ.get("LOCAL_RANK", os.environ.get("DOPT_DEVICE", 0))))
+
+
+def _pack(workers, n_features):
+    rows = np.array([w.X_local.shape[0] for w in workers], dtype=np.int64)
+    off = np.zeros(len(workers) + 1, dtype=np.int64)
+    np.cumsum(rows, out=off[1:])
+    if off[-1] > 0:
+        X = np.concatenate([np.asarray(w.X_local, dtype=np.float64).reshape(-1, n_features) for w in workers])
+        y = np.concatenate([np.asarray(w.y_local, dtype=np.float64).reshape(-1) for w in workers])
+    else:
+        X, y = np.zeros((0, n_features)), np.zeros(0)
+    return X, y, off
+
+
+def _data_key(workers):
+    return tuple((id(w.X_local), w.X_local.shape, id(w.y_local)) for w in workers)
+
+
+def _same_rows(A, ya, B, yb):
+    """True when (A, ya) and (B, yb) hold the same multiset of (row, label) pairs."""
+    A = np.asarray(A, dtype=np.float64)
+    B = np.asarray(B, dtype=np.float64)
+    ya = np.asarray(ya, dtype=np.float64).reshape(-1)
+    yb = np.asarray(yb, dtype=np.float64).reshape(-1)
+    if A.shape != B.shape or ya.shape[0] != A.shape[0] or yb.shape[0] != B.shape[0]:
+        return False
+    if np.array_equal(A, B) and np.array_equal(ya, yb):
+        return True
+    v = np.random.default_rng(12345).standard_normal(A.shape[1] + 1)
+    ha = A @ v[:-1] + ya * v[-1]
+    hb = B @ v[:-1] + yb * v[-1]
+    oa, ob = np.argsort(ha, kind="stable"), np.argsort(hb, kind="stable")
+    return bool(np.array_equal(A[oa], B[ob]) and np.array_equal(ya[oa], yb[ob]))
+
+
+_ENGINES = {}
+
+
+def _engine(workers, n_features, config):
+    """One resident engine per (device, dtype, problem, shard set), reused by the
+    four trainers Simulator.run_all builds over the same worker data."""
+    key = (_device(config), config.get("dtype", "float64"), config["problem_type"], _data_key(workers))
+    eng = _ENGINES.get(key)
+    if eng is None:
+        for k in [k for k in _ENGINES if k[:2] == key[:2]]:
+            _ENGINES.pop(k).close()  # free the previous data set's HBM
+        eng = _dopt.Engine(key[0], key[1])
+        X, y, off = _pack(workers, n_features)
+        eng.load_shards(config["problem_type"], X, y, off)
+        eng.obj_key = None
+        _ENGINES[key] = eng
+    return eng
+
+
+def _set_objective_data(eng, workers, n_features, X_full, y_full):
+    """trainer.py:188: the objective is recorded only when X_full and y_full are given.
+    When they hold exactly the shard rows (the Simulator case) the objective is fused
+    into the round's pass over the shards; otherwise X_full is uploaded separately."""
+    if X_full is None or y_full is None:
+        if eng.obj_key is not None:
+            eng.clear_objective_data()
+            eng.obj_key = None
+        return False
+    key = (id(X_full), np.shape(X_full), id(y_full))
+    if eng.obj_key != key:
+        X, y, _ = _pack(workers, n_features)
+        if _same_rows(X_full, y_full, X, y):
+            eng.clear_objective_data()
+        else:
+            eng.load_objective_data(np.asarray(X_full).reshape(-1, n_features), y_full)
+        eng.obj_key = key
+    return True
+
+
+def _batch_size(workers):
+    bs = {int(w.batch_size) for w in workers}
+    if len(bs) > 1:
+        raise NotImplementedError("workers with different batch sizes")
+    return bs.pop() if bs else 0
+
+
+def _index_chunks(workers, T, config):
+    """Yield (t_start, n_rounds, idx or None): minibatch indices drawn on the host in
+    trainer order (trainer.py:47-50 / :166), `None` when every batch is the full shard."""
+    b = _batch_size(workers)
+    rows = np.array([w.n_local_samples for w in workers], dtype=np.int64)
+    full = b >= (rows.max() if len(rows) else 0)
+    skip_rng = full and config.get("sampling", "legacy") == "full"
+    ch = max(1, IDX_CHUNK_ELEMS // max(1, len(workers) * max(b, 1)))
+    for t in range(0, T, ch):
+        n = min(ch, T - t)
+        if skip_rng:
+            yield t, n, b, None
+            continue
+        idx = _dopt.mt_choice_rounds(n, rows, b)  # advances np.random exactly like the reference
+        yield t, n, b, (None if full else idx)
+
+
+# ---------------------------------------------------------------------------- centralized
+class CentralizedTrainer:
+    def __init__(self, workers, n_features, config):
+        self.workers = workers
+        self.n_workers = len(workers)
+        self.x_global = np.zeros(n_features)
+        self.config = config
+        self.history = {"objective": [], "time": []}
+        self.n_features = n_features
+        self.total_floats_transmitted = 0
+
+    def _get_learning_rate(self, t):
+        return self.config["learning_rate_eta0"] / np.sqrt(t + 1)
+
+    def _get_objective_func(self):
+        problem_type = self.config["problem_type"]
+        if problem_type == "logistic":
+            return logistic_objective
+        elif problem_type == "quadratic":
+            return quadratic_objective
+        raise ValueError(f"Unknown problem type: {problem_type}")
+
+    def _get_regularization_param(self):
+        return self.config["l2_regularization_lambda"]
+
+    def run(self, n_iterations, X_full=None, y_full=None, f_opt=0.0):
+        print("\n--- Running Centralized Synchronous mini-batch SGD ---")
+        start_time = time.time()
+        self._get_objective_func()
+        reg_param = self._get_regularization_param()
+        self.total_floats_transmitted = 0
+        cfg = self.config
+        lam_grad = cfg["l2_regularization_lambda"] if cfg["problem_type"] == "logistic" else cfg["strong_convexity_mu"]
+        eng = _engine(self.workers, self.n_features, cfg)
+        want_obj = _set_objective_data(eng, self.workers, self.n_features, X_full, y_full)
+        eng.set_global(self.x_global)
+        for t0, n, b, idx in _index_chunks(self.workers, int(n_iterations), cfg):
+            t_host = time.time() - start_time
+            obj, tim = eng.run_centralized(n, cfg["learning_rate_eta0"], b, lam_grad, reg_param, f_opt, idx=idx,
+                                           t0=t0, objective=want_obj)
+            if want_obj:
+                self.history["objective"].extend(list(obj))
+            self.history["time"].extend((tim + t_host).tolist())
+            # trainer.py:50,60-61: N*d up + N*d down per round (Python ints)
+            self.total_floats_transmitted += n * (self.n_workers * self.n_features * 2)
+        self.x_global = eng.get_global()
+        print(f"C-SGD training finished. Time: {time.time() - start_time:.2f}sseconds")
+        return self.history, self.x_global
+
+
+# ---------------------------------------------------------------------------- decentralized
+class DecentralizedTrainer:
+    def __init__(self, workers, topology, n_features, config):
+        self.workers = workers
+        self.n_workers = len(workers)
+        self.topology = topology
+        self.n_features = n_features
+        self.config = config
+        self.adj = None
+        self.degrees = None
+        self.W = self._create_mixing_matrix()
+        print(f"\n--- Running Decentralized SGD ({self.topology} - {self.config['problem_type']}) ---")
+        self.history = {"objective": [], "consensus_error": [], "time": []}
+        self.total_floats_transmitted = 0
+
+    def _create_mixing_matrix(self):
+        """Metropolis-Hastings mixing matrix (trainer.py:91-136), built sparse."""
+        topo = _topology.build(self.topology, self.n_workers, self.config)
+        self._topo = topo
+        self.degrees = topo.degrees
+        dense = self.n_workers <= DENSE_LIMIT
+        self.adj = topo.dense_adjacency() if dense else None
+        W = topo.dense_W() if dense else topo.sparse_W()
+        if self.n_workers > 0:
+            topo.check()
+            if self.n_workers > 1 and self.config.get("spectral_gap", dense):
+                print(f"Mixing Matrix Spectral gap (1 - rho): {topo.spectral_gap():.4f} for topology: {self.topology}")
+        return W
+
+    def _get_learning_rate(self, t):
+        return self.config["learning_rate_eta0"] / np.sqrt(t + 1)
+
+    def _get_objective_func(self):
+        problem_type = self.config["problem_type"]
+        if problem_type == "logistic":
+            return logistic_objective
+        elif problem_type == "quadratic":
+            return quadratic_objective
+        raise NotImplementedError(f"Wrong {problem_type}")
+
+    def _get_regularization_param(self):
+        return self.config["l2_regularization_lambda"]
+
+    def run(self, n_iterations, X_full=None, y_full=None, f_opt=0.0):
+        start_time = time.time()
+        self._get_objective_func()
+        reg_param = self._get_regularization_param()
+        self.total_floats_transmitted = 0
+        cfg = self.config
+        lam_grad = cfg["l2_regularization_lambda"] if cfg["problem_type"] == "logistic" else cfg["strong_convexity_mu"]
+        eng = _engine(self.workers, self.n_features, cfg)
+        want_obj = _set_objective_data(eng, self.workers, self.n_features, X_full, y_full)
+        t = self._topo
+        eng.set_topology(t.row_ptr, t.col, t.w)
+        eng.set_models(np.stack([np.asarray(w.x, dtype=np.float64) for w in self.workers]))
+        iteration_transmission = np.sum(self.degrees) * self.n_features  # trainer.py:169
+        for t0, n, b, idx in _index_chunks(self.workers, int(n_iterations), cfg):
+            t_host = time.time() - start_time
+            obj, cons, tim = eng.run_dsgd(n, cfg["learning_rate_eta0"], b, lam_grad, reg_param, f_opt, idx=idx,
+                                          t0=t0, objective=want_obj, consensus=True)
+            self.history["consensus_error"].extend(list(cons))
+            if want_obj:
+                self.history["objective"].extend(list(obj))
+            self.history["time"].extend((tim + t_host).tolist())
+            for _ in range(n):
+                self.total_floats_transmitted += iteration_transmission
+        models = eng.get_models()
+        for i, worker in enumerate(self.workers):  # trainer.py:178-179: row views
+            worker.x = models[i, :]
+        print(f"Decentralized ({self.topology}) training finished. Time: {time.time() - start_time:.2f}s")
+        final_avg_model = np.mean([worker.x for worker in self.workers], axis=0)
+        return self.history, final_avg_model

@@ -1,0 +1,162 @@
+/*
+ * dopt.h -- C ABI of libdopt.so, the MI355X (gfx950) engine for the
+ * decentralized-SGD round of scavenx/distributed-optimization.
+ *
+ * The reference is pure Python/numpy and has no FFI of its own; this ABI is
+ * what its Python call sites bind to (over ctypes).  Each
+ * entry point names the reference code it replaces (file:line in the reference).
+ *
+ * Conventions
+ *   - Every call returns int: DOPT_OK (0) or a negative DOPT_ERR_* code;
+ *     dopt_last_error() then returns a message (thread-local, valid until the
+ *     next failing call on that thread).
+ *   - Host pointers are borrowed for the duration of the call and copied in/out.
+ *     All device memory is owned by the context and freed by dopt_destroy().
+ *   - One host thread per context; calls are synchronous at return.
+ *   - Load the HIP runtime your process already uses first (import torch
+ *     before loading libdopt.so when torch is in the process).
+ *   - Shards are stored back to back: worker i owns rows
+ *     [shard_offsets[i], shard_offsets[i+1]) of X (row-major, n_rows x d) and y.
+ *   - Model state is N x d row-major float64 at the boundary; the engine keeps
+ *     it on the device in the context's compute dtype.
+ */
+#ifndef DOPT_H_
+#define DOPT_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DOPT_ABI_VERSION 1
+
+typedef struct dopt_ctx dopt_ctx;
+
+/* status codes */
+#define DOPT_OK 0
+#define DOPT_ERR_INVALID (-1)     /* bad argument (maps to ValueError on the Python side) */
+#define DOPT_ERR_HIP (-2)         /* HIP runtime failure */
+#define DOPT_ERR_STATE (-3)       /* call out of order (no data / topology loaded) */
+#define DOPT_ERR_UNSUPPORTED (-4) /* shape outside what this build handles (NotImplementedError) */
+#define DOPT_ERR_COMM (-5)        /* RCCL failure */
+
+/* problems: obj_problems.py:3-20 (logistic), obj_problems.py:39-53 (quadratic) */
+#define DOPT_LOGISTIC 0
+#define DOPT_QUADRATIC 1
+
+/* compute dtypes (the reference computes in float64) */
+#define DOPT_F32 0
+#define DOPT_F64 1
+
+/* run flags */
+#define DOPT_RUN_OBJECTIVE 1u /* record history['objective'] (trainer.py:188-191: X_full given) */
+#define DOPT_RUN_CONSENSUS 2u /* record history['consensus_error'] (trainer.py:182-186) */
+
+int dopt_abi_version(void);
+const char *dopt_last_error(void);
+
+/* ------------------------------------------------------------------ host only
+ * Legacy-MT19937 minibatch sampler: bit-exact with np.random.choice(m, b,
+ * replace=False) == RandomState.permutation(m)[:b] as called by
+ * Worker.get_mini_batch (worker.py:15-28, the draw at worker.py:27).
+ * key/pos are numpy's legacy state (np.random.get_state()[1], [2]) and are
+ * advanced in place.  m == 0 draws nothing (worker.py:17-18).
+ */
+int dopt_mt_choice(uint32_t key[624], int32_t *pos, int64_t m, int64_t b, int64_t *out);
+
+/* T rounds x N workers of Worker.get_mini_batch draws in worker order, as the
+ * trainer loops draw them (trainer.py:47-50, trainer.py:166).  out is
+ * [T][N][b] int32 local row ids; entries past min(b, m_i) are set to -1. */
+int dopt_mt_choice_rounds(uint32_t key[624], int32_t *pos, int64_t T, int64_t n_workers,
+                          const int64_t *shard_rows, int64_t b, int32_t *out);
+
+/* ------------------------------------------------------------------ device */
+int dopt_device_count(int *count);
+
+/* Replaces the state the reference keeps in Python objects (Worker.x,
+ * Trainer.W ...): one context per GPU. */
+int dopt_create(int device, int dtype, dopt_ctx **out);
+int dopt_destroy(dopt_ctx *ctx);
+
+/* Load the worker shards (utils.py:38-43 layout, Worker.X_local / y_local,
+ * worker.py:7-10).  X is n_rows x d float64 (src_f32 = 0) or float32
+ * (src_f32 = 1), host memory.  problem: DOPT_LOGISTIC / DOPT_QUADRATIC. */
+int dopt_load_shards(dopt_ctx *ctx, int problem, int64_t n_workers, int64_t d,
+                     const int64_t *shard_offsets, const void *X, const void *y, int src_f32);
+
+/* Synthetic shards generated on the device (BASELINE.json config C3 shape):
+ * X ~ N(0,1) with a ones bias column (utils.py:28), y from a planted w* --
+ * logistic: sign(X w*) with a fraction `flip` of labels flipped; quadratic:
+ * X w* + noise * N(0,1).  Every worker gets `rows_per_worker` rows. */
+int dopt_generate_shards(dopt_ctx *ctx, int problem, int64_t n_workers, int64_t d,
+                         int64_t rows_per_worker, uint64_t seed, double flip, double noise);
+
+/* Objective dataset when it is NOT the union of the shards (the X_full /
+ * y_full arguments of Trainer.run, trainer.py:154,188-189).  Without this
+ * call the objective is taken over the shard rows. */
+int dopt_load_objective_data(dopt_ctx *ctx, int64_t n_rows, const void *X,
+                             const void *y, int src_f32);
+
+/* Drop the separate objective dataset: the objective is again taken over the
+ * shard rows (X_full == the union of the shards, the Simulator case). */
+int dopt_clear_objective_data(dopt_ctx *ctx);
+
+/* Copy worker i's shard back to the host in float64 (n_rows = shard size,
+ * X_out[n_rows x d], y_out[n_rows]); used by parity checks at full size. */
+int dopt_get_shard(dopt_ctx *ctx, int64_t worker, double *X_out, double *y_out);
+
+/* Mixing matrix in CSR, diagonal included, float64 weights as the reference
+ * computes them (trainer.py:91-136, Metropolis-Hastings).  row_ptr[N+1],
+ * col[nnz] ascending per row, w[nnz]. */
+int dopt_set_topology(dopt_ctx *ctx, int64_t n_workers, const int64_t *row_ptr,
+                      const int32_t *col, const double *w);
+
+/* Worker iterates (Worker.x, worker.py:13; trainer.py:162-163, :178-179). */
+int dopt_set_models(dopt_ctx *ctx, const double *x);
+int dopt_get_models(dopt_ctx *ctx, double *x);
+/* The shared iterate of the centralized trainer (trainer.py:11). */
+int dopt_set_global(dopt_ctx *ctx, const double *x);
+int dopt_get_global(dopt_ctx *ctx, double *x);
+
+/* T rounds of DecentralizedTrainer.run (trainer.py:161-193), rounds t0..t0+T-1:
+ *   g_i = grad f_i(x_i; minibatch)   (worker.py:30-44, obj_problems.py)
+ *   x_i <- sum_j W_ij x_j - eta0/sqrt(t+1) * g_i   (trainer.py:173-175)
+ *   history[t] = (objective(xbar) - f_opt, mean_i ||x_i - xbar||^2)
+ * idx: [T][N][batch] local row ids from dopt_mt_choice_rounds, or NULL when
+ * every worker uses its full shard (batch >= every shard size).
+ * lam_grad: l2_regularization_lambda (logistic) / strong_convexity_mu
+ * (quadratic) (worker.py:36-42); lam_obj: l2_regularization_lambda for both
+ * (trainer.py:151-152, :189).  obj_out/cons_out/time_out: [T] or NULL. */
+int dopt_run_dsgd(dopt_ctx *ctx, int64_t t0, int64_t T, double eta0, int64_t batch,
+                  const int32_t *idx, double lam_grad, double lam_obj, double f_opt,
+                  uint32_t flags, double *obj_out, double *cons_out, double *time_out);
+
+/* T rounds of CentralizedTrainer.run (trainer.py:41-71): every worker's
+ * gradient at the shared iterate, their mean, one step; objective at the
+ * shared iterate.  Same argument meaning as dopt_run_dsgd. */
+int dopt_run_centralized(dopt_ctx *ctx, int64_t t0, int64_t T, double eta0,
+                         int64_t batch, const int32_t *idx, double lam_grad, double lam_obj,
+                         double f_opt, uint32_t flags, double *obj_out, double *time_out);
+
+/* Single evaluations on the device in float64 (the obj_problems.py API):
+ * stochastic gradient over b rows (obj_problems.py:13-20 / :46-53) and the
+ * objective over n rows (obj_problems.py:3-11 / :39-44). */
+int dopt_eval_gradient(dopt_ctx *ctx, int problem, int64_t b, int64_t d,
+                       const double *w, const double *X, const double *y, double reg,
+                       double *g_out);
+int dopt_eval_objective(dopt_ctx *ctx, int problem, int64_t n, int64_t d,
+                        const double *w, const double *X, const double *y, double reg,
+                        double *out);
+
+/* Device time of the last run's dominant kernel (the fused round kernel):
+ * launches and summed milliseconds, measured with HIP events on the engine's
+ * stream.  Used by bench.py for the roofline figure. */
+int dopt_kernel_stats(dopt_ctx *ctx, int64_t *launches, double *total_ms);
+int dopt_set_profiling(dopt_ctx *ctx, int enable);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DOPT_H_ */

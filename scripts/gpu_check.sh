@@ -1,0 +1,24 @@
+#!/bin/bash
+# One GPU-box session: smoke -> gpu tests -> bench -> rocprofv3 kernel trace.
+# Stops at the first crash-type exit (abort/segv/timeout); ordinary test failures continue.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+step() {  # step <name> <timeout-s> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name" ; date +%T
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "rc($name)=$rc"; tail -n 25 "gpurun_out/$name.log"
+  case $rc in 0|1|5) return 0 ;; *) echo "STOP after $name (rc=$rc)"; exit $rc ;; esac
+}
+STEPS=${STEPS:-"smoke tests bench prof"}
+for s in $STEPS; do
+  case $s in
+    smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ;;
+    bench) step bench 600 python -u bench.py ${BENCH_ARGS:-} ;;
+    prof)  (cd /tmp && export TMPDIR=/tmp) ; step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python -u bench.py --no-cpu-baseline ${BENCH_ARGS:-} ;;
+  esac
+done
+echo "=== done"

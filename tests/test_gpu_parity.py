@@ -1,0 +1,243 @@
+"""GPU parity: the HIP engine (through libdopt.so's C ABI) against the reference.
+
+Golden fixtures come from running the reference itself (tests/golden/make_golden.py).
+Tolerances: float64 engine vs float64 reference, rtol 1e-9 on every per-round
+objective / consensus value (summation order differs: BLAS vs wave reductions);
+float32 engine vs the float32 oracle, rtol 1e-5 / 5e-5 (objective / consensus) over
+300 rounds.  Index work (RNG stream, iterations-to-threshold, floats transmitted)
+is bit-exact.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import _dopt
+import data as odata
+import dsgd_oracle as O
+import topology
+from trainer import CentralizedTrainer, DecentralizedTrainer
+from worker import Worker
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+RTOL64 = 1e-9
+
+
+def _load(tag):
+    meta = json.load(open(os.path.join(G, f"traj_{tag}.json")))
+    z = np.load(os.path.join(G, f"traj_{tag}.npz"))
+    return meta, z
+
+
+def _state(z, j):
+    return ("MT19937", z[f"state{j}_key"], int(z[f"state{j}_pos"]), 0, 0.0)
+
+
+def _shards(meta, z):
+    shards, Xf, yf = odata.generate(meta["config"], order=z["order"])
+    assert odata.digest(shards) == meta["data_sha256"], "regenerated shards differ from the fixture"
+    return shards, Xf, yf
+
+
+def _make_trainer(label, shards, cfg):
+    d = shards[0][0].shape[1]
+    ws = [Worker(i, {"X": X, "y": y}, cfg["local_batch_size"], d, cfg) for i, (X, y) in enumerate(shards)]
+    if label == "Centralized":
+        return CentralizedTrainer(ws, d, cfg)
+    topo = {"D-SGD (Ring)": "ring", "D-SGD (Grid)": "grid", "D-SGD (Fully Connected)": "fully_connected"}[label]
+    return DecentralizedTrainer(ws, topo, d, cfg)
+
+
+def _close(a, b, rtol):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    assert a.shape == b.shape
+    np.testing.assert_allclose(a, b, rtol=rtol, atol=1e-300)
+
+
+# ---------------------------------------------------------------------------- single evaluations
+def test_objectives_and_gradients_vs_golden():
+    import obj_problems as P
+
+    z = np.load(os.path.join(G, "grads.npz"))
+    for k, (prob, d, b, scale) in enumerate(z["cases"]):
+        w, X, y = z[f"c{k}_w"], z[f"c{k}_X"], z[f"c{k}_y"]
+        if prob == 0:
+            g = P.logistic_stochastic_gradient(w, X, y, 1e-4)
+            f = P.logistic_objective(w, X, y, 1e-4)
+        else:
+            g = P.quadratic_stochastic_gradient(w, X, y, 1e-4)
+            f = P.quadratic_objective(w, X, y, 1e-4)
+        np.testing.assert_allclose(g, z[f"c{k}_g"], rtol=1e-12, atol=1e-14, err_msg=f"case {k}")
+        np.testing.assert_allclose(f, z[f"c{k}_f"], rtol=1e-12, atol=1e-14, err_msg=f"case {k}")
+    for prob, fn in (("logistic", P.logistic_full_gradient), ("quadratic", P.quadratic_full_gradient)):
+        class W_:
+            def __init__(self, X, y):
+                self.X_local, self.y_local = X, y
+        ws = [W_(z[f"full_{prob}_X{j}"], z[f"full_{prob}_y{j}"]) for j in range(3)]
+        np.testing.assert_allclose(fn(z[f"full_{prob}_w"], ws, 1e-4), z[f"full_{prob}_g"], rtol=1e-12, atol=1e-14)
+        np.testing.assert_array_equal(fn(z[f"full_{prob}_w"], [ws[1]], 1e-4), z[f"full_{prob}_gempty"])
+
+
+def test_worker_compute_gradient_matches_oracle():
+    rng = np.random.default_rng(3)
+    X = np.hstack([rng.standard_normal((50, 9)), np.ones((50, 1))])
+    y = rng.choice(np.array([-1, 1]), 50)
+    cfg = {"problem_type": "logistic", "l2_regularization_lambda": 1e-3, "strong_convexity_mu": 2e-3}
+    w = Worker(0, {"X": X, "y": y}, 16, 10, cfg)
+    w.x = rng.standard_normal(10)
+    np.random.seed(9)
+    g = w.compute_gradient()
+    np.random.seed(9)
+    idx = np.random.choice(50, 16, replace=False)
+    np.testing.assert_allclose(g, O.logistic_gradient(w.x, X[idx], y[idx], 1e-3), rtol=1e-12)
+    cfg["problem_type"] = "hinge"
+    with pytest.raises(NotImplementedError):
+        w.compute_gradient()
+
+
+# ---------------------------------------------------------------------------- trajectories
+TAGS = ["c2", "c1", "fullbatch", "n1", "n2", "n4", "ragged"]
+
+
+@pytest.mark.parametrize("tag", TAGS)
+def test_trajectories_vs_reference(tag):
+    meta, z = _load(tag)
+    cfg = dict(meta["config"])
+    shards, Xf, yf = _shards(meta, z)
+    T = cfg["n_iterations"]
+    for j, label in enumerate(meta["labels"]):
+        np.random.set_state(_state(z, j))
+        tr = _make_trainer(label, shards, cfg)
+        hist, _ = tr.run(T, Xf, yf, meta["f_opt"])
+        _close(hist["objective"], z[f"L{j}_objective"], RTOL64)
+        assert len(hist["time"]) == T
+        if label != "Centralized":
+            _close(hist["consensus_error"], z[f"L{j}_consensus"], RTOL64)
+        nr = meta["numerical_results"][label]
+        assert O.iterations_to_threshold(hist["objective"], cfg["suboptimality_threshold"]) == nr["iterations_to_threshold"]
+        assert tr.total_floats_transmitted == nr["total_transmission_floats"]
+        # the next trainer's RNG state is where this one left numpy's stream
+        if j + 1 < len(meta["labels"]):
+            st = np.random.get_state()
+            assert st[2] == int(z[f"state{j + 1}_pos"])
+            np.testing.assert_array_equal(st[1], z[f"state{j + 1}_key"])
+
+
+def test_direct_fixtures_empty_and_tiny_shards():
+    z = np.load(os.path.join(G, "direct.npz"))
+    meta = json.load(open(os.path.join(G, "direct.json")))
+    for prob in ("logistic", "quadratic"):
+        shards = [(z[f"{prob}_X{j}"], z[f"{prob}_y{j}"]) for j in range(6)]
+        d = shards[0][0].shape[1]
+        Xf = np.vstack([s[0] for s in shards])
+        yf = np.concatenate([s[1] for s in shards])
+        cfg = {"n_workers": 6, "local_batch_size": 2, "learning_rate_eta0": 0.05, "l2_regularization_lambda": 1e-4,
+               "strong_convexity_mu": 1e-4, "problem_type": prob}
+        for name, topo in (("central", None), ("ring", "ring"), ("fc", "fully_connected")):
+            np.random.seed(203)
+            ws = [Worker(i, {"X": X, "y": y}, 2, d, cfg) for i, (X, y) in enumerate(shards)]
+            tr = CentralizedTrainer(ws, d, cfg) if topo is None else DecentralizedTrainer(ws, topo, d, cfg)
+            hist, xf = tr.run(40, Xf, yf, 0.125)
+            _close(hist["objective"], z[f"{prob}_{name}_objective"], RTOL64)
+            if topo:
+                _close(hist["consensus_error"], z[f"{prob}_{name}_consensus"], RTOL64)
+            np.testing.assert_allclose(xf, z[f"{prob}_{name}_final"], rtol=RTOL64, atol=1e-14)
+            assert np.random.get_state()[2] == int(z[f"{prob}_{name}_final_pos"])
+            assert float(tr.total_floats_transmitted) == meta[f"{prob}_{name}_tx"]
+        # X_full that is not the union of the shards -> separate objective dataset
+        np.random.seed(203)
+        ws = [Worker(i, {"X": X, "y": y}, 2, d, cfg) for i, (X, y) in enumerate(shards)]
+        hist, _ = DecentralizedTrainer(ws, "ring", d, cfg).run(40, Xf[:5], yf[:5], 0.0)
+        _close(hist["objective"], z[f"{prob}_subset_objective"], RTOL64)
+        np.random.seed(203)
+        ws = [Worker(i, {"X": X, "y": y}, 2, d, cfg) for i, (X, y) in enumerate(shards)]
+        hist, _ = DecentralizedTrainer(ws, "ring", d, cfg).run(7, None, None, 0.0)
+        assert [len(hist["objective"]), len(hist["consensus_error"]), len(hist["time"])] == meta[f"{prob}_noobj_lens"]
+
+
+def test_table2_simulator_end_to_end():
+    """main.py's quadratic N=25 experiment (T=10^4, four trainers, one RNG stream):
+    iterations-to-threshold must be the report's Table II exactly."""
+    from main import make_config
+    from simulator import Simulator
+
+    meta, z = _load("table2")
+    np.random.seed(203)
+    sim = Simulator(make_config())
+    assert abs(sim.f_opt - meta["f_opt"]) <= 1e-9 * abs(meta["f_opt"])
+    sim.run_all()
+    for j, label in enumerate(meta["labels"]):
+        assert sim.numerical_results[label] == meta["numerical_results"][label]
+        _close(sim.results[label]["objective"], z[f"L{j}_objective"], 1e-8)
+    got = [sim.numerical_results[k]["iterations_to_threshold"] for k in meta["labels"]]
+    assert got == [5425, 7214, 5666, 5549]
+
+
+def test_float32_engine_vs_float32_oracle():
+    meta, z = _load("c2")
+    cfg = dict(meta["config"])
+    cfg["dtype"] = "float32"
+    shards, Xf, yf = _shards(meta, z)
+    T = 300
+    np.random.set_state(_state(z, 1))
+    tr = _make_trainer("D-SGD (Ring)", shards, cfg)
+    hist, _ = tr.run(T, Xf, yf, meta["f_opt"])
+    W = topology.ring(len(shards)).dense_W()
+    h32, _, _, _ = O.run_decentralized(shards, W, T, cfg, Xf, yf, meta["f_opt"], rng_state=_state(z, 1),
+                                       dtype=np.float32)
+    np.testing.assert_allclose(hist["objective"], h32["objective"], rtol=1e-5)
+    np.testing.assert_allclose(hist["consensus_error"], h32["consensus_error"], rtol=5e-5)
+    # and against the float64 reference itself, at the horizon-dependent fp32 bound
+    np.testing.assert_allclose(hist["objective"], z["L1_objective"][:T], rtol=2e-5)
+
+
+# ---------------------------------------------------------------------------- full size (config C3)
+def _c3_engine(dtype, n=4096, d=1024, m=512, seed=7):
+    eng = _dopt.Engine(0, dtype)
+    eng.generate_shards("logistic", n, d, m, seed=seed, flip=0.05)
+    top = topology.random_regular(n, 4, seed=0)
+    eng.set_topology(top.row_ptr, top.col, top.w)
+    return eng, top
+
+
+def test_c3_full_size_round_spot_check():
+    """N=4096, d=1024, m=512 fp32: one full-shard round, 12 workers recomputed on the
+    host in float64 from their downloaded shards and neighbour iterates."""
+    eng, top = _c3_engine("float32")
+    rng = np.random.default_rng(0)
+    x0 = (rng.standard_normal((4096, 1024)) * 0.01).astype(np.float32).astype(np.float64)
+    eng.set_models(x0)
+    obj, cons, _ = eng.run_dsgd(1, 0.05, 512, 1e-4, 1e-4, 0.0)
+    x1 = eng.get_models()
+    eta = 0.05
+    for i in rng.choice(4096, 12, replace=False):
+        X, y = eng.get_shard(i)
+        g = O.logistic_gradient(x0[i], X, y, 1e-4)
+        s, e = top.row_ptr[i], top.row_ptr[i + 1]
+        mix = sum(top.w[k].astype(np.float32).astype(np.float64) * x0[top.col[k]] for k in range(s, e))
+        np.testing.assert_allclose(x1[i], mix - eta * g, rtol=2e-4, atol=2e-6)
+    xbar = x1.mean(axis=0)
+    ref_cons = np.mean(np.sum((x1 - xbar) ** 2, axis=1))
+    np.testing.assert_allclose(cons[0], ref_cons, rtol=1e-4)
+    eng.close()
+
+
+def test_c3_deterministic_and_fp32_tracks_fp64():
+    """Bitwise run-to-run reproducibility (no atomics), and fp32 vs fp64 engines on the
+    same generated data stay within the fp32 tolerance over 5 rounds."""
+    e32, _ = _c3_engine("float32", n=1024)
+    a = e32.run_dsgd(5, 0.05, 512, 1e-4, 1e-4, 0.0)
+    xa = e32.get_models()
+    e32.set_models(np.zeros((1024, 1024)))
+    b = e32.run_dsgd(5, 0.05, 512, 1e-4, 1e-4, 0.0)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(xa, e32.get_models())
+    e32.close()
+    e64, _ = _c3_engine("float64", n=1024)
+    c = e64.run_dsgd(5, 0.05, 512, 1e-4, 1e-4, 0.0)
+    np.testing.assert_allclose(a[0], c[0], rtol=1e-5)
+    np.testing.assert_allclose(a[1], c[1], rtol=1e-3)
+    e64.close()

@@ -1,0 +1,72 @@
+"""libdopt.so's legacy-MT19937 sampler (host code, no GPU) vs numpy and the fixtures."""
+import os
+
+import numpy as np
+import pytest
+
+import _dopt
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_choice_matches_fixture_stream():
+    z = np.load(os.path.join(G, "rng.npz"))
+    np.random.seed(203)
+    for k, (m, b) in enumerate(z["specs"]):
+        np.testing.assert_array_equal(_dopt.mt_choice(int(m), int(b)), z[f"call{k}_idx"])
+        assert np.random.get_state()[2] == z[f"call{k}_pos"]
+    np.testing.assert_array_equal(np.random.get_state()[1], z["final_key"])
+
+
+def test_rounds_match_fixture():
+    z = np.load(os.path.join(G, "rng.npz"))
+    np.random.seed(203)
+    np.testing.assert_array_equal(_dopt.mt_choice_rounds(3, [500] * 10, 16), z["rounds_c2"])
+
+
+@pytest.mark.parametrize("seed", [0, 1, 203, 2 ** 31 - 1])
+def test_choice_matches_numpy_random_shapes(seed):
+    rng = np.random.default_rng(seed)
+    np.random.seed(seed)
+    calls = [(int(rng.integers(0, 3000)), int(rng.integers(0, 700))) for _ in range(200)]
+    ours = [_dopt.mt_choice(m, b) for m, b in calls]
+    st_ours = np.random.get_state()
+    np.random.seed(seed)
+    for (m, b), got in zip(calls, ours):
+        eb = 0 if m == 0 else min(b, m)
+        want = np.random.choice(m, eb, replace=False) if eb > 0 else np.zeros(0, dtype=np.int64)
+        np.testing.assert_array_equal(got, want)
+    st = np.random.get_state()
+    assert st[2] == st_ours[2]
+    np.testing.assert_array_equal(st[1], st_ours[1])
+
+
+def test_rounds_padding_and_ragged():
+    np.random.seed(5)
+    rows = [0, 1, 3, 7, 600]
+    out = _dopt.mt_choice_rounds(4, rows, 5)
+    np.random.seed(5)
+    for t in range(4):
+        for i, m in enumerate(rows):
+            eb = 0 if m == 0 else min(5, m)
+            want = np.random.choice(m, eb, replace=False) if eb else np.zeros(0, dtype=np.int64)
+            np.testing.assert_array_equal(out[t, i, :eb], want)
+            assert np.all(out[t, i, eb:] == -1)
+
+
+def test_large_interval_uses_numpy_semantics():
+    np.random.seed(77)
+    got = _dopt.mt_choice(100003, 3)
+    np.random.seed(77)
+    np.testing.assert_array_equal(got, np.random.choice(100003, 3, replace=False))
+
+
+def test_bad_state_rejected():
+    key = np.zeros(624, dtype=np.uint32)
+    import ctypes
+
+    pos = ctypes.c_int32(1000)
+    out = np.zeros(4, dtype=np.int64)
+    rc = _dopt.lib().dopt_mt_choice(key.ctypes.data_as(ctypes.c_void_p), ctypes.byref(pos), 10, 4,
+                                    out.ctypes.data_as(ctypes.c_void_p))
+    assert rc == _dopt.ERR_INVALID
