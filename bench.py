@@ -32,6 +32,23 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+def pmc_traffic(kernel_name):
+    """Per-dispatch HBM bytes of `kernel_name` from the newest committed rocprofv3 PMC
+    summary (profiles/<tag>_pmc.json, written by scripts/pmc_summary.py from separate
+    FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 correction)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    for f in reversed(files):
+        try:
+            rec = json.load(open(f)).get(kernel_name)
+        except Exception:
+            continue
+        if rec:
+            return rec["hbm_bytes_per_dispatch"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def cpu_baseline(seconds, n_workers=64, d=1024, m=512, seed=11):
     """The oracle (numpy restatement of the reference round, float64) on a bounded
     sample: n_workers workers of the C3 shape, same per-round work as the reference
@@ -63,10 +80,11 @@ def cpu_baseline(seconds, n_workers=64, d=1024, m=512, seed=11):
     W = topology.random_regular(n_workers, 4, seed=0).dense_W()
     cfg = {"problem_type": "logistic", "local_batch_size": m, "learning_rate_eta0": 0.05,
            "l2_regularization_lambda": 1e-4, "strong_convexity_mu": 1e-4}
+    O.run_decentralized(shards, W, 1, cfg, Xf, yf, 0.0)  # warm caches / BLAS threads
     t0 = time.perf_counter()
-    O.run_decentralized(shards, W, 1, cfg, Xf, yf, 0.0)
-    t1 = time.perf_counter() - t0
-    rounds = max(1, min(200, int(seconds / max(t1, 1e-3))))
+    O.run_decentralized(shards, W, 2, cfg, Xf, yf, 0.0)
+    t1 = (time.perf_counter() - t0) / 2
+    rounds = max(1, min(400, int(seconds / max(t1, 1e-3))))
     t0 = time.perf_counter()
     O.run_decentralized(shards, W, rounds, cfg, Xf, yf, 0.0)
     dt = time.perf_counter() - t0
@@ -85,7 +103,7 @@ def main():
     ap.add_argument("--m", type=int, default=512)
     ap.add_argument("--dtype", default="float32")
     ap.add_argument("--degree", type=int, default=4)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -135,6 +153,12 @@ def main():
         raise RuntimeError("non-finite metrics")
 
     esz = 4 if args.dtype in ("float32", "fp32", "f32") else 8
+    tname = "float" if esz == 4 else "double"
+    cpl = 1
+    while cpl * 64 < (d + (16 // esz) - 1) // (16 // esz):
+        cpl *= 2
+    kname = f"void dopt::k_round<{tname}, {cpl}, 0, true, true>(dopt::RoundArgs)"
+    traffic, traffic_src = pmc_traffic(kname)
     bytes_per_launch = esz * n * (m * d + m + 2 * d)  # X_b + y_b + x read + x write
     avg_s = (kr_ms / launches) * 1e-3 if launches else float("nan")
     achieved = bytes_per_launch / avg_s / 1e9
@@ -157,8 +181,9 @@ def main():
                    "workers_per_gpu": n, "d": d, "rows_per_worker": m, "batch": m, "topology": "random_regular",
                    "degree": args.degree, "parallelism": f"dp{world} (independent worker graphs per GPU)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "k_round<float,4,logistic,grad,metrics>", "kernel_avg_ms": avg_s * 1e3,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
+                     "kernel": kname, "kernel_avg_ms": avg_s * 1e3,
                      "bytes_per_launch": bytes_per_launch},
         "final_objective": float(obj[-1]),
         "final_consensus": float(cons[-1]),
