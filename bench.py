@@ -7,8 +7,10 @@ batches (b = m), random 4-regular topology with Metropolis-Hastings weights, fp3
 objective + consensus recorded EVERY round (as trainer.py:182-191 does).
 A step = one D-SGD round over every worker (gradient, mix, step, metrics).
 
-Multi-GPU (`--gpus N` under torch.distributed.run): every rank holds its own 4096
-workers (weak scaling); see DESIGN.md for the exchange plan.
+Multi-GPU (`--gpus N` under torch.distributed.run): ONE random 4-regular graph over
+4096 x N workers (weak scaling), each rank owning a contiguous slice; halo rows of
+the iterates move by grouped send/recv (RCCL) while the gradient kernel runs, and
+the average model is all-reduced every round (distributed.py).
 
 Prints ONE JSON line on rank 0 (driver contract), with `roofline` for the fused
 round kernel (HIP-event timed, same timed region) and `cpu_baseline` (the oracle,
@@ -105,6 +107,7 @@ def main():
     ap.add_argument("--degree", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (gloo: 1-GPU rehearsal)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -113,39 +116,57 @@ def main():
     import torch  # plumbing only: barrier + max-over-ranks (one HIP runtime, loaded first)
     import torch.distributed as dist
 
+    dev = local % max(1, torch.cuda.device_count())
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(dev)
+        dist.init_process_group(args.backend)
+
+    import numpy as np
 
     import _dopt
+    import distributed
     import topology
 
     n, d, m = args.workers, args.d, args.m
-    log(f"rank {rank}/{world}: generating {n} x {m} x {d} {args.dtype} shards on device {local}")
-    eng = _dopt.Engine(local, args.dtype)
-    eng.generate_shards("logistic", n, d, m, seed=1000 + rank, flip=0.05)
-    top = topology.random_regular(n, args.degree, seed=0)
-    eng.set_topology(top.row_ptr, top.col, top.w)
+    n_global = n * world
+    top = topology.random_regular(n_global, args.degree, seed=0)
+    plan = distributed.build_plan(top, world, rank)
+    log(f"rank {rank}/{world}: generating {plan.n_local} x {m} x {d} {args.dtype} shards on device {dev}")
+    eng = _dopt.Engine(dev, args.dtype)
+    eng.generate_shards("logistic", plan.n_local, d, m, seed=1000, flip=0.05, first_worker=plan.lo)
     lam = 1e-4
+    if world > 1:
+        runner = distributed.DistributedDSGD(eng, plan, n_global, n_global * m, device=dev)
+        log(f"halo: {plan.n_halo} rows in, {len(plan.send_ids)} rows out per round")
+
+        def rounds(k):
+            return runner.run(k, 0.05, m, lam, lam, 0.0)
+    else:
+        eng.set_topology(top.row_ptr, top.col, top.w)
+
+        def rounds(k):
+            obj, cons, _ = eng.run_dsgd(k, 0.05, m, lam, lam, 0.0)
+            return obj, cons
     log("warmup")
     if args.warmup > 0:
-        eng.run_dsgd(args.warmup, 0.05, m, lam, lam, 0.0)
-    eng.set_models(__import__("numpy").zeros((n, d)))
+        rounds(args.warmup)
+    eng.set_models(np.zeros((plan.n_local, d)))
+    eng.kernel_stats()  # reset the event window
 
     def barrier():
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize(local)
+        torch.cuda.synchronize(dev)
 
     eng.set_profiling(True)
     barrier()
     log(f"timing {args.steps} rounds")
     t0 = time.perf_counter()
-    obj, cons, _ = eng.run_dsgd(args.steps, 0.05, m, lam, lam, 0.0, t0=0)
+    obj, cons = rounds(args.steps)
     barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}" if args.backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     launches, kr_ms = eng.kernel_stats()
@@ -162,7 +183,7 @@ def main():
     bytes_per_launch = esz * n * (m * d + m + 2 * d)  # X_b + y_b + x read + x write
     avg_s = (kr_ms / launches) * 1e-3 if launches else float("nan")
     achieved = bytes_per_launch / avg_s / 1e9
-    value = world * n * args.steps / dt
+    value = n_global * args.steps / dt
     out = {
         "metric": METRIC,
         "value": value,
@@ -179,7 +200,9 @@ def main():
         "config": {"workload": "C3: logistic, 4096 workers/GPU, d=1024, m=b=512, random 4-regular MH mixing, "
                                "objective+consensus every round",
                    "workers_per_gpu": n, "d": d, "rows_per_worker": m, "batch": m, "topology": "random_regular",
-                   "degree": args.degree, "parallelism": f"dp{world} (independent worker graphs per GPU)"},
+                   "degree": args.degree,
+                   "parallelism": f"dp{world}: one graph of {n_global} workers, contiguous slices, halo send/recv"
+                                  + (f" ({args.backend})" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_unit": "bytes/launch", "traffic_source": traffic_src,

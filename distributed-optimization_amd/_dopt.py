@@ -44,7 +44,7 @@ _SIGS = {
     "dopt_create": ([ctypes.c_int, ctypes.c_int, _P], ctypes.c_int),
     "dopt_destroy": ([_P], ctypes.c_int),
     "dopt_load_shards": ([_P, ctypes.c_int, _I64, _I64, _P, _P, _P, ctypes.c_int], ctypes.c_int),
-    "dopt_generate_shards": ([_P, ctypes.c_int, _I64, _I64, _I64, ctypes.c_uint64, _D, _D], ctypes.c_int),
+    "dopt_generate_shards": ([_P, ctypes.c_int, _I64, _I64, _I64, ctypes.c_uint64, _D, _D, _I64], ctypes.c_int),
     "dopt_load_objective_data": ([_P, _I64, _P, _P, ctypes.c_int], ctypes.c_int),
     "dopt_clear_objective_data": ([_P], ctypes.c_int),
     "dopt_get_shard": ([_P, _I64, _P, _P], ctypes.c_int),
@@ -57,6 +57,19 @@ _SIGS = {
     "dopt_run_centralized": ([_P, _I64, _I64, _D, _I64, _P, _D, _D, _D, ctypes.c_uint32, _P, _P], ctypes.c_int),
     "dopt_eval_gradient": ([_P, ctypes.c_int, _I64, _I64, _P, _P, _P, _D, _P], ctypes.c_int),
     "dopt_eval_objective": ([_P, ctypes.c_int, _I64, _I64, _P, _P, _P, _D, _P], ctypes.c_int),
+    "dopt_set_stream": ([_P, _P], ctypes.c_int),
+    "dopt_get_layout": ([_P, _P, _P], ctypes.c_int),
+    "dopt_set_partition": ([_P, _I64, _I64], ctypes.c_int),
+    "dopt_set_halo": ([_P, _I64, _P, _I64, _P, _P], ctypes.c_int),
+    "dopt_phase_gather": ([_P], ctypes.c_int),
+    "dopt_phase_grad": ([_P, _I64, _P, _D, ctypes.c_uint32], ctypes.c_int),
+    "dopt_phase_mix": ([_P, _I64, _D], ctypes.c_int),
+    "dopt_phase_colsum": ([_P, _P], ctypes.c_int),
+    "dopt_phase_xbar": ([_P, _P], ctypes.c_int),
+    "dopt_phase_metrics_pass": ([_P, ctypes.c_uint32], ctypes.c_int),
+    "dopt_phase_metrics": ([_P, ctypes.c_uint32, ctypes.c_int, _P], ctypes.c_int),
+    "dopt_sync": ([_P], ctypes.c_int),
+    "dopt_finalize_metrics": ([ctypes.c_int, _I64, _P, _I64, _I64, _D, _D, _P, _P], ctypes.c_int),
     "dopt_kernel_stats": ([_P, _P, _P], ctypes.c_int),
     "dopt_set_profiling": ([_P, ctypes.c_int], ctypes.c_int),
 }
@@ -186,10 +199,11 @@ class Engine:
         self.n, self.d, self.problem = n, d, problem
         self.shard_rows = np.diff(off)
 
-    def generate_shards(self, problem, n_workers, d, rows_per_worker, seed=0, flip=0.05, noise=10.0):
+    def generate_shards(self, problem, n_workers, d, rows_per_worker, seed=0, flip=0.05, noise=10.0,
+                        first_worker=0):
         check(lib().dopt_generate_shards(self._h, PROBLEMS[problem], int(n_workers), int(d),
                                          int(rows_per_worker), int(seed) & (2 ** 64 - 1), float(flip),
-                                         float(noise)))
+                                         float(noise), int(first_worker)))
         self.n, self.d, self.problem = int(n_workers), int(d), problem
         self.shard_rows = np.full(int(n_workers), int(rows_per_worker), dtype=np.int64)
 
@@ -278,6 +292,49 @@ class Engine:
                                         _ptr(y), float(reg), _ptr(out)))
         return np.float64(out[0])
 
+    # -- multi-GPU phases (enqueue only; pointers are device addresses)
+    def set_stream(self, stream_handle):
+        check(lib().dopt_set_stream(self._h, ctypes.c_void_p(stream_handle) if stream_handle else None))
+
+    def layout(self):
+        ld, esz = ctypes.c_int64(0), ctypes.c_int64(0)
+        check(lib().dopt_get_layout(self._h, ctypes.byref(ld), ctypes.byref(esz)))
+        return ld.value, esz.value
+
+    def set_partition(self, n_global, rows_global):
+        check(lib().dopt_set_partition(self._h, int(n_global), int(rows_global)))
+
+    def set_halo(self, n_halo, halo_ptr, send_ids, send_ptr):
+        ids = np.ascontiguousarray(send_ids, dtype=np.int32)
+        check(lib().dopt_set_halo(self._h, int(n_halo), ctypes.c_void_p(halo_ptr) if halo_ptr else None, len(ids),
+                                  ctypes.c_void_p(send_ptr) if send_ptr else None, _ptr(ids)))
+
+    def phase_gather(self):
+        check(lib().dopt_phase_gather(self._h))
+
+    def phase_grad(self, batch, lam_grad, metric_flags=0, idx=None):
+        if idx is not None:
+            idx = np.ascontiguousarray(idx, dtype=np.int32)
+        check(lib().dopt_phase_grad(self._h, int(batch), _ptr(idx), float(lam_grad), int(metric_flags)))
+
+    def phase_mix(self, t, eta0):
+        check(lib().dopt_phase_mix(self._h, int(t), float(eta0)))
+
+    def phase_colsum(self, sum_ptr):
+        check(lib().dopt_phase_colsum(self._h, ctypes.c_void_p(sum_ptr)))
+
+    def phase_xbar(self, sum_ptr):
+        check(lib().dopt_phase_xbar(self._h, ctypes.c_void_p(sum_ptr)))
+
+    def phase_metrics_pass(self, flags):
+        check(lib().dopt_phase_metrics_pass(self._h, int(flags)))
+
+    def phase_metrics(self, flags, include_xnorm, out_ptr):
+        check(lib().dopt_phase_metrics(self._h, int(flags), 1 if include_xnorm else 0, ctypes.c_void_p(out_ptr)))
+
+    def sync(self):
+        check(lib().dopt_sync(self._h))
+
     # -- profiling
     def set_profiling(self, on):
         check(lib().dopt_set_profiling(self._h, 1 if on else 0))
@@ -287,6 +344,16 @@ class Engine:
         ms = ctypes.c_double(0.0)
         check(lib().dopt_kernel_stats(self._h, ctypes.byref(n), ctypes.byref(ms)))
         return n.value, ms.value
+
+
+def finalize_metrics(problem, raw, n_workers, m_obj, lam_obj, f_opt):
+    """raw [T, 3] metric sums -> (objective, consensus) with the engine's own formula."""
+    raw = np.ascontiguousarray(raw, dtype=np.float64).reshape(-1, 3)
+    T = raw.shape[0]
+    obj, cons = np.zeros(T), np.zeros(T)
+    check(lib().dopt_finalize_metrics(PROBLEMS[problem], T, _ptr(raw), int(n_workers), int(m_obj),
+                                      float(lam_obj), float(f_opt), _ptr(obj), _ptr(cons)))
+    return obj, cons
 
 
 _default = {}

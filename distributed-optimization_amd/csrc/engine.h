@@ -37,9 +37,11 @@ struct RoundArgs {
   double* slab_loss;      // [n]
   double eta;             // eta0 / sqrt(t+1)  (trainer.py:138-140)
   double lam;             // gradient regulariser (worker.py:36-42)
+  const void* halo;       // [n_halo x ld] remote iterates (multi-GPU); CSR columns >= n_local index it
   int64_t ld;             // padded row stride in elements (multiple of the 16-byte vector)
   int32_t nchunks;        // ld / elements-per-16B
   int32_t flags;
+  int32_t n_local;        // rows of x_old owned by this rank (columns below it are local)
 };
 
 // Kernel launchers (kernels.hip).  dtype: 0 = float, 1 = double.
@@ -52,18 +54,27 @@ int max_chunks_per_lane();
 hipError_t launch_colsum_partial(int dtype, const void* x, int64_t n, int64_t ld, int32_t nchunks,
                                  int32_t rpg, double* part, uint64_t* stamp, hipStream_t s);
 // out = sum_g part / n (mode 0, the average model, trainer.py:182), or
-// out = base - eta * (sum_g part / n) (mode 1, centralized update, trainer.py:53-57).
+// out = base - eta * (sum_g part / n) (mode 1, centralized update, trainer.py:53-57);
+// with raw != null the column sums themselves go to raw[ld] (float64) instead.
 hipError_t launch_colsum_final(int dtype, const double* part, int32_t groups, int64_t n, int64_t ld,
                                int32_t nchunks, void* out, const void* base, double eta, int mode,
-                               hipStream_t s);
-// history[h] from the slabs (one workgroup, fixed reduction order).
-hipError_t launch_history(int dtype, int problem, const double* slab_cons, const double* slab_loss,
-                          int64_t n, int64_t n_loss_groups, int64_t m_obj, const void* xbar,
-                          int64_t ld, int32_t nchunks, double lam_obj, double f_opt, double* obj_out,
-                          double* cons_out, int64_t h, hipStream_t s);
+                               hipStream_t s, double* raw = nullptr);
+// Raw metric sums of one round (one workgroup, fixed reduction order):
+// out[0] = sum(slab_cons[0:n]), out[1] = sum(slab_loss[0:ng]), out[2] = ||xbar||^2 (0 if !xnorm).
+// The host turns them into history values (runtime.cpp: finish_metrics) after any
+// cross-rank sum.
+hipError_t launch_history(int dtype, const double* slab_cons, const double* slab_loss, int64_t n,
+                          int64_t ng, const void* xbar, int64_t ld, int32_t nchunks, bool xnorm,
+                          double* out, hipStream_t s);
+// x_next[i] = sum_e cw[e] * src(ci[e]) - eta * G[i]  (trainer.py:173-175), src = x_old or halo.
+hipError_t launch_mix(int dtype, const RoundArgs& a, const void* G, int n_workers, hipStream_t s);
+// dst[k] = x[ids[k]] rows (halo send buffer).
+hipError_t launch_gather_rows(int dtype, const void* x, const int32_t* ids, int64_t n, int64_t ld,
+                              int32_t nchunks, void* dst, hipStream_t s);
 // Synthetic shards (rows_per_worker rows per worker), X ~ N(0,1) + bias column.
 hipError_t launch_generate(int dtype, int problem, void* X, void* y, int64_t rows, int64_t d,
-                           int64_t ld, uint64_t seed, double flip, double noise, hipStream_t s);
+                           int64_t ld, uint64_t seed, double flip, double noise, int64_t row_base,
+                           hipStream_t s);
 // One thread writes the constant-rate wall clock (trainer.py:181 timestamps).
 hipError_t launch_stamp(uint64_t* out, hipStream_t s);
 // float64 host data -> T rows padded to ld (zero padding).

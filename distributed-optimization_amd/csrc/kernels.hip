@@ -214,7 +214,10 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
         V acc = V(0);
         for (int64_t e = e0; e < e1; ++e) {
           const T wt = ((const T*)a.cw)[e];
-          acc += wt * *(const V*)((const T*)a.x_old + (int64_t)a.ci[e] * ld + (int64_t)c * VN);
+          const int col = a.ci[e];
+          const T* src = col < a.n_local ? (const T*)a.x_old + (int64_t)col * ld
+                                         : (const T*)a.halo + (int64_t)(col - a.n_local) * ld;
+          acc += wt * *(const V*)(src + (int64_t)c * VN);
         }
         *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = acc - inv_eta * gc;
       } else if (flags & F_GOUT) {
@@ -336,7 +339,7 @@ __global__ __launch_bounds__(NT) void k_colsum_part(const T* __restrict__ x, int
 template <typename T>
 __global__ __launch_bounds__(NT) void k_colsum_final(const double* __restrict__ part, int groups,
                                                      int64_t n, int64_t ld, int nch, T* out,
-                                                     const T* base, double eta, int mode) {
+                                                     const T* base, double eta, int mode, double* raw) {
   constexpr int VN = VT<T>::n;
   __shared__ double red[NW][64 * VN];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -371,6 +374,10 @@ __global__ __launch_bounds__(NT) void k_colsum_final(const double* __restrict__ 
       double s = red[0][lane * VN + e];
 #pragma unroll
       for (int q = 1; q < NW; ++q) s += red[q][lane * VN + e];
+      if (raw) {  // local column sums for a cross-rank all-reduce
+        raw[col] = s;
+        continue;
+      }
       const double mean = s / (double)n;  // np.mean: sum / count
       if (mode == 0)
         out[col] = (T)mean;
@@ -395,37 +402,36 @@ hipError_t launch_colsum_partial(int dtype, const void* x, int64_t n, int64_t ld
 
 hipError_t launch_colsum_final(int dtype, const double* part, int32_t groups, int64_t n, int64_t ld,
                                int32_t nchunks, void* out, const void* base, double eta, int mode,
-                               hipStream_t s) {
+                               hipStream_t s, double* raw) {
   const dim3 grid((nchunks + 63) / 64);
   if (dtype == 0)
     hipLaunchKernelGGL(k_colsum_final<float>, grid, dim3(NT), 0, s, part, groups, n, ld, nchunks,
-                       (float*)out, (const float*)base, eta, mode);
+                       (float*)out, (const float*)base, eta, mode, raw);
   else
     hipLaunchKernelGGL(k_colsum_final<double>, grid, dim3(NT), 0, s, part, groups, n, ld, nchunks,
-                       (double*)out, (const double*)base, eta, mode);
+                       (double*)out, (const double*)base, eta, mode, raw);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------- history
 template <typename T>
 __global__ __launch_bounds__(NT) void k_history(const double* sc, const double* sl, int64_t n,
-                                                int64_t ng, int64_t m_obj, const T* xbar, int64_t ld,
-                                                int nch, int problem, double lam_obj, double f_opt,
-                                                double* obj_out, double* cons_out, int64_t h) {
+                                                int64_t ng, const T* xbar, int64_t ld, int nch,
+                                                int xnorm, double* out) {
   constexpr int VN = VT<T>::n;
   __shared__ double part[3][NW];
   double a = 0.0, b = 0.0, q = 0.0;
-  if (cons_out)
+  if (sc)
     for (int64_t k = threadIdx.x; k < n; k += NT) a += sc[k];
-  if (obj_out) {
+  if (sl)
     for (int64_t k = threadIdx.x; k < ng; k += NT) b += sl[k];
+  if (xnorm)
     for (int c = threadIdx.x; c < nch; c += NT)
 #pragma unroll
       for (int e = 0; e < VN; ++e) {
         const double v = (double)xbar[(int64_t)c * VN + e];
         q += v * v;
       }
-  }
   a = wave_sum(a);
   b = wave_sum(b);
   q = wave_sum(q);
@@ -443,30 +449,85 @@ __global__ __launch_bounds__(NT) void k_history(const double* sc, const double* 
       sb += part[1][k];
       sq += part[2][k];
     }
-    if (cons_out) cons_out[h] = sa / (double)n;  // trainer.py:185 np.mean over workers
-    if (obj_out) {
-      double obj = 0.0;  // obj_problems.py:4,40: empty data -> 0.0 (no regulariser)
-      if (m_obj > 0) {
-        const double data = (problem == 0) ? sb / (double)m_obj : 0.5 * (sb / (double)m_obj);
-        obj = data + (lam_obj / 2.0) * sq;
-      }
-      obj_out[h] = obj - f_opt;  // trainer.py:190
-    }
+    out[0] = sa;
+    out[1] = sb;
+    out[2] = sq;
   }
 }
 
-hipError_t launch_history(int dtype, int problem, const double* slab_cons, const double* slab_loss,
-                          int64_t n, int64_t n_loss_groups, int64_t m_obj, const void* xbar,
-                          int64_t ld, int32_t nchunks, double lam_obj, double f_opt, double* obj_out,
-                          double* cons_out, int64_t h, hipStream_t s) {
+hipError_t launch_history(int dtype, const double* slab_cons, const double* slab_loss, int64_t n,
+                          int64_t ng, const void* xbar, int64_t ld, int32_t nchunks, bool xnorm,
+                          double* out, hipStream_t s) {
   if (dtype == 0)
-    hipLaunchKernelGGL(k_history<float>, dim3(1), dim3(NT), 0, s, slab_cons, slab_loss, n,
-                       n_loss_groups, m_obj, (const float*)xbar, ld, nchunks, problem, lam_obj,
-                       f_opt, obj_out, cons_out, h);
+    hipLaunchKernelGGL(k_history<float>, dim3(1), dim3(NT), 0, s, slab_cons, slab_loss, n, ng,
+                       (const float*)xbar, ld, nchunks, xnorm ? 1 : 0, out);
   else
-    hipLaunchKernelGGL(k_history<double>, dim3(1), dim3(NT), 0, s, slab_cons, slab_loss, n,
-                       n_loss_groups, m_obj, (const double*)xbar, ld, nchunks, problem, lam_obj,
-                       f_opt, obj_out, cons_out, h);
+    hipLaunchKernelGGL(k_history<double>, dim3(1), dim3(NT), 0, s, slab_cons, slab_loss, n, ng,
+                       (const double*)xbar, ld, nchunks, xnorm ? 1 : 0, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------- mix (multi-GPU)
+// One wave per worker: lane l owns 16-byte chunks l, l+64, ...  The neighbour rows
+// are local iterates or halo rows received from other ranks; same CSR order as the
+// fused kernel, so the result is bitwise the single-GPU one.
+template <typename T>
+__global__ __launch_bounds__(NT) void k_mix(const RoundArgs a, const T* __restrict__ G, int n) {
+  using V = typename VT<T>::v;
+  constexpr int VN = VT<T>::n;
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * NW + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (i >= n) return;
+  const int64_t ld = a.ld;
+  const int64_t e0 = a.rp[i], e1 = a.rp[i + 1];
+  const T eta = (T)a.eta;
+  for (int c = lane; c < a.nchunks; c += 64) {
+    V acc = V(0);
+    for (int64_t e = e0; e < e1; ++e) {
+      const T wt = ((const T*)a.cw)[e];
+      const int col = a.ci[e];
+      const T* src = col < a.n_local ? (const T*)a.x_old + (int64_t)col * ld
+                                     : (const T*)a.halo + (int64_t)(col - a.n_local) * ld;
+      acc += wt * *(const V*)(src + (int64_t)c * VN);
+    }
+    const V gc = *(const V*)(G + (int64_t)i * ld + (int64_t)c * VN);
+    *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = acc - eta * gc;
+  }
+}
+
+hipError_t launch_mix(int dtype, const RoundArgs& a, const void* G, int n_workers, hipStream_t s) {
+  if (n_workers <= 0) return hipSuccess;
+  const dim3 grid((n_workers + NW - 1) / NW);
+  if (dtype == 0)
+    hipLaunchKernelGGL(k_mix<float>, grid, dim3(NT), 0, s, a, (const float*)G, n_workers);
+  else
+    hipLaunchKernelGGL(k_mix<double>, grid, dim3(NT), 0, s, a, (const double*)G, n_workers);
+  return hipGetLastError();
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void k_gather_rows(const T* __restrict__ x, const int32_t* ids, int64_t n,
+                                                    int64_t ld, int nch, T* __restrict__ dst) {
+  using V = typename VT<T>::v;
+  constexpr int VN = VT<T>::n;
+  const int lane = threadIdx.x & 63;
+  const int64_t k = (int64_t)blockIdx.x * NW + (threadIdx.x >> 6);
+  if (k >= n) return;
+  const int64_t r = ids[k];
+  for (int c = lane; c < nch; c += 64)
+    *(V*)(dst + k * ld + (int64_t)c * VN) = *(const V*)(x + r * ld + (int64_t)c * VN);
+}
+
+hipError_t launch_gather_rows(int dtype, const void* x, const int32_t* ids, int64_t n, int64_t ld,
+                              int32_t nchunks, void* dst, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((n + NW - 1) / NW));
+  if (dtype == 0)
+    hipLaunchKernelGGL(k_gather_rows<float>, grid, dim3(NT), 0, s, (const float*)x, ids, n, ld, nchunks,
+                       (float*)dst);
+  else
+    hipLaunchKernelGGL(k_gather_rows<double>, grid, dim3(NT), 0, s, (const double*)x, ids, n, ld, nchunks,
+                       (double*)dst);
   return hipGetLastError();
 }
 
@@ -489,10 +550,12 @@ __device__ __forceinline__ double normal_at(uint64_t seed, uint64_t a, uint64_t 
 template <typename T>
 __global__ __launch_bounds__(NT) void k_generate(T* X, T* y, int64_t rows, int64_t d, int64_t ld,
                                                  uint64_t seed, double flip, double noise,
-                                                 int problem) {
+                                                 int problem, int64_t row_base) {
   const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * NW + (threadIdx.x >> 6);
-  if (r >= rows) return;
+  const int64_t rl = (int64_t)blockIdx.x * NW + (threadIdx.x >> 6);
+  if (rl >= rows) return;
+  const int64_t r = row_base + rl;  // values depend on the GLOBAL row: a rank's slice equals
+                                    // the same rows of the single-GPU data set
   double dot = 0.0;
   for (int64_t c = lane; c < ld; c += 64) {
     double v = 0.0;
@@ -500,7 +563,7 @@ __global__ __launch_bounds__(NT) void k_generate(T* X, T* y, int64_t rows, int64
       v = normal_at(seed, (uint64_t)r + 1, (uint64_t)c);
     else if (c == d - 1)
       v = 1.0;  // bias column, utils.py:28
-    X[r * ld + c] = (T)v;
+    X[rl * ld + c] = (T)v;
     // labels from the float64 values, so float32 and float64 engines get the same labels
     if (c < d) dot += v * normal_at(seed ^ 0x5DEECE66Dull, 0, (uint64_t)c);  // planted w*
   }
@@ -509,22 +572,23 @@ __global__ __launch_bounds__(NT) void k_generate(T* X, T* y, int64_t rows, int64
     if (problem == 0) {
       T lab = dot >= 0.0 ? T(1) : T(-1);
       if (unif01(mix64(seed ^ mix64(~(uint64_t)r))) <= flip) lab = -lab;
-      y[r] = lab;
+      y[rl] = lab;
     } else {
-      y[r] = (T)(dot + noise * normal_at(seed ^ 0xA5A5A5A5ull, (uint64_t)r, 0xFFFFFFFFull));
+      y[rl] = (T)(dot + noise * normal_at(seed ^ 0xA5A5A5A5ull, (uint64_t)r, 0xFFFFFFFFull));
     }
   }
 }
 
 hipError_t launch_generate(int dtype, int problem, void* X, void* y, int64_t rows, int64_t d,
-                           int64_t ld, uint64_t seed, double flip, double noise, hipStream_t s) {
+                           int64_t ld, uint64_t seed, double flip, double noise, int64_t row_base,
+                           hipStream_t s) {
   const dim3 grid((unsigned)((rows + NW - 1) / NW));
   if (dtype == 0)
     hipLaunchKernelGGL(k_generate<float>, grid, dim3(NT), 0, s, (float*)X, (float*)y, rows, d, ld,
-                       seed, flip, noise, problem);
+                       seed, flip, noise, problem, row_base);
   else
     hipLaunchKernelGGL(k_generate<double>, grid, dim3(NT), 0, s, (double*)X, (double*)y, rows, d, ld,
-                       seed, flip, noise, problem);
+                       seed, flip, noise, problem, row_base);
   return hipGetLastError();
 }
 

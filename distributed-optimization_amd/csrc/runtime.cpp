@@ -70,7 +70,8 @@ struct dopt_ctx {
   int dtype = DOPT_F64;
   size_t esz = 8;
   int vn = 2;  // elements per 16-byte vector
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;      // the stream every launch goes to
+  hipStream_t own_stream = nullptr;  // created by dopt_create; dopt_set_stream may override
   double clock_hz = 1e8;
 
   // problem
@@ -82,6 +83,8 @@ struct dopt_ctx {
   void* y = nullptr;
   int64_t* off = nullptr;
   std::vector<int64_t> off_h;
+  // global divisors when this context holds one rank's slice (dopt_set_partition)
+  int64_t n_global = 0, rows_global = 0;
 
   // separate objective dataset (X_full that is not the union of the shards)
   bool obj_sep = false;
@@ -97,6 +100,7 @@ struct dopt_ctx {
   int gcur = 0;
   void* G = nullptr;
   void* xbar[2] = {nullptr, nullptr};
+  int xb = 0;  // xbar[xb] = average of the current iterates
   double* part = nullptr;
   int groups = 0;
   double* slab_cons = nullptr;
@@ -108,11 +112,17 @@ struct dopt_ctx {
   int32_t* ci = nullptr;
   void* cw = nullptr;
 
+  // halo plan (multi-GPU): remote iterates land in `halo` (caller-owned device memory),
+  // rows send_ids of the current iterates are gathered into `send` (caller-owned)
+  int64_t n_halo = 0, n_send = 0;
+  void* halo = nullptr;
+  void* send = nullptr;
+  int32_t* send_ids = nullptr;
+
   // per-run buffers
   int32_t* idx = nullptr;
   size_t idx_cap = 0;
-  double* hobj = nullptr;
-  double* hcons = nullptr;
+  double* hraw = nullptr;  // [T x 3] raw metric sums per round (cons, loss, ||xbar||^2)
   uint64_t* stamps = nullptr;
   size_t hcap = 0;
   void* staging = nullptr;
@@ -123,9 +133,8 @@ struct dopt_ctx {
 
   // profiling of k_round
   bool prof = false;
-  std::vector<hipEvent_t> ev;
-  int64_t kr_launches = 0;
-  double kr_ms = 0.0;
+  std::vector<hipEvent_t> ev;  // (start, stop) pairs around every gradient-kernel launch
+  int64_t prof_n = 0;          // pairs recorded since the last dopt_kernel_stats
 };
 
 namespace {
@@ -224,6 +233,7 @@ int alloc_state(dopt_ctx* c) {
   dfree(c->G);  // allocated on first centralized run
   c->cur = 0;
   c->gcur = 0;
+  c->xb = 0;
   c->groups = (int)((std::max<int64_t>(1, c->n) + kRowsPerGroup - 1) / kRowsPerGroup);
   if ((rc = dalloc_t(&c->part, (size_t)c->groups * c->ld * sizeof(double)))) return rc;
   if ((rc = dalloc_t(&c->slab_cons, (size_t)std::max<int64_t>(1, c->n) * sizeof(double)))) return rc;
@@ -251,15 +261,17 @@ int set_layout(dopt_ctx* c, int problem, int64_t n, int64_t d) {
   c->cpl = cpl;
   c->have_topo = false;
   c->obj_sep = false;
+  c->n_global = c->rows_global = 0;
+  c->n_halo = c->n_send = 0;
+  c->halo = c->send = nullptr;
   return DOPT_OK;
 }
 
 int ensure_hist(dopt_ctx* c, int64_t T) {
-  if ((size_t)T <= c->hcap && c->hobj) return DOPT_OK;
+  if ((size_t)T <= c->hcap && c->hraw) return DOPT_OK;
   const size_t cap = (size_t)std::max<int64_t>(T, 16);
   int rc;
-  if ((rc = dalloc_t(&c->hobj, cap * sizeof(double)))) return rc;
-  if ((rc = dalloc_t(&c->hcons, cap * sizeof(double)))) return rc;
+  if ((rc = dalloc_t(&c->hraw, 3 * cap * sizeof(double)))) return rc;
   if ((rc = dalloc_t(&c->stamps, (cap + 1) * sizeof(uint64_t)))) return rc;
   c->hcap = cap;
   return DOPT_OK;
@@ -275,6 +287,11 @@ RoundArgs base_args(dopt_ctx* c) {
   a.nchunks = (int32_t)c->nch;
   a.slab_cons = c->slab_cons;
   a.slab_loss = c->slab_loss;
+  a.halo = c->halo;
+  a.n_local = (int32_t)c->n;
+  a.rp = c->rp;
+  a.ci = c->ci;
+  a.cw = c->cw;
   return a;
 }
 
@@ -295,7 +312,31 @@ int metrics_pass(dopt_ctx* c, const void* x_state, const void* point, bool share
   return DOPT_OK;
 }
 
-int64_t obj_rows(dopt_ctx* c) { return c->obj_sep ? c->rows_o : c->rows; }
+int64_t obj_rows(dopt_ctx* c) { return c->obj_sep ? c->rows_o : (c->rows_global ? c->rows_global : c->rows); }
+int64_t n_div(dopt_ctx* c) { return c->n_global ? c->n_global : c->n; }
+
+// Raw sums of round h -> history values (trainer.py:185, :189-190, obj_problems.py:3-11/:39-44).
+void finalize_metrics(const double* raw, int64_t T, int problem, int64_t n, int64_t m_obj, double lam_obj,
+                      double f_opt, double* obj_out, double* cons_out) {
+  for (int64_t h = 0; h < T; ++h) {
+    const double* r = raw + 3 * h;
+    if (cons_out) cons_out[h] = r[0] / (double)n;
+    if (obj_out) {
+      double obj = 0.0;  // empty data -> 0.0, no regulariser (obj_problems.py:4,40)
+      if (m_obj > 0) {
+        const double data = (problem == DOPT_LOGISTIC) ? r[1] / (double)m_obj : 0.5 * (r[1] / (double)m_obj);
+        obj = data + (lam_obj / 2.0) * r[2];
+      }
+      obj_out[h] = obj - f_opt;
+    }
+  }
+}
+
+int history(dopt_ctx* c, int64_t h, const void* point, bool cons, bool loss, int64_t ng) {
+  HIPOK(launch_history(c->dtype, cons ? c->slab_cons : nullptr, loss ? c->slab_loss : nullptr, c->n, ng, point,
+                       c->ld, (int32_t)c->nch, loss, c->hraw + 3 * h, c->stream));
+  return DOPT_OK;
+}
 
 int upload_idx_chunk(dopt_ctx* c, const int32_t* idx, int64_t h0, int64_t nr, int64_t b) {
   const size_t bytes = (size_t)(nr * c->n * b) * sizeof(int32_t);
@@ -308,37 +349,32 @@ int upload_idx_chunk(dopt_ctx* c, const int32_t* idx, int64_t h0, int64_t nr, in
   return DOPT_OK;
 }
 
-int prof_event(dopt_ctx* c, size_t k) {
+int prof_event(dopt_ctx* c, bool stop) {
+  const size_t k = (size_t)(2 * c->prof_n + (stop ? 1 : 0));
   while (c->ev.size() <= k) {
     hipEvent_t e;
     HIPOK(hipEventCreate(&e));
     c->ev.push_back(e);
   }
   HIPOK(hipEventRecord(c->ev[k], c->stream));
+  if (stop) c->prof_n++;
   return DOPT_OK;
 }
 
-int finish_run(dopt_ctx* c, int64_t T, int64_t launches, double* obj_out, double* cons_out,
-               double* time_out) {
+int finish_run(dopt_ctx* c, int64_t T, int64_t launches, double lam_obj, double f_opt, double* obj_out,
+               double* cons_out, double* time_out) {
   HIPOK(hipStreamSynchronize(c->stream));
-  if (obj_out && T > 0) HIPOK(hipMemcpy(obj_out, c->hobj, (size_t)T * sizeof(double), hipMemcpyDeviceToHost));
-  if (cons_out && T > 0)
-    HIPOK(hipMemcpy(cons_out, c->hcons, (size_t)T * sizeof(double), hipMemcpyDeviceToHost));
+  if ((obj_out || cons_out) && T > 0) {
+    std::vector<double> raw((size_t)(3 * T));
+    HIPOK(hipMemcpy(raw.data(), c->hraw, raw.size() * sizeof(double), hipMemcpyDeviceToHost));
+    finalize_metrics(raw.data(), T, c->problem, n_div(c), obj_rows(c), lam_obj, f_opt, obj_out, cons_out);
+  }
   if (time_out && T > 0) {
     std::vector<uint64_t> st((size_t)T + 1);
     HIPOK(hipMemcpy(st.data(), c->stamps, st.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
     for (int64_t h = 0; h < T; ++h) time_out[h] = (double)(st[(size_t)h + 1] - st[0]) / c->clock_hz;
   }
-  c->kr_launches = 0;
-  c->kr_ms = 0.0;
-  if (c->prof) {
-    for (int64_t k = 0; k < launches; ++k) {
-      float ms = 0.f;
-      HIPOK(hipEventElapsedTime(&ms, c->ev[(size_t)(2 * k)], c->ev[(size_t)(2 * k + 1)]));
-      c->kr_ms += ms;
-    }
-    c->kr_launches = launches;
-  }
+  (void)launches;
   return DOPT_OK;
 }
 
@@ -387,7 +423,8 @@ int dopt_create(int device, int dtype, dopt_ctx** out) {
   c->esz = dtype == DOPT_F32 ? 4 : 8;
   c->vn = dtype == DOPT_F32 ? 4 : 2;
   hipError_t e = hipSetDevice(device);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+  c->stream = c->own_stream;
   if (e != hipSuccess) {
     delete c;
     return fail(DOPT_ERR_HIP, "context init: %s", hipGetErrorString(e));
@@ -403,6 +440,7 @@ int dopt_destroy(dopt_ctx* c) {
   if (!c) return DOPT_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
   for (void** p : {&c->X, &c->y, &c->Xo, &c->yo, &c->xs[0], &c->xs[1], &c->xg[0], &c->xg[1], &c->G,
                    &c->xbar[0], &c->xbar[1], &c->cw, &c->staging, &c->sx})
     dfree(*p);
@@ -414,11 +452,11 @@ int dopt_destroy(dopt_ctx* c) {
   dfree_t(c->rp);
   dfree_t(c->ci);
   dfree_t(c->idx);
-  dfree_t(c->hobj);
-  dfree_t(c->hcons);
+  dfree_t(c->hraw);
+  dfree_t(c->send_ids);
   dfree_t(c->stamps);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return DOPT_OK;
 }
@@ -454,7 +492,7 @@ int dopt_load_shards(dopt_ctx* c, int problem, int64_t n_workers, int64_t d, con
 }
 
 int dopt_generate_shards(dopt_ctx* c, int problem, int64_t n_workers, int64_t d, int64_t rpw,
-                         uint64_t seed, double flip, double noise) {
+                         uint64_t seed, double flip, double noise, int64_t first_worker) {
   CHECK_ARG(c, "ctx is NULL");
   int rc;
   if ((rc = set_device(c))) return rc;
@@ -471,7 +509,9 @@ int dopt_generate_shards(dopt_ctx* c, int problem, int64_t n_workers, int64_t d,
   if ((rc = dalloc_t(&c->off, (size_t)(n_workers + 1) * sizeof(int64_t)))) return rc;
   HIPOK(hipMemcpy(c->off, c->off_h.data(), (size_t)(n_workers + 1) * sizeof(int64_t),
                   hipMemcpyHostToDevice));
-  HIPOK(launch_generate(c->dtype, problem, c->X, c->y, rows, d, c->ld, seed, flip, noise, c->stream));
+  CHECK_ARG(first_worker >= 0, "first_worker must be >= 0");
+  HIPOK(launch_generate(c->dtype, problem, c->X, c->y, rows, d, c->ld, seed, flip, noise, first_worker * rpw,
+                        c->stream));
   HIPOK(hipStreamSynchronize(c->stream));
   if ((rc = alloc_state(c))) return rc;
   c->have_data = true;
@@ -531,7 +571,9 @@ int dopt_set_topology(dopt_ctx* c, int64_t n_workers, const int64_t* row_ptr, co
   for (int64_t i = 0; i < n_workers; ++i) CHECK_ARG(row_ptr[i + 1] >= row_ptr[i], "row_ptr not monotone");
   const int64_t nnz = row_ptr[n_workers];
   CHECK_ARG(nnz == 0 || (col && w), "col / w are NULL");
-  for (int64_t e = 0; e < nnz; ++e) CHECK_ARG(col[e] >= 0 && col[e] < n_workers, "col out of range");
+  for (int64_t e = 0; e < nnz; ++e)
+    CHECK_ARG(col[e] >= 0 && col[e] < n_workers + c->n_halo, "col %d out of range (%lld local + %lld halo rows)",
+              col[e], (long long)n_workers, (long long)c->n_halo);
   int rc;
   if ((rc = set_device(c))) return rc;
   if ((rc = dalloc_t(&c->rp, (size_t)(n_workers + 1) * sizeof(int64_t)))) return rc;
@@ -596,9 +638,7 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
   const bool metrics = want_obj || want_cons;
   const bool fused = batch >= c->max_m && !c->obj_sep;
   const int64_t CH = idx ? idx_chunk_rounds(c, T, batch) : 1;
-  double* hobj = want_obj ? c->hobj : nullptr;
-  double* hcons = want_cons ? c->hcons : nullptr;
-  int xb = 0;  // xbar[xb] = average of the current iterates (valid once computed)
+  int& xb = c->xb;
   HIPOK(launch_stamp(c->stamps, c->stream));
 
   for (int64_t h = 0; h < T; ++h) {
@@ -612,41 +652,33 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
     a.x_old = c->xs[c->cur];
     a.x_new = c->xs[c->cur ^ 1];
     a.xbar = c->xbar[xb];
-    a.rp = c->rp;
-    a.ci = c->ci;
-    a.cw = c->cw;
     a.eta = eta0 / sqrt((double)(t + 1));  // trainer.py:138-140
     a.lam = lam_grad;
     const bool met = fused && metrics && h > 0;
     a.flags = F_STEP | (met && want_cons ? F_CONS : 0) | (met && want_obj ? F_LOSS : 0);
-    if (c->prof && (rc = prof_event(c, (size_t)(2 * h)))) return rc;
+    if (c->prof && (rc = prof_event(c, false))) return rc;
     HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, met, a, (int)c->n, c->stream));
-    if (c->prof && (rc = prof_event(c, (size_t)(2 * h + 1)))) return rc;
+    if (c->prof && (rc = prof_event(c, true))) return rc;
     // xbar_{t+1} (trainer.py:182); the stamp marks the end of round t's update (trainer.py:181)
     HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur ^ 1], c->n, c->ld, (int32_t)c->nch, kRowsPerGroup,
                                 c->part, c->stamps + h + 1, c->stream));
-    HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nch, c->xbar[xb ^ 1],
+    HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, n_div(c), c->ld, (int32_t)c->nch, c->xbar[xb ^ 1],
                               nullptr, 0.0, 0, c->stream));
     if (met) {
-      HIPOK(launch_history(c->dtype, c->problem, c->slab_cons, c->slab_loss, c->n, c->n, obj_rows(c),
-                           c->xbar[xb], c->ld, (int32_t)c->nch, lam_obj, f_opt, hobj, hcons, h - 1,
-                           c->stream));
+      if ((rc = history(c, h - 1, c->xbar[xb], want_cons, want_obj, c->n))) return rc;
     } else if (!fused && metrics) {
       if ((rc = metrics_pass(c, c->xs[c->cur ^ 1], c->xbar[xb ^ 1], false, want_cons, want_obj))) return rc;
-      HIPOK(launch_history(c->dtype, c->problem, c->slab_cons, c->slab_loss, c->n, c->n, obj_rows(c),
-                           c->xbar[xb ^ 1], c->ld, (int32_t)c->nch, lam_obj, f_opt, hobj, hcons, h,
-                           c->stream));
+      if ((rc = history(c, h, c->xbar[xb ^ 1], want_cons, want_obj, c->n))) return rc;
     }
     c->cur ^= 1;
     xb ^= 1;
   }
   if (fused && metrics && T > 0) {  // history[T-1]: one metrics pass over x_T
     if ((rc = metrics_pass(c, c->xs[c->cur], c->xbar[xb], false, want_cons, want_obj))) return rc;
-    HIPOK(launch_history(c->dtype, c->problem, c->slab_cons, c->slab_loss, c->n, c->n, obj_rows(c),
-                         c->xbar[xb], c->ld, (int32_t)c->nch, lam_obj, f_opt, hobj, hcons, T - 1,
-                         c->stream));
+    if ((rc = history(c, T - 1, c->xbar[xb], want_cons, want_obj, c->n))) return rc;
   }
-  return finish_run(c, T, T, obj_out, cons_out, time_out);
+  return finish_run(c, T, T, lam_obj, f_opt, want_obj ? obj_out : nullptr, want_cons ? cons_out : nullptr,
+                    time_out);
 }
 
 int dopt_run_centralized(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch,
@@ -676,9 +708,9 @@ int dopt_run_centralized(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_
     a.lam = lam_grad;
     const bool met = fused && want_obj && h > 0;
     a.flags = F_GOUT | F_SHARED | (met ? (F_LOSS | F_LOSS_FROM_Z) : 0);
-    if (c->prof && (rc = prof_event(c, (size_t)(2 * h)))) return rc;
+    if (c->prof && (rc = prof_event(c, false))) return rc;
     HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, met, a, (int)c->n, c->stream));
-    if (c->prof && (rc = prof_event(c, (size_t)(2 * h + 1)))) return rc;
+    if (c->prof && (rc = prof_event(c, true))) return rc;
     // mean of the worker gradients and the step (trainer.py:53-57)
     HIPOK(launch_colsum_partial(c->dtype, c->G, c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part,
                                 c->stamps + h + 1, c->stream));
@@ -686,24 +718,18 @@ int dopt_run_centralized(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_
                               c->xg[c->gcur ^ 1], c->xg[c->gcur], eta0 / sqrt((double)(t + 1)), 1,
                               c->stream));
     if (met) {
-      HIPOK(launch_history(c->dtype, c->problem, nullptr, c->slab_loss, c->n, c->n, obj_rows(c),
-                           c->xg[c->gcur], c->ld, (int32_t)c->nch, lam_obj, f_opt, c->hobj, nullptr,
-                           h - 1, c->stream));
+      if ((rc = history(c, h - 1, c->xg[c->gcur], false, true, c->n))) return rc;
     } else if (!fused && want_obj) {
       if ((rc = metrics_pass(c, nullptr, c->xg[c->gcur ^ 1], true, false, true))) return rc;
-      HIPOK(launch_history(c->dtype, c->problem, nullptr, c->slab_loss, c->n, c->n, obj_rows(c),
-                           c->xg[c->gcur ^ 1], c->ld, (int32_t)c->nch, lam_obj, f_opt, c->hobj, nullptr,
-                           h, c->stream));
+      if ((rc = history(c, h, c->xg[c->gcur ^ 1], false, true, c->n))) return rc;
     }
     c->gcur ^= 1;
   }
   if (fused && want_obj && T > 0) {
     if ((rc = metrics_pass(c, nullptr, c->xg[c->gcur], true, false, true))) return rc;
-    HIPOK(launch_history(c->dtype, c->problem, nullptr, c->slab_loss, c->n, c->n, obj_rows(c),
-                         c->xg[c->gcur], c->ld, (int32_t)c->nch, lam_obj, f_opt, c->hobj, nullptr,
-                         T - 1, c->stream));
+    if ((rc = history(c, T - 1, c->xg[c->gcur], false, true, c->n))) return rc;
   }
-  return finish_run(c, T, T, want_obj ? obj_out : nullptr, nullptr, time_out);
+  return finish_run(c, T, T, lam_obj, f_opt, want_obj ? obj_out : nullptr, nullptr, time_out);
 }
 
 // ---------------------------------------------------------------------------- single evaluations
@@ -728,7 +754,7 @@ int eval_common(dopt_ctx* c, int problem, int64_t rows, int64_t d, const double*
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const size_t bX = al((size_t)rows * ld * 8), by = al((size_t)rows * 8), bw = al((size_t)ld * 8),
                bg = al((size_t)ld * 8), bo = al((size_t)(groups + 1) * 8), bs = al((size_t)groups * 8),
-               bout = al(8);
+               bout = al(3 * 8);
   const size_t need = bX + by + bw + bg + bo + bs + bout;
   if (need > c->sx_cap) {
     if ((rc = dalloc(&c->sx, need))) return rc;
@@ -758,6 +784,7 @@ int eval_common(dopt_ctx* c, int problem, int64_t rows, int64_t d, const double*
   a.lam = reg;
   a.ld = ld;
   a.nchunks = (int32_t)nch;
+  a.n_local = 1;
   a.slab_loss = dslab;
   if (grad) {
     a.flags = F_GOUT | F_SHARED;
@@ -769,10 +796,11 @@ int eval_common(dopt_ctx* c, int problem, int64_t rows, int64_t d, const double*
   } else {
     a.flags = F_SHARED | F_LOSS | F_LOSS_FROM_Z;
     HIPOK(launch_round(DOPT_F64, problem, cpl, false, true, a, (int)groups, c->stream));
-    HIPOK(launch_history(DOPT_F64, problem, nullptr, dslab, 1, groups, rows, dw, ld, (int32_t)nch, reg, 0.0,
-                         dout, nullptr, 0, c->stream));
-    HIPOK(hipMemcpyAsync(out, dout, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPOK(launch_history(DOPT_F64, nullptr, dslab, 1, groups, dw, ld, (int32_t)nch, true, dout, c->stream));
+    double raw[3];
+    HIPOK(hipMemcpyAsync(raw, dout, sizeof(raw), hipMemcpyDeviceToHost, c->stream));
     HIPOK(hipStreamSynchronize(c->stream));
+    finalize_metrics(raw, 1, problem, 1, rows, reg, 0.0, out, nullptr);
   }
   return DOPT_OK;
 }
@@ -796,8 +824,149 @@ int dopt_set_profiling(dopt_ctx* c, int enable) {
 
 int dopt_kernel_stats(dopt_ctx* c, int64_t* launches, double* total_ms) {
   CHECK_ARG(c && launches && total_ms, "NULL argument");
-  *launches = c->kr_launches;
-  *total_ms = c->kr_ms;
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  HIPOK(hipStreamSynchronize(c->stream));
+  double ms_sum = 0.0;
+  for (int64_t k = 0; k < c->prof_n; ++k) {
+    float ms = 0.f;
+    HIPOK(hipEventElapsedTime(&ms, c->ev[(size_t)(2 * k)], c->ev[(size_t)(2 * k + 1)]));
+    ms_sum += ms;
+  }
+  *launches = c->prof_n;
+  *total_ms = ms_sum;
+  c->prof_n = 0;  // the next statistics window starts here
+  return DOPT_OK;
+}
+
+// ---------------------------------------------------------------------------- multi-GPU phases
+int dopt_set_stream(dopt_ctx* c, void* stream) {
+  CHECK_ARG(c, "ctx is NULL");
+  c->stream = stream ? (hipStream_t)stream : c->own_stream;
+  return DOPT_OK;
+}
+
+int dopt_get_layout(dopt_ctx* c, int64_t* ld, int64_t* elem_bytes) {
+  CHECK_ARG(c && ld && elem_bytes, "NULL argument");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
+  *ld = c->ld;
+  *elem_bytes = (int64_t)c->esz;
+  return DOPT_OK;
+}
+
+int dopt_set_partition(dopt_ctx* c, int64_t n_global, int64_t rows_global) {
+  CHECK_ARG(c, "ctx is NULL");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");
+  CHECK_ARG(n_global >= c->n && rows_global >= c->rows, "global sizes smaller than the local slice");
+  c->n_global = n_global;
+  c->rows_global = rows_global;
+  return DOPT_OK;
+}
+
+int dopt_set_halo(dopt_ctx* c, int64_t n_halo, void* halo_dev, int64_t n_send, void* send_dev,
+                  const int32_t* send_ids) {
+  CHECK_ARG(c, "ctx is NULL");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");
+  CHECK_ARG(n_halo >= 0 && n_send >= 0, "negative sizes");
+  CHECK_ARG(n_halo == 0 || halo_dev, "halo buffer is NULL");
+  CHECK_ARG(n_send == 0 || (send_dev && send_ids), "send buffer / ids are NULL");
+  for (int64_t k = 0; k < n_send; ++k) CHECK_ARG(send_ids[k] >= 0 && send_ids[k] < c->n, "send id out of range");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  if ((rc = dalloc_t(&c->send_ids, (size_t)std::max<int64_t>(1, n_send) * sizeof(int32_t)))) return rc;
+  if (n_send) HIPOK(hipMemcpy(c->send_ids, send_ids, (size_t)n_send * sizeof(int32_t), hipMemcpyHostToDevice));
+  c->n_halo = n_halo;
+  c->halo = halo_dev;
+  c->n_send = n_send;
+  c->send = send_dev;
+  c->have_topo = false;  // the CSR must be re-set in the local+halo index space
+  return DOPT_OK;
+}
+
+int dopt_phase_gather(dopt_ctx* c) {
+  CHECK_ARG(c, "ctx is NULL");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
+  HIPOK(launch_gather_rows(c->dtype, c->xs[c->cur], c->send_ids, c->n_send, c->ld, (int32_t)c->nch, c->send,
+                           c->stream));
+  return DOPT_OK;
+}
+
+int dopt_phase_grad(dopt_ctx* c, int64_t batch, const int32_t* idx, double lam_grad, uint32_t metric_flags) {
+  CHECK_ARG(c, "ctx is NULL");
+  int rc;
+  if ((rc = check_run(c, 1, batch, idx, false))) return rc;
+  if (!c->G && (rc = dalloc(&c->G, (size_t)c->n * c->ld * c->esz))) return rc;
+  if (idx && (rc = upload_idx_chunk(c, idx, 0, 1, batch))) return rc;
+  const bool cons = metric_flags & DOPT_RUN_CONSENSUS, loss = metric_flags & DOPT_RUN_OBJECTIVE;
+  if ((cons || loss) && (batch < c->max_m || c->obj_sep))
+    return fail(DOPT_ERR_UNSUPPORTED, "fused metrics need full-shard batches over the shard rows");
+  RoundArgs a = base_args(c);
+  a.idx = idx ? c->idx : nullptr;
+  a.b = batch;
+  a.x_old = c->xs[c->cur];
+  a.g_out = c->G;
+  a.xbar = c->xbar[c->xb];
+  a.lam = lam_grad;
+  a.flags = F_GOUT | (cons ? F_CONS : 0) | (loss ? F_LOSS : 0);
+  if (c->prof && (rc = prof_event(c, false))) return rc;
+  HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, cons || loss, a, (int)c->n, c->stream));
+  if (c->prof && (rc = prof_event(c, true))) return rc;
+  return DOPT_OK;
+}
+
+int dopt_phase_mix(dopt_ctx* c, int64_t t, double eta0) {
+  CHECK_ARG(c, "ctx is NULL");
+  if (!c->have_topo || !c->G) return fail(DOPT_ERR_STATE, "topology / gradient phase missing");
+  RoundArgs a = base_args(c);
+  a.x_old = c->xs[c->cur];
+  a.x_new = c->xs[c->cur ^ 1];
+  a.eta = eta0 / sqrt((double)(t + 1));  // trainer.py:138-140
+  HIPOK(launch_mix(c->dtype, a, c->G, (int)c->n, c->stream));
+  c->cur ^= 1;
+  return DOPT_OK;
+}
+
+int dopt_phase_colsum(dopt_ctx* c, double* sum_dev) {
+  CHECK_ARG(c && sum_dev, "NULL argument");
+  HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur], c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part,
+                              nullptr, c->stream));
+  HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nch, nullptr, nullptr, 0.0, 0,
+                            c->stream, sum_dev));
+  return DOPT_OK;
+}
+
+int dopt_phase_xbar(dopt_ctx* c, const double* sum_dev) {
+  CHECK_ARG(c && sum_dev, "NULL argument");
+  HIPOK(launch_colsum_final(c->dtype, sum_dev, 1, n_div(c), c->ld, (int32_t)c->nch, c->xbar[c->xb ^ 1], nullptr,
+                            0.0, 0, c->stream));
+  c->xb ^= 1;
+  return DOPT_OK;
+}
+
+int dopt_phase_metrics_pass(dopt_ctx* c, uint32_t flags) {
+  CHECK_ARG(c, "ctx is NULL");
+  return metrics_pass(c, c->xs[c->cur], c->xbar[c->xb], false, flags & DOPT_RUN_CONSENSUS,
+                      flags & DOPT_RUN_OBJECTIVE);
+}
+
+int dopt_phase_metrics(dopt_ctx* c, uint32_t flags, int include_xnorm, double* out_dev) {
+  CHECK_ARG(c && out_dev, "NULL argument");
+  const bool cons = flags & DOPT_RUN_CONSENSUS, loss = flags & DOPT_RUN_OBJECTIVE;
+  HIPOK(launch_history(c->dtype, cons ? c->slab_cons : nullptr, loss ? c->slab_loss : nullptr, c->n, c->n,
+                       c->xbar[c->xb], c->ld, (int32_t)c->nch, loss && include_xnorm, out_dev, c->stream));
+  return DOPT_OK;
+}
+
+int dopt_sync(dopt_ctx* c) {
+  CHECK_ARG(c, "ctx is NULL");
+  HIPOK(hipStreamSynchronize(c->stream));
+  return DOPT_OK;
+}
+
+int dopt_finalize_metrics(int problem, int64_t T, const double* raw, int64_t n_workers, int64_t m_obj,
+                          double lam_obj, double f_opt, double* obj_out, double* cons_out) {
+  CHECK_ARG(raw && T >= 0 && n_workers >= 1 && m_obj >= 0, "bad arguments");
+  finalize_metrics(raw, T, problem, n_workers, m_obj, lam_obj, f_opt, obj_out, cons_out);
   return DOPT_OK;
 }
 

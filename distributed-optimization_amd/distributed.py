@@ -1,0 +1,196 @@
+"""Multi-GPU D-SGD: one process per GPU, contiguous worker slices, halo exchange.
+
+The reference simulates every worker in one process (trainer.py:161-193).  Here
+rank r of a torch.distributed job (backend "nccl" = RCCL over xGMI on MI355X;
+"gloo" in tests) owns workers [lo_r, hi_r) -- their shards, iterates and rows of
+W -- on its own GPU.  Per round:
+
+  gather x_t rows the peers need --> grouped isend/irecv ------------.
+  gradient of every local worker at x_t (+ metrics of x_t) ---------+--> mix + step
+  local column sums --> all_reduce(d doubles) --> xbar_{t+1}
+
+The mix uses the same CSR entry order as the single-GPU kernel, so the iterates
+are bitwise the single-GPU iterates; only the metric sums are reduced in a
+different order (per rank, then across ranks).  Metric partial sums stay on the
+device per round and are all-reduced once per run.
+
+Plan construction (`build_plan`) is pure host logic over the global CSR, so it
+is tested on CPU with gloo against the oracle (tests/test_distributed_cpu.py).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+import _dopt
+
+
+def partition_bounds(n, world):
+    """Contiguous slices, np.array_split sizes (the first n % world ranks get one more)."""
+    sizes = [n // world + (1 if r < n % world else 0) for r in range(world)]
+    return np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+
+
+@dataclass
+class HaloPlan:
+    rank: int
+    world: int
+    bounds: np.ndarray      # [world+1] global worker ranges
+    lo: int
+    hi: int
+    halo_ids: np.ndarray    # [n_halo] global ids of the remote rows this rank reads, ascending
+    recv_off: np.ndarray    # [world+1] halo rows coming from each peer (contiguous blocks)
+    send_ids: np.ndarray    # [n_send] LOCAL ids of rows peers need, grouped by peer, ascending
+    send_off: np.ndarray    # [world+1]
+    row_ptr: np.ndarray     # local CSR, columns in local (< n_local) + halo (>= n_local) space
+    col: np.ndarray
+    w: np.ndarray
+
+    @property
+    def n_local(self):
+        return self.hi - self.lo
+
+    @property
+    def n_halo(self):
+        return len(self.halo_ids)
+
+    def peers(self):
+        return [p for p in range(self.world) if p != self.rank and
+                (self.send_off[p + 1] > self.send_off[p] or self.recv_off[p + 1] > self.recv_off[p])]
+
+
+def build_plan(topo, world, rank):
+    """Halo plan of `rank` for a topology.Topology (global CSR incl. diagonal)."""
+    bounds = partition_bounds(topo.n, world)
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    e0, e1 = topo.row_ptr[lo], topo.row_ptr[hi]
+    cols = topo.col[e0:e1].astype(np.int64)
+    remote = np.unique(cols[(cols < lo) | (cols >= hi)])
+    n_local = hi - lo
+    local_col = np.where((cols >= lo) & (cols < hi), cols - lo, n_local + np.searchsorted(remote, cols))
+    recv_off = np.searchsorted(remote, bounds).astype(np.int64)
+    send, send_off = [], [0]
+    for p in range(world):
+        if p != rank:
+            pc = topo.col[topo.row_ptr[bounds[p]]:topo.row_ptr[bounds[p + 1]]].astype(np.int64)
+            need = np.unique(pc[(pc >= lo) & (pc < hi)])
+            send.append(need - lo)
+        else:
+            send.append(np.zeros(0, np.int64))
+        send_off.append(send_off[-1] + len(send[-1]))
+    return HaloPlan(rank=rank, world=world, bounds=bounds, lo=lo, hi=hi, halo_ids=remote, recv_off=recv_off,
+                    send_ids=np.concatenate(send).astype(np.int32), send_off=np.array(send_off, np.int64),
+                    row_ptr=(topo.row_ptr[lo:hi + 1] - e0).astype(np.int64), col=local_col.astype(np.int32),
+                    w=topo.w[e0:e1].copy())
+
+
+class DistributedDSGD:
+    """Drives one rank's engine through the round phases with torch.distributed."""
+
+    def __init__(self, engine, plan, n_global, rows_global, device=0, group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist = torch, dist
+        self.eng, self.plan, self.group = engine, plan, group
+        self.n_global, self.rows_global = int(n_global), int(rows_global)
+        self.dev = torch.device("cuda", device)
+        self.device_comm = dist.get_backend(group) == "nccl"
+        self.stream = torch.cuda.Stream(self.dev)
+        ld, esz = engine.layout()
+        self.ld = ld
+        tdt = torch.float32 if esz == 4 else torch.float64
+        self.halo = torch.zeros((max(1, plan.n_halo), ld), dtype=tdt, device=self.dev)
+        self.send = torch.zeros((max(1, len(plan.send_ids)), ld), dtype=tdt, device=self.dev)
+        self.sum = torch.zeros(ld, dtype=torch.float64, device=self.dev)
+        engine.set_partition(self.n_global, self.rows_global)
+        engine.set_halo(plan.n_halo, self.halo.data_ptr(), plan.send_ids, self.send.data_ptr())
+        engine.set_topology(plan.row_ptr, plan.col, plan.w)
+        engine.set_stream(self.stream.cuda_stream)
+        self._peers = plan.peers()
+
+    # -- transport
+    def _start_exchange(self):
+        P = self.plan
+        if not self._peers:
+            return None
+        if self.device_comm:
+            ops = []
+            for p in self._peers:
+                s0, s1 = P.send_off[p], P.send_off[p + 1]
+                r0, r1 = P.recv_off[p], P.recv_off[p + 1]
+                if s1 > s0:
+                    ops.append(self.dist.P2POp(self.dist.isend, self.send[s0:s1], p, self.group))
+                if r1 > r0:
+                    ops.append(self.dist.P2POp(self.dist.irecv, self.halo[r0:r1], p, self.group))
+            return self.dist.batch_isend_irecv(ops)
+        # gloo: stage through host memory, synchronously
+        send = self.send.cpu()
+        halo = self.halo.cpu()
+        works = []
+        for p in self._peers:
+            s0, s1 = P.send_off[p], P.send_off[p + 1]
+            r0, r1 = P.recv_off[p], P.recv_off[p + 1]
+            if s1 > s0:
+                works.append(self.dist.isend(send[s0:s1], p, group=self.group))
+            if r1 > r0:
+                works.append(self.dist.irecv(halo[r0:r1], p, group=self.group))
+        for w in works:
+            w.wait()
+        self.halo.copy_(halo)
+        return None
+
+    def _finish_exchange(self, works):
+        for w in works or ():
+            w.wait()
+
+    def _all_reduce(self, t):
+        if self.device_comm:
+            self.dist.all_reduce(t, group=self.group)
+        else:
+            c = t.cpu()
+            self.dist.all_reduce(c, group=self.group)
+            t.copy_(c)
+
+    # -- rounds
+    def run(self, T, eta0, batch, lam_grad, lam_obj, f_opt=0.0, t0=0, objective=True, consensus=True):
+        """T rounds; returns the GLOBAL (objective, consensus) history on every rank."""
+        torch = self.torch
+        eng = self.eng
+        flags = (_dopt.RUN_OBJECTIVE if objective else 0) | (_dopt.RUN_CONSENSUS if consensus else 0)
+        xnorm = self.plan.rank == 0  # ||xbar||^2 is global already: count it once
+        with torch.cuda.stream(self.stream):
+            partials = torch.zeros((max(1, T), 3), dtype=torch.float64, device=self.dev)
+            for h in range(T):
+                eng.phase_gather()
+                pending = self._start_exchange()
+                eng.phase_grad(batch, lam_grad, flags if h > 0 else 0)
+                if h > 0 and flags:
+                    eng.phase_metrics(flags, xnorm, partials[h - 1].data_ptr())
+                self._finish_exchange(pending)
+                eng.phase_mix(t0 + h, eta0)
+                eng.phase_colsum(self.sum.data_ptr())
+                self._all_reduce(self.sum)
+                eng.phase_xbar(self.sum.data_ptr())
+            if flags and T > 0:
+                eng.phase_metrics_pass(flags)
+                eng.phase_metrics(flags, xnorm, partials[T - 1].data_ptr())
+            self._all_reduce(partials)
+            raw = partials[:T].cpu().numpy()
+        self.stream.synchronize()
+        obj, cons = _dopt.finalize_metrics(self.eng.problem, raw, self.n_global, self.rows_global, lam_obj, f_opt)
+        return (obj if objective else None), (cons if consensus else None)
+
+    def gather_models(self):
+        """All ranks' iterates, concatenated in global worker order (on every rank)."""
+        torch = self.torch
+        sizes = np.diff(self.plan.bounds)
+        top = int(sizes.max())
+        x = torch.zeros((top, self.eng.d), dtype=torch.float64)
+        x[:self.plan.n_local] = torch.from_numpy(self.eng.get_models())
+        if self.device_comm:
+            x = x.to(self.dev)
+        buf = [torch.zeros_like(x) for _ in sizes]
+        self.dist.all_gather(buf, x, group=self.group)
+        return torch.cat([b[:int(s)] for b, s in zip(buf, sizes)]).cpu().numpy()

@@ -88,9 +88,13 @@ int dopt_load_shards(dopt_ctx *ctx, int problem, int64_t n_workers, int64_t d,
 /* Synthetic shards generated on the device (BASELINE.json config C3 shape):
  * X ~ N(0,1) with a ones bias column (utils.py:28), y from a planted w* --
  * logistic: sign(X w*) with a fraction `flip` of labels flipped; quadratic:
- * X w* + noise * N(0,1).  Every worker gets `rows_per_worker` rows. */
+ * X w* + noise * N(0,1).  Every worker gets `rows_per_worker` rows.  Values are a
+ * function of the GLOBAL row id, so a rank generating workers
+ * [first_worker, first_worker + n_workers) gets exactly those rows of the
+ * single-GPU data set. */
 int dopt_generate_shards(dopt_ctx *ctx, int problem, int64_t n_workers, int64_t d,
-                         int64_t rows_per_worker, uint64_t seed, double flip, double noise);
+                         int64_t rows_per_worker, uint64_t seed, double flip, double noise,
+                         int64_t first_worker);
 
 /* Objective dataset when it is NOT the union of the shards (the X_full /
  * y_full arguments of Trainer.run, trainer.py:154,188-189).  Without this
@@ -148,6 +152,52 @@ int dopt_eval_gradient(dopt_ctx *ctx, int problem, int64_t b, int64_t d,
 int dopt_eval_objective(dopt_ctx *ctx, int problem, int64_t n, int64_t d,
                         const double *w, const double *X, const double *y, double reg,
                         double *out);
+
+/* ------------------------------------------------------------------ multi-GPU phases
+ * One process per GPU, each context holding a contiguous slice of the workers.
+ * The round of trainer.py:161-193 is split into enqueue-only phases on the
+ * context's stream, so the caller can interleave the collectives
+ * (torch.distributed over RCCL, or gloo in tests) between them:
+ *   gather -> [halo send/recv of x_t rows] || grad(x_t) -> metrics(prev)
+ *          -> mix -> colsum -> [all-reduce of d doubles] -> xbar
+ * Device pointers (halo, send, sum, out) are caller-owned device memory. */
+
+/* Launch on `stream` (a hipStream_t, e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL restores the context's own stream. */
+int dopt_set_stream(dopt_ctx *ctx, void *stream);
+/* Row stride (elements) and element size of the device rows (halo / send buffers). */
+int dopt_get_layout(dopt_ctx *ctx, int64_t *ld, int64_t *elem_bytes);
+/* Global worker and row counts: divisors of xbar (trainer.py:182), the
+ * consensus mean (:185) and the objective mean (obj_problems.py:6/:42). */
+int dopt_set_partition(dopt_ctx *ctx, int64_t n_global, int64_t rows_global);
+/* Halo plan: CSR columns >= n_local address halo rows [n_halo x ld]; rows
+ * send_ids[n_send] (local ids) are gathered into send [n_send x ld].  Call
+ * before dopt_set_topology (the local CSR indexes local + halo rows). */
+int dopt_set_halo(dopt_ctx *ctx, int64_t n_halo, void *halo_dev, int64_t n_send, void *send_dev,
+                  const int32_t *send_ids);
+int dopt_phase_gather(dopt_ctx *ctx);
+/* Gradients of every local worker at its current iterate (worker.py:30-44);
+ * metric_flags (DOPT_RUN_*) also accumulate the current iterate's metric
+ * partials at the current xbar (fused, full-shard batches only). */
+int dopt_phase_grad(dopt_ctx *ctx, int64_t batch, const int32_t *idx, double lam_grad,
+                    uint32_t metric_flags);
+/* x_{t+1} = W [x_t | halo] - eta0/sqrt(t+1) g  (trainer.py:173-175). */
+int dopt_phase_mix(dopt_ctx *ctx, int64_t t, double eta0);
+/* Local column sums of the current iterates -> sum_dev[ld] (float64). */
+int dopt_phase_colsum(dopt_ctx *ctx, double *sum_dev);
+/* xbar = sum_dev / n_global. */
+int dopt_phase_xbar(dopt_ctx *ctx, const double *sum_dev);
+/* Metrics-only pass over the local shard rows at the current xbar. */
+int dopt_phase_metrics_pass(dopt_ctx *ctx, uint32_t flags);
+/* Raw sums -> out_dev[3] = (sum of consensus partials, sum of loss terms,
+ * ||xbar||^2 if include_xnorm else 0). */
+int dopt_phase_metrics(dopt_ctx *ctx, uint32_t flags, int include_xnorm, double *out_dev);
+int dopt_sync(dopt_ctx *ctx);
+/* Host: raw[T x 3] (summed over ranks) -> history values, the exact formula
+ * the single-GPU path applies. */
+int dopt_finalize_metrics(int problem, int64_t T, const double *raw, int64_t n_workers,
+                          int64_t m_obj, double lam_obj, double f_opt, double *obj_out,
+                          double *cons_out);
 
 /* Device time of the last run's dominant kernel (the fused round kernel):
  * launches and summed milliseconds, measured with HIP events on the engine's

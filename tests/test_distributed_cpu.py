@@ -1,0 +1,105 @@
+"""Multi-rank logic on CPU (gloo, world 2 and 3): the halo plan that the GPU ranks use
+(distributed.build_plan) drives a partitioned restatement of the round with real
+torch.distributed send/recv of the halo rows; the result must equal the
+unpartitioned oracle round bit for bit (last paragraph)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import distributed as D
+import dsgd_oracle as O
+import topology as TP
+
+CFG = {"problem_type": "logistic", "local_batch_size": 7, "learning_rate_eta0": 0.05,
+       "l2_regularization_lambda": 1e-3, "strong_convexity_mu": 1e-3}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _data(n, d=6, m=7, seed=0):
+    rng = np.random.default_rng(seed)
+    return [(np.hstack([rng.standard_normal((m, d - 1)), np.ones((m, 1))]), rng.choice([-1.0, 1.0], m))
+            for _ in range(n)]
+
+
+def _topo(name, n):
+    return TP.random_regular(n, 4, seed=3) if name == "random_regular" else TP.build(name, n)
+
+
+def _rank_main(rank, world, port, name, n, T, out):
+    import torch
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    topo = _topo(name, n)
+    plan = D.build_plan(topo, world, rank)
+    shards = _data(n)
+    x = np.zeros((plan.n_local, shards[0][0].shape[1]))
+    for t in range(T):
+        g = np.stack([O.gradient("logistic", x[i], *shards[plan.lo + i], CFG) for i in range(plan.n_local)])
+        send = torch.from_numpy(np.ascontiguousarray(x[plan.send_ids]))
+        halo = torch.zeros((plan.n_halo, x.shape[1]), dtype=torch.float64)
+        works = []
+        for p in plan.peers():
+            s0, s1, r0, r1 = plan.send_off[p], plan.send_off[p + 1], plan.recv_off[p], plan.recv_off[p + 1]
+            if s1 > s0:
+                works.append(dist.isend(send[s0:s1].contiguous(), p))
+            if r1 > r0:
+                buf = torch.zeros((r1 - r0, x.shape[1]), dtype=torch.float64)
+                works.append((dist.irecv(buf, p), r0, buf))
+        for w in works:
+            if isinstance(w, tuple):
+                w[0].wait()
+                halo[w[1]:w[1] + w[2].shape[0]] = w[2]
+            else:
+                w.wait()
+        H = halo.numpy()
+        new = np.empty_like(x)
+        for i in range(plan.n_local):
+            acc = np.zeros(x.shape[1])
+            for e in range(plan.row_ptr[i], plan.row_ptr[i + 1]):
+                c = plan.col[e]
+                acc = acc + plan.w[e] * (x[c] if c < plan.n_local else H[c - plan.n_local])
+            new[i] = acc
+        x = new - np.asarray(O._lr(CFG["learning_rate_eta0"], t)) * g
+    np.save(os.path.join(out, f"rank{rank}.npy"), x)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,n,world", [("ring", 10, 2), ("grid", 16, 3), ("random_regular", 24, 3),
+                                          ("fully_connected", 9, 2)])
+def test_partitioned_rounds_match_oracle(tmp_path, name, n, world):
+    T = 4
+    mp.start_processes(_rank_main, args=(world, _free_port(), name, n, T, str(tmp_path)), nprocs=world,
+                       join=True, start_method="fork")
+    got = np.concatenate([np.load(tmp_path / f"rank{r}.npy") for r in range(world)])
+    topo = _topo(name, n)
+    shards = _data(n)
+    idx = [[np.arange(7)] * n] * T
+    _, _, ref, _ = O.run_decentralized(shards, topo.dense_W(), T, CFG, mixing="sparse", indices=idx)
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_plan_structure():
+    topo = TP.grid(256 * 256 // 64)  # 32 x 32 torus
+    plans = [D.build_plan(topo, 8, r) for r in range(8)]
+    for p in plans:
+        # every halo row comes from exactly the peer that owns it, in ascending order
+        for q in range(8):
+            ids = p.halo_ids[p.recv_off[q]:p.recv_off[q + 1]]
+            assert np.all((ids >= p.bounds[q]) & (ids < p.bounds[q + 1]))
+            # ... and the peer sends exactly those rows
+            sent = plans[q].send_ids[plans[q].send_off[p.rank]:plans[q].send_off[p.rank + 1]] + plans[q].lo
+            np.testing.assert_array_equal(np.sort(sent), ids)
+        assert p.n_halo == 2 * 32  # strips of 4 torus rows: one boundary row above, one below
+    np.testing.assert_array_equal(D.partition_bounds(10, 3), [0, 4, 7, 10])

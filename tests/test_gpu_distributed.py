@@ -1,0 +1,66 @@
+"""The multi-GPU code path on one GPU: 2 ranks (gloo transport, both contexts on
+device 0) run the phase API with the halo plan; the iterates must equal the
+single-context fused run bit for bit, the metrics to rtol 1e-12 (reordered sums)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+N, D, M, T = 64, 100, 32, 6
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, dtype, out):
+    import torch  # noqa: F401  (one HIP runtime, loaded before libdopt)
+    import torch.distributed as dist
+
+    import _dopt
+    import distributed as Dm
+    import topology as TP
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    top = TP.random_regular(N, 4, seed=2)
+    plan = Dm.build_plan(top, world, rank)
+    eng = _dopt.Engine(0, dtype)
+    eng.generate_shards("logistic", plan.n_local, D, M, seed=9, first_worker=plan.lo)
+    run = Dm.DistributedDSGD(eng, plan, N, N * M, device=0)
+    obj, cons = run.run(T, 0.05, M, 1e-3, 1e-3, 0.25)
+    x = run.gather_models()
+    if rank == 0:
+        np.savez(os.path.join(out, "dist.npz"), obj=obj, cons=cons, x=x)
+    dist.barrier()
+    eng.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+def test_two_ranks_match_single_context(tmp_path, dtype):
+    import torch.multiprocessing as mp
+
+    import _dopt
+    import topology as TP
+
+    mp.start_processes(_rank_main, args=(2, _free_port(), dtype, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    got = np.load(tmp_path / "dist.npz")
+    eng = _dopt.Engine(0, dtype)
+    eng.generate_shards("logistic", N, D, M, seed=9)
+    top = TP.random_regular(N, 4, seed=2)
+    eng.set_topology(top.row_ptr, top.col, top.w)
+    obj, cons, _ = eng.run_dsgd(T, 0.05, M, 1e-3, 1e-3, 0.25)
+    x = eng.get_models()
+    eng.close()
+    np.testing.assert_array_equal(got["x"], x)
+    np.testing.assert_allclose(got["obj"], obj, rtol=1e-12 if dtype == "float64" else 1e-6)
+    np.testing.assert_allclose(got["cons"], cons, rtol=1e-12 if dtype == "float64" else 1e-5)
