@@ -108,6 +108,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (gloo: 1-GPU rehearsal)")
+    ap.add_argument("--config", default="c3", choices=["c3", "c4", "c5"],
+                    help="c3 (default, the metric's config); c4: 256x256 torus, 65536 workers total; "
+                         "c5: quadratic, d=2^20, m=b=16, 1024 workers total, complete graph")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -127,22 +130,45 @@ def main():
     import distributed
     import topology
 
-    n, d, m = args.workers, args.d, args.m
-    n_global = n * world
-    top = topology.random_regular(n_global, args.degree, seed=0)
-    plan = distributed.build_plan(top, world, rank)
+    problem, mean = "logistic", None
+    if args.config == "c3":
+        n, d, m = args.workers, args.d, args.m
+        n_global = n * world
+        top = topology.random_regular(n_global, args.degree, seed=0)
+        workload = (f"C3: logistic, {n} workers/GPU, d={d}, m=b={m}, random {args.degree}-regular MH mixing, "
+                    "objective+consensus every round")
+    elif args.config == "c4":
+        d, m, n_global = 1024, 512, 65536
+        top = topology.grid(n_global)
+        workload = "C4: logistic, 65536 workers total on a 256x256 torus, d=1024, m=b=512"
+    else:
+        problem, d, m, n_global = "quadratic", 1 << 20, 16, 1024
+        top = topology.fully_connected(n_global)
+        mean = top.uniform_offdiag()
+        workload = "C5: quadratic, 1024 workers total, d=2^20, m=b=16, complete graph (column-sum mixing)"
+    plan = distributed.build_plan(top, world, rank) if mean is None else None
+    if plan is None:  # complete graph: contiguous slices, no halo plan needed
+        bounds = distributed.partition_bounds(n_global, world)
+        plan = distributed.HaloPlan(rank, world, bounds, int(bounds[rank]), int(bounds[rank + 1]),
+                                    np.zeros(0, np.int64), np.zeros(world + 1, np.int64), np.zeros(0, np.int32),
+                                    np.zeros(world + 1, np.int64), None, None, None)
+    n = plan.n_local
     log(f"rank {rank}/{world}: generating {plan.n_local} x {m} x {d} {args.dtype} shards on device {dev}")
     eng = _dopt.Engine(dev, args.dtype)
-    eng.generate_shards("logistic", plan.n_local, d, m, seed=1000, flip=0.05, first_worker=plan.lo)
+    eng.generate_shards(problem, plan.n_local, d, m, seed=1000, flip=0.05, first_worker=plan.lo)
     lam = 1e-4
     if world > 1:
-        runner = distributed.DistributedDSGD(eng, plan, n_global, n_global * m, device=dev)
+        mean_local = None if mean is None else (mean[0], mean[1][plan.lo:plan.hi])
+        runner = distributed.DistributedDSGD(eng, plan, n_global, n_global * m, device=dev, mean=mean_local)
         log(f"halo: {plan.n_halo} rows in, {len(plan.send_ids)} rows out per round")
 
         def rounds(k):
             return runner.run(k, 0.05, m, lam, lam, 0.0)
     else:
-        eng.set_topology(top.row_ptr, top.col, top.w)
+        if mean is not None:
+            eng.set_mixing_mean(*mean)
+        else:
+            eng.set_topology(top.row_ptr, top.col, top.w)
 
         def rounds(k):
             obj, cons, _ = eng.run_dsgd(k, 0.05, m, lam, lam, 0.0)
@@ -178,8 +204,11 @@ def main():
     cpl = 1
     while cpl * 64 < (d + (16 // esz) - 1) // (16 // esz):
         cpl *= 2
-    kname = f"void dopt::k_round<{tname}, {cpl}, 0, true, true>(dopt::RoundArgs)"
-    traffic, traffic_src = pmc_traffic(kname)
+    if cpl <= 16:
+        kname = f"void dopt::k_round<{tname}, {cpl}, {0 if problem == 'logistic' else 1}, true, true>(dopt::RoundArgs)"
+    else:
+        kname = f"void dopt::k_split_step<{tname}, true, true>(dopt::RoundArgs)"
+    traffic, traffic_src = pmc_traffic(kname) if args.config == "c3" and n == 4096 and world == 1 else (None, None)
     bytes_per_launch = esz * n * (m * d + m + 2 * d)  # X_b + y_b + x read + x write
     avg_s = (kr_ms / launches) * 1e-3 if launches else float("nan")
     achieved = bytes_per_launch / avg_s / 1e9
@@ -197,10 +226,9 @@ def main():
         "vs_baseline": None,
         "dtype": "f32" if esz == 4 else "f64",
         "data": "synthetic (device-generated X~N(0,1)+bias, planted-w* labels, 5% flips)",
-        "config": {"workload": "C3: logistic, 4096 workers/GPU, d=1024, m=b=512, random 4-regular MH mixing, "
-                               "objective+consensus every round",
-                   "workers_per_gpu": n, "d": d, "rows_per_worker": m, "batch": m, "topology": "random_regular",
-                   "degree": args.degree,
+        "config": {"workload": workload,
+                   "workers_per_gpu": n, "d": d, "rows_per_worker": m, "batch": m, "topology": top.name,
+                   "degree": args.degree if args.config == "c3" else None,
                    "parallelism": f"dp{world}: one graph of {n_global} workers, contiguous slices, halo send/recv"
                                   + (f" ({args.backend})" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -211,7 +239,10 @@ def main():
         "final_objective": float(obj[-1]),
         "final_consensus": float(cons[-1]),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if args.config != "c3":
+        out["metric"] = f"worker-iters/sec ({args.config.upper()}, secondary config)"
+        out["scaling"] = "strong"
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
         log("cpu baseline")
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:

@@ -49,6 +49,7 @@ _SIGS = {
     "dopt_clear_objective_data": ([_P], ctypes.c_int),
     "dopt_get_shard": ([_P, _I64, _P, _P], ctypes.c_int),
     "dopt_set_topology": ([_P, _I64, _P, _P, _P], ctypes.c_int),
+    "dopt_set_mixing_mean": ([_P, _I64, _D, _P], ctypes.c_int),
     "dopt_set_models": ([_P, _P], ctypes.c_int),
     "dopt_get_models": ([_P, _P], ctypes.c_int),
     "dopt_set_global": ([_P, _P], ctypes.c_int),
@@ -227,6 +228,10 @@ class Engine:
         ci = np.ascontiguousarray(col, dtype=np.int32)
         cw = np.ascontiguousarray(w, dtype=np.float64)
         check(lib().dopt_set_topology(self._h, len(rp) - 1, _ptr(rp), _ptr(ci), _ptr(cw)))
+
+    def set_mixing_mean(self, w_off, w_diag):
+        wd = np.ascontiguousarray(w_diag, dtype=np.float64)
+        check(lib().dopt_set_mixing_mean(self._h, len(wd), float(w_off), _ptr(wd)))
 
     def set_models(self, x):
         x = np.ascontiguousarray(x, dtype=np.float64).reshape(self.n, self.d)

@@ -15,6 +15,7 @@ enum : int32_t {
   F_CONS = 8,          // consensus partial ||x_i - xbar||^2 (trainer.py:185)
   F_LOSS = 16,         // objective partial at xbar over this workgroup's rows (trainer.py:189)
   F_LOSS_FROM_Z = 32,  // the objective point IS the gradient point: reuse z = x.w
+  F_MEAN = 64,         // complete graph: sum_j W_ij x_j = w_off (S - x_i) + W_ii x_i, S = column sums
 };
 
 // One workgroup per worker (or per objective-row chunk).  All pointers are
@@ -42,6 +43,17 @@ struct RoundArgs {
   int32_t nchunks;        // ld / elements-per-16B
   int32_t flags;
   int32_t n_local;        // rows of x_old owned by this rank (columns below it are local)
+  // complete-graph mixing (F_MEAN)
+  const double* colsum;   // [ld] column sums of x_old (all workers, all ranks)
+  const void* wdiag;      // [n] T diagonal weights W_ii
+  double w_off;           // the uniform off-diagonal weight
+  // column-blocked (large d) rounds
+  const void* coef;       // [n x bcap] T per-row coefficients c(z_k) of the current round
+  double* zpart;          // [n x bcap x groups] partial dots for the next coefficients
+  double* upart;          // [n x bcap x groups] partial dots with xbar (objective)
+  double* cpart;          // [n x groups] partial ||x_i - xbar||^2
+  int32_t bcap;           // row capacity per worker in coef / partials
+  int32_t groups;         // column-block groups = gridDim.y
 };
 
 // Kernel launchers (kernels.hip).  dtype: 0 = float, 1 = double.
@@ -49,6 +61,21 @@ struct RoundArgs {
 hipError_t launch_round(int dtype, int problem, int cpl, bool grad, bool met, const RoundArgs& a,
                         int n_groups, hipStream_t s);
 int max_chunks_per_lane();
+
+// ---- large d (column-blocked): one workgroup per (worker, group of 64-chunk column blocks)
+constexpr int kSplitMaxRows = 64;  // rows held in registers by a step workgroup (16 per wave)
+// Step: g_i = (1/nb) sum_k coef_k x_k + lam x_i, x_i' = mix - eta g_i (block by block); with
+// znext also the partial dots x_k . x_i' for the next round's coefficients (rows still in
+// registers); with met the metric partials of x_i at xbar.  nb <= kSplitMaxRows.
+hipError_t launch_split_step(int dtype, bool znext, bool met, const RoundArgs& a, int n_workers,
+                             hipStream_t s);
+// Dots only: mode 0 -> zpart = x_k . x_i (minibatch rows via idx, or all rows);
+// mode 1 -> upart = x_k . xbar over all rows, cpart = ||x_i - xbar||^2 partials.
+hipError_t launch_split_dots(int dtype, int mode, const RoundArgs& a, int n_workers, hipStream_t s);
+// Per worker: z_k = sum_g zpart -> coef (mode bit 1), sum_k loss(u_k) -> slab_loss and
+// sum_g cpart -> slab_cons (mode bit 2).  Fixed reduction order.
+hipError_t launch_split_coef(int dtype, int problem, int mode, const RoundArgs& a, int n_workers,
+                             hipStream_t s);
 
 // Column sums of an [n x ld] matrix into fp64 partials [G x ld], G = ceil(n / rpg).
 hipError_t launch_colsum_partial(int dtype, const void* x, int64_t n, int64_t ld, int32_t nchunks,

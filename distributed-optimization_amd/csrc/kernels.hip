@@ -84,6 +84,33 @@ __device__ __forceinline__ double row_loss(T yv, T u) {
   }
 }
 
+// sum_j W_ij x_j for the 16-byte chunk c of worker i: CSR over local / halo rows, or, for the
+// complete graph (F_MEAN), w_off (S - x_i) + W_ii x_i from the column sums S (trainer.py:173).
+template <typename T>
+__device__ __forceinline__ typename VT<T>::v mix_chunk(const RoundArgs& a, int i, int c,
+                                                       typename VT<T>::v own) {
+  using V = typename VT<T>::v;
+  constexpr int VN = VT<T>::n;
+  V acc = V(0);
+  if (a.flags & F_MEAN) {
+    const double wii = (double)((const T*)a.wdiag)[i];
+#pragma unroll
+    for (int e = 0; e < VN; ++e) {
+      const double x = (double)own[e];
+      acc[e] = (T)(a.w_off * (a.colsum[(int64_t)c * VN + e] - x) + wii * x);
+    }
+    return acc;
+  }
+  for (int64_t e = a.rp[i]; e < a.rp[i + 1]; ++e) {
+    const T wt = ((const T*)a.cw)[e];
+    const int col = a.ci[e];
+    const T* src = col < a.n_local ? (const T*)a.x_old + (int64_t)col * a.ld
+                                   : (const T*)a.halo + (int64_t)(col - a.n_local) * a.ld;
+    acc += wt * *(const V*)(src + (int64_t)c * VN);
+  }
+  return acc;
+}
+
 // ---------------------------------------------------------------------------- k_round
 template <typename T, int CPL, int PROB, bool GRAD, bool MET>
 __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
@@ -203,7 +230,6 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
   if (GRAD) {
     const T inv_eta = (T)a.eta;
     const T lam = (T)a.lam;
-    const int64_t e0 = a.rp ? a.rp[i] : 0, e1 = a.rp ? a.rp[i + 1] : 0;
     for (int c = threadIdx.x; c < nch; c += NT) {
       V s = red[c];
 #pragma unroll
@@ -211,14 +237,7 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
       const V wc = *(const V*)(wsrc + (int64_t)c * VN);
       const V gc = (nb > 0) ? (s / (T)nb + lam * wc) : V(0);
       if (flags & F_STEP) {
-        V acc = V(0);
-        for (int64_t e = e0; e < e1; ++e) {
-          const T wt = ((const T*)a.cw)[e];
-          const int col = a.ci[e];
-          const T* src = col < a.n_local ? (const T*)a.x_old + (int64_t)col * ld
-                                         : (const T*)a.halo + (int64_t)(col - a.n_local) * ld;
-          acc += wt * *(const V*)(src + (int64_t)c * VN);
-        }
+        const V acc = mix_chunk<T>(a, i, c, wc);
         *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = acc - inv_eta * gc;
       } else if (flags & F_GOUT) {
         *(V*)((T*)a.g_out + (int64_t)i * ld + (int64_t)c * VN) = gc;
@@ -284,6 +303,243 @@ hipError_t launch_round(int dtype, int problem, int cpl, bool grad, bool met, co
 }
 
 int max_chunks_per_lane() { return MAX_CPL; }
+
+
+// ---------------------------------------------------------------------------- large d
+// Column-blocked round for rows too long to hold in registers (config C5: d = 2^20).
+// Workgroup (i, g) walks column blocks cb = g, g + G, ... of 64 16-byte chunks.  The
+// mix is column-local for every topology, so per block: rows' segments -> gradient
+// block -> x_i' block (waves meet in LDS) -> the next round's partial dots x_k . x_i'
+// from the SAME row registers.  Per-row partial dots go to fp64 slabs [n][bcap][G]
+// that k_split_coef folds in a fixed order.  One pass over the shard per round.
+template <typename T, bool ZNEXT, bool MET>
+__global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
+  using V = typename VT<T>::v;
+  constexpr int VN = VT<T>::n;
+  constexpr int RPW = kSplitMaxRows / NW;
+  __shared__ V gred[NW][64];
+  __shared__ V xs[64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int i = blockIdx.x, grp = blockIdx.y, G = gridDim.y;
+  const int nch = a.nchunks, nblk = (nch + 63) / 64;
+  const int64_t ld = a.ld;
+  const int64_t row0 = a.off[i], m = a.off[i + 1] - row0;
+  const int64_t nb = a.idx ? (a.b < m ? a.b : m) : m;  // <= kSplitMaxRows (host-checked)
+  const T* __restrict__ X = (const T*)a.X;
+  const bool shared = (a.flags & F_SHARED) != 0;  // centralized: every worker at w_shared
+  const T* own_p = shared ? (const T*)a.w_shared : (const T*)a.x_old + (int64_t)i * ld;
+  int64_t rowp[RPW];
+  T coef[RPW];
+  double zacc[RPW], uacc[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int k = wave + NW * r;
+    const bool ok = k < nb;
+    const int64_t lr = ok ? (a.idx ? (int64_t)a.idx[(int64_t)i * a.b + k] : (int64_t)k) : 0;
+    rowp[r] = ok ? (row0 + lr) * ld : -1;
+    coef[r] = ok ? ((const T*)a.coef)[(int64_t)i * a.bcap + k] : T(0);
+    zacc[r] = 0.0;
+    uacc[r] = 0.0;
+  }
+  double cacc = 0.0;
+  for (int cb = grp; cb < nblk; cb += G) {
+    const int c = cb * 64 + lane;
+    const bool in = c < nch;
+    const V own = in ? *(const V*)(own_p + (int64_t)c * VN) : V(0);
+    const V xb = (MET && in) ? *(const V*)((const T*)a.xbar + (int64_t)c * VN) : V(0);
+    V rv[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) rv[r] = (rowp[r] >= 0 && in) ? *(const V*)(X + rowp[r] + (int64_t)c * VN) : V(0);
+    V gp = V(0);
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) gp += coef[r] * rv[r];
+    gred[wave][lane] = gp;
+    __syncthreads();
+    if (wave == 0) {
+      V g = V(0);
+      if (nb > 0) g = (gred[0][lane] + gred[1][lane] + gred[2][lane] + gred[3][lane]) / (T)nb + (T)a.lam * own;
+      V xn = V(0);
+      if (in && (a.flags & F_GOUT)) {
+        *(V*)((T*)a.g_out + (int64_t)i * ld + (int64_t)c * VN) = g;
+      } else if (in) {
+        xn = mix_chunk<T>(a, i, c, own) - (T)a.eta * g;
+        *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = xn;
+      }
+      xs[lane] = xn;
+    }
+    __syncthreads();
+    if (ZNEXT) {
+      const V xn = xs[lane];
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) zacc[r] += (double)hsum<T>(rv[r] * xn);
+    }
+    if (MET) {
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) uacc[r] += (double)hsum<T>(rv[r] * xb);
+      if (wave == 0) {
+        const V dv = own - xb;
+        cacc += (double)hsum<T>(dv * dv);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int k = wave + NW * r;
+    const int64_t slot = ((int64_t)i * a.bcap + k) * G + grp;
+    if (ZNEXT) {
+      const double z = wave_sum(zacc[r]);
+      if (lane == 0 && k < nb) a.zpart[slot] = z;
+    }
+    if (MET) {
+      const double u = wave_sum(uacc[r]);
+      if (lane == 0 && k < nb) a.upart[slot] = u;
+    }
+  }
+  if (MET && wave == 0) {
+    const double cs = wave_sum(cacc);
+    if (lane == 0) a.cpart[(int64_t)i * G + grp] = cs;
+  }
+}
+
+template <typename T, int MODE>
+__global__ __launch_bounds__(NT) void k_split_dots(const RoundArgs a) {
+  using V = typename VT<T>::v;
+  constexpr int VN = VT<T>::n;
+  constexpr int RPW = kSplitMaxRows / NW;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int i = blockIdx.x, grp = blockIdx.y, G = gridDim.y;
+  const int nch = a.nchunks, nblk = (nch + 63) / 64;
+  const int64_t ld = a.ld;
+  const int64_t row0 = a.off[i], m = a.off[i + 1] - row0;
+  const int64_t nb = (MODE == 0 && a.idx) ? (a.b < m ? a.b : m) : m;
+  const T* __restrict__ X = (const T*)a.X;
+  const T* own_p = (a.flags & F_SHARED) ? (const T*)a.w_shared : (const T*)a.x_old + (int64_t)i * ld;
+  const T* pt = MODE == 0 ? own_p : (const T*)a.xbar;
+  double* out = MODE == 0 ? a.zpart : a.upart;
+  if (MODE == 1 && wave == 0 && (a.flags & F_CONS)) {  // ||x_i - xbar||^2 partial over this group's blocks
+    double cacc = 0.0;
+    for (int cb = grp; cb < nblk; cb += G) {
+      const int c = cb * 64 + lane;
+      if (c < nch) {
+        const V dv = *(const V*)(own_p + (int64_t)c * VN) - *(const V*)(pt + (int64_t)c * VN);
+        cacc += (double)hsum<T>(dv * dv);
+      }
+    }
+    cacc = wave_sum(cacc);
+    if (lane == 0) a.cpart[(int64_t)i * G + grp] = cacc;
+  }
+  if (MODE == 1 && !(a.flags & F_LOSS)) return;
+  for (int64_t rc = 0; rc < nb; rc += kSplitMaxRows) {
+    int64_t rowp[RPW];
+    double acc[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const int64_t k = rc + wave + NW * r;
+      const bool ok = k < nb;
+      const int64_t lr = ok ? ((MODE == 0 && a.idx) ? (int64_t)a.idx[(int64_t)i * a.b + k] : k) : 0;
+      rowp[r] = ok ? (row0 + lr) * ld : -1;
+      acc[r] = 0.0;
+    }
+    for (int cb = grp; cb < nblk; cb += G) {
+      const int c = cb * 64 + lane;
+      if (c >= nch) continue;
+      const V pv = *(const V*)(pt + (int64_t)c * VN);
+#pragma unroll
+      for (int r = 0; r < RPW; ++r)
+        if (rowp[r] >= 0) acc[r] += (double)hsum<T>(*(const V*)(X + rowp[r] + (int64_t)c * VN) * pv);
+    }
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const int64_t k = rc + wave + NW * r;
+      const double z = wave_sum(acc[r]);
+      if (lane == 0 && k < nb) out[((int64_t)i * a.bcap + k) * G + grp] = z;
+    }
+  }
+}
+
+template <typename T, int PROB>
+__global__ __launch_bounds__(NT) void k_split_coef(const RoundArgs a, int mode) {
+  __shared__ double red[NW];
+  const int i = blockIdx.x, G = a.groups;
+  const int64_t row0 = a.off[i], m = a.off[i + 1] - row0;
+  const T* Y = (const T*)a.y;
+  if (mode & 1) {  // next coefficients from the partial dots (obj_problems.py:16-17 / :49-50)
+    const int64_t nb = a.idx ? (a.b < m ? a.b : m) : m;
+    for (int64_t k = threadIdx.x; k < nb; k += NT) {
+      double z = 0.0;
+      for (int q = 0; q < G; ++q) z += a.zpart[((int64_t)i * a.bcap + k) * G + q];
+      const int64_t lr = a.idx ? (int64_t)a.idx[(int64_t)i * a.b + k] : k;
+      const double yv = (double)Y[row0 + lr];
+      const double cf = (PROB == 0) ? -yv * (1.0 / (1.0 + exp(yv * z))) : z - yv;
+      ((T*)a.coef)[(int64_t)i * a.bcap + k] = (T)cf;
+    }
+  }
+  if (mode & 2) {  // objective partial over ALL rows of the worker, consensus partial
+    double l = 0.0;
+    for (int64_t k = threadIdx.x; k < m; k += NT) {
+      double u = 0.0;
+      for (int q = 0; q < G; ++q) u += a.upart[((int64_t)i * a.bcap + k) * G + q];
+      l += row_loss<double, PROB>((double)Y[row0 + k], u);
+    }
+    l = wave_sum(l);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = l;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = 0.0, cs = 0.0;
+      for (int q = 0; q < NW; ++q) s += red[q];
+      for (int q = 0; q < G; ++q) cs += a.cpart[(int64_t)i * G + q];
+      if (a.flags & F_LOSS) a.slab_loss[i] = s;
+      if (a.flags & F_CONS) a.slab_cons[i] = cs;
+    }
+  }
+}
+
+hipError_t launch_split_step(int dtype, bool znext, bool met, const RoundArgs& a, int n_workers,
+                             hipStream_t s) {
+  if (n_workers <= 0) return hipSuccess;
+  const dim3 grid(n_workers, a.groups);
+#define SPLIT_STEP(T_)                                                                              \
+  if (znext && met) hipLaunchKernelGGL((k_split_step<T_, true, true>), grid, dim3(NT), 0, s, a);    \
+  else if (znext) hipLaunchKernelGGL((k_split_step<T_, true, false>), grid, dim3(NT), 0, s, a);     \
+  else if (met) hipLaunchKernelGGL((k_split_step<T_, false, true>), grid, dim3(NT), 0, s, a);       \
+  else hipLaunchKernelGGL((k_split_step<T_, false, false>), grid, dim3(NT), 0, s, a);
+  if (dtype == 0) {
+    SPLIT_STEP(float)
+  } else {
+    SPLIT_STEP(double)
+  }
+#undef SPLIT_STEP
+  return hipGetLastError();
+}
+
+hipError_t launch_split_dots(int dtype, int mode, const RoundArgs& a, int n_workers, hipStream_t s) {
+  if (n_workers <= 0) return hipSuccess;
+  const dim3 grid(n_workers, a.groups);
+  if (dtype == 0) {
+    if (mode == 0) hipLaunchKernelGGL((k_split_dots<float, 0>), grid, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((k_split_dots<float, 1>), grid, dim3(NT), 0, s, a);
+  } else {
+    if (mode == 0) hipLaunchKernelGGL((k_split_dots<double, 0>), grid, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((k_split_dots<double, 1>), grid, dim3(NT), 0, s, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_split_coef(int dtype, int problem, int mode, const RoundArgs& a, int n_workers,
+                             hipStream_t s) {
+  if (n_workers <= 0) return hipSuccess;
+  const dim3 grid(n_workers);
+  if (dtype == 0) {
+    if (problem == 0) hipLaunchKernelGGL((k_split_coef<float, 0>), grid, dim3(NT), 0, s, a, mode);
+    else hipLaunchKernelGGL((k_split_coef<float, 1>), grid, dim3(NT), 0, s, a, mode);
+  } else {
+    if (problem == 0) hipLaunchKernelGGL((k_split_coef<double, 0>), grid, dim3(NT), 0, s, a, mode);
+    else hipLaunchKernelGGL((k_split_coef<double, 1>), grid, dim3(NT), 0, s, a, mode);
+  }
+  return hipGetLastError();
+}
 
 // ---------------------------------------------------------------------------- column sums
 // Stage 1: workgroup (g, cb) sums rows [g*rpg, (g+1)*rpg) of the 64-chunk column block cb;
@@ -374,9 +630,9 @@ __global__ __launch_bounds__(NT) void k_colsum_final(const double* __restrict__ 
       double s = red[0][lane * VN + e];
 #pragma unroll
       for (int q = 1; q < NW; ++q) s += red[q][lane * VN + e];
-      if (raw) {  // local column sums for a cross-rank all-reduce
+      if (raw) {  // column sums (cross-rank all-reduce input, or S for complete-graph mixing)
         raw[col] = s;
-        continue;
+        if (!out) continue;
       }
       const double mean = s / (double)n;  // np.mean: sum / count
       if (mode == 0)
@@ -479,17 +735,10 @@ __global__ __launch_bounds__(NT) void k_mix(const RoundArgs a, const T* __restri
   const int i = blockIdx.x * NW + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (i >= n) return;
   const int64_t ld = a.ld;
-  const int64_t e0 = a.rp[i], e1 = a.rp[i + 1];
   const T eta = (T)a.eta;
   for (int c = lane; c < a.nchunks; c += 64) {
-    V acc = V(0);
-    for (int64_t e = e0; e < e1; ++e) {
-      const T wt = ((const T*)a.cw)[e];
-      const int col = a.ci[e];
-      const T* src = col < a.n_local ? (const T*)a.x_old + (int64_t)col * ld
-                                     : (const T*)a.halo + (int64_t)(col - a.n_local) * ld;
-      acc += wt * *(const V*)(src + (int64_t)c * VN);
-    }
+    const V own = *(const V*)((const T*)a.x_old + (int64_t)i * ld + (int64_t)c * VN);
+    const V acc = mix_chunk<T>(a, i, c, own);
     const V gc = *(const V*)(G + (int64_t)i * ld + (int64_t)c * VN);
     *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = acc - eta * gc;
   }

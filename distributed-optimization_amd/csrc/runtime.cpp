@@ -79,6 +79,8 @@ struct dopt_ctx {
   int problem = DOPT_LOGISTIC;
   int64_t n = 0, d = 0, ld = 0, nch = 0, rows = 0, max_m = 0;
   int cpl = 1;
+  bool split = false;  // d too long for the row-resident kernel: column-blocked rounds
+  int split_groups = 1;
   void* X = nullptr;
   void* y = nullptr;
   int64_t* off = nullptr;
@@ -101,6 +103,19 @@ struct dopt_ctx {
   void* G = nullptr;
   void* xbar[2] = {nullptr, nullptr};
   int xb = 0;  // xbar[xb] = average of the current iterates
+  double* S = nullptr;             // [ld] column sums of the current iterates (complete-graph mixing)
+  const double* S_ext = nullptr;   // all-reduced sums (multi-GPU), used by the mix when set
+  // complete-graph mixing: sum_j W_ij x_j = w_off (S - x_i) + W_ii x_i
+  bool mean_mix = false;
+  double w_off = 0.0;
+  void* wdiag = nullptr;
+  // column-blocked buffers
+  void* coef = nullptr;
+  double* zpart = nullptr;
+  double* upart = nullptr;
+  double* cpart = nullptr;
+  int64_t bcap = 0;
+  size_t split_cap = 0;
   double* part = nullptr;
   int groups = 0;
   double* slab_cons = nullptr;
@@ -238,6 +253,8 @@ int alloc_state(dopt_ctx* c) {
   if ((rc = dalloc_t(&c->part, (size_t)c->groups * c->ld * sizeof(double)))) return rc;
   if ((rc = dalloc_t(&c->slab_cons, (size_t)std::max<int64_t>(1, c->n) * sizeof(double)))) return rc;
   if ((rc = dalloc_t(&c->slab_loss, (size_t)std::max<int64_t>(1, c->n) * sizeof(double)))) return rc;
+  if ((rc = dalloc_t(&c->S, (size_t)c->ld * sizeof(double)))) return rc;
+  HIPOK(hipMemsetAsync(c->S, 0, (size_t)c->ld * sizeof(double), c->stream));
   HIPOK(hipStreamSynchronize(c->stream));
   return DOPT_OK;
 }
@@ -250,10 +267,14 @@ int set_layout(dopt_ctx* c, int problem, int64_t n, int64_t d) {
   const int64_t ld = (d + c->vn - 1) / c->vn * c->vn;
   const int64_t nch = ld / c->vn;
   const int cpl = cpl_for(nch);
-  if (cpl > max_chunks_per_lane())
-    return fail(DOPT_ERR_UNSUPPORTED, "d = %lld exceeds the row-resident kernel limit (%d)", (long long)d,
-                max_chunks_per_lane() * 64 * c->vn);
+  c->split = cpl > max_chunks_per_lane();
+  if (c->split) {  // enough workgroups to fill 256 CUs several times over
+    const int64_t nblk = (nch + 63) / 64;
+    c->split_groups = (int)std::max<int64_t>(1, std::min<int64_t>(nblk, (4096 + n - 1) / n));
+  }
   c->problem = problem;
+  c->mean_mix = false;
+  c->S_ext = nullptr;
   c->n = n;
   c->d = d;
   c->ld = ld;
@@ -292,6 +313,18 @@ RoundArgs base_args(dopt_ctx* c) {
   a.rp = c->rp;
   a.ci = c->ci;
   a.cw = c->cw;
+  if (c->mean_mix) {
+    a.flags |= F_MEAN;
+    a.colsum = c->S_ext ? c->S_ext : c->S;
+    a.wdiag = c->wdiag;
+    a.w_off = c->w_off;
+  }
+  a.coef = c->coef;
+  a.zpart = c->zpart;
+  a.upart = c->upart;
+  a.cpart = c->cpart;
+  a.bcap = (int32_t)c->bcap;
+  a.groups = c->split_groups;
   return a;
 }
 
@@ -307,7 +340,7 @@ int metrics_pass(dopt_ctx* c, const void* x_state, const void* point, bool share
   a.x_old = x_state;
   a.xbar = point;
   a.w_shared = point;
-  a.flags = (cons ? F_CONS : 0) | (loss ? F_LOSS : 0) | (shared ? (F_SHARED | F_LOSS_FROM_Z) : 0);
+  a.flags |= (cons ? F_CONS : 0) | (loss ? F_LOSS : 0) | (shared ? (F_SHARED | F_LOSS_FROM_Z) : 0);
   HIPOK(launch_round(c->dtype, c->problem, c->cpl, false, true, a, (int)c->n, c->stream));
   return DOPT_OK;
 }
@@ -378,6 +411,169 @@ int finish_run(dopt_ctx* c, int64_t T, int64_t launches, double lam_obj, double 
   return DOPT_OK;
 }
 
+int64_t idx_chunk_rounds(dopt_ctx* c, int64_t T, int64_t b) {
+  const int64_t per = std::max<int64_t>(1, c->n * b * (int64_t)sizeof(int32_t));
+  return std::max<int64_t>(1, std::min<int64_t>(T, (int64_t)(256ll << 20) / per));
+}
+
+// xbar[xb] and S of the current iterates (run prologue).
+int colsum_current(dopt_ctx* c) {
+  HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur], c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part,
+                              nullptr, c->stream));
+  HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, n_div(c), c->ld, (int32_t)c->nch, c->xbar[c->xb], nullptr,
+                            0.0, 0, c->stream, c->S));
+  return DOPT_OK;
+}
+
+// Column-blocked buffers: coefficients [n x bcap] and fp64 partial slabs.
+int ensure_split(dopt_ctx* c) {
+  int64_t bcap = std::max<int64_t>(1, c->max_m);
+  if (c->obj_sep) bcap = std::max<int64_t>(bcap, (c->rows_o + c->n - 1) / c->n);
+  const size_t need = (size_t)(c->n * bcap * c->split_groups);
+  if (c->coef && bcap <= c->bcap && need <= c->split_cap) return DOPT_OK;
+  int rc;
+  if ((rc = dalloc(&c->coef, (size_t)(c->n * bcap) * c->esz))) return rc;
+  if ((rc = dalloc_t(&c->zpart, need * sizeof(double)))) return rc;
+  if ((rc = dalloc_t(&c->upart, need * sizeof(double)))) return rc;
+  if ((rc = dalloc_t(&c->cpart, (size_t)(c->n * c->split_groups) * sizeof(double)))) return rc;
+  c->bcap = bcap;
+  c->split_cap = need;
+  return DOPT_OK;
+}
+
+// Metrics of the current iterates at `point` over the objective rows, column-blocked:
+// partial dots -> per-worker loss / consensus slabs.
+int split_metrics(dopt_ctx* c, const void* x_state, const void* point, bool shared, bool cons, bool loss) {
+  RoundArgs a = base_args(c);
+  if (c->obj_sep) {
+    a.X = c->Xo;
+    a.y = c->yo;
+    a.off = c->offo;
+  }
+  a.x_old = x_state;
+  a.w_shared = point;
+  a.xbar = point;
+  a.flags = (cons ? F_CONS : 0) | (loss ? F_LOSS : 0) | (shared ? F_SHARED : 0);
+  HIPOK(launch_split_dots(c->dtype, 1, a, (int)c->n, c->stream));
+  HIPOK(launch_split_coef(c->dtype, c->problem, 2, a, (int)c->n, c->stream));
+  return DOPT_OK;
+}
+
+// D-SGD rounds for rows longer than the row-resident kernel takes (config C5).
+int run_dsgd_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch, const int32_t* idx,
+                   double lam_grad, double lam_obj, double f_opt, uint32_t flags, double* obj_out,
+                   double* cons_out, double* time_out) {
+  int rc;
+  const bool want_obj = flags & DOPT_RUN_OBJECTIVE, want_cons = flags & DOPT_RUN_CONSENSUS;
+  const bool metrics = want_obj || want_cons;
+  const bool full = batch >= c->max_m;
+  const int64_t nb_max = std::min(batch, c->max_m);
+  if (nb_max > kSplitMaxRows)
+    return fail(DOPT_ERR_UNSUPPORTED, "d = %lld with %lld rows per minibatch: the column-blocked kernel holds "
+                "at most %d rows", (long long)c->d, (long long)nb_max, kSplitMaxRows);
+  const bool fused_met = full && !c->obj_sep;
+  if ((rc = ensure_split(c))) return rc;
+  const int64_t CH = idx ? idx_chunk_rounds(c, T, batch) : 1;
+  int& xb = c->xb;
+  if ((rc = colsum_current(c))) return rc;
+  RoundArgs p = base_args(c);
+  p.x_old = c->xs[c->cur];
+  if (full) {  // prologue: coefficients of the starting iterates
+    HIPOK(launch_split_dots(c->dtype, 0, p, (int)c->n, c->stream));
+    HIPOK(launch_split_coef(c->dtype, c->problem, 1, p, (int)c->n, c->stream));
+  }
+  HIPOK(launch_stamp(c->stamps, c->stream));
+  for (int64_t h = 0; h < T; ++h) {
+    const int64_t t = t0 + h;
+    RoundArgs a = base_args(c);
+    if (!full) {
+      if (h % CH == 0 && (rc = upload_idx_chunk(c, idx, h, std::min(CH, T - h), batch))) return rc;
+      a.idx = c->idx + (h % CH) * c->n * batch;
+      a.b = batch;
+    }
+    a.x_old = c->xs[c->cur];
+    a.x_new = c->xs[c->cur ^ 1];
+    a.xbar = c->xbar[xb];
+    a.eta = eta0 / sqrt((double)(t + 1));  // trainer.py:138-140
+    a.lam = lam_grad;
+    if (!full) {  // this round's minibatch coefficients
+      HIPOK(launch_split_dots(c->dtype, 0, a, (int)c->n, c->stream));
+      HIPOK(launch_split_coef(c->dtype, c->problem, 1, a, (int)c->n, c->stream));
+    }
+    const bool met = fused_met && metrics && h > 0;
+    a.flags |= (met && want_cons ? F_CONS : 0) | (met && want_obj ? F_LOSS : 0);
+    if (c->prof && (rc = prof_event(c, false))) return rc;
+    HIPOK(launch_split_step(c->dtype, full, met, a, (int)c->n, c->stream));
+    if (c->prof && (rc = prof_event(c, true))) return rc;
+    if (full || met) {  // next coefficients (rows of the full shard) and the metric slabs
+      RoundArgs q = a;
+      q.idx = nullptr;
+      HIPOK(launch_split_coef(c->dtype, c->problem, (full ? 1 : 0) | (met ? 2 : 0), q, (int)c->n, c->stream));
+    }
+    HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur ^ 1], c->n, c->ld, (int32_t)c->nch, kRowsPerGroup,
+                                c->part, c->stamps + h + 1, c->stream));
+    HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, n_div(c), c->ld, (int32_t)c->nch, c->xbar[xb ^ 1],
+                              nullptr, 0.0, 0, c->stream, c->S));
+    if (met) {
+      if ((rc = history(c, h - 1, c->xbar[xb], want_cons, want_obj, c->n))) return rc;
+    } else if (!fused_met && metrics) {
+      if ((rc = split_metrics(c, c->xs[c->cur ^ 1], c->xbar[xb ^ 1], false, want_cons, want_obj))) return rc;
+      if ((rc = history(c, h, c->xbar[xb ^ 1], want_cons, want_obj, c->n))) return rc;
+    }
+    c->cur ^= 1;
+    xb ^= 1;
+  }
+  if (fused_met && metrics && T > 0) {
+    if ((rc = split_metrics(c, c->xs[c->cur], c->xbar[xb], false, want_cons, want_obj))) return rc;
+    if ((rc = history(c, T - 1, c->xbar[xb], want_cons, want_obj, c->n))) return rc;
+  }
+  return finish_run(c, T, T, lam_obj, f_opt, want_obj ? obj_out : nullptr, want_cons ? cons_out : nullptr,
+                    time_out);
+}
+
+// Centralized rounds, column-blocked: dots at the shared iterate -> coefficients ->
+// per-worker gradients -> deterministic mean -> step (trainer.py:41-71).
+int run_centralized_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch, const int32_t* idx,
+                          double lam_grad, double lam_obj, double f_opt, bool want_obj, double* obj_out,
+                          double* time_out) {
+  int rc;
+  if (std::min(batch, c->max_m) > kSplitMaxRows)
+    return fail(DOPT_ERR_UNSUPPORTED, "d = %lld with more than %d rows per minibatch", (long long)c->d,
+                kSplitMaxRows);
+  if ((rc = ensure_split(c))) return rc;
+  if (!c->G && (rc = dalloc(&c->G, (size_t)c->n * c->ld * c->esz))) return rc;
+  const int64_t CH = idx ? idx_chunk_rounds(c, T, batch) : 1;
+  HIPOK(launch_stamp(c->stamps, c->stream));
+  for (int64_t h = 0; h < T; ++h) {
+    const int64_t t = t0 + h;
+    RoundArgs a = base_args(c);
+    if (idx) {
+      if (h % CH == 0 && (rc = upload_idx_chunk(c, idx, h, std::min(CH, T - h), batch))) return rc;
+      a.idx = c->idx + (h % CH) * c->n * batch;
+      a.b = batch;
+    }
+    a.w_shared = c->xg[c->gcur];
+    a.g_out = c->G;
+    a.lam = lam_grad;
+    a.flags = F_SHARED | F_GOUT;  // no mixing here
+    HIPOK(launch_split_dots(c->dtype, 0, a, (int)c->n, c->stream));
+    HIPOK(launch_split_coef(c->dtype, c->problem, 1, a, (int)c->n, c->stream));
+    if (c->prof && (rc = prof_event(c, false))) return rc;
+    HIPOK(launch_split_step(c->dtype, false, false, a, (int)c->n, c->stream));
+    if (c->prof && (rc = prof_event(c, true))) return rc;
+    HIPOK(launch_colsum_partial(c->dtype, c->G, c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part,
+                                c->stamps + h + 1, c->stream));
+    HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nch, c->xg[c->gcur ^ 1],
+                              c->xg[c->gcur], eta0 / sqrt((double)(t + 1)), 1, c->stream));
+    if (want_obj) {
+      if ((rc = split_metrics(c, nullptr, c->xg[c->gcur ^ 1], true, false, true))) return rc;
+      if ((rc = history(c, h, c->xg[c->gcur ^ 1], false, true, c->n))) return rc;
+    }
+    c->gcur ^= 1;
+  }
+  return finish_run(c, T, T, lam_obj, f_opt, want_obj ? obj_out : nullptr, nullptr, time_out);
+}
+
 int check_run(dopt_ctx* c, int64_t T, int64_t batch, const int32_t* idx, bool need_topo) {
   if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
   if (need_topo && !c->have_topo) return fail(DOPT_ERR_STATE, "no topology set");
@@ -389,10 +585,6 @@ int check_run(dopt_ctx* c, int64_t T, int64_t batch, const int32_t* idx, bool ne
   return DOPT_OK;
 }
 
-int64_t idx_chunk_rounds(dopt_ctx* c, int64_t T, int64_t b) {
-  const int64_t per = std::max<int64_t>(1, c->n * b * (int64_t)sizeof(int32_t));
-  return std::max<int64_t>(1, std::min<int64_t>(T, (int64_t)(256ll << 20) / per));
-}
 
 }  // namespace
 
@@ -442,7 +634,7 @@ int dopt_destroy(dopt_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
   for (void** p : {&c->X, &c->y, &c->Xo, &c->yo, &c->xs[0], &c->xs[1], &c->xg[0], &c->xg[1], &c->G,
-                   &c->xbar[0], &c->xbar[1], &c->cw, &c->staging, &c->sx})
+                   &c->xbar[0], &c->xbar[1], &c->cw, &c->staging, &c->sx, &c->wdiag, &c->coef})
     dfree(*p);
   dfree_t(c->off);
   dfree_t(c->offo);
@@ -453,6 +645,10 @@ int dopt_destroy(dopt_ctx* c) {
   dfree_t(c->ci);
   dfree_t(c->idx);
   dfree_t(c->hraw);
+  dfree_t(c->S);
+  dfree_t(c->zpart);
+  dfree_t(c->upart);
+  dfree_t(c->cpart);
   dfree_t(c->send_ids);
   dfree_t(c->stamps);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
@@ -591,6 +787,26 @@ int dopt_set_topology(dopt_ctx* c, int64_t n_workers, const int64_t* row_ptr, co
     }
   }
   c->have_topo = true;
+  c->mean_mix = false;
+  return DOPT_OK;
+}
+
+int dopt_set_mixing_mean(dopt_ctx* c, int64_t n_workers, double w_off, const double* w_diag) {
+  CHECK_ARG(c && w_diag, "NULL argument");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");
+  CHECK_ARG(n_workers == c->n, "mixing has %lld workers, data has %lld", (long long)n_workers, (long long)c->n);
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  if ((rc = dalloc(&c->wdiag, (size_t)n_workers * c->esz))) return rc;
+  if (c->dtype == DOPT_F64) {
+    HIPOK(hipMemcpy(c->wdiag, w_diag, (size_t)n_workers * sizeof(double), hipMemcpyHostToDevice));
+  } else {
+    std::vector<float> wf(w_diag, w_diag + n_workers);
+    HIPOK(hipMemcpy(c->wdiag, wf.data(), (size_t)n_workers * sizeof(float), hipMemcpyHostToDevice));
+  }
+  c->w_off = w_off;
+  c->mean_mix = true;
+  c->have_topo = true;
   return DOPT_OK;
 }
 
@@ -639,6 +855,9 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
   const bool fused = batch >= c->max_m && !c->obj_sep;
   const int64_t CH = idx ? idx_chunk_rounds(c, T, batch) : 1;
   int& xb = c->xb;
+  if (c->split) return run_dsgd_split(c, t0, T, eta0, batch, idx, lam_grad, lam_obj, f_opt, flags, obj_out,
+                                      cons_out, time_out);
+  if ((rc = colsum_current(c))) return rc;  // xbar and S of the starting iterates
   HIPOK(launch_stamp(c->stamps, c->stream));
 
   for (int64_t h = 0; h < T; ++h) {
@@ -655,7 +874,7 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
     a.eta = eta0 / sqrt((double)(t + 1));  // trainer.py:138-140
     a.lam = lam_grad;
     const bool met = fused && metrics && h > 0;
-    a.flags = F_STEP | (met && want_cons ? F_CONS : 0) | (met && want_obj ? F_LOSS : 0);
+    a.flags |= F_STEP | (met && want_cons ? F_CONS : 0) | (met && want_obj ? F_LOSS : 0);
     if (c->prof && (rc = prof_event(c, false))) return rc;
     HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, met, a, (int)c->n, c->stream));
     if (c->prof && (rc = prof_event(c, true))) return rc;
@@ -663,7 +882,7 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
     HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur ^ 1], c->n, c->ld, (int32_t)c->nch, kRowsPerGroup,
                                 c->part, c->stamps + h + 1, c->stream));
     HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, n_div(c), c->ld, (int32_t)c->nch, c->xbar[xb ^ 1],
-                              nullptr, 0.0, 0, c->stream));
+                              nullptr, 0.0, 0, c->stream, c->S));
     if (met) {
       if ((rc = history(c, h - 1, c->xbar[xb], want_cons, want_obj, c->n))) return rc;
     } else if (!fused && metrics) {
@@ -691,6 +910,8 @@ int dopt_run_centralized(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_
   if ((rc = ensure_hist(c, T))) return rc;
   if (!c->G && (rc = dalloc(&c->G, (size_t)c->n * c->ld * c->esz))) return rc;
   const bool want_obj = flags & DOPT_RUN_OBJECTIVE;
+  if (c->split) return run_centralized_split(c, t0, T, eta0, batch, idx, lam_grad, lam_obj, f_opt, want_obj,
+                                             obj_out, time_out);
   const bool fused = batch >= c->max_m && !c->obj_sep;
   const int64_t CH = idx ? idx_chunk_rounds(c, T, batch) : 1;
   HIPOK(launch_stamp(c->stamps, c->stream));
@@ -707,7 +928,7 @@ int dopt_run_centralized(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_
     a.g_out = c->G;
     a.lam = lam_grad;
     const bool met = fused && want_obj && h > 0;
-    a.flags = F_GOUT | F_SHARED | (met ? (F_LOSS | F_LOSS_FROM_Z) : 0);
+    a.flags |= F_GOUT | F_SHARED | (met ? (F_LOSS | F_LOSS_FROM_Z) : 0);
     if (c->prof && (rc = prof_event(c, false))) return rc;
     HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, met, a, (int)c->n, c->stream));
     if (c->prof && (rc = prof_event(c, true))) return rc;
@@ -907,7 +1128,7 @@ int dopt_phase_grad(dopt_ctx* c, int64_t batch, const int32_t* idx, double lam_g
   a.g_out = c->G;
   a.xbar = c->xbar[c->xb];
   a.lam = lam_grad;
-  a.flags = F_GOUT | (cons ? F_CONS : 0) | (loss ? F_LOSS : 0);
+  a.flags |= F_GOUT | (cons ? F_CONS : 0) | (loss ? F_LOSS : 0);
   if (c->prof && (rc = prof_event(c, false))) return rc;
   HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, cons || loss, a, (int)c->n, c->stream));
   if (c->prof && (rc = prof_event(c, true))) return rc;
@@ -940,6 +1161,7 @@ int dopt_phase_xbar(dopt_ctx* c, const double* sum_dev) {
   HIPOK(launch_colsum_final(c->dtype, sum_dev, 1, n_div(c), c->ld, (int32_t)c->nch, c->xbar[c->xb ^ 1], nullptr,
                             0.0, 0, c->stream));
   c->xb ^= 1;
+  c->S_ext = sum_dev;  // the complete-graph mix of the next round uses the global sums
   return DOPT_OK;
 }
 

@@ -88,7 +88,9 @@ def build_plan(topo, world, rank):
 class DistributedDSGD:
     """Drives one rank's engine through the round phases with torch.distributed."""
 
-    def __init__(self, engine, plan, n_global, rows_global, device=0, group=None):
+    def __init__(self, engine, plan, n_global, rows_global, device=0, group=None, mean=None):
+        """`mean` = (w_off, W_ii of the local workers) for the complete graph: the mix then
+        uses the all-reduced column sums and no halo rows move at all."""
         import torch
         import torch.distributed as dist
 
@@ -105,10 +107,15 @@ class DistributedDSGD:
         self.send = torch.zeros((max(1, len(plan.send_ids)), ld), dtype=tdt, device=self.dev)
         self.sum = torch.zeros(ld, dtype=torch.float64, device=self.dev)
         engine.set_partition(self.n_global, self.rows_global)
-        engine.set_halo(plan.n_halo, self.halo.data_ptr(), plan.send_ids, self.send.data_ptr())
-        engine.set_topology(plan.row_ptr, plan.col, plan.w)
+        if mean is None:
+            engine.set_halo(plan.n_halo, self.halo.data_ptr(), plan.send_ids, self.send.data_ptr())
+            engine.set_topology(plan.row_ptr, plan.col, plan.w)
+            self._peers = plan.peers()
+        else:
+            engine.set_halo(0, None, np.zeros(0, np.int32), None)
+            engine.set_mixing_mean(mean[0], mean[1])
+            self._peers = []
         engine.set_stream(self.stream.cuda_stream)
-        self._peers = plan.peers()
 
     # -- transport
     def _start_exchange(self):
@@ -162,8 +169,13 @@ class DistributedDSGD:
         xnorm = self.plan.rank == 0  # ||xbar||^2 is global already: count it once
         with torch.cuda.stream(self.stream):
             partials = torch.zeros((max(1, T), 3), dtype=torch.float64, device=self.dev)
+            # prologue: global column sums / xbar of the starting iterates (complete-graph mix, metrics)
+            eng.phase_colsum(self.sum.data_ptr())
+            self._all_reduce(self.sum)
+            eng.phase_xbar(self.sum.data_ptr())
             for h in range(T):
-                eng.phase_gather()
+                if self._peers:
+                    eng.phase_gather()
                 pending = self._start_exchange()
                 eng.phase_grad(batch, lam_grad, flags if h > 0 else 0)
                 if h > 0 and flags:

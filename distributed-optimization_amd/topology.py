@@ -57,6 +57,18 @@ class Topology:
 
         return csr_matrix((self.w, self.col, self.row_ptr), shape=(self.n, self.n))
 
+    def uniform_offdiag(self):
+        """(w_off, diag) when every off-diagonal weight is present and equal (the
+        complete graph), else None: then sum_j W_ij x_j = w_off (S - x_i) + W_ii x_i."""
+        n = self.n
+        if n < 2 or self.nnz != n * n:
+            return None
+        diag_mask = self.col == np.repeat(np.arange(n), n)
+        off = self.w[~diag_mask]
+        if not np.all(off == off[0]):
+            return None
+        return float(off[0]), self.w[diag_mask].copy()
+
     def check(self):
         """trainer.py:129-131 on the CSR form: rows sum to 1 and W is symmetric."""
         if self.n == 0:

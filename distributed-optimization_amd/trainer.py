@@ -29,6 +29,7 @@ import topology as _topology
 from obj_problems import logistic_objective, quadratic_objective
 
 DENSE_LIMIT = 4096          # dense adj / W attributes up to this many workers
+MEAN_MIX_MIN = 128          # complete graphs from this size mix through the column sums
 IDX_CHUNK_ELEMS = 1 << 24   # host index buffer per device call (64 MiB of int32)
 
 
@@ -236,7 +237,11 @@ class DecentralizedTrainer:
         eng = _engine(self.workers, self.n_features, cfg)
         want_obj = _set_objective_data(eng, self.workers, self.n_features, X_full, y_full)
         t = self._topo
-        eng.set_topology(t.row_ptr, t.col, t.w)
+        uni = t.uniform_offdiag() if self.n_workers >= cfg.get("mean_mixing_min", MEAN_MIX_MIN) else None
+        if uni is not None:  # complete graph: w_off (S - x_i) + W_ii x_i, no N^2 neighbour reads
+            eng.set_mixing_mean(*uni)
+        else:
+            eng.set_topology(t.row_ptr, t.col, t.w)
         eng.set_models(np.stack([np.asarray(w.x, dtype=np.float64) for w in self.workers]))
         iteration_transmission = np.sum(self.degrees) * self.n_features  # trainer.py:169
         for t0, n, b, idx in _index_chunks(self.workers, int(n_iterations), cfg):

@@ -116,6 +116,12 @@ int dopt_get_shard(dopt_ctx *ctx, int64_t worker, double *X_out, double *y_out);
 int dopt_set_topology(dopt_ctx *ctx, int64_t n_workers, const int64_t *row_ptr,
                       const int32_t *col, const double *w);
 
+/* Complete graph (topology 'fully_connected', trainer.py:109-110) without the N^2
+ * CSR: every off-diagonal weight equals w_off (MH: 1/N), so
+ * sum_j W_ij x_j = w_off * (S - x_i) + W_ii x_i with S the column sums of the
+ * iterates -- one all-reduce instead of N neighbour rows.  w_diag[N] = W_ii. */
+int dopt_set_mixing_mean(dopt_ctx *ctx, int64_t n_workers, double w_off, const double *w_diag);
+
 /* Worker iterates (Worker.x, worker.py:13; trainer.py:162-163, :178-179). */
 int dopt_set_models(dopt_ctx *ctx, const double *x);
 int dopt_get_models(dopt_ctx *ctx, double *x);

@@ -20,7 +20,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, dtype, out):
+def _rank_main(rank, world, port, dtype, out, mean=False):
     import torch  # noqa: F401  (one HIP runtime, loaded before libdopt)
     import torch.distributed as dist
 
@@ -30,11 +30,13 @@ def _rank_main(rank, world, port, dtype, out):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    top = TP.random_regular(N, 4, seed=2)
+    top = TP.fully_connected(N) if mean else TP.random_regular(N, 4, seed=2)
     plan = Dm.build_plan(top, world, rank)
     eng = _dopt.Engine(0, dtype)
     eng.generate_shards("logistic", plan.n_local, D, M, seed=9, first_worker=plan.lo)
-    run = Dm.DistributedDSGD(eng, plan, N, N * M, device=0)
+    uni = top.uniform_offdiag() if mean else None
+    run = Dm.DistributedDSGD(eng, plan, N, N * M, device=0,
+                             mean=None if uni is None else (uni[0], uni[1][plan.lo:plan.hi]))
     obj, cons = run.run(T, 0.05, M, 1e-3, 1e-3, 0.25)
     x = run.gather_models()
     if rank == 0:
@@ -44,23 +46,29 @@ def _rank_main(rank, world, port, dtype, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dtype", ["float64", "float32"])
-def test_two_ranks_match_single_context(tmp_path, dtype):
+@pytest.mark.parametrize("dtype,mean", [("float64", False), ("float32", False), ("float64", True)])
+def test_two_ranks_match_single_context(tmp_path, dtype, mean):
     import torch.multiprocessing as mp
 
     import _dopt
     import topology as TP
 
-    mp.start_processes(_rank_main, args=(2, _free_port(), dtype, str(tmp_path)), nprocs=2, join=True,
+    mp.start_processes(_rank_main, args=(2, _free_port(), dtype, str(tmp_path), mean), nprocs=2, join=True,
                        start_method="spawn")
     got = np.load(tmp_path / "dist.npz")
     eng = _dopt.Engine(0, dtype)
     eng.generate_shards("logistic", N, D, M, seed=9)
-    top = TP.random_regular(N, 4, seed=2)
-    eng.set_topology(top.row_ptr, top.col, top.w)
+    if mean:
+        eng.set_mixing_mean(*TP.fully_connected(N).uniform_offdiag())
+    else:
+        top = TP.random_regular(N, 4, seed=2)
+        eng.set_topology(top.row_ptr, top.col, top.w)
     obj, cons, _ = eng.run_dsgd(T, 0.05, M, 1e-3, 1e-3, 0.25)
     x = eng.get_models()
     eng.close()
-    np.testing.assert_array_equal(got["x"], x)
+    if mean:  # the column sums are reduced per rank then across ranks: last-bit differences
+        np.testing.assert_allclose(got["x"], x, rtol=1e-12, atol=1e-15)
+    else:
+        np.testing.assert_array_equal(got["x"], x)
     np.testing.assert_allclose(got["obj"], obj, rtol=1e-12 if dtype == "float64" else 1e-6)
     np.testing.assert_allclose(got["cons"], cons, rtol=1e-12 if dtype == "float64" else 1e-5)

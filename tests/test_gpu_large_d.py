@@ -1,0 +1,105 @@
+"""Column-blocked rounds (d beyond the row-resident kernel: config C5, d = 2^20) and
+complete-graph mean mixing, against the oracle (float64, rtol 1e-9) and against
+host recomputation at full C5 row length."""
+import numpy as np
+import pytest
+
+import _dopt
+import dsgd_oracle as O
+import topology as TP
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(n, d, m, seed, problem):
+    rng = np.random.default_rng(seed)
+    shards = []
+    for _ in range(n):
+        X = np.hstack([rng.standard_normal((m, d - 1)), np.ones((m, 1))])
+        y = rng.choice([-1.0, 1.0], m) if problem == "logistic" else rng.standard_normal(m) * 3
+        shards.append((X, y))
+    return shards
+
+
+def _engine(shards, problem, dtype="float64"):
+    eng = _dopt.Engine(0, dtype)
+    off = np.concatenate([[0], np.cumsum([len(s[1]) for s in shards])])
+    eng.load_shards(problem, np.vstack([s[0] for s in shards]), np.concatenate([s[1] for s in shards]), off)
+    return eng
+
+
+@pytest.mark.parametrize("problem,topo,batch,mean", [
+    ("logistic", "ring", 12, False),        # full shard: next-round dots fused into the step
+    ("logistic", "ring", 5, False),         # minibatches: separate dots pass per round
+    ("quadratic", "fully_connected", 12, True),   # complete graph through column sums
+    ("quadratic", "grid", 4, False),
+])
+def test_split_rounds_vs_oracle(problem, topo, batch, mean):
+    n, d, m, T = 9, 2100, 12, 6  # d = 2100 fp64 -> 1050 chunks > 1024: column-blocked path
+    shards = _data(n, d, m, 1, problem)
+    cfg = {"problem_type": problem, "local_batch_size": batch, "learning_rate_eta0": 0.05,
+           "l2_regularization_lambda": 1e-3, "strong_convexity_mu": 2e-3}
+    top = TP.build(topo, n)
+    eng = _engine(shards, problem)
+    if mean:
+        eng.set_mixing_mean(*top.uniform_offdiag())
+    else:
+        eng.set_topology(top.row_ptr, top.col, top.w)
+    np.random.seed(4)
+    st = np.random.get_state()
+    idx = None if batch >= m else _dopt.mt_choice_rounds(T, [m] * n, batch)
+    lam_g = cfg["l2_regularization_lambda"] if problem == "logistic" else cfg["strong_convexity_mu"]
+    Xf = np.vstack([s[0] for s in shards])
+    yf = np.concatenate([s[1] for s in shards])
+    obj, cons, _ = eng.run_dsgd(T, 0.05, batch, lam_g, 1e-3, 0.1, idx=idx)
+    x = eng.get_models()
+    h, _, xr, _ = O.run_decentralized(shards, top.dense_W(), T, dict(cfg, l2_regularization_lambda=1e-3), Xf, yf,
+                                      0.1, rng_state=st)
+    np.testing.assert_allclose(x, xr, rtol=1e-9, atol=1e-13)
+    np.testing.assert_allclose(obj, h["objective"], rtol=1e-9)
+    np.testing.assert_allclose(cons, h["consensus_error"], rtol=1e-9)
+    eng.close()
+
+
+def test_split_centralized_vs_oracle():
+    n, d, m, T, b = 5, 2100, 10, 4, 3
+    shards = _data(n, d, m, 2, "logistic")
+    cfg = {"problem_type": "logistic", "local_batch_size": b, "learning_rate_eta0": 0.05,
+           "l2_regularization_lambda": 1e-3, "strong_convexity_mu": 1e-3}
+    eng = _engine(shards, "logistic")
+    np.random.seed(8)
+    st = np.random.get_state()
+    idx = _dopt.mt_choice_rounds(T, [m] * n, b)
+    Xf = np.vstack([s[0] for s in shards])
+    yf = np.concatenate([s[1] for s in shards])
+    obj, _ = eng.run_centralized(T, 0.05, b, 1e-3, 1e-3, 0.0, idx=idx)
+    h, xg, _ = O.run_centralized(shards, T, cfg, Xf, yf, 0.0, rng_state=st)
+    np.testing.assert_allclose(obj, h["objective"], rtol=1e-9)
+    np.testing.assert_allclose(eng.get_global(), xg, rtol=1e-9, atol=1e-13)
+    eng.close()
+
+
+def test_c5_shape_round_spot_check():
+    """C5 row length: quadratic, d = 2^20, m = b = 16, complete graph via column sums,
+    fp32; 128 workers (8 GiB) on one GPU.  Two workers recomputed on the host."""
+    n, d, m = 128, 1 << 20, 16
+    eng = _dopt.Engine(0, "float32")
+    eng.generate_shards("quadratic", n, d, m, seed=3, noise=10.0)
+    top = TP.fully_connected(n)
+    eng.set_mixing_mean(*top.uniform_offdiag())
+    rng = np.random.default_rng(1)
+    x0 = (rng.standard_normal((n, d)) * 1e-3).astype(np.float32).astype(np.float64)
+    eng.set_models(x0)
+    obj, cons, _ = eng.run_dsgd(1, 0.05, m, 1e-4, 1e-4, 0.0)
+    x1 = eng.get_models()
+    S = x0.sum(axis=0)
+    w_off, diag = top.uniform_offdiag()
+    for i in (0, 77):
+        X, y = eng.get_shard(i)
+        g = O.quadratic_gradient(x0[i], X, y, 1e-4)
+        mix = w_off * (S - x0[i]) + diag[i] * x0[i]
+        np.testing.assert_allclose(x1[i], mix - 0.05 * g, rtol=1e-3, atol=1e-5)
+    xbar = x1.mean(axis=0)
+    np.testing.assert_allclose(cons[0], np.mean(np.sum((x1 - xbar) ** 2, axis=1)), rtol=1e-3)
+    assert np.isfinite(obj[0])
+    eng.close()

@@ -1,0 +1,100 @@
+// bw_probe.hip -- HBM read-bandwidth ceiling on this MI355X for the access shape the
+// D-SGD round uses (whole 4 KiB rows, 16-byte lanes, one workgroup per 2 MiB shard).
+// Build: hipcc --offload-arch=gfx950 -O3 -o bw_probe bw_probe.hip
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+template <int RB, bool NT>
+__global__ __launch_bounds__(256) void k_shard_read(const f4* __restrict__ x, int rows_per_wg, float* out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const f4* base = x + (size_t)blockIdx.x * rows_per_wg * 256;
+  f4 acc = f4(0);
+  for (int r0 = wave * RB; r0 < rows_per_wg; r0 += 4 * RB) {
+    f4 v[RB][4];
+#pragma unroll
+    for (int k = 0; k < RB; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f4* p = base + (size_t)(r0 + k) * 256 + lane + 64 * j;
+        v[k][j] = NT ? __builtin_nontemporal_load(p) : *p;
+      }
+#pragma unroll
+    for (int k = 0; k < RB; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc += v[k][j];
+  }
+  if (acc.x == 1234.5f) out[0] = acc.y + acc.z + acc.w;
+}
+
+__global__ __launch_bounds__(256) void k_grid_read(const f4* __restrict__ x, size_t n, float* out) {
+  f4 acc = f4(0);
+  const size_t stride = (size_t)gridDim.x * 256;
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    f4 a = x[i], b = x[i + stride], c = x[i + 2 * stride], d = x[i + 3 * stride];
+    acc += a + b + c + d;
+  }
+  for (; i < n; i += stride) acc += x[i];
+  if (acc.x == 1234.5f) out[0] = acc.y;
+}
+
+__global__ __launch_bounds__(256) void k_copy(const f4* __restrict__ x, f4* __restrict__ y, size_t n) {
+  const size_t stride = (size_t)gridDim.x * 256;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) y[i] = x[i];
+}
+
+#define CK(e) do { hipError_t r = (e); if (r != hipSuccess) { printf("HIP %s\n", hipGetErrorString(r)); exit(1); } } while (0)
+
+template <typename F>
+double timeit(F f, int reps) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  f();
+  CK(hipDeviceSynchronize());
+  float best = 1e30f;
+  for (int r = 0; r < reps; ++r) {
+    CK(hipEventRecord(a));
+    f();
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    if (ms < best) best = ms;
+  }
+  return best;
+}
+
+int main() {
+  const size_t bytes = 8ull << 30;  // 8 GiB = 4096 workers x 512 rows x 4 KiB
+  const size_t n4 = bytes / 16;
+  f4 *x, *y;
+  float* out;
+  CK(hipMalloc(&x, bytes));
+  CK(hipMalloc(&y, bytes / 4));
+  CK(hipMalloc(&out, 64));
+  CK(hipMemset(x, 0, bytes));
+  const int wg = 4096, rpw = 512;
+  auto gbs = [&](double ms, size_t b) { return b / (ms * 1e-3) / 1e9; };
+  double ms;
+  ms = timeit([&] { hipLaunchKernelGGL((k_shard_read<2, false>), dim3(wg), dim3(256), 0, 0, x, rpw, out); }, 5);
+  printf("shard_read RB=2        %.3f ms  %.0f GB/s\n", ms, gbs(ms, bytes));
+  ms = timeit([&] { hipLaunchKernelGGL((k_shard_read<2, true>), dim3(wg), dim3(256), 0, 0, x, rpw, out); }, 5);
+  printf("shard_read RB=2 nt     %.3f ms  %.0f GB/s\n", ms, gbs(ms, bytes));
+  ms = timeit([&] { hipLaunchKernelGGL((k_shard_read<4, false>), dim3(wg), dim3(256), 0, 0, x, rpw, out); }, 5);
+  printf("shard_read RB=4        %.3f ms  %.0f GB/s\n", ms, gbs(ms, bytes));
+  ms = timeit([&] { hipLaunchKernelGGL((k_shard_read<1, false>), dim3(wg), dim3(256), 0, 0, x, rpw, out); }, 5);
+  printf("shard_read RB=1        %.3f ms  %.0f GB/s\n", ms, gbs(ms, bytes));
+  // finer shards: same bytes, 8192 workgroups of 256 rows
+  ms = timeit([&] { hipLaunchKernelGGL((k_shard_read<2, false>), dim3(wg * 2), dim3(256), 0, 0, x, rpw / 2, out); }, 5);
+  printf("shard_read RB=2 x2 WGs %.3f ms  %.0f GB/s\n", ms, gbs(ms, bytes));
+  for (int g : {1024, 2048, 4096, 8192}) {
+    ms = timeit([&] { hipLaunchKernelGGL(k_grid_read, dim3(g), dim3(256), 0, 0, x, n4, out); }, 5);
+    printf("grid_read %5d WGs     %.3f ms  %.0f GB/s\n", g, ms, gbs(ms, bytes));
+  }
+  ms = timeit([&] { hipLaunchKernelGGL(k_copy, dim3(8192), dim3(256), 0, 0, x, y, n4 / 4); }, 5);
+  printf("copy 2 GiB             %.3f ms  %.0f GB/s (read+write)\n", ms, gbs(ms, bytes / 2));
+  return 0;
+}
