@@ -62,7 +62,13 @@ _SIGS = {
     "dopt_get_layout": ([_P, _P, _P], ctypes.c_int),
     "dopt_set_partition": ([_P, _I64, _I64], ctypes.c_int),
     "dopt_set_halo": ([_P, _I64, _P, _I64, _P, _P], ctypes.c_int),
+    "dopt_phase_begin": ([_P, _I64], ctypes.c_int),
     "dopt_phase_gather": ([_P], ctypes.c_int),
+    "dopt_phase_grad_shared": ([_P, _I64, _P, _D, ctypes.c_int], ctypes.c_int),
+    "dopt_phase_colsum_grad": ([_P, _P], ctypes.c_int),
+    "dopt_phase_central_step": ([_P, _P, _I64, _D], ctypes.c_int),
+    "dopt_phase_metrics_pass_shared": ([_P], ctypes.c_int),
+    "dopt_phase_metrics_shared": ([_P, ctypes.c_int, _P], ctypes.c_int),
     "dopt_phase_grad": ([_P, _I64, _P, _D, ctypes.c_uint32], ctypes.c_int),
     "dopt_phase_mix": ([_P, _I64, _D], ctypes.c_int),
     "dopt_phase_colsum": ([_P, _P], ctypes.c_int),
@@ -313,6 +319,26 @@ class Engine:
         ids = np.ascontiguousarray(send_ids, dtype=np.int32)
         check(lib().dopt_set_halo(self._h, int(n_halo), ctypes.c_void_p(halo_ptr) if halo_ptr else None, len(ids),
                                   ctypes.c_void_p(send_ptr) if send_ptr else None, _ptr(ids)))
+
+    def phase_begin(self, batch):
+        check(lib().dopt_phase_begin(self._h, int(batch)))
+
+    def phase_grad_shared(self, batch, lam_grad, fuse_loss=False, idx=None):
+        if idx is not None:
+            idx = np.ascontiguousarray(idx, dtype=np.int32)
+        check(lib().dopt_phase_grad_shared(self._h, int(batch), _ptr(idx), float(lam_grad), 1 if fuse_loss else 0))
+
+    def phase_colsum_grad(self, sum_ptr):
+        check(lib().dopt_phase_colsum_grad(self._h, ctypes.c_void_p(sum_ptr)))
+
+    def phase_central_step(self, sum_ptr, t, eta0):
+        check(lib().dopt_phase_central_step(self._h, ctypes.c_void_p(sum_ptr), int(t), float(eta0)))
+
+    def phase_metrics_pass_shared(self):
+        check(lib().dopt_phase_metrics_pass_shared(self._h))
+
+    def phase_metrics_shared(self, include_xnorm, out_ptr):
+        check(lib().dopt_phase_metrics_shared(self._h, 1 if include_xnorm else 0, ctypes.c_void_p(out_ptr)))
 
     def phase_gather(self):
         check(lib().dopt_phase_gather(self._h))

@@ -27,6 +27,9 @@
 // No atomics anywhere: every reduction has a fixed order, so runs are bitwise
 // reproducible.
 #include <math.h>
+#include <stdlib.h>
+
+#include <type_traits>
 
 #include "engine.h"
 
@@ -54,6 +57,41 @@ __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+
+// Wave-wide sum by DPP: quad swaps, row_shr 4/8, row_bcast 15/31 (GFX9-family DPP), then
+// one v_readlane of lane 63 -- the result lands in an SGPR (the coefficient is wave-uniform).
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, RM, BM, false);
+}
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ float dpp_add(float v) {
+  return v + __builtin_bit_cast(float, dpp_i<CTRL, RM, BM>(__builtin_bit_cast(int, v)));
+}
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ double dpp_add(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = dpp_i<CTRL, RM, BM>((int)(b & 0xffffffffll));
+  const int hi = dpp_i<CTRL, RM, BM>((int)(b >> 32));
+  return v + __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+template <typename T>
+__device__ __forceinline__ T wave_sum_dpp(T v) {
+  v = dpp_add<0xb1, 0xf, 0xf>(v);   // quad_perm [1,0,3,2]
+  v = dpp_add<0x4e, 0xf, 0xf>(v);   // quad_perm [2,3,0,1]
+  v = dpp_add<0x114, 0xf, 0xe>(v);  // row_shr:4
+  v = dpp_add<0x118, 0xf, 0xc>(v);  // row_shr:8
+  v = dpp_add<0x142, 0xa, 0xf>(v);  // row_bcast:15
+  v = dpp_add<0x143, 0xc, 0xf>(v);  // row_bcast:31  -> lane 63 holds the sum
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+  } else {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), 63);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __builtin_bit_cast(T, ((long long)hi << 32) | (unsigned int)lo);
+  }
 }
 
 template <typename T, typename V>
@@ -112,11 +150,13 @@ __device__ __forceinline__ typename VT<T>::v mix_chunk(const RoundArgs& a, int i
 }
 
 // ---------------------------------------------------------------------------- k_round
-template <typename T, int CPL, int PROB, bool GRAD, bool MET>
+// VAR (tuning variants, C3 instantiation only; 0 = default): bit 0 nontemporal row loads,
+// bit 1 DPP wave reduction, bit 2 twice the rows in flight.
+template <typename T, int CPL, int PROB, bool GRAD, bool MET, int VAR = 0>
 __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
   using V = typename VT<T>::v;
   constexpr int VN = VT<T>::n;
-  constexpr int RB = CPL >= 8 ? 1 : 8 / CPL;  // rows in flight per wave
+  constexpr int RB = (CPL >= 8 ? 1 : 8 / CPL) * ((VAR & 4) ? 2 : 1);  // rows in flight per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int lane = threadIdx.x & 63;
@@ -166,7 +206,10 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
 #pragma unroll
         for (int j = 0; j < CPL; ++j) {
           const int c = lane + 64 * j;
-          xr[k][j] = (ok && c < nch) ? *(const V*)(xp + (int64_t)c * VN) : V(0);
+          if (VAR & 1)
+            xr[k][j] = (ok && c < nch) ? __builtin_nontemporal_load((const V*)(xp + (int64_t)c * VN)) : V(0);
+          else
+            xr[k][j] = (ok && c < nch) ? *(const V*)(xp + (int64_t)c * VN) : V(0);
         }
       }
       T z[RB], u[RB];
@@ -183,8 +226,8 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
       }
 #pragma unroll
       for (int k = 0; k < RB; ++k) {
-        if (compute_z) z[k] = wave_sum(z[k]);
-        if (compute_u) u[k] = wave_sum(u[k]);
+        if (compute_z) z[k] = (VAR & 2) ? wave_sum_dpp(z[k]) : wave_sum(z[k]);
+        if (compute_u) u[k] = (VAR & 2) ? wave_sum_dpp(u[k]) : wave_sum(u[k]);
       }
 #pragma unroll
       for (int k = 0; k < RB; ++k) {
@@ -256,23 +299,48 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
   }
 }
 
-template <typename T, int CPL, int PROB, bool GRAD, bool MET>
+template <typename T, int CPL, int PROB, bool GRAD, bool MET, int VAR = 0>
 static hipError_t launch_round_t(const RoundArgs& a, int groups, hipStream_t s) {
   const size_t lds = (GRAD ? (size_t)NW * a.nchunks * 16 : 0) + 2 * NW * sizeof(double);
   static bool attr_set = false;
   if (!attr_set) {
     const size_t max_lds = (size_t)NW * MAX_CPL * 64 * 16 + 2 * NW * sizeof(double);
-    hipError_t e = hipFuncSetAttribute((const void*)k_round<T, CPL, PROB, GRAD, MET>,
+    hipError_t e = hipFuncSetAttribute((const void*)k_round<T, CPL, PROB, GRAD, MET, VAR>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((k_round<T, CPL, PROB, GRAD, MET>), dim3(groups), dim3(NT), lds, s, a);
+  hipLaunchKernelGGL((k_round<T, CPL, PROB, GRAD, MET, VAR>), dim3(groups), dim3(NT), lds, s, a);
   return hipGetLastError();
+}
+
+// Tuning variants of the C3 kernel (float, 4 chunks per lane, logistic), selected by
+// DOPT_KR_VARIANT for in-process A/B runs (tools/kr_variants.py).
+template <bool GRAD, bool MET>
+static hipError_t dispatch_variant(int var, const RoundArgs& a, int groups, hipStream_t s) {
+  switch (var) {
+    case 1: return launch_round_t<float, 4, 0, GRAD, MET, 1>(a, groups, s);
+    case 2: return launch_round_t<float, 4, 0, GRAD, MET, 2>(a, groups, s);
+    case 3: return launch_round_t<float, 4, 0, GRAD, MET, 3>(a, groups, s);
+    case 4: return launch_round_t<float, 4, 0, GRAD, MET, 4>(a, groups, s);
+    case 6: return launch_round_t<float, 4, 0, GRAD, MET, 6>(a, groups, s);
+    case 7: return launch_round_t<float, 4, 0, GRAD, MET, 7>(a, groups, s);
+    default: return launch_round_t<float, 4, 0, GRAD, MET, 0>(a, groups, s);
+  }
+}
+
+static int kr_variant() {
+  const char* v = getenv("DOPT_KR_VARIANT");
+  return v ? atoi(v) : 0;
 }
 
 template <typename T, int CPL, int PROB>
 static hipError_t dispatch_mode(bool grad, bool met, const RoundArgs& a, int groups, hipStream_t s) {
+  if constexpr (std::is_same<T, float>::value && CPL == 4 && PROB == 0) {
+    const int var = kr_variant();
+    if (var && grad && met) return dispatch_variant<true, true>(var, a, groups, s);
+    if (var && grad) return dispatch_variant<true, false>(var, a, groups, s);
+  }
   if (grad && met) return launch_round_t<T, CPL, PROB, true, true>(a, groups, s);
   if (grad) return launch_round_t<T, CPL, PROB, true, false>(a, groups, s);
   if (met) return launch_round_t<T, CPL, PROB, false, true>(a, groups, s);
@@ -670,19 +738,21 @@ hipError_t launch_colsum_final(int dtype, const double* part, int32_t groups, in
 }
 
 // ---------------------------------------------------------------------------- history
+constexpr int NTH = 1024;  // k_history: 16 waves, so each thread folds only a few slabs
 template <typename T>
-__global__ __launch_bounds__(NT) void k_history(const double* sc, const double* sl, int64_t n,
-                                                int64_t ng, const T* xbar, int64_t ld, int nch,
-                                                int xnorm, double* out) {
+__global__ __launch_bounds__(NTH) void k_history(const double* sc, const double* sl, int64_t n,
+                                                 int64_t ng, const T* xbar, int64_t ld, int nch,
+                                                 int xnorm, double* out) {
   constexpr int VN = VT<T>::n;
-  __shared__ double part[3][NW];
+  constexpr int NWH = NTH / 64;
+  __shared__ double part[3][NWH];
   double a = 0.0, b = 0.0, q = 0.0;
   if (sc)
-    for (int64_t k = threadIdx.x; k < n; k += NT) a += sc[k];
+    for (int64_t k = threadIdx.x; k < n; k += NTH) a += sc[k];
   if (sl)
-    for (int64_t k = threadIdx.x; k < ng; k += NT) b += sl[k];
+    for (int64_t k = threadIdx.x; k < ng; k += NTH) b += sl[k];
   if (xnorm)
-    for (int c = threadIdx.x; c < nch; c += NT)
+    for (int c = threadIdx.x; c < nch; c += NTH)
 #pragma unroll
       for (int e = 0; e < VN; ++e) {
         const double v = (double)xbar[(int64_t)c * VN + e];
@@ -700,7 +770,7 @@ __global__ __launch_bounds__(NT) void k_history(const double* sc, const double* 
   __syncthreads();
   if (threadIdx.x == 0) {
     double sa = 0.0, sb = 0.0, sq = 0.0;
-    for (int k = 0; k < NW; ++k) {
+    for (int k = 0; k < NWH; ++k) {
       sa += part[0][k];
       sb += part[1][k];
       sq += part[2][k];
@@ -715,10 +785,10 @@ hipError_t launch_history(int dtype, const double* slab_cons, const double* slab
                           int64_t ng, const void* xbar, int64_t ld, int32_t nchunks, bool xnorm,
                           double* out, hipStream_t s) {
   if (dtype == 0)
-    hipLaunchKernelGGL(k_history<float>, dim3(1), dim3(NT), 0, s, slab_cons, slab_loss, n, ng,
+    hipLaunchKernelGGL(k_history<float>, dim3(1), dim3(NTH), 0, s, slab_cons, slab_loss, n, ng,
                        (const float*)xbar, ld, nchunks, xnorm ? 1 : 0, out);
   else
-    hipLaunchKernelGGL(k_history<double>, dim3(1), dim3(NT), 0, s, slab_cons, slab_loss, n, ng,
+    hipLaunchKernelGGL(k_history<double>, dim3(1), dim3(NTH), 0, s, slab_cons, slab_loss, n, ng,
                        (const double*)xbar, ld, nchunks, xnorm ? 1 : 0, out);
   return hipGetLastError();
 }

@@ -116,6 +116,11 @@ struct dopt_ctx {
   double* cpart = nullptr;
   int64_t bcap = 0;
   size_t split_cap = 0;
+  // phase API bookkeeping (column-blocked mode defers the step to dopt_phase_mix)
+  int64_t ph_batch = 0;
+  double ph_lam = 0.0;
+  uint32_t ph_flags = 0;
+  bool ph_have_idx = false;
   double* part = nullptr;
   int groups = 0;
   double* slab_cons = nullptr;
@@ -1112,6 +1117,24 @@ int dopt_phase_gather(dopt_ctx* c) {
   return DOPT_OK;
 }
 
+int dopt_phase_begin(dopt_ctx* c, int64_t batch) {
+  CHECK_ARG(c, "ctx is NULL");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
+  int rc;
+  if (c->split) {
+    if ((rc = ensure_split(c))) return rc;
+    if (std::min(batch, c->max_m) > kSplitMaxRows)
+      return fail(DOPT_ERR_UNSUPPORTED, "column-blocked rounds hold at most %d rows per minibatch", kSplitMaxRows);
+    if (batch >= c->max_m) {  // coefficients of the starting iterates
+      RoundArgs p = base_args(c);
+      p.x_old = c->xs[c->cur];
+      HIPOK(launch_split_dots(c->dtype, 0, p, (int)c->n, c->stream));
+      HIPOK(launch_split_coef(c->dtype, c->problem, 1, p, (int)c->n, c->stream));
+    }
+  }
+  return DOPT_OK;
+}
+
 int dopt_phase_grad(dopt_ctx* c, int64_t batch, const int32_t* idx, double lam_grad, uint32_t metric_flags) {
   CHECK_ARG(c, "ctx is NULL");
   int rc;
@@ -1121,6 +1144,21 @@ int dopt_phase_grad(dopt_ctx* c, int64_t batch, const int32_t* idx, double lam_g
   const bool cons = metric_flags & DOPT_RUN_CONSENSUS, loss = metric_flags & DOPT_RUN_OBJECTIVE;
   if ((cons || loss) && (batch < c->max_m || c->obj_sep))
     return fail(DOPT_ERR_UNSUPPORTED, "fused metrics need full-shard batches over the shard rows");
+  if (c->split) {  // the gradient is produced block by block inside the step (dopt_phase_mix)
+    c->ph_batch = batch;
+    c->ph_lam = lam_grad;
+    c->ph_flags = metric_flags;
+    c->ph_have_idx = idx != nullptr;
+    if (idx) {  // this round's minibatch coefficients
+      RoundArgs a = base_args(c);
+      a.idx = c->idx;
+      a.b = batch;
+      a.x_old = c->xs[c->cur];
+      HIPOK(launch_split_dots(c->dtype, 0, a, (int)c->n, c->stream));
+      HIPOK(launch_split_coef(c->dtype, c->problem, 1, a, (int)c->n, c->stream));
+    }
+    return DOPT_OK;
+  }
   RoundArgs a = base_args(c);
   a.idx = idx ? c->idx : nullptr;
   a.b = batch;
@@ -1142,8 +1180,96 @@ int dopt_phase_mix(dopt_ctx* c, int64_t t, double eta0) {
   a.x_old = c->xs[c->cur];
   a.x_new = c->xs[c->cur ^ 1];
   a.eta = eta0 / sqrt((double)(t + 1));  // trainer.py:138-140
-  HIPOK(launch_mix(c->dtype, a, c->G, (int)c->n, c->stream));
+  if (c->split) {  // gradient + mix + step (+ next coefficients, + metric partials) in one pass
+    const bool full = !c->ph_have_idx;
+    const bool cons = c->ph_flags & DOPT_RUN_CONSENSUS, loss = c->ph_flags & DOPT_RUN_OBJECTIVE;
+    a.idx = full ? nullptr : c->idx;
+    a.b = c->ph_batch;
+    a.lam = c->ph_lam;
+    a.xbar = c->xbar[c->xb];
+    a.flags |= (cons ? F_CONS : 0) | (loss ? F_LOSS : 0);
+    int rc;
+    if (c->prof && (rc = prof_event(c, false))) return rc;
+    HIPOK(launch_split_step(c->dtype, full, cons || loss, a, (int)c->n, c->stream));
+    if (c->prof && (rc = prof_event(c, true))) return rc;
+    if (full || cons || loss) {
+      RoundArgs q = a;
+      q.idx = nullptr;
+      HIPOK(launch_split_coef(c->dtype, c->problem, (full ? 1 : 0) | ((cons || loss) ? 2 : 0), q, (int)c->n,
+                              c->stream));
+    }
+  } else {
+    HIPOK(launch_mix(c->dtype, a, c->G, (int)c->n, c->stream));
+  }
   c->cur ^= 1;
+  return DOPT_OK;
+}
+
+// ---- centralized trainer across ranks (trainer.py:41-71): per-rank gradients at the
+// shared iterate, all-reduced column sums of the gradients, the step.
+int dopt_phase_grad_shared(dopt_ctx* c, int64_t batch, const int32_t* idx, double lam_grad, int fuse_loss) {
+  CHECK_ARG(c, "ctx is NULL");
+  int rc;
+  if ((rc = check_run(c, 1, batch, idx, false))) return rc;
+  if (!c->G && (rc = dalloc(&c->G, (size_t)c->n * c->ld * c->esz))) return rc;
+  if (idx && (rc = upload_idx_chunk(c, idx, 0, 1, batch))) return rc;
+  if (fuse_loss && (batch < c->max_m || c->obj_sep))
+    return fail(DOPT_ERR_UNSUPPORTED, "a fused objective needs full-shard batches over the shard rows");
+  RoundArgs a = base_args(c);
+  a.idx = idx ? c->idx : nullptr;
+  a.b = batch;
+  a.w_shared = c->xg[c->gcur];
+  a.g_out = c->G;
+  a.lam = lam_grad;
+  a.flags |= F_GOUT | F_SHARED | (fuse_loss ? (F_LOSS | F_LOSS_FROM_Z) : 0);
+  if (c->split) {
+    if (fuse_loss) return fail(DOPT_ERR_UNSUPPORTED, "column-blocked rounds: use dopt_phase_metrics_pass_shared");
+    if ((rc = ensure_split(c))) return rc;
+    HIPOK(launch_split_dots(c->dtype, 0, a, (int)c->n, c->stream));
+    HIPOK(launch_split_coef(c->dtype, c->problem, 1, a, (int)c->n, c->stream));
+    if (c->prof && (rc = prof_event(c, false))) return rc;
+    HIPOK(launch_split_step(c->dtype, false, false, a, (int)c->n, c->stream));
+    if (c->prof && (rc = prof_event(c, true))) return rc;
+    return DOPT_OK;
+  }
+  if (c->prof && (rc = prof_event(c, false))) return rc;
+  HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, fuse_loss != 0, a, (int)c->n, c->stream));
+  if (c->prof && (rc = prof_event(c, true))) return rc;
+  return DOPT_OK;
+}
+
+int dopt_phase_colsum_grad(dopt_ctx* c, double* sum_dev) {
+  CHECK_ARG(c && sum_dev, "NULL argument");
+  if (!c->G) return fail(DOPT_ERR_STATE, "no gradient phase yet");
+  HIPOK(launch_colsum_partial(c->dtype, c->G, c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part, nullptr,
+                              c->stream));
+  HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nch, nullptr, nullptr, 0.0, 0,
+                            c->stream, sum_dev));
+  return DOPT_OK;
+}
+
+int dopt_phase_central_step(dopt_ctx* c, const double* sum_dev, int64_t t, double eta0) {
+  CHECK_ARG(c && sum_dev, "NULL argument");
+  HIPOK(launch_colsum_final(c->dtype, sum_dev, 1, n_div(c), c->ld, (int32_t)c->nch, c->xg[c->gcur ^ 1],
+                            c->xg[c->gcur], eta0 / sqrt((double)(t + 1)), 1, c->stream));
+  c->gcur ^= 1;
+  return DOPT_OK;
+}
+
+int dopt_phase_metrics_pass_shared(dopt_ctx* c) {
+  CHECK_ARG(c, "ctx is NULL");
+  if (c->split) {
+    int rc;
+    if ((rc = ensure_split(c))) return rc;
+    return split_metrics(c, nullptr, c->xg[c->gcur], true, false, true);
+  }
+  return metrics_pass(c, nullptr, c->xg[c->gcur], true, false, true);
+}
+
+int dopt_phase_metrics_shared(dopt_ctx* c, int include_xnorm, double* out_dev) {
+  CHECK_ARG(c && out_dev, "NULL argument");
+  HIPOK(launch_history(c->dtype, nullptr, c->slab_loss, c->n, c->n, c->xg[c->gcur], c->ld, (int32_t)c->nch,
+                       include_xnorm != 0, out_dev, c->stream));
   return DOPT_OK;
 }
 
@@ -1167,6 +1293,12 @@ int dopt_phase_xbar(dopt_ctx* c, const double* sum_dev) {
 
 int dopt_phase_metrics_pass(dopt_ctx* c, uint32_t flags) {
   CHECK_ARG(c, "ctx is NULL");
+  if (c->split) {
+    int rc;
+    if ((rc = ensure_split(c))) return rc;
+    return split_metrics(c, c->xs[c->cur], c->xbar[c->xb], false, flags & DOPT_RUN_CONSENSUS,
+                         flags & DOPT_RUN_OBJECTIVE);
+  }
   return metrics_pass(c, c->xs[c->cur], c->xbar[c->xb], false, flags & DOPT_RUN_CONSENSUS,
                       flags & DOPT_RUN_OBJECTIVE);
 }

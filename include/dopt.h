@@ -181,13 +181,17 @@ int dopt_set_partition(dopt_ctx *ctx, int64_t n_global, int64_t rows_global);
  * before dopt_set_topology (the local CSR indexes local + halo rows). */
 int dopt_set_halo(dopt_ctx *ctx, int64_t n_halo, void *halo_dev, int64_t n_send, void *send_dev,
                   const int32_t *send_ids);
+/* Start of a run of phases: column-blocked contexts (large d) compute the
+ * coefficients of the starting iterates here (full-shard batches). */
+int dopt_phase_begin(dopt_ctx *ctx, int64_t batch);
 int dopt_phase_gather(dopt_ctx *ctx);
 /* Gradients of every local worker at its current iterate (worker.py:30-44);
  * metric_flags (DOPT_RUN_*) also accumulate the current iterate's metric
  * partials at the current xbar (fused, full-shard batches only). */
 int dopt_phase_grad(dopt_ctx *ctx, int64_t batch, const int32_t *idx, double lam_grad,
                     uint32_t metric_flags);
-/* x_{t+1} = W [x_t | halo] - eta0/sqrt(t+1) g  (trainer.py:173-175). */
+/* x_{t+1} = W [x_t | halo] - eta0/sqrt(t+1) g  (trainer.py:173-175).  Column-blocked
+ * contexts compute the gradient here, block by block, in the same pass. */
 int dopt_phase_mix(dopt_ctx *ctx, int64_t t, double eta0);
 /* Local column sums of the current iterates -> sum_dev[ld] (float64). */
 int dopt_phase_colsum(dopt_ctx *ctx, double *sum_dev);
@@ -198,6 +202,19 @@ int dopt_phase_metrics_pass(dopt_ctx *ctx, uint32_t flags);
 /* Raw sums -> out_dev[3] = (sum of consensus partials, sum of loss terms,
  * ||xbar||^2 if include_xnorm else 0). */
 int dopt_phase_metrics(dopt_ctx *ctx, uint32_t flags, int include_xnorm, double *out_dev);
+/* Centralized trainer across ranks (trainer.py:41-71): gradients of the local
+ * workers at the shared iterate (fuse_loss: the objective partial of the shared
+ * iterate over the same rows, full shards only), local column sums of the
+ * gradients, then x <- x - eta0/sqrt(t+1) * sum_dev / n_global once the sums
+ * are all-reduced. */
+int dopt_phase_grad_shared(dopt_ctx *ctx, int64_t batch, const int32_t *idx, double lam_grad,
+                           int fuse_loss);
+int dopt_phase_colsum_grad(dopt_ctx *ctx, double *sum_dev);
+int dopt_phase_central_step(dopt_ctx *ctx, const double *sum_dev, int64_t t, double eta0);
+/* Objective partial at the shared iterate over the local rows, and its raw sums
+ * out_dev[3] = (0, sum of loss terms, ||x||^2 if include_xnorm). */
+int dopt_phase_metrics_pass_shared(dopt_ctx *ctx);
+int dopt_phase_metrics_shared(dopt_ctx *ctx, int include_xnorm, double *out_dev);
 int dopt_sync(dopt_ctx *ctx);
 /* Host: raw[T x 3] (summed over ranks) -> history values, the exact formula
  * the single-GPU path applies. */

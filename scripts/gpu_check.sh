@@ -20,6 +20,7 @@ for s in $STEPS; do
     bench) step bench 600 python -u bench.py ${BENCH_ARGS:-} ;;
     dist2) step dist2 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --backend gloo --workers 1024 --steps 5 --warmup 1 ;;
     probe) step probe 120 ./tools/bw_probe ;;
+    variants) step variants 600 python -u tools/kr_variants.py ;;
     c5)    step c5 600 python -u bench.py --config c5 --steps 5 --warmup 1 --no-cpu-baseline ;;
     c4)    step c4 900 python -u bench.py --config c4 --steps 5 --warmup 1 --no-cpu-baseline ;;
     prof)  (cd /tmp && export TMPDIR=/tmp) ; step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python -u bench.py --no-cpu-baseline ${BENCH_ARGS:-} ;;
