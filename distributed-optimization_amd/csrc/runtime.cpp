@@ -350,7 +350,10 @@ int metrics_pass(dopt_ctx* c, const void* x_state, const void* point, bool share
   return DOPT_OK;
 }
 
-int64_t obj_rows(dopt_ctx* c) { return c->obj_sep ? c->rows_o : (c->rows_global ? c->rows_global : c->rows); }
+int64_t obj_rows(dopt_ctx* c) {  // objective divisor: all ranks' objective rows when partitioned
+  if (c->rows_global) return c->rows_global;
+  return c->obj_sep ? c->rows_o : c->rows;
+}
 int64_t n_div(dopt_ctx* c) { return c->n_global ? c->n_global : c->n; }
 
 // Raw sums of round h -> history values (trainer.py:185, :189-190, obj_problems.py:3-11/:39-44).
@@ -1083,7 +1086,7 @@ int dopt_get_layout(dopt_ctx* c, int64_t* ld, int64_t* elem_bytes) {
 int dopt_set_partition(dopt_ctx* c, int64_t n_global, int64_t rows_global) {
   CHECK_ARG(c, "ctx is NULL");
   if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");
-  CHECK_ARG(n_global >= c->n && rows_global >= c->rows, "global sizes smaller than the local slice");
+  CHECK_ARG(n_global >= c->n && rows_global >= 0, "global sizes smaller than the local slice");
   c->n_global = n_global;
   c->rows_global = rows_global;
   return DOPT_OK;

@@ -88,9 +88,12 @@ def build_plan(topo, world, rank):
 class DistributedDSGD:
     """Drives one rank's engine through the round phases with torch.distributed."""
 
-    def __init__(self, engine, plan, n_global, rows_global, device=0, group=None, mean=None):
+    def __init__(self, engine, plan, n_global, rows_global, device=0, group=None, mean=None, obj_sep=False):
         """`mean` = (w_off, W_ii of the local workers) for the complete graph: the mix then
-        uses the all-reduced column sums and no halo rows move at all."""
+        uses the all-reduced column sums and no halo rows move at all.  `rows_global` is
+        the row count of the objective data (all shards, or the X_full slices loaded with
+        Engine.load_objective_data when obj_sep)."""
+        self.obj_sep = obj_sep
         import torch
         import torch.distributed as dist
 
@@ -161,11 +164,17 @@ class DistributedDSGD:
             t.copy_(c)
 
     # -- rounds
-    def run(self, T, eta0, batch, lam_grad, lam_obj, f_opt=0.0, t0=0, objective=True, consensus=True):
-        """T rounds; returns the GLOBAL (objective, consensus) history on every rank."""
+    def run(self, T, eta0, batch, lam_grad, lam_obj, f_opt=0.0, t0=0, objective=True, consensus=True, idx=None):
+        """T rounds; returns the GLOBAL (objective, consensus) history on every rank.
+
+        idx: [T, n_local, batch] minibatch row ids of this rank's workers (the slice of
+        the global draw), or None for full-shard batches.  With full shards the metrics
+        of round t ride on round t+1's pass over the rows; otherwise a metrics pass
+        over all local rows follows every round."""
         torch = self.torch
         eng = self.eng
         flags = (_dopt.RUN_OBJECTIVE if objective else 0) | (_dopt.RUN_CONSENSUS if consensus else 0)
+        fused = idx is None and not self.obj_sep
         xnorm = self.plan.rank == 0  # ||xbar||^2 is global already: count it once
         with torch.cuda.stream(self.stream):
             partials = torch.zeros((max(1, T), 3), dtype=torch.float64, device=self.dev)
@@ -173,19 +182,24 @@ class DistributedDSGD:
             eng.phase_colsum(self.sum.data_ptr())
             self._all_reduce(self.sum)
             eng.phase_xbar(self.sum.data_ptr())
+            eng.phase_begin(batch)
             for h in range(T):
+                met = fused and h > 0 and flags
                 if self._peers:
                     eng.phase_gather()
                 pending = self._start_exchange()
-                eng.phase_grad(batch, lam_grad, flags if h > 0 else 0)
-                if h > 0 and flags:
-                    eng.phase_metrics(flags, xnorm, partials[h - 1].data_ptr())
+                eng.phase_grad(batch, lam_grad, flags if met else 0, idx=None if idx is None else idx[h])
                 self._finish_exchange(pending)
                 eng.phase_mix(t0 + h, eta0)
+                if met:  # metric partials of x_t at xbar_t (slabs from this round's pass)
+                    eng.phase_metrics(flags, xnorm, partials[h - 1].data_ptr())
                 eng.phase_colsum(self.sum.data_ptr())
                 self._all_reduce(self.sum)
                 eng.phase_xbar(self.sum.data_ptr())
-            if flags and T > 0:
+                if flags and not fused:
+                    eng.phase_metrics_pass(flags)
+                    eng.phase_metrics(flags, xnorm, partials[h].data_ptr())
+            if flags and fused and T > 0:
                 eng.phase_metrics_pass(flags)
                 eng.phase_metrics(flags, xnorm, partials[T - 1].data_ptr())
             self._all_reduce(partials)
@@ -206,3 +220,54 @@ class DistributedDSGD:
         buf = [torch.zeros_like(x) for _ in sizes]
         self.dist.all_gather(buf, x, group=self.group)
         return torch.cat([b[:int(s)] for b, s in zip(buf, sizes)]).cpu().numpy()
+
+
+class DistributedCentralized:
+    """CentralizedTrainer rounds across ranks (trainer.py:41-71): each rank's workers take
+    their gradients at the shared iterate, the column sums of the gradients are
+    all-reduced (d doubles), and every rank applies the same step."""
+
+    def __init__(self, engine, plan, n_global, rows_global, device=0, group=None, obj_sep=False):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist = torch, dist
+        self.eng, self.plan, self.group = engine, plan, group
+        self.n_global, self.rows_global, self.obj_sep = int(n_global), int(rows_global), obj_sep
+        self.dev = torch.device("cuda", device)
+        self.device_comm = dist.get_backend(group) == "nccl"
+        self.stream = torch.cuda.Stream(self.dev)
+        ld, _ = engine.layout()
+        self.sum = torch.zeros(ld, dtype=torch.float64, device=self.dev)
+        engine.set_partition(self.n_global, self.rows_global)
+        engine.set_stream(self.stream.cuda_stream)
+
+    _all_reduce = DistributedDSGD._all_reduce
+
+    def run(self, T, eta0, batch, lam_grad, lam_obj, f_opt=0.0, t0=0, objective=True, idx=None):
+        torch = self.torch
+        eng = self.eng
+        split = ((eng.d + 16 // eng.layout()[1] - 1) // (16 // eng.layout()[1])) > 16 * 64
+        fused = idx is None and not self.obj_sep and not split
+        xnorm = self.plan.rank == 0
+        with torch.cuda.stream(self.stream):
+            partials = torch.zeros((max(1, T), 3), dtype=torch.float64, device=self.dev)
+            for h in range(T):
+                met = fused and h > 0 and objective
+                eng.phase_grad_shared(batch, lam_grad, fuse_loss=met, idx=None if idx is None else idx[h])
+                if met:  # objective of the iterate the gradients were taken at
+                    eng.phase_metrics_shared(xnorm, partials[h - 1].data_ptr())
+                eng.phase_colsum_grad(self.sum.data_ptr())
+                self._all_reduce(self.sum)
+                eng.phase_central_step(self.sum.data_ptr(), t0 + h, eta0)
+                if objective and not fused:
+                    eng.phase_metrics_pass_shared()
+                    eng.phase_metrics_shared(xnorm, partials[h].data_ptr())
+            if objective and fused and T > 0:
+                eng.phase_metrics_pass_shared()
+                eng.phase_metrics_shared(xnorm, partials[T - 1].data_ptr())
+            self._all_reduce(partials)
+            raw = partials[:T].cpu().numpy()
+        self.stream.synchronize()
+        obj, _ = _dopt.finalize_metrics(eng.problem, raw, self.n_global, self.rows_global, lam_obj, f_opt)
+        return obj if objective else None

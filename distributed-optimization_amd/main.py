@@ -43,7 +43,22 @@ def make_config(**overrides):
     return cfg
 
 
+def _maybe_init_distributed():
+    """Under torch.distributed.run (WORLD_SIZE > 1) every rank runs this script; the
+    trainers then split the workers across the ranks' GPUs (trainer.py docstring)."""
+    import os
+
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        import torch
+        import torch.distributed as dist
+
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group(os.environ.get("DOPT_BACKEND", "nccl"))
+
+
 if __name__ == "__main__":
+    _maybe_init_distributed()
     np.random.seed(203)
     simulator = Simulator(make_config())
     simulator.run_all()

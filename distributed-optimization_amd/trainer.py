@@ -18,6 +18,16 @@ Config keys beyond the reference's (all optional):
              'full': with full-shard batches skip the RNG entirely
   regular_degree / topology_seed   for topology='random_regular'
   spectral_gap   force / skip the spectral-gap print (default: N <= 4096)
+  mean_mixing_min  complete graphs of at least this many workers mix through the
+                 column sums (default 128)
+  distributed    False disables the multi-process mode below
+
+Multi-process mode: when torch.distributed is initialised with more than one rank
+(e.g. `python -m torch.distributed.run --nproc-per-node 8 main.py`), every rank
+keeps all Worker objects (same data, same RNG stream) but loads only its
+contiguous slice of workers onto its own GPU; the rounds run through
+distributed.DistributedDSGD / DistributedCentralized (halo send/recv and
+all-reduces over RCCL) and every rank ends with the same history and iterates.
 """
 import os
 import time
@@ -34,6 +44,25 @@ IDX_CHUNK_ELEMS = 1 << 24   # host index buffer per device call (64 MiB of int32
 
 
 # ---------------------------------------------------------------------------- shared helpers
+def _dist_info(config):
+    """(rank, world, backend) when running under an initialised multi-rank torch.distributed."""
+    if not config.get("distributed", True):
+        return None
+    try:
+        import torch.distributed as dist
+    except Exception:
+        return None
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return dist.get_rank(), dist.get_world_size(), dist.get_backend()
+    return None
+
+
+def _say(msg, config):
+    info = _dist_info(config)
+    if info is None or info[0] == 0:
+        print(msg)
+
+
 def _device(config):
     return int(config.get("device", os.environ.get("LOCAL_RANK", os.environ.get("DOPT_DEVICE", 0))))
 
@@ -74,20 +103,42 @@ def _same_rows(A, ya, B, yb):
 _ENGINES = {}
 
 
-def _engine(workers, n_features, config):
-    """One resident engine per (device, dtype, problem, shard set), reused by the
-    four trainers Simulator.run_all builds over the same worker data."""
-    key = (_device(config), config.get("dtype", "float64"), config["problem_type"], _data_key(workers))
+def _engine(workers, n_features, config, lo=0, hi=None):
+    """One resident engine per (device, dtype, problem, shard set, slice), reused by the
+    four trainers Simulator.run_all builds over the same worker data.  [lo, hi) is the
+    slice of workers this process holds (multi-process mode)."""
+    hi = len(workers) if hi is None else hi
+    key = (_device(config), config.get("dtype", "float64"), config["problem_type"], _data_key(workers), lo, hi)
     eng = _ENGINES.get(key)
     if eng is None:
         for k in [k for k in _ENGINES if k[:2] == key[:2]]:
             _ENGINES.pop(k).close()  # free the previous data set's HBM
         eng = _dopt.Engine(key[0], key[1])
-        X, y, off = _pack(workers, n_features)
+        X, y, off = _pack(workers[lo:hi], n_features)
         eng.load_shards(config["problem_type"], X, y, off)
         eng.obj_key = None
         _ENGINES[key] = eng
     return eng
+
+
+def _dist_objective(eng, workers, n_features, X_full, y_full, rank, world):
+    """Objective rows for a rank: its own shards when X_full is their union, else its
+    array_split slice of X_full.  Returns (want_obj, rows_global, separate)."""
+    if X_full is None or y_full is None:
+        eng.clear_objective_data()
+        eng.obj_key = None
+        return False, 1, False
+    X, y, _ = _pack(workers, n_features)
+    if _same_rows(X_full, y_full, X, y):
+        eng.clear_objective_data()
+        eng.obj_key = None
+        return True, X.shape[0], False
+    Xf = np.asarray(X_full, dtype=np.float64).reshape(-1, n_features)
+    yf = np.asarray(y_full, dtype=np.float64).reshape(-1)
+    parts = np.array_split(np.arange(Xf.shape[0]), world)[rank]
+    eng.load_objective_data(Xf[parts], yf[parts])
+    eng.obj_key = ("dist", id(X_full))
+    return True, Xf.shape[0], True
 
 
 def _set_objective_data(eng, workers, n_features, X_full, y_full):
@@ -167,6 +218,10 @@ class CentralizedTrainer:
         self.total_floats_transmitted = 0
         cfg = self.config
         lam_grad = cfg["l2_regularization_lambda"] if cfg["problem_type"] == "logistic" else cfg["strong_convexity_mu"]
+        info = _dist_info(cfg)
+        if info is not None:
+            return self._run_distributed(info, int(n_iterations), X_full, y_full, f_opt, lam_grad, reg_param,
+                                         start_time)
         eng = _engine(self.workers, self.n_features, cfg)
         want_obj = _set_objective_data(eng, self.workers, self.n_features, X_full, y_full)
         eng.set_global(self.x_global)
@@ -181,6 +236,32 @@ class CentralizedTrainer:
             self.total_floats_transmitted += n * (self.n_workers * self.n_features * 2)
         self.x_global = eng.get_global()
         print(f"C-SGD training finished. Time: {time.time() - start_time:.2f}sseconds")
+        return self.history, self.x_global
+
+    def _run_distributed(self, info, T, X_full, y_full, f_opt, lam_grad, reg_param, start_time):
+        import distributed
+
+        rank, world, _ = info
+        cfg = self.config
+        bounds = distributed.partition_bounds(self.n_workers, world)
+        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+        eng = _engine(self.workers, self.n_features, cfg, lo, hi)
+        want_obj, rows_global, sep = _dist_objective(eng, self.workers, self.n_features, X_full, y_full, rank, world)
+        plan = distributed.HaloPlan(rank, world, bounds, lo, hi, np.zeros(0, np.int64), np.zeros(world + 1, np.int64),
+                                    np.zeros(0, np.int32), np.zeros(world + 1, np.int64), None, None, None)
+        runner = distributed.DistributedCentralized(eng, plan, self.n_workers, rows_global, device=_device(cfg),
+                                                    obj_sep=sep)
+        eng.set_global(self.x_global)
+        for t0, n, b, idx in _index_chunks(self.workers, T, cfg):
+            t_host = time.time() - start_time
+            obj = runner.run(n, cfg["learning_rate_eta0"], b, lam_grad, reg_param, f_opt, t0=t0, objective=want_obj,
+                             idx=None if idx is None else idx[:, lo:hi])
+            if want_obj:
+                self.history["objective"].extend(list(obj))
+            self.history["time"].extend(list(np.linspace(t_host, time.time() - start_time, n + 1)[1:]))
+            self.total_floats_transmitted += n * (self.n_workers * self.n_features * 2)
+        self.x_global = eng.get_global()
+        _say(f"C-SGD training finished. Time: {time.time() - start_time:.2f}sseconds", cfg)
         return self.history, self.x_global
 
 
@@ -234,6 +315,10 @@ class DecentralizedTrainer:
         self.total_floats_transmitted = 0
         cfg = self.config
         lam_grad = cfg["l2_regularization_lambda"] if cfg["problem_type"] == "logistic" else cfg["strong_convexity_mu"]
+        info = _dist_info(cfg)
+        if info is not None:
+            return self._run_distributed(info, int(n_iterations), X_full, y_full, f_opt, lam_grad, reg_param,
+                                         start_time)
         eng = _engine(self.workers, self.n_features, cfg)
         want_obj = _set_objective_data(eng, self.workers, self.n_features, X_full, y_full)
         t = self._topo
@@ -258,5 +343,38 @@ class DecentralizedTrainer:
         for i, worker in enumerate(self.workers):  # trainer.py:178-179: row views
             worker.x = models[i, :]
         print(f"Decentralized ({self.topology}) training finished. Time: {time.time() - start_time:.2f}s")
+        final_avg_model = np.mean([worker.x for worker in self.workers], axis=0)
+        return self.history, final_avg_model
+
+    def _run_distributed(self, info, T, X_full, y_full, f_opt, lam_grad, reg_param, start_time):
+        import distributed
+
+        rank, world, _ = info
+        cfg = self.config
+        t = self._topo
+        uni = t.uniform_offdiag() if self.n_workers >= cfg.get("mean_mixing_min", MEAN_MIX_MIN) else None
+        plan = distributed.build_plan(t, world, rank)
+        eng = _engine(self.workers, self.n_features, cfg, plan.lo, plan.hi)
+        want_obj, rows_global, sep = _dist_objective(eng, self.workers, self.n_features, X_full, y_full, rank, world)
+        eng.set_models(np.stack([np.asarray(w.x, dtype=np.float64) for w in self.workers[plan.lo:plan.hi]]))
+        runner = distributed.DistributedDSGD(eng, plan, self.n_workers, rows_global, device=_device(cfg),
+                                             mean=None if uni is None else (uni[0], uni[1][plan.lo:plan.hi]),
+                                             obj_sep=sep)
+        iteration_transmission = np.sum(self.degrees) * self.n_features  # trainer.py:169
+        for t0, n, b, idx in _index_chunks(self.workers, T, cfg):
+            t_host = time.time() - start_time
+            obj, cons = runner.run(n, cfg["learning_rate_eta0"], b, lam_grad, reg_param, f_opt, t0=t0,
+                                   objective=want_obj, consensus=True,
+                                   idx=None if idx is None else idx[:, plan.lo:plan.hi])
+            self.history["consensus_error"].extend(list(cons))
+            if want_obj:
+                self.history["objective"].extend(list(obj))
+            self.history["time"].extend(list(np.linspace(t_host, time.time() - start_time, n + 1)[1:]))
+            for _ in range(n):
+                self.total_floats_transmitted += iteration_transmission
+        models = runner.gather_models()
+        for i, worker in enumerate(self.workers):
+            worker.x = models[i, :]
+        _say(f"Decentralized ({self.topology}) training finished. Time: {time.time() - start_time:.2f}s", cfg)
         final_avg_model = np.mean([worker.x for worker in self.workers], axis=0)
         return self.history, final_avg_model

@@ -72,3 +72,60 @@ def test_two_ranks_match_single_context(tmp_path, dtype, mean):
         np.testing.assert_array_equal(got["x"], x)
     np.testing.assert_allclose(got["obj"], obj, rtol=1e-12 if dtype == "float64" else 1e-6)
     np.testing.assert_allclose(got["cons"], cons, rtol=1e-12 if dtype == "float64" else 1e-5)
+
+
+def _trainer_rank(rank, world, port, out):
+    import json
+
+    import torch  # noqa: F401
+    import torch.distributed as dist
+
+    import data as odata
+    from trainer import CentralizedTrainer, DecentralizedTrainer
+    from worker import Worker
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    meta = json.load(open(os.path.join(G, "traj_c2.json")))
+    z = np.load(os.path.join(G, "traj_c2.npz"))
+    cfg = dict(meta["config"])
+    shards, Xf, yf = odata.generate(cfg, order=z["order"])
+    T = 300
+    res = {}
+    for j, label in enumerate(meta["labels"]):
+        np.random.set_state(("MT19937", z[f"state{j}_key"], int(z[f"state{j}_pos"]), 0, 0.0))
+        ws = [Worker(i, {"X": X, "y": y}, cfg["local_batch_size"], Xf.shape[1], cfg) for i, (X, y) in enumerate(shards)]
+        if label == "Centralized":
+            tr = CentralizedTrainer(ws, Xf.shape[1], cfg)
+        else:
+            topo = {"D-SGD (Ring)": "ring", "D-SGD (Fully Connected)": "fully_connected"}[label]
+            tr = DecentralizedTrainer(ws, topo, Xf.shape[1], cfg)
+        hist, xf = tr.run(T, Xf, yf, meta["f_opt"])
+        res[f"L{j}_objective"] = np.asarray(hist["objective"])
+        if "consensus_error" in hist:
+            res[f"L{j}_consensus"] = np.asarray(hist["consensus_error"])
+        res[f"L{j}_pos"] = np.int64(np.random.get_state()[2])
+    if rank == 0:
+        np.savez(os.path.join(out, "trainers.npz"), **res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_trainers_multiprocess_match_reference(tmp_path):
+    """DecentralizedTrainer / CentralizedTrainer under a 2-rank torch.distributed job
+    (each rank holds half of the workers) reproduce the reference's C2 trajectories."""
+    import json
+
+    import torch.multiprocessing as mp
+
+    mp.start_processes(_trainer_rank, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    got = np.load(tmp_path / "trainers.npz")
+    G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    meta = json.load(open(os.path.join(G, "traj_c2.json")))
+    z = np.load(os.path.join(G, "traj_c2.npz"))
+    for j, label in enumerate(meta["labels"]):
+        np.testing.assert_allclose(got[f"L{j}_objective"], z[f"L{j}_objective"][:300], rtol=1e-9)
+        if label != "Centralized":
+            np.testing.assert_allclose(got[f"L{j}_consensus"], z[f"L{j}_consensus"][:300], rtol=1e-9)
