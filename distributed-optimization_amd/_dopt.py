@@ -77,6 +77,7 @@ _SIGS = {
     "dopt_phase_metrics": ([_P, ctypes.c_uint32, ctypes.c_int, _P], ctypes.c_int),
     "dopt_sync": ([_P], ctypes.c_int),
     "dopt_finalize_metrics": ([ctypes.c_int, _I64, _P, _I64, _I64, _D, _D, _P, _P], ctypes.c_int),
+    "dopt_eval_full": ([_P, _P, _D, _P, _P], ctypes.c_int),
     "dopt_kernel_stats": ([_P, _P, _P], ctypes.c_int),
     "dopt_set_profiling": ([_P, ctypes.c_int], ctypes.c_int),
 }
@@ -365,6 +366,14 @@ class Engine:
 
     def sync(self):
         check(lib().dopt_sync(self._h))
+
+    def eval_full(self, w, reg):
+        """(objective, gradient) over all loaded rows at w, one device pass."""
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        g = np.empty(self.d, dtype=np.float64)
+        f = np.zeros(1)
+        check(lib().dopt_eval_full(self._h, _ptr(w), float(reg), _ptr(f), _ptr(g)))
+        return float(f[0]), g
 
     # -- profiling
     def set_profiling(self, on):

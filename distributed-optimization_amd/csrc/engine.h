@@ -16,6 +16,7 @@ enum : int32_t {
   F_LOSS = 16,         // objective partial at xbar over this workgroup's rows (trainer.py:189)
   F_LOSS_FROM_Z = 32,  // the objective point IS the gradient point: reuse z = x.w
   F_MEAN = 64,         // complete graph: sum_j W_ij x_j = w_off (S - x_i) + W_ii x_i, S = column sums
+  F_GSUM = 128,        // with F_GOUT: store the raw sum of coef * row (no 1/b, no lam) -- full gradients
 };
 
 // One workgroup per worker (or per objective-row chunk).  All pointers are

@@ -278,7 +278,7 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
 #pragma unroll
       for (int q = 1; q < NW; ++q) s += red[q * nch + c];  // fixed order
       const V wc = *(const V*)(wsrc + (int64_t)c * VN);
-      const V gc = (nb > 0) ? (s / (T)nb + lam * wc) : V(0);
+      const V gc = (flags & F_GSUM) ? s : ((nb > 0) ? (s / (T)nb + lam * wc) : V(0));
       if (flags & F_STEP) {
         const V acc = mix_chunk<T>(a, i, c, wc);
         *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = acc - inv_eta * gc;

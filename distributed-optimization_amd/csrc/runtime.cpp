@@ -1045,6 +1045,46 @@ int dopt_eval_objective(dopt_ctx* c, int problem, int64_t n, int64_t d, const do
   return eval_common(c, problem, n, d, w, X, y, false, reg, out);
 }
 
+int dopt_eval_full(dopt_ctx* c, const double* w, double reg, double* f_out, double* g_out) {
+  CHECK_ARG(c && w && f_out && g_out, "NULL argument");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
+  if (c->split) return fail(DOPT_ERR_UNSUPPORTED, "full-data evaluation of column-blocked rows");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  if (!c->G && (rc = dalloc(&c->G, (size_t)c->n * c->ld * c->esz))) return rc;
+  if ((rc = ensure_hist(c, 1))) return rc;
+  if ((rc = upload_rows(c, c->dtype, w, 0, c->xg[c->gcur ^ 1], 1, c->d, c->ld))) return rc;
+  RoundArgs a = base_args(c);
+  if (c->obj_sep) {
+    a.X = c->Xo;
+    a.y = c->yo;
+    a.off = c->offo;
+  }
+  a.w_shared = c->xg[c->gcur ^ 1];
+  a.g_out = c->G;
+  a.flags = F_GOUT | F_GSUM | F_SHARED | F_LOSS | F_LOSS_FROM_Z;
+  HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, true, a, (int)c->n, c->stream));
+  HIPOK(launch_colsum_partial(c->dtype, c->G, c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part, nullptr,
+                              c->stream));
+  if ((rc = history(c, 0, a.w_shared, false, true, c->n))) return rc;
+  std::vector<double> colsum((size_t)c->ld), raw(3);
+  double* dsum = nullptr;
+  if ((rc = dalloc_t(&dsum, (size_t)c->ld * sizeof(double)))) return rc;
+  hipError_t e = launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nch, nullptr, nullptr,
+                                     0.0, 0, c->stream, dsum);
+  if (e == hipSuccess) e = hipMemcpyAsync(colsum.data(), dsum, (size_t)c->ld * sizeof(double), hipMemcpyDeviceToHost,
+                                          c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(raw.data(), c->hraw, 3 * sizeof(double), hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  dfree_t(dsum);
+  if (e != hipSuccess) return fail(DOPT_ERR_HIP, "dopt_eval_full: %s", hipGetErrorString(e));
+  const int64_t M = obj_rows(c);
+  // full-data mean over every row (obj_problems.py:22-36 / :55-69), objective (:3-11 / :39-44)
+  for (int64_t k = 0; k < c->d; ++k) g_out[k] = (M > 0 ? colsum[(size_t)k] / (double)M : 0.0) + reg * w[k];
+  finalize_metrics(raw.data(), 1, c->problem, 1, M, reg, 0.0, f_out, nullptr);
+  return DOPT_OK;
+}
+
 int dopt_set_profiling(dopt_ctx* c, int enable) {
   CHECK_ARG(c, "ctx is NULL");
   c->prof = enable != 0;

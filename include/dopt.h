@@ -222,6 +222,14 @@ int dopt_finalize_metrics(int problem, int64_t T, const double *raw, int64_t n_w
                           int64_t m_obj, double lam_obj, double f_opt, double *obj_out,
                           double *cons_out);
 
+/* Full-data objective and gradient at w over every loaded row (or the separate
+ * objective dataset): f = mean loss + reg/2 ||w||^2 (obj_problems.py:3-11 /
+ * :39-44), g = mean_k c_k x_k + reg w (the full-gradient shape of
+ * obj_problems.py:22-36 / :55-69).  One pass over the data; the building block
+ * of the device f(x*) solver (solver.py) that replaces sklearn's saga at sizes
+ * sklearn cannot handle (simulator.py:32-69). */
+int dopt_eval_full(dopt_ctx *ctx, const double *w, double reg, double *f_out, double *g_out);
+
 /* Device time of the last run's dominant kernel (the fused round kernel):
  * launches and summed milliseconds, measured with HIP events on the engine's
  * stream.  Used by bench.py for the roofline figure. */

@@ -241,3 +241,27 @@ def test_c3_deterministic_and_fp32_tracks_fp64():
     np.testing.assert_allclose(a[0], c[0], rtol=1e-5)
     np.testing.assert_allclose(a[1], c[1], rtol=1e-3)
     e64.close()
+
+
+def test_full_evaluation_and_device_optimum():
+    """dopt_eval_full vs the oracle's objective / full gradient (float64), and the
+    device L-BFGS optimum is a stationary point no worse than sklearn's."""
+    import solver
+
+    meta, z = _load("c2")
+    cfg = meta["config"]
+    shards, Xf, yf = _shards(meta, z)
+    eng = _dopt.Engine(0, "float64")
+    off = np.concatenate([[0], np.cumsum([len(s[1]) for s in shards])])
+    eng.load_shards("logistic", Xf[np.concatenate(np.array_split(z["order"], 10))], yf[z["order"]], off)
+    rng = np.random.default_rng(0)
+    for _ in range(3):
+        w = rng.standard_normal(Xf.shape[1]) * 0.3
+        f, g = eng.eval_full(w, 1e-4)
+        np.testing.assert_allclose(f, O.logistic_objective(w, Xf, yf, 1e-4), rtol=1e-12)
+        np.testing.assert_allclose(g, O.full_gradient("logistic", w, shards, 1e-4), rtol=1e-10, atol=1e-14)
+    f_opt, w_opt, info = solver.reference_optimum(eng, 1e-4)
+    assert info["grad_norm"] < 1e-7
+    assert f_opt <= meta["f_opt"] + 1e-12  # sklearn leaves the intercept unregularised
+    assert f_opt > meta["f_opt"] - 1e-3
+    eng.close()
