@@ -130,7 +130,7 @@ def main():
     import distributed
     import topology
 
-    problem, mean = "logistic", None
+    problem, mean, eta0 = "logistic", None, 0.05
     if args.config == "c3":
         n, d, m = args.workers, args.d, args.m
         n_global = n * world
@@ -143,6 +143,7 @@ def main():
         workload = "C4: logistic, 65536 workers total on a 256x256 torus, d=1024, m=b=512"
     else:
         problem, d, m, n_global = "quadratic", 1 << 20, 16, 1024
+        eta0 = 1e-5  # L ~ d/b for N(0,1) rows of length 2^20: eta0 = 0.05 (set for d = 81) diverges
         top = topology.fully_connected(n_global)
         mean = top.uniform_offdiag()
         workload = "C5: quadratic, 1024 workers total, d=2^20, m=b=16, complete graph (column-sum mixing)"
@@ -163,7 +164,7 @@ def main():
         log(f"halo: {plan.n_halo} rows in, {len(plan.send_ids)} rows out per round")
 
         def rounds(k):
-            return runner.run(k, 0.05, m, lam, lam, 0.0)
+            return runner.run(k, eta0, m, lam, lam, 0.0)
     else:
         if mean is not None:
             eng.set_mixing_mean(*mean)
@@ -171,7 +172,7 @@ def main():
             eng.set_topology(top.row_ptr, top.col, top.w)
 
         def rounds(k):
-            obj, cons, _ = eng.run_dsgd(k, 0.05, m, lam, lam, 0.0)
+            obj, cons, _ = eng.run_dsgd(k, eta0, m, lam, lam, 0.0)
             return obj, cons
     log("warmup")
     if args.warmup > 0:
@@ -205,9 +206,10 @@ def main():
     while cpl * 64 < (d + (16 // esz) - 1) // (16 // esz):
         cpl *= 2
     if cpl <= 16:
-        kname = f"void dopt::k_round<{tname}, {cpl}, {0 if problem == 'logistic' else 1}, true, true>(dopt::RoundArgs)"
+        kname = (f"void dopt::k_round<{tname}, {cpl}, {0 if problem == 'logistic' else 1}, true, true, 3>"
+                 "(dopt::RoundArgs)")
     else:
-        kname = f"void dopt::k_split_step<{tname}, true, true>(dopt::RoundArgs)"
+        kname = f"void dopt::k_split_step<{tname}, {4 if m <= 16 else 16}, true, true>(dopt::RoundArgs)"
     traffic, traffic_src = pmc_traffic(kname) if args.config == "c3" and n == 4096 and world == 1 else (None, None)
     bytes_per_launch = esz * n * (m * d + m + 2 * d)  # X_b + y_b + x read + x write
     avg_s = (kr_ms / launches) * 1e-3 if launches else float("nan")

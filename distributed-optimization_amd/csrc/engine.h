@@ -54,6 +54,7 @@ struct RoundArgs {
   double* upart;          // [n x bcap x groups] partial dots with xbar (objective)
   double* cpart;          // [n x groups] partial ||x_i - xbar||^2
   int32_t bcap;           // row capacity per worker in coef / partials
+  int32_t b_rows;         // max rows per worker a column-blocked step touches (picks the kernel)
   int32_t groups;         // column-block groups = gridDim.y
 };
 

@@ -150,9 +150,12 @@ __device__ __forceinline__ typename VT<T>::v mix_chunk(const RoundArgs& a, int i
 }
 
 // ---------------------------------------------------------------------------- k_round
-// VAR (tuning variants, C3 instantiation only; 0 = default): bit 0 nontemporal row loads,
-// bit 1 DPP wave reduction, bit 2 twice the rows in flight.
-template <typename T, int CPL, int PROB, bool GRAD, bool MET, int VAR = 0>
+// VAR: bit 0 nontemporal row loads (rows are read once per round: +11 % on MI355X,
+// 6.28 -> 7.15 TB/s on the bare access pattern, tools/bw_probe.hip), bit 1 DPP wave
+// reduction (readlane to an SGPR; ~0.5-1 %), bit 2 twice the rows in flight (no gain).
+// Default 3; the others stay reachable through DOPT_KR_VARIANT for A/B runs.
+constexpr int KR_DEFAULT_VAR = 3;
+template <typename T, int CPL, int PROB, bool GRAD, bool MET, int VAR = KR_DEFAULT_VAR>
 __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
   using V = typename VT<T>::v;
   constexpr int VN = VT<T>::n;
@@ -299,7 +302,7 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
   }
 }
 
-template <typename T, int CPL, int PROB, bool GRAD, bool MET, int VAR = 0>
+template <typename T, int CPL, int PROB, bool GRAD, bool MET, int VAR = KR_DEFAULT_VAR>
 static hipError_t launch_round_t(const RoundArgs& a, int groups, hipStream_t s) {
   const size_t lds = (GRAD ? (size_t)NW * a.nchunks * 16 : 0) + 2 * NW * sizeof(double);
   static bool attr_set = false;
@@ -325,21 +328,24 @@ static hipError_t dispatch_variant(int var, const RoundArgs& a, int groups, hipS
     case 4: return launch_round_t<float, 4, 0, GRAD, MET, 4>(a, groups, s);
     case 6: return launch_round_t<float, 4, 0, GRAD, MET, 6>(a, groups, s);
     case 7: return launch_round_t<float, 4, 0, GRAD, MET, 7>(a, groups, s);
-    default: return launch_round_t<float, 4, 0, GRAD, MET, 0>(a, groups, s);
+    case 0: return launch_round_t<float, 4, 0, GRAD, MET, 0>(a, groups, s);
+    default: return launch_round_t<float, 4, 0, GRAD, MET>(a, groups, s);
   }
 }
 
-static int kr_variant() {
+static int kr_variant() {  // -1: the default build
   const char* v = getenv("DOPT_KR_VARIANT");
-  return v ? atoi(v) : 0;
+  return v ? atoi(v) : -1;
 }
 
 template <typename T, int CPL, int PROB>
 static hipError_t dispatch_mode(bool grad, bool met, const RoundArgs& a, int groups, hipStream_t s) {
   if constexpr (std::is_same<T, float>::value && CPL == 4 && PROB == 0) {
     const int var = kr_variant();
-    if (var && grad && met) return dispatch_variant<true, true>(var, a, groups, s);
-    if (var && grad) return dispatch_variant<true, false>(var, a, groups, s);
+    if (var >= 0 && var != KR_DEFAULT_VAR) {
+      if (grad && met) return dispatch_variant<true, true>(var, a, groups, s);
+      if (grad) return dispatch_variant<true, false>(var, a, groups, s);
+    }
   }
   if (grad && met) return launch_round_t<T, CPL, PROB, true, true>(a, groups, s);
   if (grad) return launch_round_t<T, CPL, PROB, true, false>(a, groups, s);
@@ -380,22 +386,29 @@ int max_chunks_per_lane() { return MAX_CPL; }
 // block -> x_i' block (waves meet in LDS) -> the next round's partial dots x_k . x_i'
 // from the SAME row registers.  Per-row partial dots go to fp64 slabs [n][bcap][G]
 // that k_split_coef folds in a fixed order.  One pass over the shard per round.
-template <typename T, bool ZNEXT, bool MET>
+template <typename T>
+__device__ __forceinline__ typename VT<T>::v ld_nt(const T* p) {
+  return __builtin_nontemporal_load((const typename VT<T>::v*)p);
+}
+
+// RPW = rows per wave held in registers (4 for <= 16 rows per worker, 16 for <= 64).
+// One barrier per block: the waves' gradient partials go to a double-buffered LDS
+// slot, every wave folds them and forms the new block itself (wave 0 stores it).
+template <typename T, int RPW, bool ZNEXT, bool MET>
 __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
   using V = typename VT<T>::v;
   constexpr int VN = VT<T>::n;
-  constexpr int RPW = kSplitMaxRows / NW;
-  __shared__ V gred[NW][64];
-  __shared__ V xs[64];
+  __shared__ V gred[2][NW][64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int i = blockIdx.x, grp = blockIdx.y, G = gridDim.y;
   const int nch = a.nchunks, nblk = (nch + 63) / 64;
   const int64_t ld = a.ld;
   const int64_t row0 = a.off[i], m = a.off[i + 1] - row0;
-  const int64_t nb = a.idx ? (a.b < m ? a.b : m) : m;  // <= kSplitMaxRows (host-checked)
+  const int64_t nb = a.idx ? (a.b < m ? a.b : m) : m;  // <= NW * RPW (host-checked)
   const T* __restrict__ X = (const T*)a.X;
   const bool shared = (a.flags & F_SHARED) != 0;  // centralized: every worker at w_shared
+  const bool gout = (a.flags & F_GOUT) != 0;
   const T* own_p = shared ? (const T*)a.w_shared : (const T*)a.x_old + (int64_t)i * ld;
   int64_t rowp[RPW];
   T coef[RPW];
@@ -411,34 +424,31 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
     uacc[r] = 0.0;
   }
   double cacc = 0.0;
-  for (int cb = grp; cb < nblk; cb += G) {
+  const T inv_eta = (T)a.eta, lam = (T)a.lam;
+  int buf = 0;
+  for (int cb = grp; cb < nblk; cb += G, buf ^= 1) {
     const int c = cb * 64 + lane;
     const bool in = c < nch;
-    const V own = in ? *(const V*)(own_p + (int64_t)c * VN) : V(0);
-    const V xb = (MET && in) ? *(const V*)((const T*)a.xbar + (int64_t)c * VN) : V(0);
     V rv[RPW];
 #pragma unroll
-    for (int r = 0; r < RPW; ++r) rv[r] = (rowp[r] >= 0 && in) ? *(const V*)(X + rowp[r] + (int64_t)c * VN) : V(0);
+    for (int r = 0; r < RPW; ++r) rv[r] = (rowp[r] >= 0 && in) ? ld_nt<T>(X + rowp[r] + (int64_t)c * VN) : V(0);
+    const V own = in ? *(const V*)(own_p + (int64_t)c * VN) : V(0);
+    const V xb = (MET && in) ? *(const V*)((const T*)a.xbar + (int64_t)c * VN) : V(0);
     V gp = V(0);
 #pragma unroll
     for (int r = 0; r < RPW; ++r) gp += coef[r] * rv[r];
-    gred[wave][lane] = gp;
+    gred[buf][wave][lane] = gp;
     __syncthreads();
-    if (wave == 0) {
-      V g = V(0);
-      if (nb > 0) g = (gred[0][lane] + gred[1][lane] + gred[2][lane] + gred[3][lane]) / (T)nb + (T)a.lam * own;
-      V xn = V(0);
-      if (in && (a.flags & F_GOUT)) {
-        *(V*)((T*)a.g_out + (int64_t)i * ld + (int64_t)c * VN) = g;
-      } else if (in) {
-        xn = mix_chunk<T>(a, i, c, own) - (T)a.eta * g;
-        *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = xn;
-      }
-      xs[lane] = xn;
+    V g = V(0);
+    if (nb > 0) g = (gred[buf][0][lane] + gred[buf][1][lane] + gred[buf][2][lane] + gred[buf][3][lane]) / (T)nb + lam * own;
+    V xn = V(0);
+    if (gout) {
+      if (wave == 0 && in) *(V*)((T*)a.g_out + (int64_t)i * ld + (int64_t)c * VN) = g;
+    } else if (in) {
+      xn = mix_chunk<T>(a, i, c, own) - inv_eta * g;
+      if (wave == 0) *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = xn;
     }
-    __syncthreads();
     if (ZNEXT) {
-      const V xn = xs[lane];
 #pragma unroll
       for (int r = 0; r < RPW; ++r) zacc[r] += (double)hsum<T>(rv[r] * xn);
     }
@@ -456,25 +466,24 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
     const int k = wave + NW * r;
     const int64_t slot = ((int64_t)i * a.bcap + k) * G + grp;
     if (ZNEXT) {
-      const double z = wave_sum(zacc[r]);
+      const double z = wave_sum_dpp(zacc[r]);
       if (lane == 0 && k < nb) a.zpart[slot] = z;
     }
     if (MET) {
-      const double u = wave_sum(uacc[r]);
+      const double u = wave_sum_dpp(uacc[r]);
       if (lane == 0 && k < nb) a.upart[slot] = u;
     }
   }
   if (MET && wave == 0) {
-    const double cs = wave_sum(cacc);
+    const double cs = wave_sum_dpp(cacc);
     if (lane == 0) a.cpart[(int64_t)i * G + grp] = cs;
   }
 }
 
-template <typename T, int MODE>
+template <typename T, int MODE, int RPW>
 __global__ __launch_bounds__(NT) void k_split_dots(const RoundArgs a) {
   using V = typename VT<T>::v;
   constexpr int VN = VT<T>::n;
-  constexpr int RPW = kSplitMaxRows / NW;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int i = blockIdx.x, grp = blockIdx.y, G = gridDim.y;
@@ -499,7 +508,7 @@ __global__ __launch_bounds__(NT) void k_split_dots(const RoundArgs a) {
     if (lane == 0) a.cpart[(int64_t)i * G + grp] = cacc;
   }
   if (MODE == 1 && !(a.flags & F_LOSS)) return;
-  for (int64_t rc = 0; rc < nb; rc += kSplitMaxRows) {
+  for (int64_t rc = 0; rc < nb; rc += NW * RPW) {
     int64_t rowp[RPW];
     double acc[RPW];
 #pragma unroll
@@ -516,7 +525,7 @@ __global__ __launch_bounds__(NT) void k_split_dots(const RoundArgs a) {
       const V pv = *(const V*)(pt + (int64_t)c * VN);
 #pragma unroll
       for (int r = 0; r < RPW; ++r)
-        if (rowp[r] >= 0) acc[r] += (double)hsum<T>(*(const V*)(X + rowp[r] + (int64_t)c * VN) * pv);
+        if (rowp[r] >= 0) acc[r] += (double)hsum<T>(ld_nt<T>(X + rowp[r] + (int64_t)c * VN) * pv);
     }
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
@@ -568,15 +577,16 @@ hipError_t launch_split_step(int dtype, bool znext, bool met, const RoundArgs& a
                              hipStream_t s) {
   if (n_workers <= 0) return hipSuccess;
   const dim3 grid(n_workers, a.groups);
-#define SPLIT_STEP(T_)                                                                              \
-  if (znext && met) hipLaunchKernelGGL((k_split_step<T_, true, true>), grid, dim3(NT), 0, s, a);    \
-  else if (znext) hipLaunchKernelGGL((k_split_step<T_, true, false>), grid, dim3(NT), 0, s, a);     \
-  else if (met) hipLaunchKernelGGL((k_split_step<T_, false, true>), grid, dim3(NT), 0, s, a);       \
-  else hipLaunchKernelGGL((k_split_step<T_, false, false>), grid, dim3(NT), 0, s, a);
+  const bool small = a.b_rows <= 4 * NW;  // rows per worker this step touches
+#define SPLIT_STEP(T_, R_)                                                                               \
+  if (znext && met) hipLaunchKernelGGL((k_split_step<T_, R_, true, true>), grid, dim3(NT), 0, s, a);     \
+  else if (znext) hipLaunchKernelGGL((k_split_step<T_, R_, true, false>), grid, dim3(NT), 0, s, a);      \
+  else if (met) hipLaunchKernelGGL((k_split_step<T_, R_, false, true>), grid, dim3(NT), 0, s, a);        \
+  else hipLaunchKernelGGL((k_split_step<T_, R_, false, false>), grid, dim3(NT), 0, s, a);
   if (dtype == 0) {
-    SPLIT_STEP(float)
+    if (small) { SPLIT_STEP(float, 4) } else { SPLIT_STEP(float, 16) }
   } else {
-    SPLIT_STEP(double)
+    if (small) { SPLIT_STEP(double, 4) } else { SPLIT_STEP(double, 16) }
   }
 #undef SPLIT_STEP
   return hipGetLastError();
@@ -585,13 +595,16 @@ hipError_t launch_split_step(int dtype, bool znext, bool met, const RoundArgs& a
 hipError_t launch_split_dots(int dtype, int mode, const RoundArgs& a, int n_workers, hipStream_t s) {
   if (n_workers <= 0) return hipSuccess;
   const dim3 grid(n_workers, a.groups);
+  const bool small = a.b_rows <= 4 * NW;  // <= 16 rows: one 4-row chunk per wave, high occupancy
+#define SPLIT_DOTS(T_, R_)                                                                       \
+  if (mode == 0) hipLaunchKernelGGL((k_split_dots<T_, 0, R_>), grid, dim3(NT), 0, s, a);        \
+  else hipLaunchKernelGGL((k_split_dots<T_, 1, R_>), grid, dim3(NT), 0, s, a);
   if (dtype == 0) {
-    if (mode == 0) hipLaunchKernelGGL((k_split_dots<float, 0>), grid, dim3(NT), 0, s, a);
-    else hipLaunchKernelGGL((k_split_dots<float, 1>), grid, dim3(NT), 0, s, a);
+    if (small) { SPLIT_DOTS(float, 4) } else { SPLIT_DOTS(float, 16) }
   } else {
-    if (mode == 0) hipLaunchKernelGGL((k_split_dots<double, 0>), grid, dim3(NT), 0, s, a);
-    else hipLaunchKernelGGL((k_split_dots<double, 1>), grid, dim3(NT), 0, s, a);
+    if (small) { SPLIT_DOTS(double, 4) } else { SPLIT_DOTS(double, 16) }
   }
+#undef SPLIT_DOTS
   return hipGetLastError();
 }
 

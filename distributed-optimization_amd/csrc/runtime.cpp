@@ -329,6 +329,7 @@ RoundArgs base_args(dopt_ctx* c) {
   a.upart = c->upart;
   a.cpart = c->cpart;
   a.bcap = (int32_t)c->bcap;
+  a.b_rows = (int32_t)std::min<int64_t>(c->max_m, kSplitMaxRows);
   a.groups = c->split_groups;
   return a;
 }
@@ -498,6 +499,7 @@ int run_dsgd_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batc
       if (h % CH == 0 && (rc = upload_idx_chunk(c, idx, h, std::min(CH, T - h), batch))) return rc;
       a.idx = c->idx + (h % CH) * c->n * batch;
       a.b = batch;
+      a.b_rows = (int32_t)std::min<int64_t>(a.b_rows, batch);
     }
     a.x_old = c->xs[c->cur];
     a.x_new = c->xs[c->cur ^ 1];
@@ -559,6 +561,7 @@ int run_centralized_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64
       if (h % CH == 0 && (rc = upload_idx_chunk(c, idx, h, std::min(CH, T - h), batch))) return rc;
       a.idx = c->idx + (h % CH) * c->n * batch;
       a.b = batch;
+      a.b_rows = (int32_t)std::min<int64_t>(a.b_rows, batch);
     }
     a.w_shared = c->xg[c->gcur];
     a.g_out = c->G;
@@ -1196,6 +1199,7 @@ int dopt_phase_grad(dopt_ctx* c, int64_t batch, const int32_t* idx, double lam_g
       RoundArgs a = base_args(c);
       a.idx = c->idx;
       a.b = batch;
+      a.b_rows = (int32_t)std::min<int64_t>(a.b_rows, batch);
       a.x_old = c->xs[c->cur];
       HIPOK(launch_split_dots(c->dtype, 0, a, (int)c->n, c->stream));
       HIPOK(launch_split_coef(c->dtype, c->problem, 1, a, (int)c->n, c->stream));
@@ -1228,6 +1232,7 @@ int dopt_phase_mix(dopt_ctx* c, int64_t t, double eta0) {
     const bool cons = c->ph_flags & DOPT_RUN_CONSENSUS, loss = c->ph_flags & DOPT_RUN_OBJECTIVE;
     a.idx = full ? nullptr : c->idx;
     a.b = c->ph_batch;
+    if (!full) a.b_rows = (int32_t)std::min<int64_t>(a.b_rows, c->ph_batch);
     a.lam = c->ph_lam;
     a.xbar = c->xbar[c->xb];
     a.flags |= (cons ? F_CONS : 0) | (loss ? F_LOSS : 0);
