@@ -23,6 +23,7 @@ for s in $STEPS; do
     variants) step variants 600 python -u tools/kr_variants.py ;;
     c5)    step c5 600 python -u bench.py --config c5 --steps 5 --warmup 1 --no-cpu-baseline ;;
     c4)    step c4 900 python -u bench.py --config c4 --steps 5 --warmup 1 --no-cpu-baseline ;;
+    mainpy) step mainpy 600 bash -c 'cd distributed-optimization_amd && MPLBACKEND=Agg python -u -c "import time, runpy; t=time.time(); import matplotlib; matplotlib.use(\"Agg\"); runpy.run_path(\"main.py\", run_name=\"__main__\"); print(\"main.py wall %.1f s\" % (time.time()-t))"' ;;
     prof)  (cd /tmp && export TMPDIR=/tmp) ; step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python -u bench.py --no-cpu-baseline ${BENCH_ARGS:-} ;;
   esac
 done
