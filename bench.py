@@ -108,6 +108,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (gloo: 1-GPU rehearsal)")
+    ap.add_argument("--phase", action="store_true",
+                    help="drive the multi-GPU phase path even on one GPU (measures its per-rank overhead)")
     ap.add_argument("--config", default="c3", choices=["c3", "c4", "c5"],
                     help="c3 (default, the metric's config); c4: 256x256 torus, 65536 workers total; "
                          "c5: quadratic, d=2^20, m=b=16, 1024 workers total, complete graph")
@@ -120,9 +122,14 @@ def main():
     import torch.distributed as dist
 
     dev = local % max(1, torch.cuda.device_count())
-    if world > 1:
+    if world > 1 or args.phase:
         torch.cuda.set_device(dev)
-        dist.init_process_group(args.backend)
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            dist.init_process_group("gloo", rank=0, world_size=1)
+        else:
+            dist.init_process_group(args.backend)
 
     import numpy as np
 
@@ -158,7 +165,7 @@ def main():
     eng = _dopt.Engine(dev, args.dtype)
     eng.generate_shards(problem, plan.n_local, d, m, seed=1000, flip=0.05, first_worker=plan.lo)
     lam = 1e-4
-    if world > 1:
+    if world > 1 or args.phase:
         mean_local = None if mean is None else (mean[0], mean[1][plan.lo:plan.hi])
         runner = distributed.DistributedDSGD(eng, plan, n_global, n_global * m, device=dev, mean=mean_local)
         log(f"halo: {plan.n_halo} rows in, {len(plan.send_ids)} rows out per round")
@@ -231,8 +238,9 @@ def main():
         "config": {"workload": workload,
                    "workers_per_gpu": n, "d": d, "rows_per_worker": m, "batch": m, "topology": top.name,
                    "degree": args.degree if args.config == "c3" else None,
-                   "parallelism": f"dp{world}: one graph of {n_global} workers, contiguous slices, halo send/recv"
-                                  + (f" ({args.backend})" if world > 1 else "")},
+                   "parallelism": (f"dp{world}: one graph of {n_global} workers, contiguous slices per GPU, "
+                                   f"halo send/recv + all-reduce ({args.backend})") if world > 1
+                                  else "single GPU: fused round kernel, one launch per round"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
@@ -250,7 +258,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()
-    if world > 1:
+    if world > 1 or args.phase:
         dist.destroy_process_group()
 
 

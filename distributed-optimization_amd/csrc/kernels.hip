@@ -164,7 +164,10 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int i = blockIdx.x;
+  // VAR bit 3: persistent workgroups, each walking workers blockIdx.x + k * gridDim.x
+  const int i_end = (VAR & 8) ? a.n_local : (int)blockIdx.x + 1;
+  const int i_step = (VAR & 8) ? (int)gridDim.x : 1;
+  for (int i = blockIdx.x; i < i_end; i += i_step) {
   const int flags = a.flags;
   const int nch = a.nchunks;
   const int64_t ld = a.ld;
@@ -300,6 +303,8 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
     if (want_cons) a.slab_cons[i] = cs;
     if (want_loss) a.slab_loss[i] = ls;
   }
+  if (VAR & 8) __syncthreads();  // LDS of this worker's epilogue is reused by the next
+  }
 }
 
 template <typename T, int CPL, int PROB, bool GRAD, bool MET, int VAR = KR_DEFAULT_VAR>
@@ -313,7 +318,8 @@ static hipError_t launch_round_t(const RoundArgs& a, int groups, hipStream_t s) 
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((k_round<T, CPL, PROB, GRAD, MET, VAR>), dim3(groups), dim3(NT), lds, s, a);
+  const int grid = (VAR & 8) ? (groups < 1024 ? groups : 1024) : groups;  // 4 workgroups per CU
+  hipLaunchKernelGGL((k_round<T, CPL, PROB, GRAD, MET, VAR>), dim3(grid), dim3(NT), lds, s, a);
   return hipGetLastError();
 }
 
@@ -328,6 +334,7 @@ static hipError_t dispatch_variant(int var, const RoundArgs& a, int groups, hipS
     case 4: return launch_round_t<float, 4, 0, GRAD, MET, 4>(a, groups, s);
     case 6: return launch_round_t<float, 4, 0, GRAD, MET, 6>(a, groups, s);
     case 7: return launch_round_t<float, 4, 0, GRAD, MET, 7>(a, groups, s);
+    case 11: return launch_round_t<float, 4, 0, GRAD, MET, 11>(a, groups, s);
     case 0: return launch_round_t<float, 4, 0, GRAD, MET, 0>(a, groups, s);
     default: return launch_round_t<float, 4, 0, GRAD, MET>(a, groups, s);
   }
@@ -394,7 +401,13 @@ __device__ __forceinline__ typename VT<T>::v ld_nt(const T* p) {
 // RPW = rows per wave held in registers (4 for <= 16 rows per worker, 16 for <= 64).
 // One barrier per block: the waves' gradient partials go to a double-buffered LDS
 // slot, every wave folds them and forms the new block itself (wave 0 stores it).
-template <typename T, int RPW, bool ZNEXT, bool MET>
+// LDS-only workgroup barrier: waits for this wave's LDS traffic, not for its global loads
+// (__syncthreads() also drains vmcnt, which would cancel the next block's prefetch).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <typename T, int RPW, bool ZNEXT, bool MET, bool PF>
 __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
   using V = typename VT<T>::v;
   constexpr int VN = VT<T>::n;
@@ -426,19 +439,39 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
   double cacc = 0.0;
   const T inv_eta = (T)a.eta, lam = (T)a.lam;
   int buf = 0;
+  V rn[RPW];  // PF: the next block's row segments, loaded one block ahead
+  if (PF) {
+    const int c = grp * 64 + lane;
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+      rn[r] = (grp < nblk && rowp[r] >= 0 && c < nch) ? ld_nt<T>(X + rowp[r] + (int64_t)c * VN) : V(0);
+  }
   for (int cb = grp; cb < nblk; cb += G, buf ^= 1) {
     const int c = cb * 64 + lane;
     const bool in = c < nch;
     V rv[RPW];
+    if (PF) {
+      const int cn = (cb + G) * 64 + lane;
+      const bool nin = cb + G < nblk && cn < nch;
 #pragma unroll
-    for (int r = 0; r < RPW; ++r) rv[r] = (rowp[r] >= 0 && in) ? ld_nt<T>(X + rowp[r] + (int64_t)c * VN) : V(0);
+      for (int r = 0; r < RPW; ++r) {
+        rv[r] = rn[r];
+        rn[r] = (nin && rowp[r] >= 0) ? ld_nt<T>(X + rowp[r] + (int64_t)cn * VN) : V(0);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) rv[r] = (rowp[r] >= 0 && in) ? ld_nt<T>(X + rowp[r] + (int64_t)c * VN) : V(0);
+    }
     const V own = in ? *(const V*)(own_p + (int64_t)c * VN) : V(0);
     const V xb = (MET && in) ? *(const V*)((const T*)a.xbar + (int64_t)c * VN) : V(0);
     V gp = V(0);
 #pragma unroll
     for (int r = 0; r < RPW; ++r) gp += coef[r] * rv[r];
     gred[buf][wave][lane] = gp;
-    __syncthreads();
+    if (PF)
+      lds_barrier();
+    else
+      __syncthreads();
     V g = V(0);
     if (nb > 0) g = (gred[buf][0][lane] + gred[buf][1][lane] + gred[buf][2][lane] + gred[buf][3][lane]) / (T)nb + lam * own;
     V xn = V(0);
@@ -578,17 +611,22 @@ hipError_t launch_split_step(int dtype, bool znext, bool met, const RoundArgs& a
   if (n_workers <= 0) return hipSuccess;
   const dim3 grid(n_workers, a.groups);
   const bool small = a.b_rows <= 4 * NW;  // rows per worker this step touches
-#define SPLIT_STEP(T_, R_)                                                                               \
-  if (znext && met) hipLaunchKernelGGL((k_split_step<T_, R_, true, true>), grid, dim3(NT), 0, s, a);     \
-  else if (znext) hipLaunchKernelGGL((k_split_step<T_, R_, true, false>), grid, dim3(NT), 0, s, a);      \
-  else if (met) hipLaunchKernelGGL((k_split_step<T_, R_, false, true>), grid, dim3(NT), 0, s, a);        \
-  else hipLaunchKernelGGL((k_split_step<T_, R_, false, false>), grid, dim3(NT), 0, s, a);
+  // A/B knob (tools/split_ab.py): next-block prefetch measured 1 % slower on C5, so off
+  const char* ev = getenv("DOPT_SPLIT_PREFETCH");
+  const bool pf = ev && ev[0] == '1';
+#define SPLIT_STEP2(T_, R_, P_)                                                                              \
+  if (znext && met) hipLaunchKernelGGL((k_split_step<T_, R_, true, true, P_>), grid, dim3(NT), 0, s, a);     \
+  else if (znext) hipLaunchKernelGGL((k_split_step<T_, R_, true, false, P_>), grid, dim3(NT), 0, s, a);      \
+  else if (met) hipLaunchKernelGGL((k_split_step<T_, R_, false, true, P_>), grid, dim3(NT), 0, s, a);        \
+  else hipLaunchKernelGGL((k_split_step<T_, R_, false, false, P_>), grid, dim3(NT), 0, s, a);
+#define SPLIT_STEP(T_, R_) if (pf) { SPLIT_STEP2(T_, R_, true) } else { SPLIT_STEP2(T_, R_, false) }
   if (dtype == 0) {
     if (small) { SPLIT_STEP(float, 4) } else { SPLIT_STEP(float, 16) }
   } else {
     if (small) { SPLIT_STEP(double, 4) } else { SPLIT_STEP(double, 16) }
   }
 #undef SPLIT_STEP
+#undef SPLIT_STEP2
   return hipGetLastError();
 }
 

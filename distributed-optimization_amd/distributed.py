@@ -156,6 +156,8 @@ class DistributedDSGD:
             w.wait()
 
     def _all_reduce(self, t):
+        if self.dist.get_world_size(self.group) == 1:
+            return
         if self.device_comm:
             self.dist.all_reduce(t, group=self.group)
         else:

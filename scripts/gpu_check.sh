@@ -21,6 +21,8 @@ for s in $STEPS; do
     dist2) step dist2 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --backend gloo --workers 1024 --steps 5 --warmup 1 ;;
     probe) step probe 120 ./tools/bw_probe ;;
     variants) step variants 600 python -u tools/kr_variants.py ;;
+    splitab) step splitab 600 python -u tools/split_ab.py ;;
+    phase1) step phase1 600 python -u bench.py --phase --no-cpu-baseline ;;
     c5)    step c5 600 python -u bench.py --config c5 --steps 5 --warmup 1 --no-cpu-baseline ;;
     c4)    step c4 900 python -u bench.py --config c4 --steps 5 --warmup 1 --no-cpu-baseline ;;
     mainpy) step mainpy 600 bash -c 'cd distributed-optimization_amd && MPLBACKEND=Agg python -u -c "import time, runpy; t=time.time(); import matplotlib; matplotlib.use(\"Agg\"); runpy.run_path(\"main.py\", run_name=\"__main__\"); print(\"main.py wall %.1f s\" % (time.time()-t))"' ;;
