@@ -62,6 +62,7 @@ int fail(int code, const char* fmt, ...) {
 
 constexpr size_t kStaging = 64ull << 20;  // host->device staging chunk
 constexpr int kRowsPerGroup = 64;         // column-sum partial group height (16 rows per wave)
+constexpr int64_t kLossChunk = 64;        // objective rows per workgroup in a separate metrics pass
 
 }  // namespace
 
@@ -124,7 +125,13 @@ struct dopt_ctx {
   double* part = nullptr;
   int groups = 0;
   double* slab_cons = nullptr;
-  double* slab_loss = nullptr;
+  double* slab_loss = nullptr;      // per worker (fused) or per 64-row chunk (metrics pass)
+  int64_t slab_cap = 0;
+  int64_t loss_groups = 0;          // valid entries of slab_loss from the last producer
+  int64_t* choff = nullptr;         // 64-row chunk offsets of the shard rows
+  int64_t n_chunks = 0;
+  int64_t* choff_o = nullptr;       // ... and of the separate objective dataset
+  int64_t n_chunks_o = 0;
 
   // topology
   bool have_topo = false;
@@ -239,6 +246,28 @@ int download_rows(dopt_ctx* c, const void* src, double* dst, int64_t rows, int64
   return DOPT_OK;
 }
 
+// Offsets of consecutive kLossChunk-row chunks of `rows` rows (device array).
+int make_chunks(dopt_ctx* c, int64_t rows, int64_t** dst, int64_t* count) {
+  const int64_t nc = (rows + kLossChunk - 1) / kLossChunk;
+  std::vector<int64_t> o((size_t)nc + 1);
+  for (int64_t k = 0; k <= nc; ++k) o[(size_t)k] = std::min(rows, k * kLossChunk);
+  int rc;
+  if ((rc = dalloc_t(dst, o.size() * sizeof(int64_t)))) return rc;
+  HIPOK(hipMemcpy(*dst, o.data(), o.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  *count = nc;
+  return DOPT_OK;
+}
+
+int ensure_slabs(dopt_ctx* c, int64_t need) {
+  need = std::max<int64_t>(need, 1);
+  if (need <= c->slab_cap && c->slab_loss) return DOPT_OK;
+  int rc;
+  if ((rc = dalloc_t(&c->slab_cons, (size_t)need * sizeof(double)))) return rc;
+  if ((rc = dalloc_t(&c->slab_loss, (size_t)need * sizeof(double)))) return rc;
+  c->slab_cap = need;
+  return DOPT_OK;
+}
+
 int alloc_state(dopt_ctx* c) {
   const size_t st = (size_t)std::max<int64_t>(1, c->n) * c->ld * c->esz;
   int rc;
@@ -256,8 +285,9 @@ int alloc_state(dopt_ctx* c) {
   c->xb = 0;
   c->groups = (int)((std::max<int64_t>(1, c->n) + kRowsPerGroup - 1) / kRowsPerGroup);
   if ((rc = dalloc_t(&c->part, (size_t)c->groups * c->ld * sizeof(double)))) return rc;
-  if ((rc = dalloc_t(&c->slab_cons, (size_t)std::max<int64_t>(1, c->n) * sizeof(double)))) return rc;
-  if ((rc = dalloc_t(&c->slab_loss, (size_t)std::max<int64_t>(1, c->n) * sizeof(double)))) return rc;
+  if ((rc = make_chunks(c, c->rows, &c->choff, &c->n_chunks))) return rc;
+  c->slab_cap = 0;
+  if ((rc = ensure_slabs(c, std::max(c->n, c->n_chunks)))) return rc;
   if ((rc = dalloc_t(&c->S, (size_t)c->ld * sizeof(double)))) return rc;
   HIPOK(hipMemsetAsync(c->S, 0, (size_t)c->ld * sizeof(double), c->stream));
   HIPOK(hipStreamSynchronize(c->stream));
@@ -335,19 +365,31 @@ RoundArgs base_args(dopt_ctx* c) {
 }
 
 // Metrics-only pass over the objective rows (shards or the separate dataset).
+// Metrics-only pass at `point` (xbar, or the shared iterate): the objective over the
+// objective rows in 64-row chunks (many workgroups even when there are few workers),
+// and ||x_i - point||^2 per worker.  (`shared` only says the point is the centralized
+// iterate; the loss is x . point either way.)
 int metrics_pass(dopt_ctx* c, const void* x_state, const void* point, bool shared, bool cons,
                  bool loss) {
-  RoundArgs a = base_args(c);
-  if (c->obj_sep) {
-    a.X = c->Xo;
-    a.y = c->yo;
-    a.off = c->offo;
+  (void)shared;
+  if (loss) {
+    RoundArgs a = base_args(c);
+    a.X = c->obj_sep ? c->Xo : c->X;
+    a.y = c->obj_sep ? c->yo : c->y;
+    a.off = c->obj_sep ? c->choff_o : c->choff;
+    a.w_shared = point;
+    a.flags |= F_LOSS | F_SHARED | F_LOSS_FROM_Z;
+    const int64_t nc = c->obj_sep ? c->n_chunks_o : c->n_chunks;
+    HIPOK(launch_round(c->dtype, c->problem, c->cpl, false, true, a, (int)nc, c->stream));
+    c->loss_groups = nc;
   }
-  a.x_old = x_state;
-  a.xbar = point;
-  a.w_shared = point;
-  a.flags |= (cons ? F_CONS : 0) | (loss ? F_LOSS : 0) | (shared ? (F_SHARED | F_LOSS_FROM_Z) : 0);
-  HIPOK(launch_round(c->dtype, c->problem, c->cpl, false, true, a, (int)c->n, c->stream));
+  if (cons) {
+    RoundArgs a = base_args(c);
+    a.x_old = x_state;
+    a.xbar = point;
+    a.flags |= F_CONS;
+    HIPOK(launch_round(c->dtype, c->problem, c->cpl, false, true, a, (int)c->n, c->stream));
+  }
   return DOPT_OK;
 }
 
@@ -374,9 +416,10 @@ void finalize_metrics(const double* raw, int64_t T, int problem, int64_t n, int6
   }
 }
 
-int history(dopt_ctx* c, int64_t h, const void* point, bool cons, bool loss, int64_t ng) {
-  HIPOK(launch_history(c->dtype, cons ? c->slab_cons : nullptr, loss ? c->slab_loss : nullptr, c->n, ng, point,
-                       c->ld, (int32_t)c->nch, loss, c->hraw + 3 * h, c->stream));
+int history(dopt_ctx* c, int64_t h, const void* point, bool cons, bool loss, int64_t ng_unused) {
+  (void)ng_unused;
+  HIPOK(launch_history(c->dtype, cons ? c->slab_cons : nullptr, loss ? c->slab_loss : nullptr, c->n,
+                       c->loss_groups, point, c->ld, (int32_t)c->nch, loss, c->hraw + 3 * h, c->stream));
   return DOPT_OK;
 }
 
@@ -463,6 +506,7 @@ int split_metrics(dopt_ctx* c, const void* x_state, const void* point, bool shar
   a.w_shared = point;
   a.xbar = point;
   a.flags = (cons ? F_CONS : 0) | (loss ? F_LOSS : 0) | (shared ? F_SHARED : 0);
+  if (a.flags & F_LOSS) c->loss_groups = c->n;  // per-worker loss slabs
   HIPOK(launch_split_dots(c->dtype, 1, a, (int)c->n, c->stream));
   HIPOK(launch_split_coef(c->dtype, c->problem, 2, a, (int)c->n, c->stream));
   return DOPT_OK;
@@ -512,6 +556,7 @@ int run_dsgd_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batc
     }
     const bool met = fused_met && metrics && h > 0;
     a.flags |= (met && want_cons ? F_CONS : 0) | (met && want_obj ? F_LOSS : 0);
+    if (a.flags & F_LOSS) c->loss_groups = c->n;  // per-worker loss slabs
     if (c->prof && (rc = prof_event(c, false))) return rc;
     HIPOK(launch_split_step(c->dtype, full, met, a, (int)c->n, c->stream));
     if (c->prof && (rc = prof_event(c, true))) return rc;
@@ -649,6 +694,8 @@ int dopt_destroy(dopt_ctx* c) {
     dfree(*p);
   dfree_t(c->off);
   dfree_t(c->offo);
+  dfree_t(c->choff);
+  dfree_t(c->choff_o);
   dfree_t(c->part);
   dfree_t(c->slab_cons);
   dfree_t(c->slab_loss);
@@ -744,6 +791,8 @@ int dopt_load_objective_data(dopt_ctx* c, int64_t n_rows, const void* X, const v
   if ((rc = dalloc_t(&c->offo, o.size() * sizeof(int64_t)))) return rc;
   HIPOK(hipMemcpy(c->offo, o.data(), o.size() * sizeof(int64_t), hipMemcpyHostToDevice));
   c->rows_o = n_rows;
+  if ((rc = make_chunks(c, n_rows, &c->choff_o, &c->n_chunks_o))) return rc;
+  if ((rc = ensure_slabs(c, std::max(c->n, c->n_chunks_o)))) return rc;
   c->obj_sep = true;
   return DOPT_OK;
 }
@@ -886,6 +935,7 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
     a.lam = lam_grad;
     const bool met = fused && metrics && h > 0;
     a.flags |= F_STEP | (met && want_cons ? F_CONS : 0) | (met && want_obj ? F_LOSS : 0);
+    if (a.flags & F_LOSS) c->loss_groups = c->n;  // per-worker loss slabs
     if (c->prof && (rc = prof_event(c, false))) return rc;
     HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, met, a, (int)c->n, c->stream));
     if (c->prof && (rc = prof_event(c, true))) return rc;
@@ -940,6 +990,7 @@ int dopt_run_centralized(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_
     a.lam = lam_grad;
     const bool met = fused && want_obj && h > 0;
     a.flags |= F_GOUT | F_SHARED | (met ? (F_LOSS | F_LOSS_FROM_Z) : 0);
+    if (a.flags & F_LOSS) c->loss_groups = c->n;  // per-worker loss slabs
     if (c->prof && (rc = prof_event(c, false))) return rc;
     HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, met, a, (int)c->n, c->stream));
     if (c->prof && (rc = prof_event(c, true))) return rc;
@@ -1214,6 +1265,7 @@ int dopt_phase_grad(dopt_ctx* c, int64_t batch, const int32_t* idx, double lam_g
   a.xbar = c->xbar[c->xb];
   a.lam = lam_grad;
   a.flags |= F_GOUT | (cons ? F_CONS : 0) | (loss ? F_LOSS : 0);
+  if (a.flags & F_LOSS) c->loss_groups = c->n;  // per-worker loss slabs
   if (c->prof && (rc = prof_event(c, false))) return rc;
   HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, cons || loss, a, (int)c->n, c->stream));
   if (c->prof && (rc = prof_event(c, true))) return rc;
@@ -1236,6 +1288,7 @@ int dopt_phase_mix(dopt_ctx* c, int64_t t, double eta0) {
     a.lam = c->ph_lam;
     a.xbar = c->xbar[c->xb];
     a.flags |= (cons ? F_CONS : 0) | (loss ? F_LOSS : 0);
+    if (a.flags & F_LOSS) c->loss_groups = c->n;  // per-worker loss slabs
     int rc;
     if (c->prof && (rc = prof_event(c, false))) return rc;
     HIPOK(launch_split_step(c->dtype, full, cons || loss, a, (int)c->n, c->stream));
@@ -1270,6 +1323,7 @@ int dopt_phase_grad_shared(dopt_ctx* c, int64_t batch, const int32_t* idx, doubl
   a.g_out = c->G;
   a.lam = lam_grad;
   a.flags |= F_GOUT | F_SHARED | (fuse_loss ? (F_LOSS | F_LOSS_FROM_Z) : 0);
+  if (a.flags & F_LOSS) c->loss_groups = c->n;  // per-worker loss slabs
   if (c->split) {
     if (fuse_loss) return fail(DOPT_ERR_UNSUPPORTED, "column-blocked rounds: use dopt_phase_metrics_pass_shared");
     if ((rc = ensure_split(c))) return rc;
@@ -1316,8 +1370,8 @@ int dopt_phase_metrics_pass_shared(dopt_ctx* c) {
 
 int dopt_phase_metrics_shared(dopt_ctx* c, int include_xnorm, double* out_dev) {
   CHECK_ARG(c && out_dev, "NULL argument");
-  HIPOK(launch_history(c->dtype, nullptr, c->slab_loss, c->n, c->n, c->xg[c->gcur], c->ld, (int32_t)c->nch,
-                       include_xnorm != 0, out_dev, c->stream));
+  HIPOK(launch_history(c->dtype, nullptr, c->slab_loss, c->n, c->loss_groups, c->xg[c->gcur], c->ld,
+                       (int32_t)c->nch, include_xnorm != 0, out_dev, c->stream));
   return DOPT_OK;
 }
 
@@ -1354,8 +1408,9 @@ int dopt_phase_metrics_pass(dopt_ctx* c, uint32_t flags) {
 int dopt_phase_metrics(dopt_ctx* c, uint32_t flags, int include_xnorm, double* out_dev) {
   CHECK_ARG(c && out_dev, "NULL argument");
   const bool cons = flags & DOPT_RUN_CONSENSUS, loss = flags & DOPT_RUN_OBJECTIVE;
-  HIPOK(launch_history(c->dtype, cons ? c->slab_cons : nullptr, loss ? c->slab_loss : nullptr, c->n, c->n,
-                       c->xbar[c->xb], c->ld, (int32_t)c->nch, loss && include_xnorm, out_dev, c->stream));
+  HIPOK(launch_history(c->dtype, cons ? c->slab_cons : nullptr, loss ? c->slab_loss : nullptr, c->n,
+                       c->loss_groups, c->xbar[c->xb], c->ld, (int32_t)c->nch, loss && include_xnorm, out_dev,
+                       c->stream));
   return DOPT_OK;
 }
 
