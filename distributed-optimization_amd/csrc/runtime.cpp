@@ -1118,6 +1118,7 @@ int dopt_eval_full(dopt_ctx* c, const double* w, double reg, double* f_out, doub
   a.g_out = c->G;
   a.flags = F_GOUT | F_GSUM | F_SHARED | F_LOSS | F_LOSS_FROM_Z;
   HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, true, a, (int)c->n, c->stream));
+  c->loss_groups = c->n;  // per-worker loss slabs
   HIPOK(launch_colsum_partial(c->dtype, c->G, c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part, nullptr,
                               c->stream));
   if ((rc = history(c, 0, a.w_shared, false, true, c->n))) return rc;
