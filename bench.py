@@ -213,7 +213,7 @@ def main():
     while cpl * 64 < (d + (16 // esz) - 1) // (16 // esz):
         cpl *= 2
     if cpl <= 16:
-        kname = (f"void dopt::k_round<{tname}, {cpl}, {0 if problem == 'logistic' else 1}, true, true, 3>"
+        kname = (f"void dopt::k_round<{tname}, {cpl}, {0 if problem == 'logistic' else 1}, true, true, 35>"
                  "(dopt::RoundArgs)")
     else:
         kname = f"void dopt::k_split_step<{tname}, {4 if m <= 16 else 16}, true, true>(dopt::RoundArgs)"

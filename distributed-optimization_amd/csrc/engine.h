@@ -55,6 +55,7 @@ struct RoundArgs {
   double* cpart;          // [n x groups] partial ||x_i - xbar||^2
   int32_t bcap;           // row capacity per worker in coef / partials
   int32_t b_rows;         // max rows per worker a column-blocked step touches (picks the kernel)
+  int32_t pre_rows;       // CSR rows per worker prefetched to LDS by the fused kernel (0: off)
   int32_t groups;         // column-block groups = gridDim.y
 };
 

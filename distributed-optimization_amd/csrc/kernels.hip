@@ -153,8 +153,11 @@ __device__ __forceinline__ typename VT<T>::v mix_chunk(const RoundArgs& a, int i
 // VAR: bit 0 nontemporal row loads (rows are read once per round: +11 % on MI355X,
 // 6.28 -> 7.15 TB/s on the bare access pattern, tools/bw_probe.hip), bit 1 DPP wave
 // reduction (readlane to an SGPR; ~0.5-1 %), bit 2 twice the rows in flight (no gain).
-// Default 3; the others stay reachable through DOPT_KR_VARIANT for A/B runs.
-constexpr int KR_DEFAULT_VAR = 3;
+// bit 3 persistent workgroups (-2 %: loses the dispatcher's dynamic balancing), bit 4 CSR
+// rows prefetched to LDS (null), bit 5 software-pipelined row loop (-0.9 %, adopted).
+// Default 35 = NT + DPP + pipelined; the others stay reachable through DOPT_KR_VARIANT
+// for A/B runs (tools/kr_variants.py).
+constexpr int KR_DEFAULT_VAR = 35;
 template <typename T, int CPL, int PROB, bool GRAD, bool MET, int VAR = KR_DEFAULT_VAR>
 __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
   using V = typename VT<T>::v;
@@ -177,6 +180,20 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
   const T* __restrict__ X = (const T*)a.X;
   const T* __restrict__ Y = (const T*)a.y;
   const T* wsrc = (flags & F_SHARED) ? (const T*)a.w_shared : (const T*)a.x_old + (int64_t)i * ld;
+  // VAR bit 4: the CSR rows of the mix (x_old, fixed during the round) go to LDS right away,
+  // overlapping the row stream, so the epilogue touches no global memory but the store.
+  constexpr bool PRE = (VAR & 16) != 0;
+  V* nbuf = (V*)(smem + (size_t)NW * nch * 16 + 64);  // after red + sred
+  const int64_t pe0 = a.rp ? a.rp[i] : 0, pe1 = a.rp ? a.rp[i + 1] : 0;
+  const bool pre = PRE && GRAD && (flags & F_STEP) && !(flags & F_MEAN) && (pe1 - pe0) <= a.pre_rows;
+  if (pre) {
+    for (int64_t e = pe0; e < pe1; ++e) {
+      const int col = a.ci[e];
+      const T* src = col < a.n_local ? (const T*)a.x_old + (int64_t)col * ld
+                                     : (const T*)a.halo + (int64_t)(col - a.n_local) * ld;
+      for (int c = threadIdx.x; c < nch; c += NT) nbuf[(e - pe0) * nch + c] = *(const V*)(src + (int64_t)c * VN);
+    }
+  }
 
   const bool loss_from_z = (flags & F_LOSS_FROM_Z) != 0;
   const bool want_loss = MET && (flags & F_LOSS);
@@ -197,7 +214,51 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
   }
   double loss = 0.0;
 
-  if (compute_z || compute_u) {
+  // VAR bit 5: software-pipelined row loop -- row k+1's loads are issued before row k's
+  // dot / reduction / accumulate, so a wave never sits with nothing in flight (same
+  // two row buffers of registers as the default RB = 2 loop).
+  constexpr bool PIPE = (VAR & 32) != 0 && CPL <= 4;  // same registers as RB = 2 only there
+  if (PIPE && (compute_z || compute_u)) {
+    auto load_row = [&](int64_t rr, V (&dst)[CPL], T& yd) {
+      int64_t lr = rr;
+      if (GRAD && a.idx) lr = a.idx[(int64_t)i * a.b + rr];
+      const T* xp = X + (row0 + lr) * ld;
+      yd = Y[row0 + lr];
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) {
+        const int c = lane + 64 * j;
+        dst[j] = c < nch ? ((VAR & 1) ? __builtin_nontemporal_load((const V*)(xp + (int64_t)c * VN))
+                                      : *(const V*)(xp + (int64_t)c * VN))
+                         : V(0);
+      }
+    };
+    V cur[CPL], nxt[CPL];
+    T ycur = T(0), ynxt = T(0);
+    int64_t r = wave;
+    if (r < nb) load_row(r, cur, ycur);
+    for (; r < nb; r += NW) {
+      if (r + NW < nb) load_row(r + NW, nxt, ynxt);
+      V az = V(0), au = V(0);
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) {
+        if (compute_z) az += cur[j] * w[j];
+        if (compute_u) au += cur[j] * xb[j];
+      }
+      T z = hsum<T>(az), u = hsum<T>(au);
+      if (compute_z) z = (VAR & 2) ? wave_sum_dpp(z) : wave_sum(z);
+      if (compute_u) u = (VAR & 2) ? wave_sum_dpp(u) : wave_sum(u);
+      if (GRAD) {
+        const T coef = (PROB == 0) ? -ycur * sigmoid_neg(ycur * z) : z - ycur;
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) g[j] += coef * cur[j];
+      }
+      if (want_loss) loss += row_loss<T, PROB>(ycur, loss_from_z ? z : u);
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) cur[j] = nxt[j];
+      ycur = ynxt;
+    }
+  }
+  if (!PIPE && (compute_z || compute_u)) {
     for (int64_t r0 = (int64_t)wave * RB; r0 < nb; r0 += NW * RB) {
       V xr[RB][CPL];
       T yv[RB];
@@ -250,7 +311,7 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
   }
 
   V* red = (V*)smem;  // [NW][nch]
-  double* sred = (double*)(smem + (GRAD ? (size_t)NW * nch * 16 : 0));
+  double* sred = (double*)(smem + (GRAD ? (size_t)NW * nch * 16 : 0));  // 2*NW doubles (64 B)
   if (GRAD) {
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
@@ -286,7 +347,12 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
       const V wc = *(const V*)(wsrc + (int64_t)c * VN);
       const V gc = (flags & F_GSUM) ? s : ((nb > 0) ? (s / (T)nb + lam * wc) : V(0));
       if (flags & F_STEP) {
-        const V acc = mix_chunk<T>(a, i, c, wc);
+        V acc = V(0);
+        if (pre) {
+          for (int64_t e = pe0; e < pe1; ++e) acc += ((const T*)a.cw)[e] * nbuf[(e - pe0) * nch + c];
+        } else {
+          acc = mix_chunk<T>(a, i, c, wc);
+        }
         *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = acc - inv_eta * gc;
       } else if (flags & F_GOUT) {
         *(V*)((T*)a.g_out + (int64_t)i * ld + (int64_t)c * VN) = gc;
@@ -309,10 +375,11 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
 
 template <typename T, int CPL, int PROB, bool GRAD, bool MET, int VAR = KR_DEFAULT_VAR>
 static hipError_t launch_round_t(const RoundArgs& a, int groups, hipStream_t s) {
-  const size_t lds = (GRAD ? (size_t)NW * a.nchunks * 16 : 0) + 2 * NW * sizeof(double);
+  const size_t pre = (VAR & 16) ? (size_t)a.pre_rows * a.nchunks * 16 : 0;
+  const size_t lds = (GRAD ? (size_t)NW * a.nchunks * 16 + 64 + pre : 64);
   static bool attr_set = false;
   if (!attr_set) {
-    const size_t max_lds = (size_t)NW * MAX_CPL * 64 * 16 + 2 * NW * sizeof(double);
+    const size_t max_lds = 160 * 1024;
     hipError_t e = hipFuncSetAttribute((const void*)k_round<T, CPL, PROB, GRAD, MET, VAR>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds);
     if (e != hipSuccess) return e;
@@ -335,6 +402,7 @@ static hipError_t dispatch_variant(int var, const RoundArgs& a, int groups, hipS
     case 6: return launch_round_t<float, 4, 0, GRAD, MET, 6>(a, groups, s);
     case 7: return launch_round_t<float, 4, 0, GRAD, MET, 7>(a, groups, s);
     case 11: return launch_round_t<float, 4, 0, GRAD, MET, 11>(a, groups, s);
+    case 19: return launch_round_t<float, 4, 0, GRAD, MET, 19>(a, groups, s);
     case 0: return launch_round_t<float, 4, 0, GRAD, MET, 0>(a, groups, s);
     default: return launch_round_t<float, 4, 0, GRAD, MET>(a, groups, s);
   }

@@ -138,6 +138,7 @@ struct dopt_ctx {
   int64_t* rp = nullptr;
   int32_t* ci = nullptr;
   void* cw = nullptr;
+  int32_t max_row_nnz = 0;  // largest CSR row (mix prefetch sizing)
 
   // halo plan (multi-GPU): remote iterates land in `halo` (caller-owned device memory),
   // rows send_ids of the current iterates are gathered into `send` (caller-owned)
@@ -360,6 +361,7 @@ RoundArgs base_args(dopt_ctx* c) {
   a.cpart = c->cpart;
   a.bcap = (int32_t)c->bcap;
   a.b_rows = (int32_t)std::min<int64_t>(c->max_m, kSplitMaxRows);
+  a.pre_rows = (c->max_row_nnz <= 6 && !c->mean_mix) ? c->max_row_nnz : 0;
   a.groups = c->split_groups;
   return a;
 }
@@ -846,6 +848,9 @@ int dopt_set_topology(dopt_ctx* c, int64_t n_workers, const int64_t* row_ptr, co
       HIPOK(hipMemcpy(c->cw, wf.data(), (size_t)nnz * sizeof(float), hipMemcpyHostToDevice));
     }
   }
+  int64_t mx = 0;
+  for (int64_t i = 0; i < n_workers; ++i) mx = std::max(mx, row_ptr[i + 1] - row_ptr[i]);
+  c->max_row_nnz = (int32_t)std::min<int64_t>(mx, 1 << 30);
   c->have_topo = true;
   c->mean_mix = false;
   return DOPT_OK;
