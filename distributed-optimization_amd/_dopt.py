@@ -376,8 +376,9 @@ class Engine:
         return float(f[0]), g
 
     # -- profiling
-    def set_profiling(self, on):
-        check(lib().dopt_set_profiling(self._h, 1 if on else 0))
+    def set_profiling(self, on, every=1):
+        """HIP-event timing of the round kernel: every `every`-th launch (0 / False: off)."""
+        check(lib().dopt_set_profiling(self._h, int(every) if on else 0))
 
     def kernel_stats(self):
         n = ctypes.c_int64(0)

@@ -161,7 +161,10 @@ struct dopt_ctx {
 
   // profiling of k_round
   bool prof = false;
-  std::vector<hipEvent_t> ev;  // (start, stop) pairs around every gradient-kernel launch
+  int64_t prof_every = 1;      // bracket every k-th gradient-kernel launch (events cost ~30 us per pair)
+  int64_t prof_seq = 0;        // gradient-kernel launches seen while profiling
+  bool prof_skip = false;      // the current launch is not sampled
+  std::vector<hipEvent_t> ev;  // (start, stop) pairs around the sampled gradient-kernel launches
   int64_t prof_n = 0;          // pairs recorded since the last dopt_kernel_stats
 };
 
@@ -437,6 +440,8 @@ int upload_idx_chunk(dopt_ctx* c, const int32_t* idx, int64_t h0, int64_t nr, in
 }
 
 int prof_event(dopt_ctx* c, bool stop) {
+  if (!stop) c->prof_skip = (c->prof_seq++ % c->prof_every) != 0;
+  if (c->prof_skip) return DOPT_OK;
   const size_t k = (size_t)(2 * c->prof_n + (stop ? 1 : 0));
   while (c->ev.size() <= k) {
     hipEvent_t e;
@@ -1147,7 +1152,10 @@ int dopt_eval_full(dopt_ctx* c, const double* w, double reg, double* f_out, doub
 
 int dopt_set_profiling(dopt_ctx* c, int enable) {
   CHECK_ARG(c, "ctx is NULL");
+  CHECK_ARG(enable >= 0, "enable must be >= 0");
   c->prof = enable != 0;
+  c->prof_every = enable > 0 ? enable : 1;
+  c->prof_seq = 0;
   return DOPT_OK;
 }
 

@@ -230,9 +230,11 @@ int dopt_finalize_metrics(int problem, int64_t T, const double *raw, int64_t n_w
  * sklearn cannot handle (simulator.py:32-69). */
 int dopt_eval_full(dopt_ctx *ctx, const double *w, double reg, double *f_out, double *g_out);
 
-/* Device time of the last run's dominant kernel (the fused round kernel):
- * launches and summed milliseconds, measured with HIP events on the engine's
- * stream.  Used by bench.py for the roofline figure. */
+/* Device time of the dominant kernel (the fused round kernel) since the last call:
+ * sampled launches and their summed milliseconds, measured with HIP events on the
+ * engine's stream.  Used by bench.py for the roofline figure.
+ * dopt_set_profiling: 0 = off; k >= 1 = bracket every k-th launch with an event pair
+ * (a pair costs ~30 us of round time on MI355X, so bench.py samples). */
 int dopt_kernel_stats(dopt_ctx *ctx, int64_t *launches, double *total_ms);
 int dopt_set_profiling(dopt_ctx *ctx, int enable);
 
