@@ -75,6 +75,11 @@ _SIGS = {
     "dopt_phase_xbar": ([_P, _P], ctypes.c_int),
     "dopt_phase_metrics_pass": ([_P, ctypes.c_uint32], ctypes.c_int),
     "dopt_phase_metrics": ([_P, ctypes.c_uint32, ctypes.c_int, _P], ctypes.c_int),
+    "dopt_phase_cons": ([_P], ctypes.c_int),
+    "dopt_phase_fold": ([_P, _P, _P, _P, ctypes.c_int], ctypes.c_int),
+    "dopt_phase_loss_pass": ([_P, ctypes.c_int], ctypes.c_int),
+    "dopt_phase_colsum_fold": ([_P, _P, _P, _P, _P], ctypes.c_int),
+    "dopt_phase_mix_lagged": ([_P, _I64, _D, _P, ctypes.c_int], ctypes.c_int),
     "dopt_sync": ([_P], ctypes.c_int),
     "dopt_finalize_metrics": ([ctypes.c_int, _I64, _P, _I64, _I64, _D, _D, _P, _P], ctypes.c_int),
     "dopt_eval_full": ([_P, _P, _D, _P, _P], ctypes.c_int),
@@ -363,6 +368,26 @@ class Engine:
 
     def phase_metrics(self, flags, include_xnorm, out_ptr):
         check(lib().dopt_phase_metrics(self._h, int(flags), 1 if include_xnorm else 0, ctypes.c_void_p(out_ptr)))
+
+    def phase_cons(self):
+        check(lib().dopt_phase_cons(self._h))
+
+    def phase_fold(self, cons_ptr=None, xnorm_ptr=None, loss_ptr=None, slab=0):
+        """Device-side sums into the given device addresses (None: skip that output)."""
+        vp = lambda p: ctypes.c_void_p(p) if p else None  # noqa: E731
+        check(lib().dopt_phase_fold(self._h, vp(cons_ptr), vp(xnorm_ptr), vp(loss_ptr), int(slab)))
+
+    def phase_colsum_fold(self, sum_ptr, cons_ptr=None, xnorm_ptr=None, loss_ptr=None):
+        vp = lambda p: ctypes.c_void_p(p) if p else None  # noqa: E731
+        check(lib().dopt_phase_colsum_fold(self._h, ctypes.c_void_p(sum_ptr), vp(cons_ptr), vp(xnorm_ptr),
+                                           vp(loss_ptr)))
+
+    def phase_mix_lagged(self, t, eta0, sum_ptr, consensus=True):
+        check(lib().dopt_phase_mix_lagged(self._h, int(t), float(eta0), ctypes.c_void_p(sum_ptr),
+                                          1 if consensus else 0))
+
+    def phase_loss_pass(self, two_points):
+        check(lib().dopt_phase_loss_pass(self._h, 1 if two_points else 0))
 
     def sync(self):
         check(lib().dopt_sync(self._h))

@@ -17,6 +17,7 @@ enum : int32_t {
   F_LOSS_FROM_Z = 32,  // the objective point IS the gradient point: reuse z = x.w
   F_MEAN = 64,         // complete graph: sum_j W_ij x_j = w_off (S - x_i) + W_ii x_i, S = column sums
   F_GSUM = 128,        // with F_GOUT: store the raw sum of coef * row (no 1/b, no lam) -- full gradients
+  F_LOSS2 = 256,       // metrics-only pass: also the objective at w_shared (from z) into slab_loss2
 };
 
 // One workgroup per worker (or per objective-row chunk).  All pointers are
@@ -37,6 +38,7 @@ struct RoundArgs {
   const void* cw;         // T-typed weights
   double* slab_cons;      // [n] per-workgroup partial sums (deterministic two-stage reduction)
   double* slab_loss;      // [n]
+  double* slab_loss2;     // [n] second objective point (F_LOSS2)
   double eta;             // eta0 / sqrt(t+1)  (trainer.py:138-140)
   double lam;             // gradient regulariser (worker.py:36-42)
   const void* halo;       // [n_halo x ld] remote iterates (multi-GPU); CSR columns >= n_local index it
@@ -57,6 +59,29 @@ struct RoundArgs {
   int32_t b_rows;         // max rows per worker a column-blocked step touches (picks the kernel)
   int32_t pre_rows;       // CSR rows per worker prefetched to LDS by the fused kernel (0: off)
   int32_t groups;         // column-block groups = gridDim.y
+  // multi-GPU send rows written by k_mix: worker i's new row also goes to send rows
+  // sslot[sptr[i] .. sptr[i+1]) (null sptr: no halo plan)
+  const int64_t* sptr;
+  const int32_t* sslot;
+  void* send;
+  // lagged multi-GPU mix: xbar of x_old from the all-reduced column sums xsum / xsum_n, written
+  // to xbar_out, and the per-worker consensus ||x_old[i] - xbar||^2 into slab_cons (if non-null)
+  const double* xsum;
+  double xsum_n;
+  void* xbar_out;
+};
+
+// History fold riding a k_colsum_final launch (one extra block): *out_c = sum sc[0:nc],
+// *out_l = sum sl[0:nl], *out_q = ||xbar||^2 (T-typed xbar); null outputs are skipped.
+struct FoldArgs {
+  const double* sc;
+  int64_t nc;
+  const double* sl;
+  int64_t nl;
+  const void* xbar;
+  double* out_c;
+  double* out_l;
+  double* out_q;
 };
 
 // Kernel launchers (kernels.hip).  dtype: 0 = float, 1 = double.
@@ -86,9 +111,10 @@ hipError_t launch_colsum_partial(int dtype, const void* x, int64_t n, int64_t ld
 // out = sum_g part / n (mode 0, the average model, trainer.py:182), or
 // out = base - eta * (sum_g part / n) (mode 1, centralized update, trainer.py:53-57);
 // with raw != null the column sums themselves go to raw[ld] (float64) instead.
+// With fold != null one extra block also folds the history slabs (FoldArgs).
 hipError_t launch_colsum_final(int dtype, const double* part, int32_t groups, int64_t n, int64_t ld,
                                int32_t nchunks, void* out, const void* base, double eta, int mode,
-                               hipStream_t s, double* raw = nullptr);
+                               hipStream_t s, double* raw = nullptr, const FoldArgs* fold = nullptr);
 // Raw metric sums of one round (one workgroup, fixed reduction order):
 // out[0] = sum(slab_cons[0:n]), out[1] = sum(slab_loss[0:ng]), out[2] = ||xbar||^2 (0 if !xnorm).
 // The host turns them into history values (runtime.cpp: finish_metrics) after any
@@ -96,6 +122,14 @@ hipError_t launch_colsum_final(int dtype, const double* part, int32_t groups, in
 hipError_t launch_history(int dtype, const double* slab_cons, const double* slab_loss, int64_t n,
                           int64_t ng, const void* xbar, int64_t ld, int32_t nchunks, bool xnorm,
                           double* out, hipStream_t s);
+// The same fold with separate (nullable) outputs: *out_c = sum sc[0:nc], *out_l = sum sl[0:nl],
+// *out_q = ||xbar||^2; null outputs are left alone (the lagged multi-GPU schedule folds the
+// consensus of one round and the objective of another in one launch).
+hipError_t launch_fold(int dtype, const double* sc, int64_t nc, const double* sl, int64_t nl, const void* xbar,
+                       int64_t ld, int32_t nchunks, double* out_c, double* out_l, double* out_q, hipStream_t s);
+// slab[g] = sum_{i in [64g, 64g+64)} ||x_i - xbar||^2, g < ceil(n / 64) (trainer.py:185).
+hipError_t launch_cons(int dtype, const void* x, const void* xbar, int64_t n, int64_t ld, int32_t nchunks,
+                       double* slab, hipStream_t s);
 // x_next[i] = sum_e cw[e] * src(ci[e]) - eta * G[i]  (trainer.py:173-175), src = x_old or halo.
 hipError_t launch_mix(int dtype, const RoundArgs& a, const void* G, int n_workers, hipStream_t s);
 // dst[k] = x[ids[k]] rows (halo send buffer).

@@ -28,6 +28,7 @@
 // reproducible.
 #include <math.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <type_traits>
 
@@ -51,6 +52,8 @@ struct VT<double> {
 constexpr int NW = 4;         // waves per workgroup
 constexpr int NT = NW * 64;   // threads per workgroup
 constexpr int MAX_CPL = 16;   // 16-byte chunks per lane: d <= 4096 (fp32) / 2048 (fp64)
+constexpr int SRED = 3 * NW * 8;  // k_round LDS: per-wave consensus / loss / second-loss partials
+static_assert(NW == 4, "k_cons folds four wave sums");
 
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
@@ -183,7 +186,7 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
   // VAR bit 4: the CSR rows of the mix (x_old, fixed during the round) go to LDS right away,
   // overlapping the row stream, so the epilogue touches no global memory but the store.
   constexpr bool PRE = (VAR & 16) != 0;
-  V* nbuf = (V*)(smem + (size_t)NW * nch * 16 + 64);  // after red + sred
+  V* nbuf = (V*)(smem + (size_t)NW * nch * 16 + SRED);  // after red + sred
   const int64_t pe0 = a.rp ? a.rp[i] : 0, pe1 = a.rp ? a.rp[i + 1] : 0;
   const bool pre = PRE && GRAD && (flags & F_STEP) && !(flags & F_MEAN) && (pe1 - pe0) <= a.pre_rows;
   if (pre) {
@@ -198,7 +201,9 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
   const bool loss_from_z = (flags & F_LOSS_FROM_Z) != 0;
   const bool want_loss = MET && (flags & F_LOSS);
   const bool want_cons = MET && (flags & F_CONS);
-  const bool compute_z = GRAD || (want_loss && loss_from_z);
+  // F_LOSS2 (metrics-only passes): a second objective at w_shared from z, next to the one at xbar
+  const bool want_loss2 = MET && !GRAD && (flags & F_LOSS2);
+  const bool compute_z = GRAD || (want_loss && loss_from_z) || want_loss2;
   const bool compute_u = want_loss && !loss_from_z;
   const bool need_w = compute_z || want_cons;
   const bool need_xb = compute_u || want_cons;
@@ -212,7 +217,7 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
     xb[j] = (need_xb && in) ? *(const V*)((const T*)a.xbar + (int64_t)c * VN) : V(0);
     g[j] = V(0);
   }
-  double loss = 0.0;
+  double loss = 0.0, loss2 = 0.0;
 
   // VAR bit 5: software-pipelined row loop -- row k+1's loads are issued before row k's
   // dot / reduction / accumulate, so a wave never sits with nothing in flight (same
@@ -253,6 +258,7 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
         for (int j = 0; j < CPL; ++j) g[j] += coef * cur[j];
       }
       if (want_loss) loss += row_loss<T, PROB>(ycur, loss_from_z ? z : u);
+      if (want_loss2) loss2 += row_loss<T, PROB>(ycur, z);
 #pragma unroll
       for (int j = 0; j < CPL; ++j) cur[j] = nxt[j];
       ycur = ynxt;
@@ -305,13 +311,14 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
             for (int j = 0; j < CPL; ++j) g[j] += coef * xr[k][j];
           }
           if (want_loss) loss += row_loss<T, PROB>(yv[k], loss_from_z ? z[k] : u[k]);
+          if (want_loss2) loss2 += row_loss<T, PROB>(yv[k], z[k]);
         }
       }
     }
   }
 
   V* red = (V*)smem;  // [NW][nch]
-  double* sred = (double*)(smem + (GRAD ? (size_t)NW * nch * 16 : 0));  // 2*NW doubles (64 B)
+  double* sred = (double*)(smem + (GRAD ? (size_t)NW * nch * 16 : 0));  // 3*NW doubles (SRED bytes)
   if (GRAD) {
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
@@ -333,6 +340,7 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
     if (lane == 0) {
       sred[wave] = cons;
       sred[NW + wave] = loss;
+      sred[2 * NW + wave] = loss2;
     }
   }
   __syncthreads();
@@ -360,14 +368,16 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
     }
   }
   if (MET && threadIdx.x == 0) {
-    double cs = 0.0, ls = 0.0;
+    double cs = 0.0, ls = 0.0, l2 = 0.0;
 #pragma unroll
     for (int q = 0; q < NW; ++q) {
       cs += sred[q];
       ls += sred[NW + q];
+      l2 += sred[2 * NW + q];
     }
     if (want_cons) a.slab_cons[i] = cs;
     if (want_loss) a.slab_loss[i] = ls;
+    if (want_loss2) a.slab_loss2[i] = l2;
   }
   if (VAR & 8) __syncthreads();  // LDS of this worker's epilogue is reused by the next
   }
@@ -376,7 +386,7 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
 template <typename T, int CPL, int PROB, bool GRAD, bool MET, int VAR = KR_DEFAULT_VAR>
 static hipError_t launch_round_t(const RoundArgs& a, int groups, hipStream_t s) {
   const size_t pre = (VAR & 16) ? (size_t)a.pre_rows * a.nchunks * 16 : 0;
-  const size_t lds = (GRAD ? (size_t)NW * a.nchunks * 16 + 64 + pre : 64);
+  const size_t lds = (GRAD ? (size_t)NW * a.nchunks * 16 + SRED + pre : SRED);
   static bool attr_set = false;
   if (!attr_set) {
     const size_t max_lds = 160 * 1024;
@@ -779,12 +789,59 @@ __global__ __launch_bounds__(NT) void k_colsum_part(const T* __restrict__ x, int
   }
 }
 
+// The history fold of k_history by one NT-thread block (fixed order): *out_c = sum sc[0:nc],
+// *out_l = sum sl[0:nl], *out_q = ||xbar||^2; null outputs are skipped.
+template <typename T>
+__device__ void fold_block(const FoldArgs& f, int nch, double (*red)[64 * VT<T>::n]) {
+  constexpr int VN = VT<T>::n;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double a = 0.0, b = 0.0, q = 0.0;
+  if (f.sc && f.out_c)
+    for (int64_t k = threadIdx.x; k < f.nc; k += NT) a += f.sc[k];
+  if (f.sl && f.out_l)
+    for (int64_t k = threadIdx.x; k < f.nl; k += NT) b += f.sl[k];
+  if (f.xbar && f.out_q)
+    for (int c = threadIdx.x; c < nch; c += NT)
+#pragma unroll
+      for (int e = 0; e < VN; ++e) {
+        const double v = (double)((const T*)f.xbar)[(int64_t)c * VN + e];
+        q += v * v;
+      }
+  a = wave_sum(a);
+  b = wave_sum(b);
+  q = wave_sum(q);
+  if (lane == 0) {
+    red[wave][0] = a;
+    red[wave][1] = b;
+    red[wave][2] = q;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double sa = 0.0, sb = 0.0, sq = 0.0;
+    for (int k = 0; k < NW; ++k) {
+      sa += red[k][0];
+      sb += red[k][1];
+      sq += red[k][2];
+    }
+    if (f.out_c) *f.out_c = sa;
+    if (f.out_l) *f.out_l = sb;
+    if (f.out_q) *f.out_q = sq;
+  }
+}
+
+// Stage 2 (+ optionally, in one extra block, the history fold of the previous round's slabs:
+// it rides this launch instead of a k_history launch of its own).
 template <typename T>
 __global__ __launch_bounds__(NT) void k_colsum_final(const double* __restrict__ part, int groups,
                                                      int64_t n, int64_t ld, int nch, T* out,
-                                                     const T* base, double eta, int mode, double* raw) {
+                                                     const T* base, double eta, int mode, double* raw,
+                                                     const FoldArgs fold) {
   constexpr int VN = VT<T>::n;
   __shared__ double red[NW][64 * VN];
+  if ((int)blockIdx.x == (nch + 63) / 64) {  // the fold block
+    fold_block<T>(fold, nch, red);
+    return;
+  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   double acc[VN];
@@ -845,32 +902,38 @@ hipError_t launch_colsum_partial(int dtype, const void* x, int64_t n, int64_t ld
 
 hipError_t launch_colsum_final(int dtype, const double* part, int32_t groups, int64_t n, int64_t ld,
                                int32_t nchunks, void* out, const void* base, double eta, int mode,
-                               hipStream_t s, double* raw) {
-  const dim3 grid((nchunks + 63) / 64);
+                               hipStream_t s, double* raw, const FoldArgs* fold) {
+  FoldArgs f;
+  memset(&f, 0, sizeof(f));
+  if (fold) f = *fold;
+  const dim3 grid((nchunks + 63) / 64 + (fold ? 1 : 0));
   if (dtype == 0)
     hipLaunchKernelGGL(k_colsum_final<float>, grid, dim3(NT), 0, s, part, groups, n, ld, nchunks,
-                       (float*)out, (const float*)base, eta, mode, raw);
+                       (float*)out, (const float*)base, eta, mode, raw, f);
   else
     hipLaunchKernelGGL(k_colsum_final<double>, grid, dim3(NT), 0, s, part, groups, n, ld, nchunks,
-                       (double*)out, (const double*)base, eta, mode, raw);
+                       (double*)out, (const double*)base, eta, mode, raw, f);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------- history
 constexpr int NTH = 1024;  // k_history: 16 waves, so each thread folds only a few slabs
+// Folds slabs into history sums: *out_c = sum sc[0:nc], *out_l = sum sl[0:nl],
+// *out_q = ||xbar||^2.  A null input contributes 0; a null output is not written, so the
+// consensus of one round and the objective of another can be folded by one launch.
 template <typename T>
-__global__ __launch_bounds__(NTH) void k_history(const double* sc, const double* sl, int64_t n,
-                                                 int64_t ng, const T* xbar, int64_t ld, int nch,
-                                                 int xnorm, double* out) {
+__global__ __launch_bounds__(NTH) void k_history(const double* sc, int64_t nc, const double* sl, int64_t nl,
+                                                 const T* xbar, int64_t ld, int nch, double* out_c,
+                                                 double* out_l, double* out_q) {
   constexpr int VN = VT<T>::n;
   constexpr int NWH = NTH / 64;
   __shared__ double part[3][NWH];
   double a = 0.0, b = 0.0, q = 0.0;
-  if (sc)
-    for (int64_t k = threadIdx.x; k < n; k += NTH) a += sc[k];
-  if (sl)
-    for (int64_t k = threadIdx.x; k < ng; k += NTH) b += sl[k];
-  if (xnorm)
+  if (sc && out_c)
+    for (int64_t k = threadIdx.x; k < nc; k += NTH) a += sc[k];
+  if (sl && out_l)
+    for (int64_t k = threadIdx.x; k < nl; k += NTH) b += sl[k];
+  if (xbar && out_q)
     for (int c = threadIdx.x; c < nch; c += NTH)
 #pragma unroll
       for (int e = 0; e < VN; ++e) {
@@ -894,21 +957,67 @@ __global__ __launch_bounds__(NTH) void k_history(const double* sc, const double*
       sb += part[1][k];
       sq += part[2][k];
     }
-    out[0] = sa;
-    out[1] = sb;
-    out[2] = sq;
+    if (out_c) *out_c = sa;
+    if (out_l) *out_l = sb;
+    if (out_q) *out_q = sq;
   }
+}
+
+hipError_t launch_fold(int dtype, const double* sc, int64_t nc, const double* sl, int64_t nl, const void* xbar,
+                       int64_t ld, int32_t nchunks, double* out_c, double* out_l, double* out_q, hipStream_t s) {
+  if (dtype == 0)
+    hipLaunchKernelGGL(k_history<float>, dim3(1), dim3(NTH), 0, s, sc, nc, sl, nl, (const float*)xbar, ld,
+                       nchunks, out_c, out_l, out_q);
+  else
+    hipLaunchKernelGGL(k_history<double>, dim3(1), dim3(NTH), 0, s, sc, nc, sl, nl, (const double*)xbar, ld,
+                       nchunks, out_c, out_l, out_q);
+  return hipGetLastError();
 }
 
 hipError_t launch_history(int dtype, const double* slab_cons, const double* slab_loss, int64_t n,
                           int64_t ng, const void* xbar, int64_t ld, int32_t nchunks, bool xnorm,
                           double* out, hipStream_t s) {
+  return launch_fold(dtype, slab_cons, n, slab_loss, ng, xnorm ? xbar : nullptr, ld, nchunks, out, out + 1,
+                     out + 2, s);
+}
+
+// ---------------------------------------------------------------------------- consensus
+// slab[g] = sum over workers i in [64 g, 64 g + 64) of ||x_i - xbar||^2 (trainer.py:185),
+// fp64, fixed order: wave w takes workers 64 g + w + 4 k, the 4 wave sums meet in LDS.
+// Per-worker terms are formed exactly as the fused k_round pass forms them.
+template <typename T>
+__global__ __launch_bounds__(NT) void k_cons(const T* __restrict__ x, const T* __restrict__ xbar, int64_t n,
+                                             int64_t ld, int nch, double* __restrict__ slab) {
+  using V = typename VT<T>::v;
+  constexpr int VN = VT<T>::n;
+  __shared__ double red[NW];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t i0 = (int64_t)blockIdx.x * 64;
+  const int64_t i1 = (i0 + 64 < n) ? i0 + 64 : n;
+  double acc = 0.0;
+  for (int64_t i = i0 + wave; i < i1; i += NW) {
+    V dv = V(0);
+    for (int c = lane; c < nch; c += 64) {
+      const V t = *(const V*)(x + i * ld + (int64_t)c * VN) - *(const V*)(xbar + (int64_t)c * VN);
+      dv += t * t;
+    }
+    acc += wave_sum((double)hsum<T>(dv));
+  }
+  if (lane == 0) red[wave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) slab[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+hipError_t launch_cons(int dtype, const void* x, const void* xbar, int64_t n, int64_t ld, int32_t nchunks,
+                       double* slab, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((n + 63) / 64));
   if (dtype == 0)
-    hipLaunchKernelGGL(k_history<float>, dim3(1), dim3(NTH), 0, s, slab_cons, slab_loss, n, ng,
-                       (const float*)xbar, ld, nchunks, xnorm ? 1 : 0, out);
+    hipLaunchKernelGGL(k_cons<float>, grid, dim3(NT), 0, s, (const float*)x, (const float*)xbar, n, ld, nchunks,
+                       slab);
   else
-    hipLaunchKernelGGL(k_history<double>, dim3(1), dim3(NTH), 0, s, slab_cons, slab_loss, n, ng,
-                       (const double*)xbar, ld, nchunks, xnorm ? 1 : 0, out);
+    hipLaunchKernelGGL(k_cons<double>, grid, dim3(NT), 0, s, (const double*)x, (const double*)xbar, n, ld,
+                       nchunks, slab);
   return hipGetLastError();
 }
 
@@ -925,11 +1034,28 @@ __global__ __launch_bounds__(NT) void k_mix(const RoundArgs a, const T* __restri
   if (i >= n) return;
   const int64_t ld = a.ld;
   const T eta = (T)a.eta;
+  V dv = V(0);  // consensus term of x_old[i] (a.xsum): formed exactly as k_round's F_CONS forms it
   for (int c = lane; c < a.nchunks; c += 64) {
     const V own = *(const V*)((const T*)a.x_old + (int64_t)i * ld + (int64_t)c * VN);
+    if (a.xsum) {  // xbar = (T)(column sum / n) of the iterates being mixed, as k_colsum_final rounds it
+      V xb;
+#pragma unroll
+      for (int e = 0; e < VN; ++e) xb[e] = (T)(a.xsum[(int64_t)c * VN + e] / a.xsum_n);
+      if (i == 0) *(V*)((T*)a.xbar_out + (int64_t)c * VN) = xb;
+      const V t = own - xb;
+      dv += t * t;
+    }
     const V acc = mix_chunk<T>(a, i, c, own);
     const V gc = *(const V*)(G + (int64_t)i * ld + (int64_t)c * VN);
-    *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = acc - eta * gc;
+    const V xn = acc - eta * gc;
+    *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = xn;
+    if (a.sptr)  // rows peers read next round: the send buffer is refreshed here, no gather kernel
+      for (int64_t s = a.sptr[i]; s < a.sptr[i + 1]; ++s)
+        *(V*)((T*)a.send + (int64_t)a.sslot[s] * ld + (int64_t)c * VN) = xn;
+  }
+  if (a.xsum && a.slab_cons) {
+    const double cs = wave_sum((double)hsum<T>(dv));
+    if (lane == 0) a.slab_cons[i] = cs;
   }
 }
 

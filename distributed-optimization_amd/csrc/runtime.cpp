@@ -126,6 +126,9 @@ struct dopt_ctx {
   int groups = 0;
   double* slab_cons = nullptr;
   double* slab_loss = nullptr;      // per worker (fused) or per 64-row chunk (metrics pass)
+  double* slab_loss_b = nullptr;    // second loss slab (lagged multi-GPU schedule, two-point pass)
+  int64_t slab_n[2] = {0, 0};       // valid entries of slab_loss / slab_loss_b (lagged schedule)
+  int64_t cons_n = 0;               // valid entries of slab_cons (per worker, or per 64 workers)
   int64_t slab_cap = 0;
   int64_t loss_groups = 0;          // valid entries of slab_loss from the last producer
   int64_t* choff = nullptr;         // 64-row chunk offsets of the shard rows
@@ -146,6 +149,9 @@ struct dopt_ctx {
   void* halo = nullptr;
   void* send = nullptr;
   int32_t* send_ids = nullptr;
+  int64_t* sptr = nullptr;   // send rows by worker: worker i's row goes to send rows sslot[sptr[i]..sptr[i+1])
+  int32_t* sslot = nullptr;
+  bool send_fresh = false;   // the last dopt_phase_mix already wrote the current iterates' send rows
 
   // per-run buffers
   int32_t* idx = nullptr;
@@ -268,6 +274,7 @@ int ensure_slabs(dopt_ctx* c, int64_t need) {
   int rc;
   if ((rc = dalloc_t(&c->slab_cons, (size_t)need * sizeof(double)))) return rc;
   if ((rc = dalloc_t(&c->slab_loss, (size_t)need * sizeof(double)))) return rc;
+  if ((rc = dalloc_t(&c->slab_loss_b, (size_t)need * sizeof(double)))) return rc;
   c->slab_cap = need;
   return DOPT_OK;
 }
@@ -324,6 +331,7 @@ int set_layout(dopt_ctx* c, int problem, int64_t n, int64_t d) {
   c->n_global = c->rows_global = 0;
   c->n_halo = c->n_send = 0;
   c->halo = c->send = nullptr;
+  c->send_fresh = false;
   return DOPT_OK;
 }
 
@@ -347,6 +355,7 @@ RoundArgs base_args(dopt_ctx* c) {
   a.nchunks = (int32_t)c->nch;
   a.slab_cons = c->slab_cons;
   a.slab_loss = c->slab_loss;
+  a.slab_loss2 = c->slab_loss_b;
   a.halo = c->halo;
   a.n_local = (int32_t)c->n;
   a.rp = c->rp;
@@ -706,6 +715,9 @@ int dopt_destroy(dopt_ctx* c) {
   dfree_t(c->part);
   dfree_t(c->slab_cons);
   dfree_t(c->slab_loss);
+  dfree_t(c->slab_loss_b);
+  dfree_t(c->sptr);
+  dfree_t(c->sslot);
   dfree_t(c->rp);
   dfree_t(c->ci);
   dfree_t(c->idx);
@@ -881,6 +893,7 @@ int dopt_set_mixing_mean(dopt_ctx* c, int64_t n_workers, double w_off, const dou
 }
 
 int dopt_set_models(dopt_ctx* c, const double* x) {
+  if (c) c->send_fresh = false;
   CHECK_ARG(c && x, "NULL argument");
   if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");
   int rc;
@@ -920,6 +933,7 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
   if ((rc = check_run(c, T, batch, idx, true))) return rc;
   if ((rc = set_device(c))) return rc;
   if ((rc = ensure_hist(c, T))) return rc;
+  c->send_fresh = false;
   const bool want_obj = flags & DOPT_RUN_OBJECTIVE, want_cons = flags & DOPT_RUN_CONSENSUS;
   const bool metrics = want_obj || want_cons;
   const bool fused = batch >= c->max_m && !c->obj_sep;
@@ -952,11 +966,13 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
     // xbar_{t+1} (trainer.py:182); the stamp marks the end of round t's update (trainer.py:181)
     HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur ^ 1], c->n, c->ld, (int32_t)c->nch, kRowsPerGroup,
                                 c->part, c->stamps + h + 1, c->stream));
+    // history[h-1] (this round's fused partials of x_h at xbar_h) rides the same launch
+    double* hr = met ? c->hraw + 3 * (h - 1) : c->hraw;
+    const FoldArgs fold = {want_cons ? c->slab_cons : nullptr, c->n, want_obj ? c->slab_loss : nullptr,
+                           c->loss_groups, want_obj ? c->xbar[xb] : nullptr, hr, hr + 1, hr + 2};
     HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, n_div(c), c->ld, (int32_t)c->nch, c->xbar[xb ^ 1],
-                              nullptr, 0.0, 0, c->stream, c->S));
-    if (met) {
-      if ((rc = history(c, h - 1, c->xbar[xb], want_cons, want_obj, c->n))) return rc;
-    } else if (!fused && metrics) {
+                              nullptr, 0.0, 0, c->stream, c->S, met ? &fold : nullptr));
+    if (!met && !fused && metrics) {
       if ((rc = metrics_pass(c, c->xs[c->cur ^ 1], c->xbar[xb ^ 1], false, want_cons, want_obj))) return rc;
       if ((rc = history(c, h, c->xbar[xb ^ 1], want_cons, want_obj, c->n))) return rc;
     }
@@ -1216,6 +1232,18 @@ int dopt_set_halo(dopt_ctx* c, int64_t n_halo, void* halo_dev, int64_t n_send, v
   c->halo = halo_dev;
   c->n_send = n_send;
   c->send = send_dev;
+  c->send_fresh = false;
+  // inverse map for dopt_phase_mix: worker -> the send rows that carry it (one row per peer)
+  std::vector<int64_t> sp((size_t)c->n + 1, 0);
+  for (int64_t k = 0; k < n_send; ++k) sp[(size_t)send_ids[k] + 1]++;
+  for (int64_t i = 0; i < c->n; ++i) sp[(size_t)i + 1] += sp[(size_t)i];
+  std::vector<int32_t> slot((size_t)std::max<int64_t>(1, n_send));
+  std::vector<int64_t> fill(sp.begin(), sp.end() - 1);
+  for (int64_t k = 0; k < n_send; ++k) slot[(size_t)fill[(size_t)send_ids[k]]++] = (int32_t)k;
+  if ((rc = dalloc_t(&c->sptr, sp.size() * sizeof(int64_t)))) return rc;
+  if ((rc = dalloc_t(&c->sslot, slot.size() * sizeof(int32_t)))) return rc;
+  HIPOK(hipMemcpy(c->sptr, sp.data(), sp.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  HIPOK(hipMemcpy(c->sslot, slot.data(), slot.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   c->have_topo = false;  // the CSR must be re-set in the local+halo index space
   return DOPT_OK;
 }
@@ -1223,6 +1251,7 @@ int dopt_set_halo(dopt_ctx* c, int64_t n_halo, void* halo_dev, int64_t n_send, v
 int dopt_phase_gather(dopt_ctx* c) {
   CHECK_ARG(c, "ctx is NULL");
   if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
+  if (c->send_fresh) return DOPT_OK;  // the last mix wrote these rows already
   HIPOK(launch_gather_rows(c->dtype, c->xs[c->cur], c->send_ids, c->n_send, c->ld, (int32_t)c->nch, c->send,
                            c->stream));
   return DOPT_OK;
@@ -1231,6 +1260,7 @@ int dopt_phase_gather(dopt_ctx* c) {
 int dopt_phase_begin(dopt_ctx* c, int64_t batch) {
   CHECK_ARG(c, "ctx is NULL");
   if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
+  c->send_fresh = false;  // the iterates may have been set since the last mix
   int rc;
   if (c->split) {
     if ((rc = ensure_split(c))) return rc;
@@ -1279,7 +1309,7 @@ int dopt_phase_grad(dopt_ctx* c, int64_t batch, const int32_t* idx, double lam_g
   a.xbar = c->xbar[c->xb];
   a.lam = lam_grad;
   a.flags |= F_GOUT | (cons ? F_CONS : 0) | (loss ? F_LOSS : 0);
-  if (a.flags & F_LOSS) c->loss_groups = c->n;  // per-worker loss slabs
+  if (a.flags & F_LOSS) c->loss_groups = c->slab_n[0] = c->n;  // per-worker loss slabs
   if (c->prof && (rc = prof_event(c, false))) return rc;
   HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, cons || loss, a, (int)c->n, c->stream));
   if (c->prof && (rc = prof_event(c, true))) return rc;
@@ -1313,8 +1343,15 @@ int dopt_phase_mix(dopt_ctx* c, int64_t t, double eta0) {
       HIPOK(launch_split_coef(c->dtype, c->problem, (full ? 1 : 0) | ((cons || loss) ? 2 : 0), q, (int)c->n,
                               c->stream));
     }
+    c->send_fresh = false;
   } else {
+    if (c->n_send > 0) {  // refresh the send rows from the new iterates (the next round's gather)
+      a.sptr = c->sptr;
+      a.sslot = c->sslot;
+      a.send = c->send;
+    }
     HIPOK(launch_mix(c->dtype, a, c->G, (int)c->n, c->stream));
+    c->send_fresh = c->n_send > 0;
   }
   c->cur ^= 1;
   return DOPT_OK;
@@ -1404,6 +1441,93 @@ int dopt_phase_xbar(dopt_ctx* c, const double* sum_dev) {
                             0.0, 0, c->stream));
   c->xb ^= 1;
   c->S_ext = sum_dev;  // the complete-graph mix of the next round uses the global sums
+  return DOPT_OK;
+}
+
+int dopt_phase_cons(dopt_ctx* c) {
+  CHECK_ARG(c, "ctx is NULL");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
+  HIPOK(launch_cons(c->dtype, c->xs[c->cur], c->xbar[c->xb], c->n, c->ld, (int32_t)c->nch, c->slab_cons,
+                    c->stream));
+  c->cons_n = (c->n + 63) / 64;
+  return DOPT_OK;
+}
+
+int dopt_phase_fold(dopt_ctx* c, double* cons_out, double* xnorm_out, double* loss_out, int slab) {
+  CHECK_ARG(c, "ctx is NULL");
+  CHECK_ARG(slab == 0 || slab == 1, "slab must be 0 or 1");
+  HIPOK(launch_fold(c->dtype, c->slab_cons, c->cons_n, slab ? c->slab_loss_b : c->slab_loss, c->slab_n[slab],
+                    c->xbar[c->xb], c->ld, (int32_t)c->nch, cons_out, loss_out, xnorm_out, c->stream));
+  return DOPT_OK;
+}
+
+int dopt_phase_colsum_fold(dopt_ctx* c, double* sum_dev, double* cons_out, double* xnorm_out, double* loss_out) {
+  CHECK_ARG(c && sum_dev, "NULL argument");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
+  HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur], c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part,
+                              nullptr, c->stream));
+  const FoldArgs fold = {c->slab_cons, c->cons_n, c->slab_loss, c->slab_n[0], c->xbar[c->xb], cons_out, loss_out,
+                         xnorm_out};
+  const bool any = cons_out || xnorm_out || loss_out;
+  HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nch, nullptr, nullptr, 0.0, 0,
+                            c->stream, sum_dev, any ? &fold : nullptr));
+  return DOPT_OK;
+}
+
+int dopt_phase_mix_lagged(dopt_ctx* c, int64_t t, double eta0, const double* sum_dev, int consensus) {
+  CHECK_ARG(c && sum_dev, "NULL argument");
+  if (!c->have_topo || !c->G) return fail(DOPT_ERR_STATE, "topology / gradient phase missing");
+  if (c->split || c->mean_mix)
+    return fail(DOPT_ERR_UNSUPPORTED, "lagged mix: row-resident contexts with CSR mixing only");
+  RoundArgs a = base_args(c);
+  a.x_old = c->xs[c->cur];
+  a.x_new = c->xs[c->cur ^ 1];
+  a.eta = eta0 / sqrt((double)(t + 1));  // trainer.py:138-140
+  if (c->n_send > 0) {
+    a.sptr = c->sptr;
+    a.sslot = c->sslot;
+    a.send = c->send;
+  }
+  a.xsum = sum_dev;
+  a.xsum_n = (double)n_div(c);
+  a.xbar_out = c->xbar[c->xb ^ 1];
+  a.slab_cons = consensus ? c->slab_cons : nullptr;
+  if (c->n > 0) {
+    HIPOK(launch_mix(c->dtype, a, c->G, (int)c->n, c->stream));
+  } else {  // no worker here: the average still has to be written
+    HIPOK(launch_colsum_final(c->dtype, sum_dev, 1, n_div(c), c->ld, (int32_t)c->nch, c->xbar[c->xb ^ 1], nullptr,
+                              0.0, 0, c->stream));
+  }
+  if (consensus) c->cons_n = c->n;
+  c->xb ^= 1;
+  c->S_ext = nullptr;
+  c->send_fresh = c->n_send > 0;
+  c->cur ^= 1;
+  return DOPT_OK;
+}
+
+int dopt_phase_loss_pass(dopt_ctx* c, int two_points) {
+  CHECK_ARG(c, "ctx is NULL");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
+  if (c->split) return fail(DOPT_ERR_UNSUPPORTED, "lagged metrics: row-resident contexts only");
+  RoundArgs a = base_args(c);
+  a.X = c->obj_sep ? c->Xo : c->X;
+  a.y = c->obj_sep ? c->yo : c->y;
+  a.off = c->obj_sep ? c->choff_o : c->choff;
+  const int64_t nc = c->obj_sep ? c->n_chunks_o : c->n_chunks;
+  a.w_shared = c->xbar[c->xb];  // current average: z -> slab B
+  if (two_points) {
+    a.xbar = c->xbar[c->xb ^ 1];  // previous average: u -> slab A
+    a.slab_loss = c->slab_loss;
+    a.slab_loss2 = c->slab_loss_b;
+    a.flags |= F_LOSS | F_SHARED | F_LOSS2;
+    c->slab_n[0] = nc;
+  } else {
+    a.slab_loss = c->slab_loss_b;
+    a.flags |= F_LOSS | F_SHARED | F_LOSS_FROM_Z;
+  }
+  c->slab_n[1] = nc;
+  HIPOK(launch_round(c->dtype, c->problem, c->cpl, false, true, a, (int)nc, c->stream));
   return DOPT_OK;
 }
 

@@ -14,11 +14,20 @@ are bitwise the single-GPU iterates; only the metric sums are reduced in a
 different order (per rank, then across ranks).  Metric partial sums stay on the
 device per round and are all-reduced once per run.
 
+With full-shard batches and CSR mixing the rounds run LAGGED (`_run_lagged`): the
+column sums of x_t are all-reduced while the gradient kernel of round t runs, and
+that kernel's fused objective pass is taken at xbar_{t-1} (history[t-2]) instead of
+xbar_t; the consensus of x_t is a separate 16 MiB pass once xbar_t has arrived.  So
+no collective sits between two rounds' kernels; the halo exchange of x_t overlaps
+the same gradient kernel, and the mix kernel writes the next round's send rows (no
+gather kernel).
+
 Plan construction (`build_plan`) is pure host logic over the global CSR, so it
 is tested on CPU with gloo against the oracle (tests/test_distributed_cpu.py).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -119,6 +128,10 @@ class DistributedDSGD:
             engine.set_mixing_mean(mean[0], mean[1])
             self._peers = []
         engine.set_stream(self.stream.cuda_stream)
+        # the lagged schedule: CSR mixing on row-resident contexts (DOPT_LAGGED=0: the serial one)
+        nch = (ld * esz) // 16
+        self._lagged_ok = (mean is None and nch <= 16 * 64 and
+                           os.environ.get("DOPT_LAGGED", "1") != "0")
 
     # -- transport
     def _start_exchange(self):
@@ -165,6 +178,17 @@ class DistributedDSGD:
             self.dist.all_reduce(c, group=self.group)
             t.copy_(c)
 
+    def _all_reduce_start(self, t):
+        """Enqueue an all-reduce of t behind the current stream's work; returns the work to
+        wait on (RCCL: the current stream waits at .wait(), the host does not), or None
+        when the reduction is already complete (world 1, gloo)."""
+        if self.dist.get_world_size(self.group) == 1:
+            return None
+        if self.device_comm:
+            return self.dist.all_reduce(t, group=self.group, async_op=True)
+        self._all_reduce(t)
+        return None
+
     # -- rounds
     def run(self, T, eta0, batch, lam_grad, lam_obj, f_opt=0.0, t0=0, objective=True, consensus=True, idx=None):
         """T rounds; returns the GLOBAL (objective, consensus) history on every rank.
@@ -177,6 +201,8 @@ class DistributedDSGD:
         eng = self.eng
         flags = (_dopt.RUN_OBJECTIVE if objective else 0) | (_dopt.RUN_CONSENSUS if consensus else 0)
         fused = idx is None and not self.obj_sep
+        if fused and flags and self._lagged_ok:
+            return self._run_lagged(T, eta0, batch, lam_grad, lam_obj, f_opt, t0, objective, consensus)
         xnorm = self.plan.rank == 0  # ||xbar||^2 is global already: count it once
         with torch.cuda.stream(self.stream):
             partials = torch.zeros((max(1, T), 3), dtype=torch.float64, device=self.dev)
@@ -206,6 +232,63 @@ class DistributedDSGD:
                 eng.phase_metrics(flags, xnorm, partials[T - 1].data_ptr())
             self._all_reduce(partials)
             raw = partials[:T].cpu().numpy()
+        self.stream.synchronize()
+        obj, cons = _dopt.finalize_metrics(self.eng.problem, raw, self.n_global, self.rows_global, lam_obj, f_opt)
+        return (obj if objective else None), (cons if consensus else None)
+
+    def _run_lagged(self, T, eta0, batch, lam_grad, lam_obj, f_opt, t0, objective, consensus):
+        """Full-shard rounds with CSR mixing; history[t] = metrics of x_{t+1}.  Round h, all
+        on the engine stream except the two transfers:
+
+          P2P(send rows of x_h) -----------------------------------------------.
+          colsum(x_h) [+ fold of history[h-2] / loss of history[h-3]] -> all-reduce --.
+          grad(x_h) + loss of every row at xbar_{h-1} ------------------------------+-+-> mix
+                                                      mix: xbar_h, consensus of x_h, x_{h+1},
+                                                           send rows of x_{h+1}
+
+        Four kernels per round and no collective between two of them; after the last
+        round xbar_T, the consensus of x_T and one pass for the losses at xbar_{T-1}, xbar_T."""
+        torch, eng = self.torch, self.eng
+        xnorm = self.plan.rank == 0  # ||xbar||^2 is global already: count it once
+        obj_f = _dopt.RUN_OBJECTIVE if objective else 0
+        if T == 0:
+            return (np.zeros(0) if objective else None), (np.zeros(0) if consensus else None)
+        with torch.cuda.stream(self.stream):
+            partials = torch.zeros((T, 3), dtype=torch.float64, device=self.dev)
+            base = partials.data_ptr()
+
+            def at(h, k, want=True):  # device address of partials[h, k], or None
+                return base + (3 * h + k) * 8 if want and 0 <= h < T else None
+
+            def colsum_fold(h):  # column sums of x_h; history[h-2] (consensus, ||xbar||^2), [h-3] (loss)
+                eng.phase_colsum_fold(self.sum.data_ptr(), at(h - 2, 0, consensus), at(h - 2, 2, objective and xnorm),
+                                      at(h - 3, 1, objective))
+
+            eng.phase_begin(batch)
+            eng.phase_gather()  # send rows of x_0; later rounds get them from the mix kernel
+            for h in range(T):
+                pending = self._start_exchange()
+                colsum_fold(h)
+                ar = self._all_reduce_start(self.sum)
+                eng.phase_grad(batch, lam_grad, obj_f if h >= 2 else 0)  # loss at xbar_{h-1}
+                if ar is not None:
+                    ar.wait()
+                self._finish_exchange(pending)
+                eng.phase_mix_lagged(t0 + h, eta0, self.sum.data_ptr(), consensus)
+            colsum_fold(T)
+            ar = self._all_reduce_start(self.sum)
+            if ar is not None:
+                ar.wait()
+            eng.phase_xbar(self.sum.data_ptr())  # xbar_T
+            if consensus:
+                eng.phase_cons()
+            if objective:  # losses at xbar_T (history[T-1]) and xbar_{T-1} (history[T-2])
+                eng.phase_loss_pass(T >= 2)
+            eng.phase_fold(at(T - 1, 0, consensus), at(T - 1, 2, objective and xnorm), at(T - 1, 1, objective), 1)
+            if objective and T >= 2:
+                eng.phase_fold(None, None, at(T - 2, 1), 0)
+            self._all_reduce(partials)
+            raw = partials.cpu().numpy()
         self.stream.synchronize()
         obj, cons = _dopt.finalize_metrics(self.eng.problem, raw, self.n_global, self.rows_global, lam_obj, f_opt)
         return (obj if objective else None), (cons if consensus else None)

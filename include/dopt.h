@@ -184,14 +184,17 @@ int dopt_set_halo(dopt_ctx *ctx, int64_t n_halo, void *halo_dev, int64_t n_send,
 /* Start of a run of phases: column-blocked contexts (large d) compute the
  * coefficients of the starting iterates here (full-shard batches). */
 int dopt_phase_begin(dopt_ctx *ctx, int64_t batch);
+/* Rows send_ids of the current iterates -> send.  A no-op when the last dopt_phase_mix
+ * already wrote them (the mix kernel refreshes the send rows as it writes the iterates). */
 int dopt_phase_gather(dopt_ctx *ctx);
 /* Gradients of every local worker at its current iterate (worker.py:30-44);
  * metric_flags (DOPT_RUN_*) also accumulate the current iterate's metric
  * partials at the current xbar (fused, full-shard batches only). */
 int dopt_phase_grad(dopt_ctx *ctx, int64_t batch, const int32_t *idx, double lam_grad,
                     uint32_t metric_flags);
-/* x_{t+1} = W [x_t | halo] - eta0/sqrt(t+1) g  (trainer.py:173-175).  Column-blocked
- * contexts compute the gradient here, block by block, in the same pass. */
+/* x_{t+1} = W [x_t | halo] - eta0/sqrt(t+1) g  (trainer.py:173-175), and the send rows
+ * of x_{t+1}.  Column-blocked contexts compute the gradient here, block by block, in the
+ * same pass (and leave the send rows to dopt_phase_gather). */
 int dopt_phase_mix(dopt_ctx *ctx, int64_t t, double eta0);
 /* Local column sums of the current iterates -> sum_dev[ld] (float64). */
 int dopt_phase_colsum(dopt_ctx *ctx, double *sum_dev);
@@ -202,6 +205,27 @@ int dopt_phase_metrics_pass(dopt_ctx *ctx, uint32_t flags);
 /* Raw sums -> out_dev[3] = (sum of consensus partials, sum of loss terms,
  * ||xbar||^2 if include_xnorm else 0). */
 int dopt_phase_metrics(dopt_ctx *ctx, uint32_t flags, int include_xnorm, double *out_dev);
+/* Lagged schedule (the cross-rank all-reduce of xbar off the critical path; distributed.py):
+ * dopt_phase_cons: consensus partials ||x_i - xbar||^2 of the current iterates at the current
+ *   average (trainer.py:185), per group of 64 workers.
+ * dopt_phase_fold: *cons_out = their sum, *xnorm_out = ||xbar||^2, *loss_out = sum of loss
+ *   slab `slab` (slab 0: the last dopt_phase_grad with DOPT_RUN_OBJECTIVE, or the previous
+ *   average's loss of a two-point pass; slab 1: the current average's loss of the last pass);
+ *   NULL outputs are skipped.
+ * dopt_phase_loss_pass: loss of every local objective row at the current average -> slab 1,
+ *   and with two_points also at the previous average -> slab 0 (one pass over the rows). */
+int dopt_phase_cons(dopt_ctx *ctx);
+int dopt_phase_fold(dopt_ctx *ctx, double *cons_out, double *xnorm_out, double *loss_out, int slab);
+int dopt_phase_loss_pass(dopt_ctx *ctx, int two_points);
+/* dopt_phase_colsum_fold: dopt_phase_colsum, plus (same launch) the fold of the consensus slab
+ *   of the last dopt_phase_mix_lagged / dopt_phase_cons, loss slab 0 and ||xbar||^2 of the
+ *   current average into the non-NULL outputs.
+ * dopt_phase_mix_lagged: dopt_phase_mix, plus xbar of the iterates being mixed from their
+ *   all-reduced column sums sum_dev (becomes the current average) and, with consensus, their
+ *   per-worker consensus terms -- so no kernel of its own sits between two rounds. */
+int dopt_phase_colsum_fold(dopt_ctx *ctx, double *sum_dev, double *cons_out, double *xnorm_out,
+                           double *loss_out);
+int dopt_phase_mix_lagged(dopt_ctx *ctx, int64_t t, double eta0, const double *sum_dev, int consensus);
 /* Centralized trainer across ranks (trainer.py:41-71): gradients of the local
  * workers at the shared iterate (fuse_loss: the objective partial of the shared
  * iterate over the same rows, full shards only), local column sums of the

@@ -1,6 +1,8 @@
 """The multi-GPU code path on one GPU: 2 ranks (gloo transport, both contexts on
 device 0) run the phase API with the halo plan; the iterates must equal the
-single-context fused run bit for bit, the metrics to rtol 1e-12 (reordered sums)."""
+single-context fused run bit for bit, the metrics to rtol 1e-12 (reordered sums).
+Full-shard CSR runs take the lagged schedule (distributed.py: _run_lagged; T = 1 and 2
+are its edge cases), DOPT_LAGGED=0 the serial one, the complete graph the serial one."""
 import os
 import socket
 
@@ -20,7 +22,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, dtype, out, mean=False):
+def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1"):
     import torch  # noqa: F401  (one HIP runtime, loaded before libdopt)
     import torch.distributed as dist
 
@@ -28,7 +30,7 @@ def _rank_main(rank, world, port, dtype, out, mean=False):
     import distributed as Dm
     import topology as TP
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DOPT_LAGGED=lagged)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     top = TP.fully_connected(N) if mean else TP.random_regular(N, 4, seed=2)
     plan = Dm.build_plan(top, world, rank)
@@ -46,16 +48,19 @@ def _rank_main(rank, world, port, dtype, out, mean=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dtype,mean", [("float64", False), ("float32", False), ("float64", True)])
-def test_two_ranks_match_single_context(tmp_path, dtype, mean):
+@pytest.mark.parametrize("dtype,mean,T,lagged", [("float64", False, T, "1"), ("float32", False, T, "1"),
+                                                ("float64", True, T, "1"), ("float64", False, 1, "1"),
+                                                ("float64", False, 2, "1"), ("float32", False, T, "0")])
+def test_two_ranks_match_single_context(tmp_path, dtype, mean, T, lagged):
     import torch.multiprocessing as mp
 
     import _dopt
     import topology as TP
 
-    mp.start_processes(_rank_main, args=(2, _free_port(), dtype, str(tmp_path), mean), nprocs=2, join=True,
-                       start_method="spawn")
+    mp.start_processes(_rank_main, args=(2, _free_port(), dtype, str(tmp_path), mean, T, lagged), nprocs=2,
+                       join=True, start_method="spawn")
     got = np.load(tmp_path / "dist.npz")
+    assert len(got["obj"]) == len(got["cons"]) == T
     eng = _dopt.Engine(0, dtype)
     eng.generate_shards("logistic", N, D, M, seed=9)
     if mean:
