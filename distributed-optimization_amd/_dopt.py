@@ -23,6 +23,7 @@ OK, ERR_INVALID, ERR_HIP, ERR_STATE, ERR_UNSUPPORTED, ERR_COMM = 0, -1, -2, -3, 
 LOGISTIC, QUADRATIC = 0, 1
 F32, F64 = 0, 1
 RUN_OBJECTIVE, RUN_CONSENSUS = 1, 2
+MAX_BIP_ROWS = 65536  # dopt.h DOPT_MAX_BIP_ROWS: minibatch gradient inside the metrics pass
 PROBLEMS = {"logistic": LOGISTIC, "quadratic": QUADRATIC}
 DTYPES = {"float32": F32, "fp32": F32, "f32": F32, np.float32: F32,
           "float64": F64, "fp64": F64, "f64": F64, np.float64: F64}

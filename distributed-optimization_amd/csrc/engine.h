@@ -18,7 +18,9 @@ enum : int32_t {
   F_MEAN = 64,         // complete graph: sum_j W_ij x_j = w_off (S - x_i) + W_ii x_i, S = column sums
   F_GSUM = 128,        // with F_GOUT: store the raw sum of coef * row (no 1/b, no lam) -- full gradients
   F_LOSS2 = 256,       // metrics-only pass: also the objective at w_shared (from z) into slab_loss2
+  F_BIP = 512,         // minibatch gradient inside the metrics pass over all rows (k_round VAR bit 6)
 };
+constexpr int64_t kMaxBipRows = 65536;  // shard rows the F_BIP byte map holds in LDS
 
 // One workgroup per worker (or per objective-row chunk).  All pointers are
 // device pointers; T-typed arrays are float or double per the launch.
@@ -59,6 +61,7 @@ struct RoundArgs {
   int32_t b_rows;         // max rows per worker a column-blocked step touches (picks the kernel)
   int32_t pre_rows;       // CSR rows per worker prefetched to LDS by the fused kernel (0: off)
   int32_t groups;         // column-block groups = gridDim.y
+  int32_t bip_rows;       // F_BIP: the largest shard (LDS byte map size)
   // multi-GPU send rows written by k_mix: worker i's new row also goes to send rows
   // sslot[sptr[i] .. sptr[i+1]) (null sptr: no halo plan)
   const int64_t* sptr;

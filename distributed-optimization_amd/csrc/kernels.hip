@@ -197,6 +197,18 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
       for (int c = threadIdx.x; c < nch; c += NT) nbuf[(e - pe0) * nch + c] = *(const V*)(src + (int64_t)c * VN);
     }
   }
+  // VAR bit 6 (minibatch in the metrics pass): the objective needs every row of the shard at
+  // xbar anyway, so the pass streams all m rows and the minibatch rows (marked in an LDS byte
+  // map) also feed the gradient -- one pass over the shard per round for every batch size.
+  constexpr bool BIP = GRAD && MET && (VAR & 64) != 0;
+  const int64_t nrow = BIP ? m : nb;
+  unsigned char* bmask = (unsigned char*)(smem + (size_t)NW * nch * 16 + SRED + (PRE ? (size_t)a.pre_rows * nch * 16 : 0));
+  if (BIP) {
+    for (int64_t r = threadIdx.x; r < m; r += NT) bmask[r] = 0;
+    __syncthreads();
+    for (int64_t k = threadIdx.x; k < nb; k += NT) bmask[a.idx[(int64_t)i * a.b + k]] = 1;
+    __syncthreads();
+  }
 
   const bool loss_from_z = (flags & F_LOSS_FROM_Z) != 0;
   const bool want_loss = MET && (flags & F_LOSS);
@@ -226,7 +238,7 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
   if (PIPE && (compute_z || compute_u)) {
     auto load_row = [&](int64_t rr, V (&dst)[CPL], T& yd) {
       int64_t lr = rr;
-      if (GRAD && a.idx) lr = a.idx[(int64_t)i * a.b + rr];
+      if (GRAD && a.idx && !BIP) lr = a.idx[(int64_t)i * a.b + rr];
       const T* xp = X + (row0 + lr) * ld;
       yd = Y[row0 + lr];
 #pragma unroll
@@ -240,19 +252,20 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
     V cur[CPL], nxt[CPL];
     T ycur = T(0), ynxt = T(0);
     int64_t r = wave;
-    if (r < nb) load_row(r, cur, ycur);
-    for (; r < nb; r += NW) {
-      if (r + NW < nb) load_row(r + NW, nxt, ynxt);
+    if (r < nrow) load_row(r, cur, ycur);
+    for (; r < nrow; r += NW) {
+      if (r + NW < nrow) load_row(r + NW, nxt, ynxt);
+      const bool g_row = !BIP || bmask[r] != 0;  // wave-uniform
       V az = V(0), au = V(0);
 #pragma unroll
       for (int j = 0; j < CPL; ++j) {
-        if (compute_z) az += cur[j] * w[j];
+        if (compute_z && g_row) az += cur[j] * w[j];
         if (compute_u) au += cur[j] * xb[j];
       }
       T z = hsum<T>(az), u = hsum<T>(au);
-      if (compute_z) z = (VAR & 2) ? wave_sum_dpp(z) : wave_sum(z);
+      if (compute_z && g_row) z = (VAR & 2) ? wave_sum_dpp(z) : wave_sum(z);
       if (compute_u) u = (VAR & 2) ? wave_sum_dpp(u) : wave_sum(u);
-      if (GRAD) {
+      if (GRAD && g_row) {
         const T coef = (PROB == 0) ? -ycur * sigmoid_neg(ycur * z) : z - ycur;
 #pragma unroll
         for (int j = 0; j < CPL; ++j) g[j] += coef * cur[j];
@@ -265,15 +278,17 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
     }
   }
   if (!PIPE && (compute_z || compute_u)) {
-    for (int64_t r0 = (int64_t)wave * RB; r0 < nb; r0 += NW * RB) {
+    for (int64_t r0 = (int64_t)wave * RB; r0 < nrow; r0 += NW * RB) {
       V xr[RB][CPL];
       T yv[RB];
+      bool g_row[RB];
 #pragma unroll
       for (int k = 0; k < RB; ++k) {
         const int64_t rr = r0 + k;
-        const bool ok = rr < nb;
+        const bool ok = rr < nrow;
+        g_row[k] = ok && (!BIP || bmask[rr] != 0);
         int64_t lr = rr;
-        if (GRAD && a.idx && ok) lr = a.idx[(int64_t)i * a.b + rr];
+        if (GRAD && a.idx && ok && !BIP) lr = a.idx[(int64_t)i * a.b + rr];
         const T* xp = X + (row0 + lr) * ld;
         yv[k] = ok ? Y[row0 + lr] : T(0);
 #pragma unroll
@@ -291,7 +306,7 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
         V az = V(0), au = V(0);
 #pragma unroll
         for (int j = 0; j < CPL; ++j) {
-          if (compute_z) az += xr[k][j] * w[j];
+          if (compute_z && (!BIP || g_row[k])) az += xr[k][j] * w[j];
           if (compute_u) au += xr[k][j] * xb[j];
         }
         z[k] = hsum<T>(az);
@@ -299,13 +314,13 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
       }
 #pragma unroll
       for (int k = 0; k < RB; ++k) {
-        if (compute_z) z[k] = (VAR & 2) ? wave_sum_dpp(z[k]) : wave_sum(z[k]);
+        if (compute_z && (!BIP || g_row[k])) z[k] = (VAR & 2) ? wave_sum_dpp(z[k]) : wave_sum(z[k]);
         if (compute_u) u[k] = (VAR & 2) ? wave_sum_dpp(u[k]) : wave_sum(u[k]);
       }
 #pragma unroll
       for (int k = 0; k < RB; ++k) {
-        if (r0 + k < nb) {
-          if (GRAD) {
+        if (r0 + k < nrow) {
+          if (GRAD && (!BIP || g_row[k])) {
             const T coef = (PROB == 0) ? -yv[k] * sigmoid_neg(yv[k] * z[k]) : z[k] - yv[k];
 #pragma unroll
             for (int j = 0; j < CPL; ++j) g[j] += coef * xr[k][j];
@@ -386,7 +401,8 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
 template <typename T, int CPL, int PROB, bool GRAD, bool MET, int VAR = KR_DEFAULT_VAR>
 static hipError_t launch_round_t(const RoundArgs& a, int groups, hipStream_t s) {
   const size_t pre = (VAR & 16) ? (size_t)a.pre_rows * a.nchunks * 16 : 0;
-  const size_t lds = (GRAD ? (size_t)NW * a.nchunks * 16 + SRED + pre : SRED);
+  const size_t bip = (VAR & 64) ? ((size_t)a.bip_rows + 15) / 16 * 16 : 0;  // minibatch byte map
+  const size_t lds = (GRAD ? (size_t)NW * a.nchunks * 16 + SRED + pre + bip : SRED);
   static bool attr_set = false;
   if (!attr_set) {
     const size_t max_lds = 160 * 1024;
@@ -432,6 +448,7 @@ static hipError_t dispatch_mode(bool grad, bool met, const RoundArgs& a, int gro
       if (grad) return dispatch_variant<true, false>(var, a, groups, s);
     }
   }
+  if (grad && met && (a.flags & F_BIP)) return launch_round_t<T, CPL, PROB, true, true, KR_DEFAULT_VAR | 64>(a, groups, s);
   if (grad && met) return launch_round_t<T, CPL, PROB, true, true>(a, groups, s);
   if (grad) return launch_round_t<T, CPL, PROB, true, false>(a, groups, s);
   if (met) return launch_round_t<T, CPL, PROB, false, true>(a, groups, s);

@@ -375,6 +375,7 @@ RoundArgs base_args(dopt_ctx* c) {
   a.b_rows = (int32_t)std::min<int64_t>(c->max_m, kSplitMaxRows);
   a.pre_rows = (c->max_row_nnz <= 6 && !c->mean_mix) ? c->max_row_nnz : 0;
   a.groups = c->split_groups;
+  a.bip_rows = (int32_t)std::min<int64_t>(c->max_m, kMaxBipRows);
   return a;
 }
 
@@ -644,6 +645,15 @@ int run_centralized_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64
     c->gcur ^= 1;
   }
   return finish_run(c, T, T, lam_obj, f_opt, want_obj ? obj_out : nullptr, nullptr, time_out);
+}
+
+// Minibatch rounds whose metrics need a pass over every shard row anyway take the gradient
+// inside that pass (k_round F_BIP).  DOPT_BIP=0: a separate metrics pass (A/B runs).
+static_assert(kMaxBipRows == DOPT_MAX_BIP_ROWS, "dopt.h and engine.h disagree");
+bool bip_possible(dopt_ctx* c, int64_t batch, const int32_t* idx) {
+  const char* v = getenv("DOPT_BIP");
+  if (v && v[0] == '0') return false;
+  return idx && batch < c->max_m && c->max_m <= kMaxBipRows && !c->obj_sep && !c->split;
 }
 
 int check_run(dopt_ctx* c, int64_t T, int64_t batch, const int32_t* idx, bool need_topo) {
@@ -936,7 +946,8 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
   c->send_fresh = false;
   const bool want_obj = flags & DOPT_RUN_OBJECTIVE, want_cons = flags & DOPT_RUN_CONSENSUS;
   const bool metrics = want_obj || want_cons;
-  const bool fused = batch >= c->max_m && !c->obj_sep;
+  const bool bip = metrics && bip_possible(c, batch, idx);
+  const bool fused = (batch >= c->max_m || bip) && !c->obj_sep;
   const int64_t CH = idx ? idx_chunk_rounds(c, T, batch) : 1;
   int& xb = c->xb;
   if (c->split) return run_dsgd_split(c, t0, T, eta0, batch, idx, lam_grad, lam_obj, f_opt, flags, obj_out,
@@ -958,7 +969,7 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
     a.eta = eta0 / sqrt((double)(t + 1));  // trainer.py:138-140
     a.lam = lam_grad;
     const bool met = fused && metrics && h > 0;
-    a.flags |= F_STEP | (met && want_cons ? F_CONS : 0) | (met && want_obj ? F_LOSS : 0);
+    a.flags |= F_STEP | (met && want_cons ? F_CONS : 0) | (met && want_obj ? F_LOSS : 0) | (met && bip ? F_BIP : 0);
     if (a.flags & F_LOSS) c->loss_groups = c->n;  // per-worker loss slabs
     if (c->prof && (rc = prof_event(c, false))) return rc;
     HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, met, a, (int)c->n, c->stream));
@@ -1283,8 +1294,10 @@ int dopt_phase_grad(dopt_ctx* c, int64_t batch, const int32_t* idx, double lam_g
   if (!c->G && (rc = dalloc(&c->G, (size_t)c->n * c->ld * c->esz))) return rc;
   if (idx && (rc = upload_idx_chunk(c, idx, 0, 1, batch))) return rc;
   const bool cons = metric_flags & DOPT_RUN_CONSENSUS, loss = metric_flags & DOPT_RUN_OBJECTIVE;
-  if ((cons || loss) && (batch < c->max_m || c->obj_sep))
-    return fail(DOPT_ERR_UNSUPPORTED, "fused metrics need full-shard batches over the shard rows");
+  const bool bip = (cons || loss) && bip_possible(c, batch, idx);
+  if ((cons || loss) && ((batch < c->max_m && !bip) || c->obj_sep))
+    return fail(DOPT_ERR_UNSUPPORTED, "fused metrics need every shard row in the pass (full shards, or "
+                "minibatches of shards of at most %lld rows)", (long long)kMaxBipRows);
   if (c->split) {  // the gradient is produced block by block inside the step (dopt_phase_mix)
     c->ph_batch = batch;
     c->ph_lam = lam_grad;
@@ -1308,7 +1321,7 @@ int dopt_phase_grad(dopt_ctx* c, int64_t batch, const int32_t* idx, double lam_g
   a.g_out = c->G;
   a.xbar = c->xbar[c->xb];
   a.lam = lam_grad;
-  a.flags |= F_GOUT | (cons ? F_CONS : 0) | (loss ? F_LOSS : 0);
+  a.flags |= F_GOUT | (cons ? F_CONS : 0) | (loss ? F_LOSS : 0) | (bip ? F_BIP : 0);
   if (a.flags & F_LOSS) c->loss_groups = c->slab_n[0] = c->n;  // per-worker loss slabs
   if (c->prof && (rc = prof_event(c, false))) return rc;
   HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, cons || loss, a, (int)c->n, c->stream));

@@ -20,53 +20,62 @@ namespace {
 constexpr int kN = 624, kM = 397;
 constexpr uint32_t kMatrixA = 0x9908b0dfu, kUpper = 0x80000000u, kLower = 0x7fffffffu;
 
+// numpy's legacy generator state with a block of tempered outputs: each twist regenerates
+// the 624 state words and tempers them in one vectorisable pass, so a draw is a load.
 struct MT {
   uint32_t* key;
   int32_t pos;
+  uint32_t out[kN];
+  int32_t out_gen = -1;  // out[] holds the tempered words of the current key (valid from pos on)
 
   void twist() {
     int i = 0;
-    uint32_t y;
     for (; i < kN - kM; ++i) {
-      y = (key[i] & kUpper) | (key[i + 1] & kLower);
+      const uint32_t y = (key[i] & kUpper) | (key[i + 1] & kLower);
       key[i] = key[i + kM] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
     }
     for (; i < kN - 1; ++i) {
-      y = (key[i] & kUpper) | (key[i + 1] & kLower);
+      const uint32_t y = (key[i] & kUpper) | (key[i + 1] & kLower);
       key[i] = key[i + (kM - kN)] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
     }
-    y = (key[kN - 1] & kUpper) | (key[0] & kLower);
+    const uint32_t y = (key[kN - 1] & kUpper) | (key[0] & kLower);
     key[kN - 1] = key[kM - 1] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
     pos = 0;
   }
-  uint32_t next32() {
-    if (pos >= kN) twist();
-    uint32_t y = key[pos++];
-    y ^= (y >> 11);
-    y ^= (y << 7) & 0x9d2c5680u;
-    y ^= (y << 15) & 0xefc60000u;
-    y ^= (y >> 18);
-    return y;
+  void temper_all() {
+    for (int k = 0; k < kN; ++k) {
+      uint32_t y = key[k];
+      y ^= (y >> 11);
+      y ^= (y << 7) & 0x9d2c5680u;
+      y ^= (y << 15) & 0xefc60000u;
+      y ^= (y >> 18);
+      out[k] = y;
+    }
+    out_gen = 0;
+  }
+  inline uint32_t next32() {
+    if (pos >= kN) {
+      twist();
+      temper_all();
+    } else if (out_gen < 0) {
+      temper_all();  // first draw from a state handed in mid-block
+    }
+    return out[pos++];
   }
   uint64_t next64() {
     const uint64_t hi = next32();
     return (hi << 32) | next32();
   }
-  // uniform integer in [0, max] by masked rejection
-  uint64_t interval(uint64_t max) {
+  // uniform integer in [0, max] by masked rejection (numpy random_interval)
+  inline uint64_t interval(uint64_t max) {
     if (max == 0) return 0;
-    uint64_t mask = max;
-    mask |= mask >> 1;
-    mask |= mask >> 2;
-    mask |= mask >> 4;
-    mask |= mask >> 8;
-    mask |= mask >> 16;
-    mask |= mask >> 32;
     uint64_t v;
     if (max <= 0xffffffffull) {
+      const uint32_t mask = 0xffffffffu >> __builtin_clz((uint32_t)max);
       while ((v = (next32() & mask)) > max) {
       }
     } else {
+      const uint64_t mask = ~0ull >> __builtin_clzll(max);
       while ((v = (next64() & mask)) > max) {
       }
     }
@@ -74,24 +83,25 @@ struct MT {
   }
 };
 
-// permutation(m)[:eb] -> out; perm is scratch of size m.
+// permutation(m)[:eb] -> out; perm is scratch of size m (m < 2^31, checked by the callers).
 template <typename I>
 void choice_prefix(MT& mt, int64_t m, int64_t eb, std::vector<int64_t>& perm, I* out) {
   perm.resize((size_t)m);
-  for (int64_t k = 0; k < m; ++k) perm[(size_t)k] = k;
+  int64_t* p = perm.data();
+  for (int64_t k = 0; k < m; ++k) p[k] = k;
   for (int64_t k = m - 1; k >= 1; --k) {
     const int64_t j = (int64_t)mt.interval((uint64_t)k);
-    const int64_t t = perm[(size_t)k];
-    perm[(size_t)k] = perm[(size_t)j];
-    perm[(size_t)j] = t;
+    const int64_t t = p[k];
+    p[k] = p[j];
+    p[j] = t;
   }
-  for (int64_t k = 0; k < eb; ++k) out[k] = (I)perm[(size_t)k];
+  for (int64_t k = 0; k < eb; ++k) out[k] = (I)p[k];
 }
 
 }  // namespace
 
 extern "C" int dopt_mt_choice(uint32_t key[624], int32_t* pos, int64_t m, int64_t b, int64_t* out) {
-  if (!key || !pos || m < 0 || b < 0 || *pos < 0 || *pos > kN) return DOPT_ERR_INVALID;
+  if (!key || !pos || m < 0 || m > 0x7fffffffLL || b < 0 || *pos < 0 || *pos > kN) return DOPT_ERR_INVALID;
   if (m == 0) return DOPT_OK;  // worker.py:17-18: no draw for an empty shard
   const int64_t eb = b < m ? b : m;
   if (eb <= 0) return DOPT_OK;  // worker.py:21-23

@@ -201,8 +201,11 @@ class DistributedDSGD:
         eng = self.eng
         flags = (_dopt.RUN_OBJECTIVE if objective else 0) | (_dopt.RUN_CONSENSUS if consensus else 0)
         fused = idx is None and not self.obj_sep
-        if fused and flags and self._lagged_ok:
-            return self._run_lagged(T, eta0, batch, lam_grad, lam_obj, f_opt, t0, objective, consensus)
+        rows = self.eng.shard_rows
+        bip = (idx is not None and not self.obj_sep and rows is not None and len(rows) > 0 and
+               batch < int(rows.max()) <= _dopt.MAX_BIP_ROWS and os.environ.get("DOPT_BIP", "1") != "0")
+        if (fused or bip) and flags and self._lagged_ok:
+            return self._run_lagged(T, eta0, batch, lam_grad, lam_obj, f_opt, t0, objective, consensus, idx)
         xnorm = self.plan.rank == 0  # ||xbar||^2 is global already: count it once
         with torch.cuda.stream(self.stream):
             partials = torch.zeros((max(1, T), 3), dtype=torch.float64, device=self.dev)
@@ -236,9 +239,10 @@ class DistributedDSGD:
         obj, cons = _dopt.finalize_metrics(self.eng.problem, raw, self.n_global, self.rows_global, lam_obj, f_opt)
         return (obj if objective else None), (cons if consensus else None)
 
-    def _run_lagged(self, T, eta0, batch, lam_grad, lam_obj, f_opt, t0, objective, consensus):
-        """Full-shard rounds with CSR mixing; history[t] = metrics of x_{t+1}.  Round h, all
-        on the engine stream except the two transfers:
+    def _run_lagged(self, T, eta0, batch, lam_grad, lam_obj, f_opt, t0, objective, consensus, idx=None):
+        """Rounds with CSR mixing whose metrics ride the gradient pass (full shards, or
+        minibatches taken inside a pass over every row); history[t] = metrics of x_{t+1}.
+        Round h, all on the engine stream except the two transfers:
 
           P2P(send rows of x_h) -----------------------------------------------.
           colsum(x_h) [+ fold of history[h-2] / loss of history[h-3]] -> all-reduce --.
@@ -270,7 +274,8 @@ class DistributedDSGD:
                 pending = self._start_exchange()
                 colsum_fold(h)
                 ar = self._all_reduce_start(self.sum)
-                eng.phase_grad(batch, lam_grad, obj_f if h >= 2 else 0)  # loss at xbar_{h-1}
+                eng.phase_grad(batch, lam_grad, obj_f if h >= 2 else 0,  # loss at xbar_{h-1}
+                               idx=None if idx is None else idx[h])
                 if ar is not None:
                     ar.wait()
                 self._finish_exchange(pending)

@@ -189,7 +189,10 @@ int dopt_phase_begin(dopt_ctx *ctx, int64_t batch);
 int dopt_phase_gather(dopt_ctx *ctx);
 /* Gradients of every local worker at its current iterate (worker.py:30-44);
  * metric_flags (DOPT_RUN_*) also accumulate the current iterate's metric
- * partials at the current xbar (fused, full-shard batches only). */
+ * partials at the current xbar from the same pass over every shard row (full-shard
+ * batches, or minibatches when every shard has at most DOPT_MAX_BIP_ROWS rows: the
+ * minibatch rows then feed the gradient inside that pass). */
+#define DOPT_MAX_BIP_ROWS 65536
 int dopt_phase_grad(dopt_ctx *ctx, int64_t batch, const int32_t *idx, double lam_grad,
                     uint32_t metric_flags);
 /* x_{t+1} = W [x_t | halo] - eta0/sqrt(t+1) g  (trainer.py:173-175), and the send rows

@@ -48,16 +48,17 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dtype,mean,T,lagged", [("float64", False, T, "1"), ("float32", False, T, "1"),
-                                                ("float64", True, T, "1"), ("float64", False, 1, "1"),
-                                                ("float64", False, 2, "1"), ("float32", False, T, "0")])
-def test_two_ranks_match_single_context(tmp_path, dtype, mean, T, lagged):
+@pytest.mark.parametrize("dtype,mean,T,lagged,world", [("float64", False, T, "1", 2), ("float32", False, T, "1", 2),
+                                                      ("float64", True, T, "1", 2), ("float64", False, 1, "1", 2),
+                                                      ("float64", False, 2, "1", 2), ("float32", False, T, "0", 2),
+                                                      ("float64", False, 3, "1", 3)])
+def test_ranks_match_single_context(tmp_path, dtype, mean, T, lagged, world):
     import torch.multiprocessing as mp
 
     import _dopt
     import topology as TP
 
-    mp.start_processes(_rank_main, args=(2, _free_port(), dtype, str(tmp_path), mean, T, lagged), nprocs=2,
+    mp.start_processes(_rank_main, args=(world, _free_port(), dtype, str(tmp_path), mean, T, lagged), nprocs=world,
                        join=True, start_method="spawn")
     got = np.load(tmp_path / "dist.npz")
     assert len(got["obj"]) == len(got["cons"]) == T

@@ -310,3 +310,32 @@ def test_table1_logistic_simulator_end_to_end():
         _close(sim.results[label]["objective"], z[f"L{j}_objective"], 1e-8)
         if label != "Centralized":
             _close(sim.results[label]["consensus_error"], z[f"L{j}_consensus"], 1e-8)
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+def test_minibatch_in_metrics_pass_matches_separate_pass(dtype, monkeypatch):
+    """Minibatch rounds with metrics take the gradient inside the pass over every shard
+    row (k_round VAR bit 6, F_BIP); DOPT_BIP=0 keeps the separate metrics pass.  Only the
+    order of the gradient sum over the batch rows differs (row order vs draw order), so the
+    trajectories agree to rounding, over ragged and empty shards too."""
+    rng = np.random.default_rng(17)
+    m_rows = [40, 33, 0, 40, 17, 5, 40, 28]
+    n, d, b, T = len(m_rows), 45, 8, 12
+    off = np.concatenate([[0], np.cumsum(m_rows)])
+    X = np.hstack([rng.standard_normal((off[-1], d - 1)), np.ones((off[-1], 1))])
+    y = rng.choice(np.array([-1.0, 1.0]), off[-1])
+    top = topology.ring(n)
+    np.random.seed(4)
+    idx = _dopt.mt_choice_rounds(T, m_rows, b)
+    runs = []
+    for bip in ("1", "0"):
+        monkeypatch.setenv("DOPT_BIP", bip)
+        eng = _dopt.Engine(0, dtype)
+        eng.load_shards("logistic", X, y, off)
+        eng.set_topology(top.row_ptr, top.col, top.w)
+        obj, cons, _ = eng.run_dsgd(T, 0.05, b, 1e-3, 1e-3, 0.0, idx=idx)
+        runs.append((obj, cons, eng.get_models()))
+        eng.close()
+    tol = 1e-12 if dtype == "float64" else 2e-6
+    for a_, b_ in zip(runs[0], runs[1]):
+        np.testing.assert_allclose(a_, b_, rtol=tol, atol=1e-14 if dtype == "float64" else 1e-7)
