@@ -113,6 +113,9 @@ def main():
                          "of round time, so the default samples 1 launch in 10 of the timed region")
     ap.add_argument("--phase", action="store_true",
                     help="drive the multi-GPU phase path even on one GPU (measures its per-rank overhead)")
+    ap.add_argument("--partition", default="spectral", choices=["spectral", "ranges"],
+                    help="C3 at N > 1: workers -> GPUs by graph partition (recursive spectral bisection, "
+                         "computed on rank 0 and broadcast) or by contiguous id ranges")
     ap.add_argument("--config", default="c3", choices=["c3", "c4", "c5"],
                     help="c3 (default, the metric's config); c4: 256x256 torus, 65536 workers total; "
                          "c5: quadratic, d=2^20, m=b=16, 1024 workers total, complete graph")
@@ -145,6 +148,10 @@ def main():
         n, d, m = args.workers, args.d, args.m
         n_global = n * world
         top = topology.random_regular(n_global, args.degree, seed=0)
+        if world > 1 and args.partition == "spectral":  # relabel so each GPU's part is an id range
+            order = [distributed.partition_order(distributed.graph_partition(top, world)) if rank == 0 else None]
+            dist.broadcast_object_list(order, src=0)
+            top = topology.relabel(top, order[0])
         workload = (f"C3: logistic, {n} workers/GPU, d={d}, m=b={m}, random {args.degree}-regular MH mixing, "
                     "objective+consensus every round")
     elif args.config == "c4":
@@ -241,8 +248,10 @@ def main():
         "config": {"workload": workload,
                    "workers_per_gpu": n, "d": d, "rows_per_worker": m, "batch": m, "topology": top.name,
                    "degree": args.degree if args.config == "c3" else None,
-                   "parallelism": (f"dp{world}: one graph of {n_global} workers, contiguous slices per GPU, "
-                                   f"halo send/recv + all-reduce ({args.backend})") if world > 1
+                   "halo_rows_per_gpu": int(plan.n_halo),
+                   "parallelism": (f"dp{world}: one graph of {n_global} workers, "
+                                   f"{'graph-partitioned' if args.config == 'c3' and args.partition == 'spectral' else 'contiguous'} "
+                                   f"slices per GPU, halo send/recv + all-reduce ({args.backend})") if world > 1
                                   else "single GPU: fused round kernel, one launch per round"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,

@@ -167,6 +167,17 @@ def random_regular(n, k, seed=0, max_tries=10000):
     raise RuntimeError("random_regular: no simple graph found")
 
 
+def relabel(topo, order):
+    """The same graph with new vertex ids: new id k is old vertex order[k] (a permutation).
+    MH weights are recomputed on the new ids (per edge the same value; W_ii can differ in
+    the last bit, as it sums the row in the new column order)."""
+    order = np.asarray(order, dtype=np.int64)
+    inv = np.empty_like(order)
+    inv[order] = np.arange(len(order))
+    nbrs = [np.sort(inv[np.asarray(topo.neighbours[o], dtype=np.int64)]) for o in order]
+    return Topology(topo.name, nbrs)
+
+
 def build(name, n, config=None):
     """trainer.py:95-112 dispatch; unknown names raise the reference's ValueError."""
     config = config or {}

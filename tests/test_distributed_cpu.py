@@ -37,11 +37,15 @@ def _topo(name, n):
 
 
 def _rank_main(rank, world, port, name, n, T, out):
+    _rank_main_topo(rank, world, port, _topo(name, n), T, out)
+
+
+def _rank_main_topo(rank, world, port, topo, T, out):
     import torch
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    topo = _topo(name, n)
+    n = topo.n
     plan = D.build_plan(topo, world, rank)
     shards = _data(n)
     x = np.zeros((plan.n_local, shards[0][0].shape[1]))
@@ -103,3 +107,37 @@ def test_plan_structure():
             np.testing.assert_array_equal(np.sort(sent), ids)
         assert p.n_halo == 2 * 32  # strips of 4 torus rows: one boundary row above, one below
     np.testing.assert_array_equal(D.partition_bounds(10, 3), [0, 4, 7, 10])
+
+
+@pytest.mark.parametrize("n,parts", [(256, 2), (512, 8), (300, 3)])
+def test_graph_partition_balanced_and_better_than_ranges(n, parts):
+    """graph_partition (recursive spectral bisection + refinement) gives exactly the
+    partition_bounds sizes, is deterministic, and cuts far fewer edges of a random regular
+    graph than contiguous id ranges; relabelling by it makes the parts contiguous slices
+    whose halo plans move fewer rows."""
+    topo = TP.random_regular(n, 4, seed=1)
+    part = D.graph_partition(topo, parts, seed=0)
+    np.testing.assert_array_equal(np.bincount(part, minlength=parts), np.diff(D.partition_bounds(n, parts)))
+    np.testing.assert_array_equal(part, D.graph_partition(topo, parts, seed=0))
+    ranges = np.repeat(np.arange(parts), np.diff(D.partition_bounds(n, parts)))
+    assert D.cut_edges(topo, part) < 0.6 * D.cut_edges(topo, ranges)
+    order = D.partition_order(part)
+    rt = TP.relabel(topo, order)
+    rt.check()
+    assert D.cut_edges(rt, ranges.astype(np.int32)) == D.cut_edges(topo, part)
+    np.testing.assert_array_equal(rt.degrees, topo.degrees[order])
+    halo_new = sum(D.build_plan(rt, parts, r).n_halo for r in range(parts))
+    halo_old = sum(D.build_plan(topo, parts, r).n_halo for r in range(parts))
+    assert halo_new < halo_old
+
+
+def test_relabelled_rounds_match_oracle(tmp_path):
+    """Partitioned rounds on a relabelled graph are the oracle's rounds on that graph."""
+    n, world, T = 24, 3, 4
+    topo = TP.relabel(_topo("random_regular", n), D.partition_order(D.graph_partition(_topo("random_regular", n), world)))
+    mp.start_processes(_rank_main_topo, args=(world, _free_port(), topo, T, str(tmp_path)), nprocs=world,
+                       join=True, start_method="fork")
+    got = np.concatenate([np.load(tmp_path / f"rank{r}.npy") for r in range(world)])
+    idx = [[np.arange(7)] * n] * T
+    _, _, ref, _ = O.run_decentralized(_data(n), topo.dense_W(), T, CFG, mixing="sparse", indices=idx)
+    np.testing.assert_array_equal(got, ref)
