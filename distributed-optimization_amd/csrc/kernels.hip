@@ -813,10 +813,22 @@ __device__ void fold_block(const FoldArgs& f, int nch, double (*red)[64 * VT<T>:
   constexpr int VN = VT<T>::n;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double a = 0.0, b = 0.0, q = 0.0;
-  if (f.sc && f.out_c)
-    for (int64_t k = threadIdx.x; k < f.nc; k += NT) a += f.sc[k];
-  if (f.sl && f.out_l)
-    for (int64_t k = threadIdx.x; k < f.nl; k += NT) b += f.sl[k];
+  // four independent accumulators per thread (fixed order), so 256 threads keep many loads in
+  // flight instead of one dependent add chain per thread
+  auto sum4 = [&](const double* v, int64_t cnt) {
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int64_t k = threadIdx.x;
+    for (; k + 3 * NT < cnt; k += 4 * NT) {
+      s0 += v[k];
+      s1 += v[k + NT];
+      s2 += v[k + 2 * NT];
+      s3 += v[k + 3 * NT];
+    }
+    for (; k < cnt; k += NT) s0 += v[k];
+    return (s0 + s1) + (s2 + s3);
+  };
+  if (f.sc && f.out_c) a = sum4(f.sc, f.nc);
+  if (f.sl && f.out_l) b = sum4(f.sl, f.nl);
   if (f.xbar && f.out_q)
     for (int c = threadIdx.x; c < nch; c += NT)
 #pragma unroll
