@@ -83,17 +83,46 @@ struct MT {
   }
 };
 
-// permutation(m)[:eb] -> out; perm is scratch of size m (m < 2^31, checked by the callers).
+// The j of every Fisher-Yates step k = m-1 .. 1 (js[t] for k = m-1-t), consuming the
+// stream exactly as m-1 calls of interval(k) would.  Written as a branchless filter over
+// the buffered words (a word is kept when (w & mask) <= k, and then k moves on), so the
+// rejections cost no branch mispredictions; k < 2^32 (m < 2^31 is checked by the callers).
+void draw_js(MT& mt, int64_t m, uint32_t* js) {
+  uint32_t k = (uint32_t)(m - 1);
+  uint32_t t = 0;
+  while (k >= 1) {
+    if (mt.pos >= kN) {
+      mt.twist();
+      mt.temper_all();
+    } else if (mt.out_gen < 0) {
+      mt.temper_all();
+    }
+    int32_t q = mt.pos;
+    while (q < kN && k >= 1) {
+      const uint32_t mask = 0xffffffffu >> __builtin_clz(k);
+      const uint32_t v = mt.out[q++] & mask;
+      const uint32_t keep = v <= k;
+      js[t] = v;
+      t += keep;
+      k -= keep;
+    }
+    mt.pos = q;
+  }
+}
+
+// permutation(m)[:eb] -> out; perm / js are scratch of size m.
 template <typename I>
-void choice_prefix(MT& mt, int64_t m, int64_t eb, std::vector<int64_t>& perm, I* out) {
+void choice_prefix(MT& mt, int64_t m, int64_t eb, std::vector<int64_t>& perm, std::vector<uint32_t>& js, I* out) {
   perm.resize((size_t)m);
+  js.resize((size_t)m);
   int64_t* p = perm.data();
   for (int64_t k = 0; k < m; ++k) p[k] = k;
-  for (int64_t k = m - 1; k >= 1; --k) {
-    const int64_t j = (int64_t)mt.interval((uint64_t)k);
-    const int64_t t = p[k];
+  draw_js(mt, m, js.data());
+  for (int64_t k = m - 1, t = 0; k >= 1; --k, ++t) {
+    const int64_t j = js[(size_t)t];
+    const int64_t v = p[k];
     p[k] = p[j];
-    p[j] = t;
+    p[j] = v;
   }
   for (int64_t k = 0; k < eb; ++k) out[k] = (I)p[k];
 }
@@ -107,7 +136,8 @@ extern "C" int dopt_mt_choice(uint32_t key[624], int32_t* pos, int64_t m, int64_
   if (eb <= 0) return DOPT_OK;  // worker.py:21-23
   MT mt{key, *pos};
   std::vector<int64_t> perm;
-  choice_prefix(mt, m, eb, perm, out);
+  std::vector<uint32_t> js;
+  choice_prefix(mt, m, eb, perm, js, out);
   *pos = mt.pos;
   return DOPT_OK;
 }
@@ -120,12 +150,13 @@ extern "C" int dopt_mt_choice_rounds(uint32_t key[624], int32_t* pos, int64_t T,
     if (shard_rows[i] < 0 || shard_rows[i] > 0x7fffffffLL) return DOPT_ERR_INVALID;
   MT mt{key, *pos};
   std::vector<int64_t> perm;
+  std::vector<uint32_t> js;
   for (int64_t t = 0; t < T; ++t) {
     for (int64_t i = 0; i < n_workers; ++i) {
       int32_t* o = out + (t * n_workers + i) * b;
       const int64_t m = shard_rows[i];
       const int64_t eb = (m == 0) ? 0 : (b < m ? b : m);
-      if (eb > 0) choice_prefix(mt, m, eb, perm, o);
+      if (eb > 0) choice_prefix(mt, m, eb, perm, js, o);
       for (int64_t k = eb; k < b; ++k) o[k] = -1;
     }
   }

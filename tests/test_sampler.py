@@ -70,3 +70,20 @@ def test_bad_state_rejected():
     rc = _dopt.lib().dopt_mt_choice(key.ctypes.data_as(ctypes.c_void_p), ctypes.byref(pos), 10, 4,
                                     out.ctypes.data_as(ctypes.c_void_p))
     assert rc == _dopt.ERR_INVALID
+
+
+@pytest.mark.parametrize("rows,b", [([500] * 10, 16), ([1, 2, 3, 700, 0, 64, 65], 9), ([4096] * 3, 4096)])
+def test_rounds_leave_numpy_state_where_numpy_does(rows, b):
+    """After T rounds the generator state (key words and position) is exactly where the
+    reference's T x N np.random.choice calls leave it, so later draws continue the stream."""
+    np.random.seed(11)
+    _dopt.mt_choice_rounds(3, rows, b)
+    ours = np.random.get_state()
+    np.random.seed(11)
+    for _ in range(3):
+        for m in rows:
+            if m > 0 and min(b, m) > 0:
+                np.random.choice(m, min(b, m), replace=False)
+    ref = np.random.get_state()
+    assert ours[2] == ref[2]
+    np.testing.assert_array_equal(ours[1], ref[1])
