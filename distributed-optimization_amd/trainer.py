@@ -41,6 +41,8 @@ from obj_problems import logistic_objective, quadratic_objective
 DENSE_LIMIT = 4096          # dense adj / W attributes up to this many workers
 MEAN_MIX_MIN = 128          # complete graphs from this size mix through the column sums
 IDX_CHUNK_ELEMS = 1 << 24   # host index buffer per device call (64 MiB of int32)
+IDX_CHUNK_ROUNDS = 512      # rounds per device call when indices are drawn (the next chunk's draw
+                            # runs on a host thread while the device runs this one)
 
 
 # ---------------------------------------------------------------------------- shared helpers
@@ -170,19 +172,43 @@ def _batch_size(workers):
 
 def _index_chunks(workers, T, config):
     """Yield (t_start, n_rounds, idx or None): minibatch indices drawn on the host in
-    trainer order (trainer.py:47-50 / :166), `None` when every batch is the full shard."""
+    trainer order (trainer.py:47-50 / :166), `None` when every batch is the full shard.
+    The legacy MT19937 stream is sequential, so the draw runs one chunk AHEAD on a host
+    thread (the C sampler releases the GIL) while the device runs the current chunk."""
     b = _batch_size(workers)
     rows = np.array([w.n_local_samples for w in workers], dtype=np.int64)
     full = b >= (rows.max() if len(rows) else 0)
     skip_rng = full and config.get("sampling", "legacy") == "full"
-    ch = max(1, IDX_CHUNK_ELEMS // max(1, len(workers) * max(b, 1)))
-    for t in range(0, T, ch):
-        n = min(ch, T - t)
-        if skip_rng:
-            yield t, n, b, None
-            continue
-        idx = _dopt.mt_choice_rounds(n, rows, b)  # advances np.random exactly like the reference
-        yield t, n, b, (None if full else idx)
+    if skip_rng:
+        ch = max(1, T)
+        for t in range(0, T, ch):
+            yield t, min(ch, T - t), b, None
+        return
+    ch = max(1, min(IDX_CHUNK_ROUNDS, IDX_CHUNK_ELEMS // max(1, len(workers) * max(b, 1))))
+
+    def draws():
+        for t in range(0, T, ch):
+            n = min(ch, T - t)
+            idx = _dopt.mt_choice_rounds(n, rows, b)  # advances np.random exactly like the reference
+            yield t, n, b, (None if full else idx)
+
+    yield from _one_ahead(draws())
+
+
+def _one_ahead(gen):
+    """Items of `gen`, each produced on a worker thread while the caller consumes the
+    previous one.  Exactly the items of gen are produced (no draw past the end)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    done = object()
+    with ThreadPoolExecutor(max_workers=1) as ex:
+        fut = ex.submit(next, gen, done)
+        while True:
+            item = fut.result()
+            if item is done:
+                return
+            fut = ex.submit(next, gen, done)
+            yield item
 
 
 # ---------------------------------------------------------------------------- centralized
