@@ -22,7 +22,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1"):
+def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, D=D, M=M):
     import torch  # noqa: F401  (one HIP runtime, loaded before libdopt)
     import torch.distributed as dist
 
@@ -55,13 +55,17 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1"):
 def test_ranks_match_single_context(tmp_path, dtype, mean, T, lagged, world):
     import torch.multiprocessing as mp
 
-    import _dopt
-    import topology as TP
-
     mp.start_processes(_rank_main, args=(world, _free_port(), dtype, str(tmp_path), mean, T, lagged), nprocs=world,
                        join=True, start_method="spawn")
     got = np.load(tmp_path / "dist.npz")
     assert len(got["obj"]) == len(got["cons"]) == T
+    _compare_single(got, dtype, mean, T)
+
+
+def _compare_single(got, dtype, mean, T, N=N, D=D, M=M, exact=True):
+    import _dopt
+    import topology as TP
+
     eng = _dopt.Engine(0, dtype)
     eng.generate_shards("logistic", N, D, M, seed=9)
     if mean:
@@ -72,7 +76,7 @@ def test_ranks_match_single_context(tmp_path, dtype, mean, T, lagged, world):
     obj, cons, _ = eng.run_dsgd(T, 0.05, M, 1e-3, 1e-3, 0.25)
     x = eng.get_models()
     eng.close()
-    if mean:  # the column sums are reduced per rank then across ranks: last-bit differences
+    if mean or not exact:  # column sums / split partial dots reduced per rank then across ranks
         np.testing.assert_allclose(got["x"], x, rtol=1e-12, atol=1e-15)
     else:
         np.testing.assert_array_equal(got["x"], x)
@@ -135,3 +139,17 @@ def test_trainers_multiprocess_match_reference(tmp_path):
         np.testing.assert_allclose(got[f"L{j}_objective"], z[f"L{j}_objective"][:300], rtol=1e-9)
         if label != "Centralized":
             np.testing.assert_allclose(got[f"L{j}_consensus"], z[f"L{j}_consensus"][:300], rtol=1e-9)
+
+
+@pytest.mark.parametrize("mean", [True, False])
+def test_column_blocked_ranks_match_single_context(tmp_path, mean):
+    """Rows too long for the row-resident kernel (fp64, d = 2100 > 2048: the column-blocked
+    k_split_* path of config C5) on 2 ranks: complete graph (all-reduced column sums) and
+    ring (halo rows), against one context."""
+    import torch.multiprocessing as mp
+
+    n, d, m, t = 16, 2100, 8, 4
+    mp.start_processes(_rank_main, args=(2, _free_port(), "float64", str(tmp_path), mean, t, "1", n, d, m),
+                       nprocs=2, join=True, start_method="spawn")
+    got = np.load(tmp_path / "dist.npz")
+    _compare_single(got, "float64", mean, t, n, d, m, exact=False)
