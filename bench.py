@@ -130,10 +130,10 @@ def main():
     dev = local % max(1, torch.cuda.device_count())
     if world > 1 or args.phase:
         torch.cuda.set_device(dev)
-        if world == 1:
+        if world == 1:  # --phase on one GPU: the multi-GPU code path incl. RCCL (one rank)
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29533")
-            dist.init_process_group("gloo", rank=0, world_size=1)
+            dist.init_process_group(args.backend, rank=0, world_size=1)
         else:
             dist.init_process_group(args.backend)
 

@@ -252,8 +252,13 @@ class DistributedDSGD:
         for w in works or ():
             w.wait()
 
+    def _solo(self):
+        """One rank: the reductions are identities and are skipped, unless
+        DOPT_FORCE_COLLECTIVES=1 (exercises the RCCL calls on a one-GPU box)."""
+        return self.dist.get_world_size(self.group) == 1 and os.environ.get("DOPT_FORCE_COLLECTIVES") != "1"
+
     def _all_reduce(self, t):
-        if self.dist.get_world_size(self.group) == 1:
+        if self._solo():
             return
         if self.device_comm:
             self.dist.all_reduce(t, group=self.group)
@@ -266,7 +271,7 @@ class DistributedDSGD:
         """Enqueue an all-reduce of t behind the current stream's work; returns the work to
         wait on (RCCL: the current stream waits at .wait(), the host does not), or None
         when the reduction is already complete (world 1, gloo)."""
-        if self.dist.get_world_size(self.group) == 1:
+        if self._solo():
             return None
         if self.device_comm:
             return self.dist.all_reduce(t, group=self.group, async_op=True)
@@ -416,6 +421,7 @@ class DistributedCentralized:
         engine.set_partition(self.n_global, self.rows_global)
         engine.set_stream(self.stream.cuda_stream)
 
+    _solo = DistributedDSGD._solo
     _all_reduce = DistributedDSGD._all_reduce
 
     def run(self, T, eta0, batch, lam_grad, lam_obj, f_opt=0.0, t0=0, objective=True, idx=None):

@@ -22,7 +22,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, D=D, M=M):
+def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, D=D, M=M, backend="gloo"):
     import torch  # noqa: F401  (one HIP runtime, loaded before libdopt)
     import torch.distributed as dist
 
@@ -30,8 +30,11 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
     import distributed as Dm
     import topology as TP
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DOPT_LAGGED=lagged)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DOPT_LAGGED=lagged,
+                      DOPT_FORCE_COLLECTIVES="1" if backend == "nccl" else "0")
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     top = TP.fully_connected(N) if mean else TP.random_regular(N, 4, seed=2)
     plan = Dm.build_plan(top, world, rank)
     eng = _dopt.Engine(0, dtype)
@@ -139,6 +142,20 @@ def test_trainers_multiprocess_match_reference(tmp_path):
         np.testing.assert_allclose(got[f"L{j}_objective"], z[f"L{j}_objective"][:300], rtol=1e-9)
         if label != "Centralized":
             np.testing.assert_allclose(got[f"L{j}_consensus"], z[f"L{j}_consensus"][:300], rtol=1e-9)
+
+
+@pytest.mark.parametrize("dtype,mean,lagged", [("float64", False, "1"), ("float32", False, "1"),
+                                               ("float64", True, "1"), ("float64", False, "0")])
+def test_rccl_one_rank_matches_single_context(tmp_path, dtype, mean, lagged):
+    """The RCCL code path on the one GPU this pool gives: backend "nccl", world 1, with the
+    all-reduces forced (DOPT_FORCE_COLLECTIVES=1) -- async all_reduce on the engine
+    stream, work.wait() ordering, object broadcast; the exchange itself has no peer here."""
+    import torch.multiprocessing as mp
+
+    mp.start_processes(_rank_main, args=(1, _free_port(), dtype, str(tmp_path), mean, T, lagged, N, D, M, "nccl"),
+                       nprocs=1, join=True, start_method="spawn")
+    got = np.load(tmp_path / "dist.npz")
+    _compare_single(got, dtype, mean, T, exact=not mean)
 
 
 @pytest.mark.parametrize("mean", [True, False])

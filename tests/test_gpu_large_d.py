@@ -28,14 +28,15 @@ def _engine(shards, problem, dtype="float64"):
     return eng
 
 
-@pytest.mark.parametrize("problem,topo,batch,mean", [
-    ("logistic", "ring", 12, False),        # full shard: next-round dots fused into the step
-    ("logistic", "ring", 5, False),         # minibatches: separate dots pass per round
-    ("quadratic", "fully_connected", 12, True),   # complete graph through column sums
-    ("quadratic", "grid", 4, False),
+@pytest.mark.parametrize("problem,topo,batch,mean,m", [
+    ("logistic", "ring", 12, False, 12),        # full shard: next-round dots fused into the step
+    ("logistic", "ring", 5, False, 12),         # minibatches: separate dots pass per round
+    ("quadratic", "fully_connected", 12, True, 12),   # complete graph through column sums
+    ("quadratic", "grid", 4, False, 12),
+    ("logistic", "ring", 24, False, 24),        # > 16 rows per worker: the row-split step kernel
 ])
-def test_split_rounds_vs_oracle(problem, topo, batch, mean):
-    n, d, m, T = 9, 2100, 12, 6  # d = 2100 fp64 -> 1050 chunks > 1024: column-blocked path
+def test_split_rounds_vs_oracle(problem, topo, batch, mean, m):
+    n, d, T = 9, 2100, 6  # d = 2100 fp64 -> 1050 chunks > 1024: column-blocked path
     shards = _data(n, d, m, 1, problem)
     cfg = {"problem_type": problem, "local_batch_size": batch, "learning_rate_eta0": 0.05,
            "l2_regularization_lambda": 1e-3, "strong_convexity_mu": 2e-3}

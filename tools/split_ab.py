@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
-"""In-process A/B of the column-blocked step with and without next-block prefetch
-(DOPT_SPLIT_PREFETCH; r1 on MI355X: 13.75 ms with, 13.58 ms without), on the C5 shape (quadratic, d = 2^20, m = b = 16, complete
-graph through column sums).  Results of both variants must agree."""
+"""In-process A/B of two column-blocked step variants selected by an environment knob
+(AB_KNOB, default DOPT_SPLIT_PREFETCH: next-block prefetch in the row-split kernel), on
+the C5 shape (quadratic, d = 2^20, m = b = 16, complete graph through column sums).
+Results of both variants must agree.  Measured on MI355X: prefetch 13.75 vs 13.58 ms;
+a barrier-free column-streaming kernel (every wave holds all 16 rows of a block, 183
+VGPRs, 2 waves/SIMD) 16.8 vs 14.1 ms -- both kept off."""
 import json
 import os
 import sys
@@ -26,7 +29,7 @@ def main():
     times, ref = {"1": [], "0": []}, None
     for rep in range(4):
         for v in ("1", "0"):
-            os.environ["DOPT_SPLIT_PREFETCH"] = v
+            os.environ[os.environ.get("AB_KNOB", "DOPT_SPLIT_PREFETCH")] = v
             eng.set_models(np.zeros((n, d), dtype=np.float32))
             eng.kernel_stats()
             obj, cons, _ = eng.run_dsgd(4, 1e-5, m, 1e-4, 1e-4, 0.0, want_time=False)
@@ -37,7 +40,7 @@ def main():
             else:
                 np.testing.assert_allclose(obj, ref[0], rtol=1e-6)
                 np.testing.assert_allclose(cons, ref[1], rtol=1e-5)
-        print(f"rep {rep}: prefetch {times['1'][-1]:.3f} ms, none {times['0'][-1]:.3f} ms", file=sys.stderr, flush=True)
+        print(f"rep {rep}: knob=1 {times['1'][-1]:.3f} ms, knob=0 {times['0'][-1]:.3f} ms", file=sys.stderr, flush=True)
     print(json.dumps({v: {"median_ms": float(np.median(t)), "tbps": bytes_per / (np.median(t) * 1e-3) / 1e12}
                       for v, t in times.items()}))
 
