@@ -134,7 +134,7 @@ hipError_t launch_fold(int dtype, const double* sc, int64_t nc, const double* sl
 hipError_t launch_cons(int dtype, const void* x, const void* xbar, int64_t n, int64_t ld, int32_t nchunks,
                        double* slab, hipStream_t s);
 // x_next[i] = sum_e cw[e] * src(ci[e]) - eta * G[i]  (trainer.py:173-175), src = x_old or halo.
-hipError_t launch_mix(int dtype, const RoundArgs& a, const void* G, int n_workers, hipStream_t s);
+hipError_t launch_mix(int dtype, int cpl, const RoundArgs& a, const void* G, int n_workers, hipStream_t s);
 // dst[k] = x[ids[k]] rows (halo send buffer).
 hipError_t launch_gather_rows(int dtype, const void* x, const int32_t* ids, int64_t n, int64_t ld,
                               int32_t nchunks, void* dst, hipStream_t s);

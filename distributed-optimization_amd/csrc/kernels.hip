@@ -1051,36 +1051,95 @@ hipError_t launch_cons(int dtype, const void* x, const void* xbar, int64_t n, in
 }
 
 // ---------------------------------------------------------------------------- mix (multi-GPU)
-// One wave per worker: lane l owns 16-byte chunks l, l+64, ...  The neighbour rows
-// are local iterates or halo rows received from other ranks; same CSR order as the
-// fused kernel, so the result is bitwise the single-GPU one.
-template <typename T>
+// One wave per worker: lane l owns 16-byte chunks l, l+64, ... (CPL per lane, as k_round).
+// The neighbour rows are local iterates or halo rows received from other ranks; same CSR
+// order and arithmetic as the fused kernel, so the result is bitwise the single-GPU one.
+// All loads of the worker (own row, gradient, up to MAXE neighbour rows) are issued before
+// the first use, so a wave has ~30 16-byte loads in flight instead of one dependent chain
+// per chunk.
+template <typename T, int CPL>
 __global__ __launch_bounds__(NT) void k_mix(const RoundArgs a, const T* __restrict__ G, int n) {
   using V = typename VT<T>::v;
   constexpr int VN = VT<T>::n;
+  constexpr int MAXE = CPL <= 4 ? 6 : 0;  // CSR entries held in registers (deg + 1 <= 5 for ring / torus / 4-regular)
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * NW + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (i >= n) return;
   const int64_t ld = a.ld;
+  const int nch = a.nchunks;
   const T eta = (T)a.eta;
+  const T* xo = (const T*)a.x_old + (int64_t)i * ld;
+  V own[CPL], gc[CPL], acc[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane + 64 * j;
+    const bool in = c < nch;
+    own[j] = in ? *(const V*)(xo + (int64_t)c * VN) : V(0);
+    gc[j] = in ? *(const V*)(G + (int64_t)i * ld + (int64_t)c * VN) : V(0);
+    acc[j] = V(0);
+  }
+  if (a.flags & F_MEAN) {
+#pragma unroll
+    for (int j = 0; j < CPL; ++j)
+      if (lane + 64 * j < nch) acc[j] = mix_chunk<T>(a, i, lane + 64 * j, own[j]);
+  } else {
+    const int64_t e0 = a.rp[i], e1 = a.rp[i + 1];
+    auto row_of = [&](int64_t e) {
+      const int col = a.ci[e];
+      return col < a.n_local ? (const T*)a.x_old + (int64_t)col * ld
+                             : (const T*)a.halo + (int64_t)(col - a.n_local) * ld;
+    };
+    if (e1 - e0 <= MAXE) {
+      V r[MAXE > 0 ? MAXE : 1][CPL];
+#pragma unroll
+      for (int k = 0; k < MAXE; ++k) {
+        if (e0 + k < e1) {
+          const T* src = row_of(e0 + k);
+#pragma unroll
+          for (int j = 0; j < CPL; ++j) {
+            const int c = lane + 64 * j;
+            r[k][j] = c < nch ? *(const V*)(src + (int64_t)c * VN) : V(0);
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < MAXE; ++k) {
+        if (e0 + k < e1) {
+          const T wt = ((const T*)a.cw)[e0 + k];
+#pragma unroll
+          for (int j = 0; j < CPL; ++j) acc[j] += wt * r[k][j];
+        }
+      }
+    } else {
+      for (int64_t e = e0; e < e1; ++e) {
+        const T wt = ((const T*)a.cw)[e];
+        const T* src = row_of(e);
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+          const int c = lane + 64 * j;
+          if (c < nch) acc[j] += wt * *(const V*)(src + (int64_t)c * VN);
+        }
+      }
+    }
+  }
   V dv = V(0);  // consensus term of x_old[i] (a.xsum): formed exactly as k_round's F_CONS forms it
-  for (int c = lane; c < a.nchunks; c += 64) {
-    const V own = *(const V*)((const T*)a.x_old + (int64_t)i * ld + (int64_t)c * VN);
+  const int64_t s0 = a.sptr ? a.sptr[i] : 0, s1 = a.sptr ? a.sptr[i + 1] : 0;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane + 64 * j;
+    if (c >= nch) continue;
     if (a.xsum) {  // xbar = (T)(column sum / n) of the iterates being mixed, as k_colsum_final rounds it
       V xb;
 #pragma unroll
       for (int e = 0; e < VN; ++e) xb[e] = (T)(a.xsum[(int64_t)c * VN + e] / a.xsum_n);
       if (i == 0) *(V*)((T*)a.xbar_out + (int64_t)c * VN) = xb;
-      const V t = own - xb;
+      const V t = own[j] - xb;
       dv += t * t;
     }
-    const V acc = mix_chunk<T>(a, i, c, own);
-    const V gc = *(const V*)(G + (int64_t)i * ld + (int64_t)c * VN);
-    const V xn = acc - eta * gc;
+    const V xn = acc[j] - eta * gc[j];
     *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = xn;
-    if (a.sptr)  // rows peers read next round: the send buffer is refreshed here, no gather kernel
-      for (int64_t s = a.sptr[i]; s < a.sptr[i + 1]; ++s)
-        *(V*)((T*)a.send + (int64_t)a.sslot[s] * ld + (int64_t)c * VN) = xn;
+    for (int64_t q = s0; q < s1; ++q)  // rows peers read next round: the send buffer is refreshed here
+      *(V*)((T*)a.send + (int64_t)a.sslot[q] * ld + (int64_t)c * VN) = xn;
   }
   if (a.xsum && a.slab_cons) {
     const double cs = wave_sum((double)hsum<T>(dv));
@@ -1088,14 +1147,24 @@ __global__ __launch_bounds__(NT) void k_mix(const RoundArgs a, const T* __restri
   }
 }
 
-hipError_t launch_mix(int dtype, const RoundArgs& a, const void* G, int n_workers, hipStream_t s) {
-  if (n_workers <= 0) return hipSuccess;
-  const dim3 grid((n_workers + NW - 1) / NW);
-  if (dtype == 0)
-    hipLaunchKernelGGL(k_mix<float>, grid, dim3(NT), 0, s, a, (const float*)G, n_workers);
-  else
-    hipLaunchKernelGGL(k_mix<double>, grid, dim3(NT), 0, s, a, (const double*)G, n_workers);
+template <typename T>
+static hipError_t launch_mix_t(int cpl, const RoundArgs& a, const T* G, int n, hipStream_t s) {
+  const dim3 grid((n + NW - 1) / NW);
+  switch (cpl) {
+    case 1: hipLaunchKernelGGL((k_mix<T, 1>), grid, dim3(NT), 0, s, a, G, n); break;
+    case 2: hipLaunchKernelGGL((k_mix<T, 2>), grid, dim3(NT), 0, s, a, G, n); break;
+    case 4: hipLaunchKernelGGL((k_mix<T, 4>), grid, dim3(NT), 0, s, a, G, n); break;
+    case 8: hipLaunchKernelGGL((k_mix<T, 8>), grid, dim3(NT), 0, s, a, G, n); break;
+    case 16: hipLaunchKernelGGL((k_mix<T, 16>), grid, dim3(NT), 0, s, a, G, n); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
+}
+
+hipError_t launch_mix(int dtype, int cpl, const RoundArgs& a, const void* G, int n_workers, hipStream_t s) {
+  if (n_workers <= 0) return hipSuccess;
+  return dtype == 0 ? launch_mix_t<float>(cpl, a, (const float*)G, n_workers, s)
+                    : launch_mix_t<double>(cpl, a, (const double*)G, n_workers, s);
 }
 
 template <typename T>

@@ -1363,7 +1363,7 @@ int dopt_phase_mix(dopt_ctx* c, int64_t t, double eta0) {
       a.sslot = c->sslot;
       a.send = c->send;
     }
-    HIPOK(launch_mix(c->dtype, a, c->G, (int)c->n, c->stream));
+    HIPOK(launch_mix(c->dtype, c->cpl, a, c->G, (int)c->n, c->stream));
     c->send_fresh = c->n_send > 0;
   }
   c->cur ^= 1;
@@ -1506,7 +1506,7 @@ int dopt_phase_mix_lagged(dopt_ctx* c, int64_t t, double eta0, const double* sum
   a.xbar_out = c->xbar[c->xb ^ 1];
   a.slab_cons = consensus ? c->slab_cons : nullptr;
   if (c->n > 0) {
-    HIPOK(launch_mix(c->dtype, a, c->G, (int)c->n, c->stream));
+    HIPOK(launch_mix(c->dtype, c->cpl, a, c->G, (int)c->n, c->stream));
   } else {  // no worker here: the average still has to be written
     HIPOK(launch_colsum_final(c->dtype, sum_dev, 1, n_div(c), c->ld, (int32_t)c->nch, c->xbar[c->xb ^ 1], nullptr,
                               0.0, 0, c->stream));
