@@ -216,6 +216,11 @@ class DistributedDSGD:
         nch = (ld * esz) // 16
         self._lagged_ok = (mean is None and nch <= 16 * 64 and
                            os.environ.get("DOPT_LAGGED", "1") != "0")
+        # every rank joins one collective before the first batched send/recv, which may
+        # involve only some ranks (a torus strip talks to two peers): with NCCL the first
+        # call in a group must include all of its ranks
+        if self.device_comm and dist.get_world_size(group) > 1:
+            dist.all_reduce(torch.zeros(1, device=self.dev), group=group)
 
     # -- transport
     def _start_exchange(self):
