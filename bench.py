@@ -104,6 +104,9 @@ def main():
     ap.add_argument("--d", type=int, default=1024)
     ap.add_argument("--m", type=int, default=512)
     ap.add_argument("--dtype", default="float32")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="C3 minibatch per worker (0: the full shard, the metric's configuration); b < m "
+                         "draws the minibatches on the device (sampling='device', Philox + Floyd)")
     ap.add_argument("--degree", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -175,6 +178,12 @@ def main():
     eng = _dopt.Engine(dev, args.dtype)
     eng.generate_shards(problem, plan.n_local, d, m, seed=1000, flip=0.05, first_worker=plan.lo)
     lam = 1e-4
+    b = args.batch if 0 < args.batch < m else m
+    if b < m:  # minibatches drawn on the device inside the pass over all rows (the metrics need them all)
+        if world > 1 or args.phase or args.config != "c3":
+            raise SystemExit("--batch < m: single-GPU C3 only (device sampling)")
+        eng.set_sampler("device", seed=7)
+        workload = workload.replace(f"m=b={m}", f"m={m}, b={b} (device-drawn minibatches)")
     if world > 1 or args.phase:
         mean_local = None if mean is None else (mean[0], mean[1][plan.lo:plan.hi])
         runner = distributed.DistributedDSGD(eng, plan, n_global, n_global * m, device=dev, mean=mean_local)
@@ -189,7 +198,7 @@ def main():
             eng.set_topology(top.row_ptr, top.col, top.w)
 
         def rounds(k):
-            obj, cons, _ = eng.run_dsgd(k, eta0, m, lam, lam, 0.0)
+            obj, cons, _ = eng.run_dsgd(k, eta0, b, lam, lam, 0.0)
             return obj, cons
     log("warmup")
     if args.warmup > 0:
@@ -246,7 +255,7 @@ def main():
         "dtype": "f32" if esz == 4 else "f64",
         "data": "synthetic (device-generated X~N(0,1)+bias, planted-w* labels, 5% flips)",
         "config": {"workload": workload,
-                   "workers_per_gpu": n, "d": d, "rows_per_worker": m, "batch": m, "topology": top.name,
+                   "workers_per_gpu": n, "d": d, "rows_per_worker": m, "batch": b, "topology": top.name,
                    "degree": args.degree if args.config == "c3" else None,
                    "halo_rows_per_gpu": int(plan.n_halo),
                    "parallelism": (f"dp{world}: one graph of {n_global} workers, "

@@ -23,6 +23,7 @@ OK, ERR_INVALID, ERR_HIP, ERR_STATE, ERR_UNSUPPORTED, ERR_COMM = 0, -1, -2, -3, 
 LOGISTIC, QUADRATIC = 0, 1
 F32, F64 = 0, 1
 RUN_OBJECTIVE, RUN_CONSENSUS = 1, 2
+SAMPLE_HOST, SAMPLE_DEVICE = 0, 1
 MAX_BIP_ROWS = 65536  # dopt.h DOPT_MAX_BIP_ROWS: minibatch gradient inside the metrics pass
 PROBLEMS = {"logistic": LOGISTIC, "quadratic": QUADRATIC}
 DTYPES = {"float32": F32, "fp32": F32, "f32": F32, np.float32: F32,
@@ -86,6 +87,7 @@ _SIGS = {
     "dopt_eval_full": ([_P, _P, _D, _P, _P], ctypes.c_int),
     "dopt_kernel_stats": ([_P, _P, _P], ctypes.c_int),
     "dopt_set_profiling": ([_P, ctypes.c_int], ctypes.c_int),
+    "dopt_set_sampler": ([_P, ctypes.c_int, ctypes.c_uint64, _I64], ctypes.c_int),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -400,6 +402,12 @@ class Engine:
         f = np.zeros(1)
         check(lib().dopt_eval_full(self._h, _ptr(w), float(reg), _ptr(f), _ptr(g)))
         return float(f[0]), g
+
+    def set_sampler(self, mode, seed=0, first_worker=0):
+        """'host' (default: minibatch rounds need idx) or 'device' (Philox + Floyd draws on
+        the GPU inside the pass over all rows; not the reference's RNG stream)."""
+        m = {"host": SAMPLE_HOST, "device": SAMPLE_DEVICE}[mode] if isinstance(mode, str) else int(mode)
+        check(lib().dopt_set_sampler(self._h, m, int(seed) & (2 ** 64 - 1), int(first_worker)))
 
     # -- profiling
     def set_profiling(self, on, every=1):

@@ -19,6 +19,7 @@ enum : int32_t {
   F_GSUM = 128,        // with F_GOUT: store the raw sum of coef * row (no 1/b, no lam) -- full gradients
   F_LOSS2 = 256,       // metrics-only pass: also the objective at w_shared (from z) into slab_loss2
   F_BIP = 512,         // minibatch gradient inside the metrics pass over all rows (k_round VAR bit 6)
+  F_DEVSAMPLE = 1024,  // with F_BIP: the minibatch is drawn on the device (Philox + Floyd), not from idx
 };
 constexpr int64_t kMaxBipRows = 65536;  // shard rows the F_BIP byte map holds in LDS
 
@@ -62,6 +63,10 @@ struct RoundArgs {
   int32_t pre_rows;       // CSR rows per worker prefetched to LDS by the fused kernel (0: off)
   int32_t groups;         // column-block groups = gridDim.y
   int32_t bip_rows;       // F_BIP: the largest shard (LDS byte map size)
+  // F_DEVSAMPLE: the minibatch of worker i in this round is a function of (seed, round, wid0 + i)
+  uint64_t seed;
+  int64_t round;
+  int64_t wid0;
   // multi-GPU send rows written by k_mix: worker i's new row also goes to send rows
   // sslot[sptr[i] .. sptr[i+1]) (null sptr: no halo plan)
   const int64_t* sptr;

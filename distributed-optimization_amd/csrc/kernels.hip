@@ -105,6 +105,41 @@ __device__ __forceinline__ T hsum(V v) {
   return s;
 }
 
+// Philox4x32-10 (Salmon et al., SC'11): counter-based, so a worker's minibatch of a round
+// is a pure function of (seed, round, worker) -- no generator state anywhere.
+struct U4 {
+  uint32_t x, y, z, w;
+};
+__device__ __forceinline__ U4 philox4x32(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+    c = U4{(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// Device minibatch (sampling = 'device', the non-parity throughput mode of SURVEY section 7):
+// Floyd's algorithm marks a uniform nb-subset of [0, m) in the LDS byte map; draw k is word
+// k % 4 of philox(counter = (k / 4, worker, round lo, round hi), key = seed), mapped to
+// [0, j] by a 32x32 multiply-high (bias <= m / 2^32).  oracle/device_sampler.py restates it.
+__device__ void floyd_sample(unsigned char* bmask, int64_t m, int64_t nb, uint64_t seed, int64_t round,
+                             int64_t worker) {
+  U4 r = {0, 0, 0, 0};
+  int64_t k = 0;
+  for (int64_t j = m - nb; j < m; ++j, ++k) {
+    if ((k & 3) == 0)
+      r = philox4x32(U4{(uint32_t)(k >> 2), (uint32_t)worker, (uint32_t)round, (uint32_t)((uint64_t)round >> 32)},
+                     (uint32_t)seed, (uint32_t)(seed >> 32));
+    const uint32_t u = (k & 3) == 0 ? r.x : (k & 3) == 1 ? r.y : (k & 3) == 2 ? r.z : r.w;
+    const int64_t t = (int64_t)(((uint64_t)u * (uint64_t)(j + 1)) >> 32);
+    if (bmask[t]) bmask[j] = 1;
+    else bmask[t] = 1;
+  }
+}
+
 // scipy.special.expit(x) = 1 / (1 + exp(-x)); the gradient needs expit(-y z).
 template <typename T>
 __device__ __forceinline__ T sigmoid_neg(T yz) {
@@ -179,7 +214,8 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
   const int64_t ld = a.ld;
   const int64_t row0 = a.off[i];
   const int64_t m = a.off[i + 1] - row0;
-  const int64_t nb = (GRAD && a.idx) ? (a.b < m ? a.b : m) : m;
+  const bool dev_sample = (flags & F_DEVSAMPLE) != 0;
+  const int64_t nb = (GRAD && (a.idx || dev_sample)) ? (a.b < m ? a.b : m) : m;
   const T* __restrict__ X = (const T*)a.X;
   const T* __restrict__ Y = (const T*)a.y;
   const T* wsrc = (flags & F_SHARED) ? (const T*)a.w_shared : (const T*)a.x_old + (int64_t)i * ld;
@@ -206,7 +242,11 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
   if (BIP) {
     for (int64_t r = threadIdx.x; r < m; r += NT) bmask[r] = 0;
     __syncthreads();
-    for (int64_t k = threadIdx.x; k < nb; k += NT) bmask[a.idx[(int64_t)i * a.b + k]] = 1;
+    if (dev_sample) {
+      if (threadIdx.x == 0) floyd_sample(bmask, m, nb, a.seed, a.round, a.wid0 + i);
+    } else {
+      for (int64_t k = threadIdx.x; k < nb; k += NT) bmask[a.idx[(int64_t)i * a.b + k]] = 1;
+    }
     __syncthreads();
   }
 

@@ -165,6 +165,11 @@ struct dopt_ctx {
   void* sx = nullptr;
   size_t sx_cap = 0;
 
+  // minibatch sampling for rounds run with idx == NULL and batch < shard (dopt_set_sampler)
+  int sampler = DOPT_SAMPLE_HOST;
+  uint64_t sample_seed = 0;
+  int64_t sample_wid0 = 0;
+
   // profiling of k_round
   bool prof = false;
   int64_t prof_every = 1;      // bracket every k-th gradient-kernel launch (events cost ~30 us per pair)
@@ -661,9 +666,14 @@ int check_run(dopt_ctx* c, int64_t T, int64_t batch, const int32_t* idx, bool ne
   if (need_topo && !c->have_topo) return fail(DOPT_ERR_STATE, "no topology set");
   CHECK_ARG(T >= 0, "T must be >= 0");
   CHECK_ARG(batch >= 0, "batch must be >= 0");
-  if (!idx && batch < c->max_m)
-    return fail(DOPT_ERR_INVALID, "idx == NULL needs full-shard batches (batch %lld < shard %lld)",
-                (long long)batch, (long long)c->max_m);
+  if (!idx && batch < c->max_m) {
+    if (c->sampler != DOPT_SAMPLE_DEVICE)
+      return fail(DOPT_ERR_INVALID, "idx == NULL needs full-shard batches (batch %lld < shard %lld) or the "
+                  "device sampler", (long long)batch, (long long)c->max_m);
+    if (c->split || c->max_m > kMaxBipRows)
+      return fail(DOPT_ERR_UNSUPPORTED, "device sampling: row-resident contexts with shards of at most %lld rows",
+                  (long long)kMaxBipRows);
+  }
   return DOPT_OK;
 }
 
@@ -946,7 +956,8 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
   c->send_fresh = false;
   const bool want_obj = flags & DOPT_RUN_OBJECTIVE, want_cons = flags & DOPT_RUN_CONSENSUS;
   const bool metrics = want_obj || want_cons;
-  const bool bip = metrics && bip_possible(c, batch, idx);
+  const bool dev = !idx && batch < c->max_m;  // device sampler (check_run)
+  const bool bip = metrics && (dev ? !c->obj_sep : bip_possible(c, batch, idx));
   const bool fused = (batch >= c->max_m || bip) && !c->obj_sep;
   const int64_t CH = idx ? idx_chunk_rounds(c, T, batch) : 1;
   int& xb = c->xb;
@@ -969,10 +980,14 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
     a.eta = eta0 / sqrt((double)(t + 1));  // trainer.py:138-140
     a.lam = lam_grad;
     const bool met = fused && metrics && h > 0;
-    a.flags |= F_STEP | (met && want_cons ? F_CONS : 0) | (met && want_obj ? F_LOSS : 0) | (met && bip ? F_BIP : 0);
+    a.flags |= F_STEP | (met && want_cons ? F_CONS : 0) | (met && want_obj ? F_LOSS : 0) |
+               ((met && bip) || dev ? F_BIP : 0) | (dev ? F_DEVSAMPLE : 0);
+    a.seed = c->sample_seed;
+    a.round = t;
+    a.wid0 = c->sample_wid0;
     if (a.flags & F_LOSS) c->loss_groups = c->n;  // per-worker loss slabs
     if (c->prof && (rc = prof_event(c, false))) return rc;
-    HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, met, a, (int)c->n, c->stream));
+    HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, met || dev, a, (int)c->n, c->stream));
     if (c->prof && (rc = prof_event(c, true))) return rc;
     // xbar_{t+1} (trainer.py:182); the stamp marks the end of round t's update (trainer.py:181)
     HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur ^ 1], c->n, c->ld, (int32_t)c->nch, kRowsPerGroup,
@@ -1004,6 +1019,7 @@ int dopt_run_centralized(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_
   CHECK_ARG(c, "ctx is NULL");
   int rc;
   if ((rc = check_run(c, T, batch, idx, false))) return rc;
+  if (!idx && batch < c->max_m) return fail(DOPT_ERR_UNSUPPORTED, "device sampling: D-SGD rounds only");
   if ((rc = set_device(c))) return rc;
   if ((rc = ensure_hist(c, T))) return rc;
   if (!c->G && (rc = dalloc(&c->G, (size_t)c->n * c->ld * c->esz))) return rc;
@@ -1177,6 +1193,16 @@ int dopt_eval_full(dopt_ctx* c, const double* w, double reg, double* f_out, doub
   return DOPT_OK;
 }
 
+int dopt_set_sampler(dopt_ctx* c, int mode, uint64_t seed, int64_t first_worker) {
+  CHECK_ARG(c, "ctx is NULL");
+  CHECK_ARG(mode == DOPT_SAMPLE_HOST || mode == DOPT_SAMPLE_DEVICE, "unknown sampler %d", mode);
+  CHECK_ARG(first_worker >= 0, "first_worker must be >= 0");
+  c->sampler = mode;
+  c->sample_seed = seed;
+  c->sample_wid0 = first_worker;
+  return DOPT_OK;
+}
+
 int dopt_set_profiling(dopt_ctx* c, int enable) {
   CHECK_ARG(c, "ctx is NULL");
   CHECK_ARG(enable >= 0, "enable must be >= 0");
@@ -1291,6 +1317,7 @@ int dopt_phase_grad(dopt_ctx* c, int64_t batch, const int32_t* idx, double lam_g
   CHECK_ARG(c, "ctx is NULL");
   int rc;
   if ((rc = check_run(c, 1, batch, idx, false))) return rc;
+  if (!idx && batch < c->max_m) return fail(DOPT_ERR_UNSUPPORTED, "device sampling: single-context rounds only");
   if (!c->G && (rc = dalloc(&c->G, (size_t)c->n * c->ld * c->esz))) return rc;
   if (idx && (rc = upload_idx_chunk(c, idx, 0, 1, batch))) return rc;
   const bool cons = metric_flags & DOPT_RUN_CONSENSUS, loss = metric_flags & DOPT_RUN_OBJECTIVE;

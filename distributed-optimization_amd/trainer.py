@@ -15,7 +15,10 @@ Config keys beyond the reference's (all optional):
   device     GPU ordinal (default: $LOCAL_RANK or $DOPT_DEVICE or 0)
   sampling   'legacy' (default): minibatch indices are the exact numpy legacy
              RNG stream (np.random.choice per worker per round, worker.py:27);
-             'full': with full-shard batches skip the RNG entirely
+             'full': with full-shard batches skip the RNG entirely;
+             'device': D-SGD minibatches drawn on the GPU (Philox + Floyd, seed
+             'sampling_seed', default 0) inside the pass over every shard row -- the
+             throughput mode, NOT the reference's stream (numpy's RNG is not advanced)
   regular_degree / topology_seed   for topology='random_regular'
   spectral_gap   force / skip the spectral-gap print (default: N <= 4096)
   mean_mixing_min  complete graphs of at least this many workers mix through the
@@ -120,6 +123,8 @@ def _engine(workers, n_features, config, lo=0, hi=None):
         eng.load_shards(config["problem_type"], X, y, off)
         eng.obj_key = None
         _ENGINES[key] = eng
+    device_sampling = config.get("sampling", "legacy") == "device"
+    eng.set_sampler("device" if device_sampling else "host", seed=int(config.get("sampling_seed", 0)), first_worker=lo)
     return eng
 
 
@@ -178,7 +183,8 @@ def _index_chunks(workers, T, config):
     b = _batch_size(workers)
     rows = np.array([w.n_local_samples for w in workers], dtype=np.int64)
     full = b >= (rows.max() if len(rows) else 0)
-    skip_rng = full and config.get("sampling", "legacy") == "full"
+    mode = config.get("sampling", "legacy")
+    skip_rng = (full and mode == "full") or mode == "device"  # device: the GPU draws the minibatches
     if skip_rng:
         ch = max(1, T)
         for t in range(0, T, ch):

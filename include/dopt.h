@@ -129,6 +129,18 @@ int dopt_get_models(dopt_ctx *ctx, double *x);
 int dopt_set_global(dopt_ctx *ctx, const double *x);
 int dopt_get_global(dopt_ctx *ctx, double *x);
 
+/* Minibatch sampling for dopt_run_dsgd calls with idx == NULL and batch < shard size.
+ * DOPT_SAMPLE_HOST (default): such calls are rejected -- parity mode draws the reference's
+ * legacy MT19937 stream on the host (dopt_mt_choice_rounds) and passes idx.
+ * DOPT_SAMPLE_DEVICE: the throughput mode of SURVEY section 7 (not the reference's
+ * stream): worker i's minibatch in round t is a uniform subset of its shard drawn on the
+ * device by Floyd's algorithm from Philox4x32-10(key = seed, counter = (k / 4, first_worker
+ * + i, t)), inside the pass over all shard rows (shards of at most DOPT_MAX_BIP_ROWS rows;
+ * D-SGD rounds on one context). */
+#define DOPT_SAMPLE_HOST 0
+#define DOPT_SAMPLE_DEVICE 1
+int dopt_set_sampler(dopt_ctx *ctx, int mode, uint64_t seed, int64_t first_worker);
+
 /* T rounds of DecentralizedTrainer.run (trainer.py:161-193), rounds t0..t0+T-1:
  *   g_i = grad f_i(x_i; minibatch)   (worker.py:30-44, obj_problems.py)
  *   x_i <- sum_j W_ij x_j - eta0/sqrt(t+1) * g_i   (trainer.py:173-175)

@@ -339,3 +339,52 @@ def test_minibatch_in_metrics_pass_matches_separate_pass(dtype, monkeypatch):
     tol = 1e-12 if dtype == "float64" else 2e-6
     for a_, b_ in zip(runs[0], runs[1]):
         np.testing.assert_allclose(a_, b_, rtol=tol, atol=1e-14 if dtype == "float64" else 1e-7)
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+def test_device_sampler_matches_host_replay(dtype):
+    """sampling = 'device' draws every minibatch on the GPU (Philox4x32-10 + Floyd inside
+    the pass over all rows).  Replaying the same minibatches, restated on the host by
+    oracle/device_sampler.py, through the index path gives the same trajectory (ragged
+    and empty shards, t0 > 0); numpy's generator is not touched."""
+    import device_sampler as DS
+
+    rng = np.random.default_rng(23)
+    m_rows = [40, 33, 0, 40, 17, 5, 40, 28]
+    n, d, b, T, t0, seed = len(m_rows), 45, 8, 12, 3, 99
+    off = np.concatenate([[0], np.cumsum(m_rows)])
+    X = np.hstack([rng.standard_normal((off[-1], d - 1)), np.ones((off[-1], 1))])
+    y = rng.choice(np.array([-1.0, 1.0]), off[-1])
+    top = topology.random_regular(n, 4, seed=5)
+    np.random.seed(1)
+    pos = np.random.get_state()[2]
+    runs = []
+    for mode in ("device", "host"):
+        eng = _dopt.Engine(0, dtype)
+        eng.load_shards("logistic", X, y, off)
+        eng.set_topology(top.row_ptr, top.col, top.w)
+        eng.set_sampler(mode, seed=seed)
+        idx = None if mode == "device" else DS.rounds(seed, t0, T, m_rows, b)
+        obj, cons, _ = eng.run_dsgd(T, 0.05, b, 1e-3, 1e-3, 0.0, idx=idx, t0=t0)
+        runs.append((obj, cons, eng.get_models()))
+        eng.close()
+    assert np.random.get_state()[2] == pos
+    tol = 1e-12 if dtype == "float64" else 2e-6
+    for a_, b_ in zip(runs[0], runs[1]):
+        np.testing.assert_allclose(a_, b_, rtol=tol, atol=1e-14 if dtype == "float64" else 1e-7)
+
+
+def test_device_sampling_trainer_mode():
+    """The drop-in trainer with config sampling='device': D-SGD runs without touching
+    numpy's stream; the centralized trainer reports the mode as unsupported."""
+    meta, z = _load("c2")
+    cfg = dict(meta["config"], sampling="device", sampling_seed=4)
+    shards, Xf, yf = _shards(meta, z)
+    np.random.seed(203)
+    pos = np.random.get_state()[2]
+    hist, _ = _make_trainer("D-SGD (Ring)", shards, cfg).run(200, Xf, yf, meta["f_opt"])
+    assert np.random.get_state()[2] == pos
+    assert len(hist["objective"]) == len(hist["consensus_error"]) == 200
+    assert np.all(np.isfinite(hist["objective"])) and hist["objective"][-1] < hist["objective"][0]
+    with pytest.raises(NotImplementedError):
+        _make_trainer("Centralized", shards, cfg).run(5, Xf, yf, meta["f_opt"])

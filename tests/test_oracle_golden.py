@@ -127,3 +127,25 @@ def test_partitioned_round_is_bit_exact():
         h, _, xp, _ = O.run_decentralized(shards, W, 30, cfg, Xf, yf, meta["f_opt"], rng_state=st, partitions=P)
         np.testing.assert_array_equal(xp, xr)
         assert h["objective"] == ref["objective"]
+
+
+def test_device_sampler_restatement_uniform_subsets():
+    """oracle/device_sampler.py (the GPU's Philox + Floyd minibatch, restated): exactly
+    min(b, m) distinct rows in [0, m), deterministic in (seed, round, worker), and uniform:
+    over 4000 draws of 5 of 20 rows each row's count stays within 5 sigma of 1000."""
+    import device_sampler as DS
+
+    for m, b in ((20, 5), (7, 7), (5, 9), (1, 1), (300, 16)):
+        s = DS.minibatch(3, 11, 2, m, b)
+        assert len(s) == min(b, m) and len(np.unique(s)) == len(s) and s.min() >= 0 and s.max() < m
+        np.testing.assert_array_equal(s, DS.minibatch(3, 11, 2, m, b))
+    assert not np.array_equal(DS.minibatch(3, 11, 2, 300, 16), DS.minibatch(3, 12, 2, 300, 16))
+    counts = np.zeros(20)
+    for t in range(4000):
+        counts[DS.minibatch(7, t, 0, 20, 5)] += 1
+    p = 5 / 20
+    assert np.all(np.abs(counts - 4000 * p) < 5 * np.sqrt(4000 * p * (1 - p)))
+    idx = DS.rounds(1, 4, 2, [3, 10, 0], 4, first_worker=5)
+    assert idx.shape == (2, 3, 4)
+    np.testing.assert_array_equal(idx[1, 1], DS.minibatch(1, 5, 6, 10, 4))
+    assert np.all(idx[:, 0, 3] == -1) and np.all(idx[:, 2] == -1)
