@@ -68,6 +68,16 @@ def _say(msg, config):
         print(msg)
 
 
+def _warn_nonfinite(history, config):
+    """Failure detection: the reference only skips non-finite values
+    when plotting (simulator.py:181-183); here a diverged run also says so once."""
+    for key in ("objective", "consensus_error"):
+        v = np.asarray(history.get(key, []), dtype=np.float64)
+        if v.size and not np.all(np.isfinite(v)):
+            first = int(np.argmin(np.isfinite(v)))
+            _say(f"Warning: non-finite {key} from round {first} on (diverged? lower learning_rate_eta0)", config)
+
+
 def _device(config):
     return int(config.get("device", os.environ.get("LOCAL_RANK", os.environ.get("DOPT_DEVICE", 0))))
 
@@ -267,6 +277,7 @@ class CentralizedTrainer:
             # trainer.py:50,60-61: N*d up + N*d down per round (Python ints)
             self.total_floats_transmitted += n * (self.n_workers * self.n_features * 2)
         self.x_global = eng.get_global()
+        _warn_nonfinite(self.history, self.config)
         print(f"C-SGD training finished. Time: {time.time() - start_time:.2f}sseconds")
         return self.history, self.x_global
 
@@ -293,6 +304,7 @@ class CentralizedTrainer:
             self.history["time"].extend(list(np.linspace(t_host, time.time() - start_time, n + 1)[1:]))
             self.total_floats_transmitted += n * (self.n_workers * self.n_features * 2)
         self.x_global = eng.get_global()
+        _warn_nonfinite(self.history, self.config)
         _say(f"C-SGD training finished. Time: {time.time() - start_time:.2f}sseconds", cfg)
         return self.history, self.x_global
 
@@ -374,6 +386,7 @@ class DecentralizedTrainer:
         models = eng.get_models()
         for i, worker in enumerate(self.workers):  # trainer.py:178-179: row views
             worker.x = models[i, :]
+        _warn_nonfinite(self.history, self.config)
         print(f"Decentralized ({self.topology}) training finished. Time: {time.time() - start_time:.2f}s")
         final_avg_model = np.mean([worker.x for worker in self.workers], axis=0)
         return self.history, final_avg_model
@@ -407,6 +420,7 @@ class DecentralizedTrainer:
         models = runner.gather_models()
         for i, worker in enumerate(self.workers):
             worker.x = models[i, :]
+        _warn_nonfinite(self.history, self.config)
         _say(f"Decentralized ({self.topology}) training finished. Time: {time.time() - start_time:.2f}s", cfg)
         final_avg_model = np.mean([worker.x for worker in self.workers], axis=0)
         return self.history, final_avg_model
