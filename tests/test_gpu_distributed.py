@@ -35,7 +35,7 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
     if backend == "nccl":
         torch.cuda.set_device(0)
     dist.init_process_group(backend, rank=rank, world_size=world)
-    top = TP.fully_connected(N) if mean else TP.random_regular(N, 4, seed=2)
+    top = _topo(mean, N, world if os.environ.get("DOPT_TEST_PARTITION") == "1" else 0)
     plan = Dm.build_plan(top, world, rank)
     eng = _dopt.Engine(0, dtype)
     eng.generate_shards("logistic", plan.n_local, D, M, seed=9, first_worker=plan.lo)
@@ -68,16 +68,29 @@ def test_ranks_match_single_context(tmp_path, dtype, mean, T, lagged, world):
     _compare_single(got, dtype, mean, T)
 
 
-def _compare_single(got, dtype, mean, T, N=N, D=D, M=M, exact=True):
-    import _dopt
+def _topo(mean, n, parts=0):
+    """The test graph; with parts > 0 relabelled by the spectral partition for that many
+    ranks (bench.py's C3 placement)."""
+    import distributed as Dm
     import topology as TP
+
+    if mean:
+        return TP.fully_connected(n)
+    top = TP.random_regular(n, 4, seed=2)
+    if parts:
+        top = TP.relabel(top, Dm.partition_order(Dm.graph_partition(top, parts)))
+    return top
+
+
+def _compare_single(got, dtype, mean, T, N=N, D=D, M=M, exact=True, parts=0):
+    import _dopt
 
     eng = _dopt.Engine(0, dtype)
     eng.generate_shards("logistic", N, D, M, seed=9)
+    top = _topo(mean, N, parts)
     if mean:
-        eng.set_mixing_mean(*TP.fully_connected(N).uniform_offdiag())
+        eng.set_mixing_mean(*top.uniform_offdiag())
     else:
-        top = TP.random_regular(N, 4, seed=2)
         eng.set_topology(top.row_ptr, top.col, top.w)
     obj, cons, _ = eng.run_dsgd(T, 0.05, M, 1e-3, 1e-3, 0.25)
     x = eng.get_models()
@@ -161,6 +174,19 @@ def test_rccl_one_rank_matches_single_context(tmp_path, dtype, mean, lagged):
                        nprocs=1, join=True, start_method="spawn")
     got = np.load(tmp_path / "dist.npz")
     _compare_single(got, dtype, mean, T, exact=not mean)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_partitioned_graph_ranks_match_single_context(tmp_path, monkeypatch, world):
+    """bench.py's placement: the random regular graph relabelled by the spectral partition,
+    2 and 4 ranks (gloo) vs one context on the same relabelled graph -- bitwise iterates."""
+    import torch.multiprocessing as mp
+
+    monkeypatch.setenv("DOPT_TEST_PARTITION", "1")
+    mp.start_processes(_rank_main, args=(world, _free_port(), "float64", str(tmp_path), False, 5, "1"),
+                       nprocs=world, join=True, start_method="spawn")
+    got = np.load(tmp_path / "dist.npz")
+    _compare_single(got, "float64", False, 5, parts=world)
 
 
 @pytest.mark.parametrize("which", ["obj", "cons"])
