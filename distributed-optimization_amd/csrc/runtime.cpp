@@ -321,7 +321,9 @@ int set_layout(dopt_ctx* c, int problem, int64_t n, int64_t d) {
   c->split = cpl > max_chunks_per_lane();
   if (c->split) {  // enough workgroups to fill 256 CUs several times over
     const int64_t nblk = (nch + 63) / 64;
-    c->split_groups = (int)std::max<int64_t>(1, std::min<int64_t>(nblk, (4096 + n - 1) / n));
+    const char* gw = getenv("DOPT_SPLIT_WGS");  // A/B knob: target workgroups per column-blocked launch
+    const int64_t target = gw ? std::max<int64_t>(1, atoll(gw)) : 4096;
+    c->split_groups = (int)std::max<int64_t>(1, std::min<int64_t>(nblk, (target + n - 1) / n));
   }
   c->problem = problem;
   c->mean_mix = false;
