@@ -180,9 +180,9 @@ def main():
     lam = 1e-4
     b = args.batch if 0 < args.batch < m else m
     if b < m:  # minibatches drawn on the device inside the pass over all rows (the metrics need them all)
-        if world > 1 or args.phase or args.config != "c3":
-            raise SystemExit("--batch < m: single-GPU C3 only (device sampling)")
-        eng.set_sampler("device", seed=7)
+        if args.config != "c3":
+            raise SystemExit("--batch < m: C3 only (device sampling)")
+        eng.set_sampler("device", seed=7, first_worker=plan.lo)
         workload = workload.replace(f"m=b={m}", f"m={m}, b={b} (device-drawn minibatches)")
     if world > 1 or args.phase:
         mean_local = None if mean is None else (mean[0], mean[1][plan.lo:plan.hi])
@@ -190,7 +190,7 @@ def main():
         log(f"halo: {plan.n_halo} rows in, {len(plan.send_ids)} rows out per round")
 
         def rounds(k):
-            return runner.run(k, eta0, m, lam, lam, 0.0)
+            return runner.run(k, eta0, b, lam, lam, 0.0)
     else:
         if mean is not None:
             eng.set_mixing_mean(*mean)

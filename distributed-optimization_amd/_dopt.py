@@ -88,6 +88,7 @@ _SIGS = {
     "dopt_kernel_stats": ([_P, _P, _P], ctypes.c_int),
     "dopt_set_profiling": ([_P, ctypes.c_int], ctypes.c_int),
     "dopt_set_sampler": ([_P, ctypes.c_int, ctypes.c_uint64, _I64], ctypes.c_int),
+    "dopt_phase_set_round": ([_P, _I64], ctypes.c_int),
 }
 EXPORTED = tuple(_SIGS)
 
@@ -348,6 +349,9 @@ class Engine:
 
     def phase_metrics_shared(self, include_xnorm, out_ptr):
         check(lib().dopt_phase_metrics_shared(self._h, 1 if include_xnorm else 0, ctypes.c_void_p(out_ptr)))
+
+    def phase_set_round(self, t):
+        check(lib().dopt_phase_set_round(self._h, int(t)))
 
     def phase_gather(self):
         check(lib().dopt_phase_gather(self._h))

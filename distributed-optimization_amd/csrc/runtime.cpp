@@ -169,6 +169,7 @@ struct dopt_ctx {
   int sampler = DOPT_SAMPLE_HOST;
   uint64_t sample_seed = 0;
   int64_t sample_wid0 = 0;
+  int64_t ph_round = 0;  // round index of the next dopt_phase_grad (device sampler counter)
 
   // profiling of k_round
   bool prof = false;
@@ -1205,6 +1206,13 @@ int dopt_set_sampler(dopt_ctx* c, int mode, uint64_t seed, int64_t first_worker)
   return DOPT_OK;
 }
 
+int dopt_phase_set_round(dopt_ctx* c, int64_t t) {
+  CHECK_ARG(c, "ctx is NULL");
+  CHECK_ARG(t >= 0, "round must be >= 0");
+  c->ph_round = t;
+  return DOPT_OK;
+}
+
 int dopt_set_profiling(dopt_ctx* c, int enable) {
   CHECK_ARG(c, "ctx is NULL");
   CHECK_ARG(enable >= 0, "enable must be >= 0");
@@ -1319,11 +1327,11 @@ int dopt_phase_grad(dopt_ctx* c, int64_t batch, const int32_t* idx, double lam_g
   CHECK_ARG(c, "ctx is NULL");
   int rc;
   if ((rc = check_run(c, 1, batch, idx, false))) return rc;
-  if (!idx && batch < c->max_m) return fail(DOPT_ERR_UNSUPPORTED, "device sampling: single-context rounds only");
+  const bool dev = !idx && batch < c->max_m;  // device sampler (check_run)
   if (!c->G && (rc = dalloc(&c->G, (size_t)c->n * c->ld * c->esz))) return rc;
   if (idx && (rc = upload_idx_chunk(c, idx, 0, 1, batch))) return rc;
   const bool cons = metric_flags & DOPT_RUN_CONSENSUS, loss = metric_flags & DOPT_RUN_OBJECTIVE;
-  const bool bip = (cons || loss) && bip_possible(c, batch, idx);
+  const bool bip = (cons || loss) && (dev ? !c->obj_sep : bip_possible(c, batch, idx));
   if ((cons || loss) && ((batch < c->max_m && !bip) || c->obj_sep))
     return fail(DOPT_ERR_UNSUPPORTED, "fused metrics need every shard row in the pass (full shards, or "
                 "minibatches of shards of at most %lld rows)", (long long)kMaxBipRows);
@@ -1350,10 +1358,13 @@ int dopt_phase_grad(dopt_ctx* c, int64_t batch, const int32_t* idx, double lam_g
   a.g_out = c->G;
   a.xbar = c->xbar[c->xb];
   a.lam = lam_grad;
-  a.flags |= F_GOUT | (cons ? F_CONS : 0) | (loss ? F_LOSS : 0) | (bip ? F_BIP : 0);
+  a.flags |= F_GOUT | (cons ? F_CONS : 0) | (loss ? F_LOSS : 0) | (bip || dev ? F_BIP : 0) | (dev ? F_DEVSAMPLE : 0);
+  a.seed = c->sample_seed;
+  a.round = c->ph_round;
+  a.wid0 = c->sample_wid0;
   if (a.flags & F_LOSS) c->loss_groups = c->slab_n[0] = c->n;  // per-worker loss slabs
   if (c->prof && (rc = prof_event(c, false))) return rc;
-  HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, cons || loss, a, (int)c->n, c->stream));
+  HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, cons || loss || dev, a, (int)c->n, c->stream));
   if (c->prof && (rc = prof_event(c, true))) return rc;
   return DOPT_OK;
 }

@@ -14,13 +14,13 @@ are bitwise the single-GPU iterates; only the metric sums are reduced in a
 different order (per rank, then across ranks).  Metric partial sums stay on the
 device per round and are all-reduced once per run.
 
-With full-shard batches and CSR mixing the rounds run LAGGED (`_run_lagged`): the
-column sums of x_t are all-reduced while the gradient kernel of round t runs, and
-that kernel's fused objective pass is taken at xbar_{t-1} (history[t-2]) instead of
-xbar_t; the consensus of x_t is a separate 16 MiB pass once xbar_t has arrived.  So
-no collective sits between two rounds' kernels; the halo exchange of x_t overlaps
-the same gradient kernel, and the mix kernel writes the next round's send rows (no
-gather kernel).
+With CSR mixing and metrics that ride the gradient pass the rounds run LAGGED
+(`_run_lagged`): the column sums of x_t are all-reduced while the gradient kernel of
+round t runs, and that kernel's fused objective pass is taken at xbar_{t-1}
+(history[t-2]) instead of xbar_t; the mix kernel forms xbar_t from the reduced sums
+and the consensus of x_t from the rows it reads anyway.  So no collective sits
+between two rounds' kernels; the halo exchange of x_t overlaps the same gradient
+kernel, and the mix kernel writes the next round's send rows (no gather kernel).
 
 Plan construction (`build_plan`) is pure host logic over the global CSR, so it
 is tested on CPU with gloo against the oracle (tests/test_distributed_cpu.py).
@@ -313,6 +313,7 @@ class DistributedDSGD:
                 if self._peers:
                     eng.phase_gather()
                 pending = self._start_exchange()
+                eng.phase_set_round(t0 + h)
                 eng.phase_grad(batch, lam_grad, flags if met else 0, idx=None if idx is None else idx[h])
                 self._finish_exchange(pending)
                 eng.phase_mix(t0 + h, eta0)
@@ -368,6 +369,7 @@ class DistributedDSGD:
                 pending = self._start_exchange()
                 colsum_fold(h)
                 ar = self._all_reduce_start(self.sum)
+                eng.phase_set_round(t0 + h)  # the device sampler's counter (sampling='device')
                 eng.phase_grad(batch, lam_grad, obj_f if h >= 2 else 0,  # loss at xbar_{h-1}
                                idx=None if idx is None else idx[h])
                 if ar is not None:

@@ -136,7 +136,7 @@ int dopt_get_global(dopt_ctx *ctx, double *x);
  * stream): worker i's minibatch in round t is a uniform subset of its shard drawn on the
  * device by Floyd's algorithm from Philox4x32-10(key = seed, counter = (k / 4, first_worker
  * + i, t)), inside the pass over all shard rows (shards of at most DOPT_MAX_BIP_ROWS rows;
- * D-SGD rounds on one context). */
+ * D-SGD rounds; the phase API takes t from dopt_phase_set_round). */
 #define DOPT_SAMPLE_HOST 0
 #define DOPT_SAMPLE_DEVICE 1
 int dopt_set_sampler(dopt_ctx *ctx, int mode, uint64_t seed, int64_t first_worker);
@@ -196,6 +196,9 @@ int dopt_set_halo(dopt_ctx *ctx, int64_t n_halo, void *halo_dev, int64_t n_send,
 /* Start of a run of phases: column-blocked contexts (large d) compute the
  * coefficients of the starting iterates here (full-shard batches). */
 int dopt_phase_begin(dopt_ctx *ctx, int64_t batch);
+/* Round index t (trainer.py:138) of the next dopt_phase_grad: the counter of the device
+ * sampler (dopt_set_sampler), so every rank draws worker i's minibatch of round t alike. */
+int dopt_phase_set_round(dopt_ctx *ctx, int64_t t);
 /* Rows send_ids of the current iterates -> send.  A no-op when the last dopt_phase_mix
  * already wrote them (the mix kernel refreshes the send rows as it writes the iterates). */
 int dopt_phase_gather(dopt_ctx *ctx);

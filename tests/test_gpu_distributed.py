@@ -39,11 +39,14 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
     plan = Dm.build_plan(top, world, rank)
     eng = _dopt.Engine(0, dtype)
     eng.generate_shards("logistic", plan.n_local, D, M, seed=9, first_worker=plan.lo)
+    B = int(os.environ.get("DOPT_TEST_BATCH", M))  # B < M: device-drawn minibatches
+    if B < M:
+        eng.set_sampler("device", seed=31, first_worker=plan.lo)
     uni = top.uniform_offdiag() if mean else None
     run = Dm.DistributedDSGD(eng, plan, N, N * M, device=0,
                              mean=None if uni is None else (uni[0], uni[1][plan.lo:plan.hi]))
     which = os.environ.get("DOPT_TEST_METRICS", "both")
-    obj, cons = run.run(T, 0.05, M, 1e-3, 1e-3, 0.25, objective=which != "cons", consensus=which != "obj")
+    obj, cons = run.run(T, 0.05, B, 1e-3, 1e-3, 0.25, objective=which != "cons", consensus=which != "obj")
     obj = np.zeros(0) if obj is None else obj
     cons = np.zeros(0) if cons is None else cons
     x = run.gather_models()
@@ -87,12 +90,15 @@ def _compare_single(got, dtype, mean, T, N=N, D=D, M=M, exact=True, parts=0):
 
     eng = _dopt.Engine(0, dtype)
     eng.generate_shards("logistic", N, D, M, seed=9)
+    B = int(os.environ.get("DOPT_TEST_BATCH", M))
+    if B < M:
+        eng.set_sampler("device", seed=31)
     top = _topo(mean, N, parts)
     if mean:
         eng.set_mixing_mean(*top.uniform_offdiag())
     else:
         eng.set_topology(top.row_ptr, top.col, top.w)
-    obj, cons, _ = eng.run_dsgd(T, 0.05, M, 1e-3, 1e-3, 0.25)
+    obj, cons, _ = eng.run_dsgd(T, 0.05, B, 1e-3, 1e-3, 0.25)
     x = eng.get_models()
     eng.close()
     if mean or not exact:  # column sums / split partial dots reduced per rank then across ranks
@@ -187,6 +193,19 @@ def test_partitioned_graph_ranks_match_single_context(tmp_path, monkeypatch, wor
                        nprocs=world, join=True, start_method="spawn")
     got = np.load(tmp_path / "dist.npz")
     _compare_single(got, "float64", False, 5, parts=world)
+
+
+@pytest.mark.parametrize("lagged", ["1", "0"])
+def test_device_sampler_ranks_match_single_context(tmp_path, monkeypatch, lagged):
+    """sampling='device' across ranks: worker i's minibatch of round t depends only on
+    (seed, t, global id), so 3 ranks (phase path, lagged or serial) reproduce one context's
+    device-sampled run bit for bit."""
+    import torch.multiprocessing as mp
+
+    monkeypatch.setenv("DOPT_TEST_BATCH", "5")
+    mp.start_processes(_rank_main, args=(3, _free_port(), "float64", str(tmp_path), False, 5, lagged), nprocs=3,
+                       join=True, start_method="spawn")
+    _compare_single(np.load(tmp_path / "dist.npz"), "float64", False, 5)
 
 
 @pytest.mark.parametrize("which", ["obj", "cons"])
