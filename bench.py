@@ -98,7 +98,8 @@ def cpu_baseline(seconds, n_workers=64, d=1024, m=512, seed=11):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=300,
+                    help="rounds timed (one run: the last round's metrics pass is amortised over them)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workers", type=int, default=4096, help="workers per GPU")
     ap.add_argument("--d", type=int, default=1024)
