@@ -11,15 +11,17 @@
 //   part   [G x ld]   f64   column-sum partials, G = ceil(N / rows_per_group)
 //   slabs  [N]        f64   per-worker consensus / objective partials
 //   rp/ci/cw                CSR mixing matrix (diagonal included), cw in T
-//   G      [N x ld]     T   per-worker gradients (centralized trainer only)
+//   G      [N x ld]     T   per-worker gradients (centralized trainer, multi-GPU phases)
 //
-// Launch schedule of one D-SGD round t (metrics fused, full-shard batches):
+// Launch schedule of one D-SGD round t (metrics every round):
 //   k_round(t)       grad + mix + step for every worker, and the consensus /
-//                    objective partials of x_t at xbar_t from the same row pass
-//   k_colsum_*(t)    xbar_{t+1}
-//   k_history(t)     history[t-1]
-// plus one metrics-only pass after the last round.  With minibatches smaller than
-// the shard, the objective needs all rows, so a metrics-only pass runs every round.
+//                    objective partials of x_t at xbar_t from the same row pass over
+//                    every shard row (minibatch rows feed the gradient: F_BIP)
+//   k_colsum_part(t) + k_colsum_final(t)   xbar_{t+1}; one extra block folds history[t-1]
+// plus one metrics-only pass after the last round.  Only a separate objective dataset
+// (X_full that is not the shards) takes a metrics-only pass every round.
+// The multi-GPU phase functions (dopt_phase_*) split the same round at its
+// communication points; distributed.py drives them.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdarg.h>
