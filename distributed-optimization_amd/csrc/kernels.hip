@@ -52,7 +52,6 @@ struct VT<double> {
 constexpr int NW = 4;         // waves per workgroup
 constexpr int NT = NW * 64;   // threads per workgroup
 constexpr int MAX_CPL = 16;   // 16-byte chunks per lane: d <= 4096 (fp32) / 2048 (fp64)
-constexpr int SRED = 3 * NW * 8;  // k_round LDS: per-wave consensus / loss / second-loss partials
 static_assert(NW == 4, "k_cons folds four wave sums");
 
 template <typename T>
@@ -192,12 +191,25 @@ __device__ __forceinline__ typename VT<T>::v mix_chunk(const RoundArgs& a, int i
 // 6.28 -> 7.15 TB/s on the bare access pattern, tools/bw_probe.hip), bit 1 DPP wave
 // reduction (readlane to an SGPR; ~0.5-1 %), bit 2 twice the rows in flight (no gain).
 // bit 3 persistent workgroups (-2 %: loses the dispatcher's dynamic balancing), bit 4 CSR
-// rows prefetched to LDS (null), bit 5 software-pipelined row loop (-0.9 %, adopted).
-// Default 35 = NT + DPP + pipelined; the others stay reachable through DOPT_KR_VARIANT
-// for A/B runs (tools/kr_variants.py).
+// rows prefetched to LDS (null), bit 5 software-pipelined row loop (-0.9 %, adopted),
+// bit 6 minibatch inside the metrics pass (F_BIP), bit 8 8 waves per workgroup (-0.8 %,
+// adopted for <= 4 chunks per lane), bit 9 16 waves (no gain).
+// Default 35 = NT + DPP + pipelined (| 256 for short rows); the others stay reachable
+// through DOPT_KR_VARIANT for A/B runs (tools/kr_variants.py).
 constexpr int KR_DEFAULT_VAR = 35;
+// Rows of up to 4 chunks per lane (d <= 1024 fp32 / 512 fp64) also take VAR bit 8: 8 waves
+// per workgroup, so a workgroup lives half as long and the launch's last generation drains
+// sooner (C3: 1.2686 vs 1.2789 ms, won 7 of 7 interleaved reps); longer rows keep 4 waves
+// (their 2x VGPRs would not fit 2 waves per SIMD per workgroup).
+template <int CPL>
+constexpr int kr_default_var() { return CPL <= 4 ? (KR_DEFAULT_VAR | 256) : KR_DEFAULT_VAR; }
 template <typename T, int CPL, int PROB, bool GRAD, bool MET, int VAR = KR_DEFAULT_VAR>
-__global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
+__global__ __launch_bounds__((VAR & 512) ? 4 * NT : (VAR & 256) ? 2 * NT : NT) void k_round(const RoundArgs a) {
+  // VAR bit 8: 8 waves per workgroup (half the workgroup duration, twice the generations);
+  // bit 9: 16 waves (one workgroup per CU)
+  constexpr int KW = (VAR & 512) ? 4 * NW : (VAR & 256) ? 2 * NW : NW;
+  constexpr int KT = KW * 64;
+  constexpr size_t KSRED = 3 * KW * 8;
   using V = typename VT<T>::v;
   constexpr int VN = VT<T>::n;
   constexpr int RB = (CPL >= 8 ? 1 : 8 / CPL) * ((VAR & 4) ? 2 : 1);  // rows in flight per wave
@@ -222,7 +234,7 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
   // VAR bit 4: the CSR rows of the mix (x_old, fixed during the round) go to LDS right away,
   // overlapping the row stream, so the epilogue touches no global memory but the store.
   constexpr bool PRE = (VAR & 16) != 0;
-  V* nbuf = (V*)(smem + (size_t)NW * nch * 16 + SRED);  // after red + sred
+  V* nbuf = (V*)(smem + (size_t)KW * nch * 16 + KSRED);  // after red + sred
   const int64_t pe0 = a.rp ? a.rp[i] : 0, pe1 = a.rp ? a.rp[i + 1] : 0;
   const bool pre = PRE && GRAD && (flags & F_STEP) && !(flags & F_MEAN) && (pe1 - pe0) <= a.pre_rows;
   if (pre) {
@@ -230,7 +242,7 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
       const int col = a.ci[e];
       const T* src = col < a.n_local ? (const T*)a.x_old + (int64_t)col * ld
                                      : (const T*)a.halo + (int64_t)(col - a.n_local) * ld;
-      for (int c = threadIdx.x; c < nch; c += NT) nbuf[(e - pe0) * nch + c] = *(const V*)(src + (int64_t)c * VN);
+      for (int c = threadIdx.x; c < nch; c += KT) nbuf[(e - pe0) * nch + c] = *(const V*)(src + (int64_t)c * VN);
     }
   }
   // VAR bit 6 (minibatch in the metrics pass): the objective needs every row of the shard at
@@ -238,14 +250,14 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
   // map) also feed the gradient -- one pass over the shard per round for every batch size.
   constexpr bool BIP = GRAD && MET && (VAR & 64) != 0;
   const int64_t nrow = BIP ? m : nb;
-  unsigned char* bmask = (unsigned char*)(smem + (size_t)NW * nch * 16 + SRED + (PRE ? (size_t)a.pre_rows * nch * 16 : 0));
+  unsigned char* bmask = (unsigned char*)(smem + (size_t)KW * nch * 16 + KSRED + (PRE ? (size_t)a.pre_rows * nch * 16 : 0));
   if (BIP) {
-    for (int64_t r = threadIdx.x; r < m; r += NT) bmask[r] = 0;
+    for (int64_t r = threadIdx.x; r < m; r += KT) bmask[r] = 0;
     __syncthreads();
     if (dev_sample) {
       if (threadIdx.x == 0) floyd_sample(bmask, m, nb, a.seed, a.round, a.wid0 + i);
     } else {
-      for (int64_t k = threadIdx.x; k < nb; k += NT) bmask[a.idx[(int64_t)i * a.b + k]] = 1;
+      for (int64_t k = threadIdx.x; k < nb; k += KT) bmask[a.idx[(int64_t)i * a.b + k]] = 1;
     }
     __syncthreads();
   }
@@ -293,8 +305,8 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
     T ycur = T(0), ynxt = T(0);
     int64_t r = wave;
     if (r < nrow) load_row(r, cur, ycur);
-    for (; r < nrow; r += NW) {
-      if (r + NW < nrow) load_row(r + NW, nxt, ynxt);
+    for (; r < nrow; r += KW) {
+      if (r + KW < nrow) load_row(r + KW, nxt, ynxt);
       const bool g_row = !BIP || bmask[r] != 0;  // wave-uniform
       V az = V(0), au = V(0);
 #pragma unroll
@@ -318,7 +330,7 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
     }
   }
   if (!PIPE && (compute_z || compute_u)) {
-    for (int64_t r0 = (int64_t)wave * RB; r0 < nrow; r0 += NW * RB) {
+    for (int64_t r0 = (int64_t)wave * RB; r0 < nrow; r0 += KW * RB) {
       V xr[RB][CPL];
       T yv[RB];
       bool g_row[RB];
@@ -372,8 +384,8 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
     }
   }
 
-  V* red = (V*)smem;  // [NW][nch]
-  double* sred = (double*)(smem + (GRAD ? (size_t)NW * nch * 16 : 0));  // 3*NW doubles (SRED bytes)
+  V* red = (V*)smem;  // [KW][nch]
+  double* sred = (double*)(smem + (GRAD ? (size_t)KW * nch * 16 : 0));  // 3*KW doubles (KSRED bytes)
   if (GRAD) {
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
@@ -394,8 +406,8 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
     }
     if (lane == 0) {
       sred[wave] = cons;
-      sred[NW + wave] = loss;
-      sred[2 * NW + wave] = loss2;
+      sred[KW + wave] = loss;
+      sred[2 * KW + wave] = loss2;
     }
   }
   __syncthreads();
@@ -403,10 +415,10 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
   if (GRAD) {
     const T inv_eta = (T)a.eta;
     const T lam = (T)a.lam;
-    for (int c = threadIdx.x; c < nch; c += NT) {
+    for (int c = threadIdx.x; c < nch; c += KT) {
       V s = red[c];
 #pragma unroll
-      for (int q = 1; q < NW; ++q) s += red[q * nch + c];  // fixed order
+      for (int q = 1; q < KW; ++q) s += red[q * nch + c];  // fixed order
       const V wc = *(const V*)(wsrc + (int64_t)c * VN);
       const V gc = (flags & F_GSUM) ? s : ((nb > 0) ? (s / (T)nb + lam * wc) : V(0));
       if (flags & F_STEP) {
@@ -425,10 +437,10 @@ __global__ __launch_bounds__(NT) void k_round(const RoundArgs a) {
   if (MET && threadIdx.x == 0) {
     double cs = 0.0, ls = 0.0, l2 = 0.0;
 #pragma unroll
-    for (int q = 0; q < NW; ++q) {
+    for (int q = 0; q < KW; ++q) {
       cs += sred[q];
-      ls += sred[NW + q];
-      l2 += sred[2 * NW + q];
+      ls += sred[KW + q];
+      l2 += sred[2 * KW + q];
     }
     if (want_cons) a.slab_cons[i] = cs;
     if (want_loss) a.slab_loss[i] = ls;
@@ -442,7 +454,9 @@ template <typename T, int CPL, int PROB, bool GRAD, bool MET, int VAR = KR_DEFAU
 static hipError_t launch_round_t(const RoundArgs& a, int groups, hipStream_t s) {
   const size_t pre = (VAR & 16) ? (size_t)a.pre_rows * a.nchunks * 16 : 0;
   const size_t bip = (VAR & 64) ? ((size_t)a.bip_rows + 15) / 16 * 16 : 0;  // minibatch byte map
-  const size_t lds = (GRAD ? (size_t)NW * a.nchunks * 16 + SRED + pre + bip : SRED);
+  constexpr int KW = (VAR & 512) ? 4 * NW : (VAR & 256) ? 2 * NW : NW;
+  constexpr size_t KSRED = 3 * KW * 8;
+  const size_t lds = (GRAD ? (size_t)KW * a.nchunks * 16 + KSRED + pre + bip : KSRED);
   static bool attr_set = false;
   if (!attr_set) {
     const size_t max_lds = 160 * 1024;
@@ -452,7 +466,7 @@ static hipError_t launch_round_t(const RoundArgs& a, int groups, hipStream_t s) 
     attr_set = true;
   }
   const int grid = (VAR & 8) ? (groups < 1024 ? groups : 1024) : groups;  // 4 workgroups per CU
-  hipLaunchKernelGGL((k_round<T, CPL, PROB, GRAD, MET, VAR>), dim3(grid), dim3(NT), lds, s, a);
+  hipLaunchKernelGGL((k_round<T, CPL, PROB, GRAD, MET, VAR>), dim3(grid), dim3(KW * 64), lds, s, a);
   return hipGetLastError();
 }
 
@@ -470,6 +484,8 @@ static hipError_t dispatch_variant(int var, const RoundArgs& a, int groups, hipS
     case 11: return launch_round_t<float, 4, 0, GRAD, MET, 11>(a, groups, s);
     case 19: return launch_round_t<float, 4, 0, GRAD, MET, 19>(a, groups, s);
     case 0: return launch_round_t<float, 4, 0, GRAD, MET, 0>(a, groups, s);
+    case 291: return launch_round_t<float, 4, 0, GRAD, MET, 291>(a, groups, s);
+    case 547: return launch_round_t<float, 4, 0, GRAD, MET, 547>(a, groups, s);
     default: return launch_round_t<float, 4, 0, GRAD, MET>(a, groups, s);
   }
 }
@@ -483,15 +499,16 @@ template <typename T, int CPL, int PROB>
 static hipError_t dispatch_mode(bool grad, bool met, const RoundArgs& a, int groups, hipStream_t s) {
   if constexpr (std::is_same<T, float>::value && CPL == 4 && PROB == 0) {
     const int var = kr_variant();
-    if (var >= 0 && var != KR_DEFAULT_VAR) {
+    if (var >= 0 && var != kr_default_var<CPL>()) {
       if (grad && met) return dispatch_variant<true, true>(var, a, groups, s);
       if (grad) return dispatch_variant<true, false>(var, a, groups, s);
     }
   }
-  if (grad && met && (a.flags & F_BIP)) return launch_round_t<T, CPL, PROB, true, true, KR_DEFAULT_VAR | 64>(a, groups, s);
-  if (grad && met) return launch_round_t<T, CPL, PROB, true, true>(a, groups, s);
-  if (grad) return launch_round_t<T, CPL, PROB, true, false>(a, groups, s);
-  if (met) return launch_round_t<T, CPL, PROB, false, true>(a, groups, s);
+  constexpr int DV = kr_default_var<CPL>();
+  if (grad && met && (a.flags & F_BIP)) return launch_round_t<T, CPL, PROB, true, true, DV | 64>(a, groups, s);
+  if (grad && met) return launch_round_t<T, CPL, PROB, true, true, DV>(a, groups, s);
+  if (grad) return launch_round_t<T, CPL, PROB, true, false, DV>(a, groups, s);
+  if (met) return launch_round_t<T, CPL, PROB, false, true, DV>(a, groups, s);
   return hipErrorInvalidValue;
 }
 
