@@ -233,7 +233,7 @@ def main():
     while cpl * 64 < (d + (16 // esz) - 1) // (16 // esz):
         cpl *= 2
     if cpl <= 16:
-        var = 35 | 256 if cpl <= 4 else 35  # kernels.hip: kr_default_var<CPL>()
+        var = 14371 | 256 if cpl <= 4 else 14371  # kernels.hip: kr_default_var<CPL>()
         kname = (f"void dopt::k_round<{tname}, {cpl}, {0 if problem == 'logistic' else 1}, true, true, {var}>"
                  "(dopt::RoundArgs)")
     else:

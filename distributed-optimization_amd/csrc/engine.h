@@ -51,6 +51,7 @@ struct RoundArgs {
   int32_t n_local;        // rows of x_old owned by this rank (columns below it are local)
   // complete-graph mixing (F_MEAN)
   const double* colsum;   // [ld] column sums of x_old (all workers, all ranks)
+  const void* colsum_t;   // the same sums rounded to T (fp32 contexts: half the bytes every worker re-reads), or null
   const void* wdiag;      // [n] T diagonal weights W_ii
   double w_off;           // the uniform off-diagonal weight
   // column-blocked (large d) rounds

@@ -145,6 +145,17 @@ __device__ __forceinline__ T sigmoid_neg(T yz) {
   return T(1) / (T(1) + exp(yz));
 }
 
+// Hardware transcendentals for float (v_exp_f32 / v_log_f32 / v_rcp_f32, ~1 ulp): the
+// library expf / logf / division add range reduction and Newton steps per row.
+__device__ __forceinline__ float sigmoid_neg_fast(float yz) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(yz));
+}
+__device__ __forceinline__ double row_loss_fast(float yv, float u) {
+  const float t = yv * u;
+  const float a = t < 0.f ? -t : t;
+  return (double)((t < 0.f ? -t : 0.f) + __logf(1.0f + __expf(-a)));
+}
+
 // obj_problems.py:5-7 (logistic, np.log(1 + exp(-|t|)) as written, not log1p)
 // and obj_problems.py:41-42 (quadratic, the 0.5 is applied once at the end).
 template <typename T, int PROB>
@@ -169,6 +180,15 @@ __device__ __forceinline__ typename VT<T>::v mix_chunk(const RoundArgs& a, int i
   V acc = V(0);
   if (a.flags & F_MEAN) {
     const double wii = (double)((const T*)a.wdiag)[i];
+    if (a.colsum_t) {  // sums rounded to T: one 16-byte load per chunk instead of VN doubles
+      const V sv = *(const V*)((const T*)a.colsum_t + (int64_t)c * VN);
+#pragma unroll
+      for (int e = 0; e < VN; ++e) {
+        const double x = (double)own[e];
+        acc[e] = (T)(a.w_off * ((double)sv[e] - x) + wii * x);
+      }
+      return acc;
+    }
 #pragma unroll
     for (int e = 0; e < VN; ++e) {
       const double x = (double)own[e];
@@ -193,10 +213,18 @@ __device__ __forceinline__ typename VT<T>::v mix_chunk(const RoundArgs& a, int i
 // bit 3 persistent workgroups (-2 %: loses the dispatcher's dynamic balancing), bit 4 CSR
 // rows prefetched to LDS (null), bit 5 software-pipelined row loop (-0.9 %, adopted),
 // bit 6 minibatch inside the metrics pass (F_BIP), bit 8 8 waves per workgroup (-0.8 %,
-// adopted for <= 4 chunks per lane), bit 9 16 waves (no gain).
-// Default 35 = NT + DPP + pipelined (| 256 for short rows); the others stay reachable
-// through DOPT_KR_VARIANT for A/B runs (tools/kr_variants.py).
-constexpr int KR_DEFAULT_VAR = 35;
+// adopted for <= 4 chunks per lane), bit 9 16 waves (no gain), bit 10 6 waves per SIMD
+// (spills: 2.7x slower), bit 11 branch-free row loads (lanes past the row re-read its last
+// chunk), bit 12 peeled pipelined loop -- with 11, the compiler's wait before a row's
+// arithmetic covers that row only (vmcnt(4) instead of vmcnt(0): the conditional and
+// lane-masked loads of the plain loop made it drain everything in flight; -0.6 %, won
+// 7 of 7 reps), bit 13 hardware exp / log / reciprocal for the float logistic row terms
+// (-0.3 %), bit 14 ping-pong buffers (the register allocator still copies at the latch:
+// no gain).
+// Default 14371 = NT + DPP + pipelined + branch-free + peeled + fast transcendentals
+// (| 256 for short rows); the others stay reachable through DOPT_KR_VARIANT for A/B runs
+// (tools/kr_variants.py).
+constexpr int KR_DEFAULT_VAR = 35 | 2048 | 4096 | 8192;
 // Rows of up to 4 chunks per lane (d <= 1024 fp32 / 512 fp64) also take VAR bit 8: 8 waves
 // per workgroup, so a workgroup lives half as long and the launch's last generation drains
 // sooner (C3: 1.2686 vs 1.2789 ms, won 7 of 7 interleaved reps); longer rows keep 4 waves
@@ -204,7 +232,8 @@ constexpr int KR_DEFAULT_VAR = 35;
 template <int CPL>
 constexpr int kr_default_var() { return CPL <= 4 ? (KR_DEFAULT_VAR | 256) : KR_DEFAULT_VAR; }
 template <typename T, int CPL, int PROB, bool GRAD, bool MET, int VAR = KR_DEFAULT_VAR>
-__global__ __launch_bounds__((VAR & 512) ? 4 * NT : (VAR & 256) ? 2 * NT : NT) void k_round(const RoundArgs a) {
+__global__ __launch_bounds__((VAR & 512) ? 4 * NT : (VAR & 256) ? 2 * NT : NT)
+__attribute__((amdgpu_waves_per_eu((VAR & 1024) ? 6 : 1))) void k_round(const RoundArgs a) {
   // VAR bit 8: 8 waves per workgroup (half the workgroup duration, twice the generations);
   // bit 9: 16 waves (one workgroup per CU)
   constexpr int KW = (VAR & 512) ? 4 * NW : (VAR & 256) ? 2 * NW : NW;
@@ -296,37 +325,85 @@ __global__ __launch_bounds__((VAR & 512) ? 4 * NT : (VAR & 256) ? 2 * NT : NT) v
 #pragma unroll
       for (int j = 0; j < CPL; ++j) {
         const int c = lane + 64 * j;
-        dst[j] = c < nch ? ((VAR & 1) ? __builtin_nontemporal_load((const V*)(xp + (int64_t)c * VN))
-                                      : *(const V*)(xp + (int64_t)c * VN))
-                         : V(0);
+        if (VAR & 2048) {  // branch-free: lanes past the row re-read its last chunk (w, xb are 0 there)
+          const int cc = c < nch ? c : nch - 1;
+          dst[j] = (VAR & 1) ? __builtin_nontemporal_load((const V*)(xp + (int64_t)cc * VN))
+                             : *(const V*)(xp + (int64_t)cc * VN);
+        } else {
+          dst[j] = c < nch ? ((VAR & 1) ? __builtin_nontemporal_load((const V*)(xp + (int64_t)c * VN))
+                                        : *(const V*)(xp + (int64_t)c * VN))
+                           : V(0);
+        }
       }
     };
     V cur[CPL], nxt[CPL];
     T ycur = T(0), ynxt = T(0);
-    int64_t r = wave;
-    if (r < nrow) load_row(r, cur, ycur);
-    for (; r < nrow; r += KW) {
-      if (r + KW < nrow) load_row(r + KW, nxt, ynxt);
-      const bool g_row = !BIP || bmask[r] != 0;  // wave-uniform
+    // VAR bit 13: hardware exp / log / reciprocal for the float logistic row terms
+    constexpr bool FAST = (VAR & 8192) && std::is_same<T, float>::value && PROB == 0;
+    auto process =[&](const V (&rv)[CPL], T yv, int64_t rr) {
+      const bool g_row = !BIP || bmask[rr] != 0;  // wave-uniform
       V az = V(0), au = V(0);
 #pragma unroll
       for (int j = 0; j < CPL; ++j) {
-        if (compute_z && g_row) az += cur[j] * w[j];
-        if (compute_u) au += cur[j] * xb[j];
+        if (compute_z && g_row) az += rv[j] * w[j];
+        if (compute_u) au += rv[j] * xb[j];
       }
       T z = hsum<T>(az), u = hsum<T>(au);
       if (compute_z && g_row) z = (VAR & 2) ? wave_sum_dpp(z) : wave_sum(z);
       if (compute_u) u = (VAR & 2) ? wave_sum_dpp(u) : wave_sum(u);
       if (GRAD && g_row) {
-        const T coef = (PROB == 0) ? -ycur * sigmoid_neg(ycur * z) : z - ycur;
+        T coef;
+        if constexpr (FAST) coef = -yv * sigmoid_neg_fast(yv * z);
+        else coef = (PROB == 0) ? -yv * sigmoid_neg(yv * z) : z - yv;
 #pragma unroll
-        for (int j = 0; j < CPL; ++j) g[j] += coef * cur[j];
+        for (int j = 0; j < CPL; ++j) g[j] += coef * rv[j];
       }
-      if (want_loss) loss += row_loss<T, PROB>(ycur, loss_from_z ? z : u);
-      if (want_loss2) loss2 += row_loss<T, PROB>(ycur, z);
+      if constexpr (FAST) {
+        if (want_loss) loss += row_loss_fast(yv, loss_from_z ? z : u);
+        if (want_loss2) loss2 += row_loss_fast(yv, z);
+      } else {
+        if (want_loss) loss += row_loss<T, PROB>(yv, loss_from_z ? z : u);
+        if (want_loss2) loss2 += row_loss<T, PROB>(yv, z);
+      }
+    };
+    int64_t r = wave;
+    if (r < nrow) load_row(r, cur, ycur);
+    if (VAR & 16384) {
+      // ping-pong: unrolled by two so that no register copy of an in-flight row ends an
+      // iteration -- while one buffer is reduced, the other's loads are in flight
+      for (; r + 2 * KW < nrow; r += 2 * KW) {
+        load_row(r + KW, nxt, ynxt);
+        process(cur, ycur, r);
+        load_row(r + 2 * KW, cur, ycur);
+        process(nxt, ynxt, r + KW);
+      }
+      if (r + KW < nrow) {
+        load_row(r + KW, nxt, ynxt);
+        process(cur, ycur, r);
+        process(nxt, ynxt, r + KW);
+      } else if (r < nrow) {
+        process(cur, ycur, r);
+      }
+    } else if (VAR & 4096) {
+      // peeled: every iteration issues the next row's loads unconditionally, so the compiler's
+      // wait before the current row's arithmetic only covers the current row (with the
+      // conditional load of the plain loop, the merged path waits for everything in flight)
+      for (; r + KW < nrow; r += KW) {
+        load_row(r + KW, nxt, ynxt);
+        process(cur, ycur, r);
 #pragma unroll
-      for (int j = 0; j < CPL; ++j) cur[j] = nxt[j];
-      ycur = ynxt;
+        for (int j = 0; j < CPL; ++j) cur[j] = nxt[j];
+        ycur = ynxt;
+      }
+      if (r < nrow) process(cur, ycur, r);
+    } else {
+      for (; r < nrow; r += KW) {
+        if (r + KW < nrow) load_row(r + KW, nxt, ynxt);
+        process(cur, ycur, r);
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) cur[j] = nxt[j];
+        ycur = ynxt;
+      }
     }
   }
   if (!PIPE && (compute_z || compute_u)) {
@@ -484,8 +561,16 @@ static hipError_t dispatch_variant(int var, const RoundArgs& a, int groups, hipS
     case 11: return launch_round_t<float, 4, 0, GRAD, MET, 11>(a, groups, s);
     case 19: return launch_round_t<float, 4, 0, GRAD, MET, 19>(a, groups, s);
     case 0: return launch_round_t<float, 4, 0, GRAD, MET, 0>(a, groups, s);
+    case 35: return launch_round_t<float, 4, 0, GRAD, MET, 35>(a, groups, s);
     case 291: return launch_round_t<float, 4, 0, GRAD, MET, 291>(a, groups, s);
     case 547: return launch_round_t<float, 4, 0, GRAD, MET, 547>(a, groups, s);
+    case 2339: return launch_round_t<float, 4, 0, GRAD, MET, 2339>(a, groups, s);
+    case 2083: return launch_round_t<float, 4, 0, GRAD, MET, 2083>(a, groups, s);
+    case 4387: return launch_round_t<float, 4, 0, GRAD, MET, 4387>(a, groups, s);
+    case 6435: return launch_round_t<float, 4, 0, GRAD, MET, 6435>(a, groups, s);
+    case 14627: return launch_round_t<float, 4, 0, GRAD, MET, 14627>(a, groups, s);
+    case 18723: return launch_round_t<float, 4, 0, GRAD, MET, 18723>(a, groups, s);
+    case 26915: return launch_round_t<float, 4, 0, GRAD, MET, 26915>(a, groups, s);
     default: return launch_round_t<float, 4, 0, GRAD, MET>(a, groups, s);
   }
 }

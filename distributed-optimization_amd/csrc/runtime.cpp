@@ -109,6 +109,7 @@ struct dopt_ctx {
   int xb = 0;  // xbar[xb] = average of the current iterates
   double* S = nullptr;             // [ld] column sums of the current iterates (complete-graph mixing)
   const double* S_ext = nullptr;   // all-reduced sums (multi-GPU), used by the mix when set
+  void* S_t = nullptr;             // [ld] T copy of the sums the mix reads (fp32 complete-graph mixing)
   // complete-graph mixing: sum_j W_ij x_j = w_off (S - x_i) + W_ii x_i
   bool mean_mix = false;
   double w_off = 0.0;
@@ -310,6 +311,7 @@ int alloc_state(dopt_ctx* c) {
   if ((rc = ensure_slabs(c, std::max(c->n, c->n_chunks)))) return rc;
   if ((rc = dalloc_t(&c->S, (size_t)c->ld * sizeof(double)))) return rc;
   HIPOK(hipMemsetAsync(c->S, 0, (size_t)c->ld * sizeof(double), c->stream));
+  if ((rc = dalloc(&c->S_t, (size_t)c->ld * c->esz))) return rc;
   HIPOK(hipStreamSynchronize(c->stream));
   return DOPT_OK;
 }
@@ -356,6 +358,20 @@ int ensure_hist(dopt_ctx* c, int64_t T) {
   return DOPT_OK;
 }
 
+// fp32 complete-graph mixing reads the column sums as T (DOPT_MEAN_SUMS_T=0: as float64)
+bool sums_t_enabled(dopt_ctx* c) {
+  if (c->dtype != DOPT_F32) return false;
+  const char* v = getenv("DOPT_MEAN_SUMS_T");
+  return !(v && v[0] == '0');
+}
+
+// The T copy of the sums the next mix reads (after every producer of S / S_ext).
+int refresh_sums_t(dopt_ctx* c) {
+  if (!c->mean_mix || !sums_t_enabled(c)) return DOPT_OK;
+  HIPOK(launch_convert(c->dtype, c->S_ext ? c->S_ext : c->S, 0, c->S_t, 1, c->ld, c->ld, c->stream));
+  return DOPT_OK;
+}
+
 RoundArgs base_args(dopt_ctx* c) {
   RoundArgs a;
   memset(&a, 0, sizeof(a));
@@ -375,6 +391,7 @@ RoundArgs base_args(dopt_ctx* c) {
   if (c->mean_mix) {
     a.flags |= F_MEAN;
     a.colsum = c->S_ext ? c->S_ext : c->S;
+    a.colsum_t = sums_t_enabled(c) ? c->S_t : nullptr;
     a.wdiag = c->wdiag;
     a.w_off = c->w_off;
   }
@@ -502,7 +519,7 @@ int colsum_current(dopt_ctx* c) {
                               nullptr, c->stream));
   HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, n_div(c), c->ld, (int32_t)c->nch, c->xbar[c->xb], nullptr,
                             0.0, 0, c->stream, c->S));
-  return DOPT_OK;
+  return refresh_sums_t(c);
 }
 
 // Column-blocked buffers: coefficients [n x bcap] and fp64 partial slabs.
@@ -597,6 +614,7 @@ int run_dsgd_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batc
                                 c->part, c->stamps + h + 1, c->stream));
     HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, n_div(c), c->ld, (int32_t)c->nch, c->xbar[xb ^ 1],
                               nullptr, 0.0, 0, c->stream, c->S));
+    if ((rc = refresh_sums_t(c))) return rc;
     if (met) {
       if ((rc = history(c, h - 1, c->xbar[xb], want_cons, want_obj, c->n))) return rc;
     } else if (!fused_met && metrics) {
@@ -749,6 +767,7 @@ int dopt_destroy(dopt_ctx* c) {
   dfree_t(c->idx);
   dfree_t(c->hraw);
   dfree_t(c->S);
+  dfree(c->S_t);
   dfree_t(c->zpart);
   dfree_t(c->upart);
   dfree_t(c->cpart);
@@ -1004,6 +1023,7 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
                            c->loss_groups, want_obj ? c->xbar[xb] : nullptr, hr, hr + 1, hr + 2};
     HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, n_div(c), c->ld, (int32_t)c->nch, c->xbar[xb ^ 1],
                               nullptr, 0.0, 0, c->stream, c->S, met ? &fold : nullptr));
+    if ((rc = refresh_sums_t(c))) return rc;
     if (!met && !fused && metrics) {
       if ((rc = metrics_pass(c, c->xs[c->cur ^ 1], c->xbar[xb ^ 1], false, want_cons, want_obj))) return rc;
       if ((rc = history(c, h, c->xbar[xb ^ 1], want_cons, want_obj, c->n))) return rc;
@@ -1497,7 +1517,7 @@ int dopt_phase_xbar(dopt_ctx* c, const double* sum_dev) {
                             0.0, 0, c->stream));
   c->xb ^= 1;
   c->S_ext = sum_dev;  // the complete-graph mix of the next round uses the global sums
-  return DOPT_OK;
+  return refresh_sums_t(c);
 }
 
 int dopt_phase_cons(dopt_ctx* c) {

@@ -29,6 +29,29 @@ __global__ __launch_bounds__(256) void k_shard_read(const f4* __restrict__ x, in
   if (acc.x == 1234.5f) out[0] = acc.y + acc.z + acc.w;
 }
 
+// Occupancy / workgroup-shape sweep: W waves per workgroup, NT loads, RB rows in flight;
+// the resident workgroups per CU are capped with dynamic LDS (the round kernel holds
+// 4 waves per SIMD, i.e. 2 workgroups of 8 waves).
+template <int W, int RB>
+__global__ __launch_bounds__(W * 64) void k_shard_read_w(const f4* __restrict__ x, int rows_per_wg, float* out) {
+  extern __shared__ char lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const f4* base = x + (size_t)blockIdx.x * rows_per_wg * 256;
+  f4 acc = f4(0);
+  for (int r0 = wave * RB; r0 < rows_per_wg; r0 += W * RB) {
+    f4 v[RB][4];
+#pragma unroll
+    for (int k = 0; k < RB; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[k][j] = __builtin_nontemporal_load(base + (size_t)(r0 + k) * 256 + lane + 64 * j);
+#pragma unroll
+    for (int k = 0; k < RB; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc += v[k][j];
+  }
+  if (acc.x == 1234.5f) { lds[threadIdx.x] = 1; out[0] = acc.y + acc.z + acc.w + lds[threadIdx.x ^ 1]; }
+}
+
 __global__ __launch_bounds__(256) void k_grid_read(const f4* __restrict__ x, size_t n, float* out) {
   f4 acc = f4(0);
   const size_t stride = (size_t)gridDim.x * 256;
@@ -94,6 +117,17 @@ int main() {
     ms = timeit([&] { hipLaunchKernelGGL(k_grid_read, dim3(g), dim3(256), 0, 0, x, n4, out); }, 5);
     printf("grid_read %5d WGs     %.3f ms  %.0f GB/s\n", g, ms, gbs(ms, bytes));
   }
+  CK(hipFuncSetAttribute((const void*)k_shard_read_w<8, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  CK(hipFuncSetAttribute((const void*)k_shard_read_w<4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  for (int per_cu : {1, 2, 3, 4, 8}) {  // resident workgroups per CU, capped by LDS
+    const size_t l = (160 * 1024) / per_cu - 1024;
+    ms = timeit([&] { hipLaunchKernelGGL((k_shard_read_w<8, 2>), dim3(wg), dim3(512), l, 0, x, rpw, out); }, 5);
+    printf("8 waves, %d WG/CU       %.3f ms  %.0f GB/s\n", per_cu, ms, gbs(ms, bytes));
+    ms = timeit([&] { hipLaunchKernelGGL((k_shard_read_w<4, 2>), dim3(wg), dim3(256), l, 0, x, rpw, out); }, 5);
+    printf("4 waves, %d WG/CU       %.3f ms  %.0f GB/s\n", per_cu, ms, gbs(ms, bytes));
+  }
+  ms = timeit([&] { hipLaunchKernelGGL((k_shard_read_w<8, 2>), dim3(wg / 2), dim3(512), 0, 0, x, rpw * 2, out); }, 5);
+  printf("8 waves, 2048 WGs x 1024 rows %.3f ms  %.0f GB/s\n", ms, gbs(ms, bytes));
   ms = timeit([&] { hipLaunchKernelGGL(k_copy, dim3(8192), dim3(256), 0, 0, x, y, n4 / 4); }, 5);
   printf("copy 2 GiB             %.3f ms  %.0f GB/s (read+write)\n", ms, gbs(ms, bytes / 2));
   return 0;
