@@ -219,8 +219,8 @@ __device__ __forceinline__ typename VT<T>::v mix_chunk(const RoundArgs& a, int i
 // arithmetic covers that row only (vmcnt(4) instead of vmcnt(0): the conditional and
 // lane-masked loads of the plain loop made it drain everything in flight; -0.6 %, won
 // 7 of 7 reps), bit 13 hardware exp / log / reciprocal for the float logistic row terms
-// (-0.3 %), bit 14 ping-pong buffers (the register allocator still copies at the latch:
-// no gain).
+// (-0.3 %).  Not kept: ping-pong row buffers (loop unrolled by two by hand; the register
+// allocator still copies the refilled buffer at the latch behind a vmcnt(0): +1.3 %).
 // Default 14371 = NT + DPP + pipelined + branch-free + peeled + fast transcendentals
 // (| 256 for short rows); the others stay reachable through DOPT_KR_VARIANT for A/B runs
 // (tools/kr_variants.py).
@@ -368,23 +368,7 @@ __attribute__((amdgpu_waves_per_eu((VAR & 1024) ? 6 : 1))) void k_round(const Ro
     };
     int64_t r = wave;
     if (r < nrow) load_row(r, cur, ycur);
-    if (VAR & 16384) {
-      // ping-pong: unrolled by two so that no register copy of an in-flight row ends an
-      // iteration -- while one buffer is reduced, the other's loads are in flight
-      for (; r + 2 * KW < nrow; r += 2 * KW) {
-        load_row(r + KW, nxt, ynxt);
-        process(cur, ycur, r);
-        load_row(r + 2 * KW, cur, ycur);
-        process(nxt, ynxt, r + KW);
-      }
-      if (r + KW < nrow) {
-        load_row(r + KW, nxt, ynxt);
-        process(cur, ycur, r);
-        process(nxt, ynxt, r + KW);
-      } else if (r < nrow) {
-        process(cur, ycur, r);
-      }
-    } else if (VAR & 4096) {
+    if (VAR & 4096) {
       // peeled: every iteration issues the next row's loads unconditionally, so the compiler's
       // wait before the current row's arithmetic only covers the current row (with the
       // conditional load of the plain loop, the merged path waits for everything in flight)
@@ -569,8 +553,6 @@ static hipError_t dispatch_variant(int var, const RoundArgs& a, int groups, hipS
     case 4387: return launch_round_t<float, 4, 0, GRAD, MET, 4387>(a, groups, s);
     case 6435: return launch_round_t<float, 4, 0, GRAD, MET, 6435>(a, groups, s);
     case 14627: return launch_round_t<float, 4, 0, GRAD, MET, 14627>(a, groups, s);
-    case 18723: return launch_round_t<float, 4, 0, GRAD, MET, 18723>(a, groups, s);
-    case 26915: return launch_round_t<float, 4, 0, GRAD, MET, 26915>(a, groups, s);
     default: return launch_round_t<float, 4, 0, GRAD, MET>(a, groups, s);
   }
 }

@@ -22,7 +22,7 @@ import topology  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="14627,291,18723")
+    ap.add_argument("--variants", default="14627,291,6435")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--workers", type=int, default=4096)
