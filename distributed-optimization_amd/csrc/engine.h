@@ -63,6 +63,7 @@ struct RoundArgs {
   int32_t b_rows;         // max rows per worker a column-blocked step touches (picks the kernel)
   int32_t pre_rows;       // CSR rows per worker prefetched to LDS by the fused kernel (0: off)
   int32_t groups;         // column-block groups = gridDim.y
+  int32_t contig;         // column-blocked kernels: contiguous block range per group (set by the launcher)
   int32_t bip_rows;       // F_BIP: the largest shard (LDS byte map size)
   // F_DEVSAMPLE: the minibatch of worker i in this round is a function of (seed, round, wid0 + i)
   uint64_t seed;

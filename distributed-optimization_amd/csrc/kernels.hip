@@ -617,24 +617,51 @@ __device__ __forceinline__ typename VT<T>::v ld_nt(const T* p) {
   return __builtin_nontemporal_load((const typename VT<T>::v*)p);
 }
 
-// RPW = rows per wave held in registers (4 for <= 16 rows per worker, 16 for <= 64).
+// RPW = rows per wave held in registers (4 for <= 16 rows per worker, 16 for <= 64);
+// CPB = 16-byte chunks per lane per column block (a block is 64 * CPB chunks of every row).
 // One barrier per block: the waves' gradient partials go to a double-buffered LDS
 // slot, every wave folds them and forms the new block itself (wave 0 stores it).
+// CPB > 1 keeps 2-4x the bytes in flight per wave between two barriers but costs
+// occupancy (C5: CPB 1 / 2 / 4 = 85 / 115 / 169 VGPRs, 15.1 / 15.5 / 16.7 ms): default 1,
+// DOPT_SPLIT_CPB selects 2 or 4 for A/B runs.  Not kept either: own / xbar / column sums
+// loaded once per workgroup and shared through LDS instead of by every wave (15.22 vs
+// 15.14 ms).  The kernel waits on memory 78 % of its wave cycles (SQ_WAIT_ANY) at 42 %
+// VALU issue per SIMD.
 // LDS-only workgroup barrier: waits for this wave's LDS traffic, not for its global loads
 // (__syncthreads() also drains vmcnt, which would cancel the next block's prefetch).
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <typename T, int RPW, bool ZNEXT, bool MET, bool PF>
+// Blocks of column-block group grp: a contiguous range (a.contig: each row of a workgroup
+// streams forward through memory) or every G-th block.
+struct BlockWalk {
+  int b0, b1, st;
+  __device__ BlockWalk(const RoundArgs& a, int grp, int G, int nblk) {
+    if (a.contig) {
+      const int per = (nblk + G - 1) / G;
+      b0 = grp * per;
+      b1 = min(nblk, b0 + per);
+      st = 1;
+    } else {
+      b0 = grp;
+      b1 = nblk;
+      st = G;
+    }
+  }
+};
+
+template <typename T, int RPW, bool ZNEXT, bool MET, bool PF, int CPB = 1>
 __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
   using V = typename VT<T>::v;
   constexpr int VN = VT<T>::n;
-  __shared__ V gred[2][NW][64];
+  constexpr int BC = 64 * CPB;  // chunks per column block
+  __shared__ V gred[2][NW][BC];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int i = blockIdx.x, grp = blockIdx.y, G = gridDim.y;
-  const int nch = a.nchunks, nblk = (nch + 63) / 64;
+  const int nch = a.nchunks, nblk = (nch + BC - 1) / BC;
+  const BlockWalk bw(a, grp, G, nblk);
   const int64_t ld = a.ld;
   const int64_t row0 = a.off[i], m = a.off[i + 1] - row0;
   const int64_t nb = a.idx ? (a.b < m ? a.b : m) : m;  // <= NW * RPW (host-checked)
@@ -658,58 +685,79 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
   double cacc = 0.0;
   const T inv_eta = (T)a.eta, lam = (T)a.lam;
   int buf = 0;
-  V rn[RPW];  // PF: the next block's row segments, loaded one block ahead
+  V rn[RPW][CPB];  // PF: the next block's row segments, loaded one block ahead
   if (PF) {
-    const int c = grp * 64 + lane;
 #pragma unroll
-    for (int r = 0; r < RPW; ++r)
-      rn[r] = (grp < nblk && rowp[r] >= 0 && c < nch) ? ld_nt<T>(X + rowp[r] + (int64_t)c * VN) : V(0);
+    for (int j = 0; j < CPB; ++j) {
+      const int c = bw.b0 * BC + j * 64 + lane;
+#pragma unroll
+      for (int r = 0; r < RPW; ++r)
+        rn[r][j] = (bw.b0 < bw.b1 && rowp[r] >= 0 && c < nch) ? ld_nt<T>(X + rowp[r] + (int64_t)c * VN) : V(0);
+    }
   }
-  for (int cb = grp; cb < nblk; cb += G, buf ^= 1) {
-    const int c = cb * 64 + lane;
-    const bool in = c < nch;
-    V rv[RPW];
+  for (int cb = bw.b0; cb < bw.b1; cb += bw.st, buf ^= 1) {
+    V rv[RPW][CPB];
     if (PF) {
-      const int cn = (cb + G) * 64 + lane;
-      const bool nin = cb + G < nblk && cn < nch;
 #pragma unroll
-      for (int r = 0; r < RPW; ++r) {
-        rv[r] = rn[r];
-        rn[r] = (nin && rowp[r] >= 0) ? ld_nt<T>(X + rowp[r] + (int64_t)cn * VN) : V(0);
+      for (int j = 0; j < CPB; ++j) {
+        const int cn = (cb + bw.st) * BC + j * 64 + lane;
+        const bool nin = cb + bw.st < bw.b1 && cn < nch;
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+          rv[r][j] = rn[r][j];
+          rn[r][j] = (nin && rowp[r] >= 0) ? ld_nt<T>(X + rowp[r] + (int64_t)cn * VN) : V(0);
+        }
       }
     } else {
 #pragma unroll
-      for (int r = 0; r < RPW; ++r) rv[r] = (rowp[r] >= 0 && in) ? ld_nt<T>(X + rowp[r] + (int64_t)c * VN) : V(0);
-    }
-    const V own = in ? *(const V*)(own_p + (int64_t)c * VN) : V(0);
-    const V xb = (MET && in) ? *(const V*)((const T*)a.xbar + (int64_t)c * VN) : V(0);
-    V gp = V(0);
+      for (int j = 0; j < CPB; ++j) {
+        const int c = cb * BC + j * 64 + lane;
 #pragma unroll
-    for (int r = 0; r < RPW; ++r) gp += coef[r] * rv[r];
-    gred[buf][wave][lane] = gp;
+        for (int r = 0; r < RPW; ++r)
+          rv[r][j] = (rowp[r] >= 0 && c < nch) ? ld_nt<T>(X + rowp[r] + (int64_t)c * VN) : V(0);
+      }
+    }
+    V own[CPB], xb[CPB];
+#pragma unroll
+    for (int j = 0; j < CPB; ++j) {
+      const int c = cb * BC + j * 64 + lane;
+      const bool in = c < nch;
+      own[j] = in ? *(const V*)(own_p + (int64_t)c * VN) : V(0);
+      xb[j] = (MET && in) ? *(const V*)((const T*)a.xbar + (int64_t)c * VN) : V(0);
+      V gp = V(0);
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) gp += coef[r] * rv[r][j];
+      gred[buf][wave][j * 64 + lane] = gp;
+    }
     if (PF)
       lds_barrier();
     else
       __syncthreads();
-    V g = V(0);
-    if (nb > 0) g = (gred[buf][0][lane] + gred[buf][1][lane] + gred[buf][2][lane] + gred[buf][3][lane]) / (T)nb + lam * own;
-    V xn = V(0);
-    if (gout) {
-      if (wave == 0 && in) *(V*)((T*)a.g_out + (int64_t)i * ld + (int64_t)c * VN) = g;
-    } else if (in) {
-      xn = mix_chunk<T>(a, i, c, own) - inv_eta * g;
-      if (wave == 0) *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = xn;
-    }
-    if (ZNEXT) {
 #pragma unroll
-      for (int r = 0; r < RPW; ++r) zacc[r] += (double)hsum<T>(rv[r] * xn);
-    }
-    if (MET) {
+    for (int j = 0; j < CPB; ++j) {
+      const int c = cb * BC + j * 64 + lane;
+      const bool in = c < nch;
+      const int q = j * 64 + lane;
+      V g = V(0);
+      if (nb > 0) g = (gred[buf][0][q] + gred[buf][1][q] + gred[buf][2][q] + gred[buf][3][q]) / (T)nb + lam * own[j];
+      V xn = V(0);
+      if (gout) {
+        if (wave == 0 && in) *(V*)((T*)a.g_out + (int64_t)i * ld + (int64_t)c * VN) = g;
+      } else if (in) {
+        xn = mix_chunk<T>(a, i, c, own[j]) - inv_eta * g;
+        if (wave == 0) *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = xn;
+      }
+      if (ZNEXT) {
 #pragma unroll
-      for (int r = 0; r < RPW; ++r) uacc[r] += (double)hsum<T>(rv[r] * xb);
-      if (wave == 0) {
-        const V dv = own - xb;
-        cacc += (double)hsum<T>(dv * dv);
+        for (int r = 0; r < RPW; ++r) zacc[r] += (double)hsum<T>(rv[r][j] * xn);
+      }
+      if (MET) {
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) uacc[r] += (double)hsum<T>(rv[r][j] * xb[j]);
+        if (wave == 0) {
+          const V dv = own[j] - xb[j];
+          cacc += (double)hsum<T>(dv * dv);
+        }
       }
     }
   }
@@ -740,6 +788,7 @@ __global__ __launch_bounds__(NT) void k_split_dots(const RoundArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int i = blockIdx.x, grp = blockIdx.y, G = gridDim.y;
   const int nch = a.nchunks, nblk = (nch + 63) / 64;
+  const BlockWalk bw(a, grp, G, nblk);
   const int64_t ld = a.ld;
   const int64_t row0 = a.off[i], m = a.off[i + 1] - row0;
   const int64_t nb = (MODE == 0 && a.idx) ? (a.b < m ? a.b : m) : m;
@@ -749,7 +798,7 @@ __global__ __launch_bounds__(NT) void k_split_dots(const RoundArgs a) {
   double* out = MODE == 0 ? a.zpart : a.upart;
   if (MODE == 1 && wave == 0 && (a.flags & F_CONS)) {  // ||x_i - xbar||^2 partial over this group's blocks
     double cacc = 0.0;
-    for (int cb = grp; cb < nblk; cb += G) {
+    for (int cb = bw.b0; cb < bw.b1; cb += bw.st) {
       const int c = cb * 64 + lane;
       if (c < nch) {
         const V dv = *(const V*)(own_p + (int64_t)c * VN) - *(const V*)(pt + (int64_t)c * VN);
@@ -771,7 +820,7 @@ __global__ __launch_bounds__(NT) void k_split_dots(const RoundArgs a) {
       rowp[r] = ok ? (row0 + lr) * ld : -1;
       acc[r] = 0.0;
     }
-    for (int cb = grp; cb < nblk; cb += G) {
+    for (int cb = bw.b0; cb < bw.b1; cb += bw.st) {
       const int c = cb * 64 + lane;
       if (c >= nch) continue;
       const V pv = *(const V*)(pt + (int64_t)c * VN);
@@ -825,25 +874,44 @@ __global__ __launch_bounds__(NT) void k_split_coef(const RoundArgs a, int mode) 
   }
 }
 
+// A/B knob DOPT_SPLIT_CONTIG: contiguous block ranges per column-block group, or every G-th
+// block (default: C5 13.91 vs 14.02 ms contiguous, won 4 of 4 interleaved reps)
+static int split_contig() {
+  const char* v = getenv("DOPT_SPLIT_CONTIG");
+  return v ? atoi(v) != 0 : 0;
+}
+
 hipError_t launch_split_step(int dtype, bool znext, bool met, const RoundArgs& a, int n_workers,
                              hipStream_t s) {
   if (n_workers <= 0) return hipSuccess;
   const dim3 grid(n_workers, a.groups);
   const bool small = a.b_rows <= 4 * NW;  // rows per worker this step touches
+  RoundArgs a2 = a;
+  a2.contig = split_contig();
   // A/B knob (tools/split_ab.py): next-block prefetch measured 1 % slower on C5, so off
   const char* ev = getenv("DOPT_SPLIT_PREFETCH");
   const bool pf = ev && ev[0] == '1';
-#define SPLIT_STEP2(T_, R_, P_)                                                                              \
-  if (znext && met) hipLaunchKernelGGL((k_split_step<T_, R_, true, true, P_>), grid, dim3(NT), 0, s, a);     \
-  else if (znext) hipLaunchKernelGGL((k_split_step<T_, R_, true, false, P_>), grid, dim3(NT), 0, s, a);      \
-  else if (met) hipLaunchKernelGGL((k_split_step<T_, R_, false, true, P_>), grid, dim3(NT), 0, s, a);        \
-  else hipLaunchKernelGGL((k_split_step<T_, R_, false, false, P_>), grid, dim3(NT), 0, s, a);
-#define SPLIT_STEP(T_, R_) if (pf) { SPLIT_STEP2(T_, R_, true) } else { SPLIT_STEP2(T_, R_, false) }
+  // 2 or 4 chunks per lane per block for <= 16 rows when every group still walks >= 2
+  // blocks (the slab layout [n][bcap][G] does not depend on the block size)
+  const char* cv = getenv("DOPT_SPLIT_CPB");
+  int cpb = cv ? atoi(cv) : 1;
+  if (!small || pf || (a.nchunks + 64 * cpb - 1) / (64 * cpb) < 2 * a.groups) cpb = 1;
+#define SPLIT_STEP2(T_, R_, P_, C_)                                                                              \
+  if (znext && met) hipLaunchKernelGGL((k_split_step<T_, R_, true, true, P_, C_>), grid, dim3(NT), 0, s, a2);     \
+  else if (znext) hipLaunchKernelGGL((k_split_step<T_, R_, true, false, P_, C_>), grid, dim3(NT), 0, s, a2);      \
+  else if (met) hipLaunchKernelGGL((k_split_step<T_, R_, false, true, P_, C_>), grid, dim3(NT), 0, s, a2);        \
+  else hipLaunchKernelGGL((k_split_step<T_, R_, false, false, P_, C_>), grid, dim3(NT), 0, s, a2);
+#define SPLIT_STEP(T_, R_) if (pf) { SPLIT_STEP2(T_, R_, true, 1) } else { SPLIT_STEP2(T_, R_, false, 1) }
+#define SPLIT_SMALL(T_)                           \
+  if (cpb == 4) { SPLIT_STEP2(T_, 4, false, 4) }  \
+  else if (cpb == 2) { SPLIT_STEP2(T_, 4, false, 2) } \
+  else { SPLIT_STEP(T_, 4) }
   if (dtype == 0) {
-    if (small) { SPLIT_STEP(float, 4) } else { SPLIT_STEP(float, 16) }
+    if (small) { SPLIT_SMALL(float) } else { SPLIT_STEP(float, 16) }
   } else {
-    if (small) { SPLIT_STEP(double, 4) } else { SPLIT_STEP(double, 16) }
+    if (small) { SPLIT_SMALL(double) } else { SPLIT_STEP(double, 16) }
   }
+#undef SPLIT_SMALL
 #undef SPLIT_STEP
 #undef SPLIT_STEP2
   return hipGetLastError();
@@ -853,9 +921,11 @@ hipError_t launch_split_dots(int dtype, int mode, const RoundArgs& a, int n_work
   if (n_workers <= 0) return hipSuccess;
   const dim3 grid(n_workers, a.groups);
   const bool small = a.b_rows <= 4 * NW;  // <= 16 rows: one 4-row chunk per wave, high occupancy
+  RoundArgs a2 = a;
+  a2.contig = split_contig();
 #define SPLIT_DOTS(T_, R_)                                                                       \
-  if (mode == 0) hipLaunchKernelGGL((k_split_dots<T_, 0, R_>), grid, dim3(NT), 0, s, a);        \
-  else hipLaunchKernelGGL((k_split_dots<T_, 1, R_>), grid, dim3(NT), 0, s, a);
+  if (mode == 0) hipLaunchKernelGGL((k_split_dots<T_, 0, R_>), grid, dim3(NT), 0, s, a2);        \
+  else hipLaunchKernelGGL((k_split_dots<T_, 1, R_>), grid, dim3(NT), 0, s, a2);
   if (dtype == 0) {
     if (small) { SPLIT_DOTS(float, 4) } else { SPLIT_DOTS(float, 16) }
   } else {

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """In-process A/B of two column-blocked step variants selected by an environment knob
-(AB_KNOB, default DOPT_SPLIT_PREFETCH: next-block prefetch in the row-split kernel), on
+(AB_KNOB, default DOPT_SPLIT_PREFETCH: next-block prefetch in the row-split kernel; AB_VALUES,
+default "1,0", the knob values interleaved), on
 the C5 shape (quadratic, d = 2^20, m = b = 16, complete graph through column sums).
 Results of both variants must agree.  Measured on MI355X: prefetch 13.75 vs 13.58 ms;
 a barrier-free column-streaming kernel (every wave holds all 16 rows of a block, 183
@@ -26,9 +27,10 @@ def main():
     eng.set_mixing_mean(*topology.fully_connected(n).uniform_offdiag())
     eng.set_profiling(True)
     bytes_per = 4 * n * (m * d + m + 2 * d)
-    times, ref = {"1": [], "0": []}, None
+    vals = os.environ.get("AB_VALUES", "1,0").split(",")
+    times, ref = {v: [] for v in vals}, None
     for rep in range(4):
-        for v in ("1", "0"):
+        for v in vals:
             os.environ[os.environ.get("AB_KNOB", "DOPT_SPLIT_PREFETCH")] = v
             eng.set_models(np.zeros((n, d), dtype=np.float32))
             eng.kernel_stats()
@@ -40,7 +42,7 @@ def main():
             else:
                 np.testing.assert_allclose(obj, ref[0], rtol=1e-6)
                 np.testing.assert_allclose(cons, ref[1], rtol=1e-5)
-        print(f"rep {rep}: knob=1 {times['1'][-1]:.3f} ms, knob=0 {times['0'][-1]:.3f} ms", file=sys.stderr, flush=True)
+        print(f"rep {rep}: " + ", ".join(f"knob={v} {times[v][-1]:.3f} ms" for v in vals), file=sys.stderr, flush=True)
     print(json.dumps({v: {"median_ms": float(np.median(t)), "tbps": bytes_per / (np.median(t) * 1e-3) / 1e12}
                       for v, t in times.items()}))
 
