@@ -131,21 +131,21 @@ def main():
     import torch  # plumbing only: barrier + max-over-ranks (one HIP runtime, loaded first)
     import torch.distributed as dist
 
+    import numpy as np
+
+    import _dopt
+    import distributed
+    import topology
+
     dev = local % max(1, torch.cuda.device_count())
     if world > 1 or args.phase:
         torch.cuda.set_device(dev)
         if world == 1:  # --phase on one GPU: the multi-GPU code path incl. RCCL (one rank)
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29533")
-            dist.init_process_group(args.backend, rank=0, world_size=1)
+            distributed.init_process_group(args.backend, rank=0, world_size=1)
         else:
-            dist.init_process_group(args.backend)
-
-    import numpy as np
-
-    import _dopt
-    import distributed
-    import topology
+            distributed.init_process_group(args.backend)
 
     problem, mean, eta0 = "logistic", None, 0.05
     if args.config == "c3":

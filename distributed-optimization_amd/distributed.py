@@ -35,6 +35,19 @@ import numpy as np
 import _dopt
 
 
+def init_process_group(backend, **kw):
+    """torch.distributed.init_process_group; for "nccl" (RCCL) with high-priority internal
+    streams, so the halo send/recv and the all-reduce of a round get CU slots ahead of the
+    4096-workgroup gradient kernel they overlap (DOPT_NCCL_HIPRI=0: default priority)."""
+    import torch.distributed as dist
+
+    if backend == "nccl" and os.environ.get("DOPT_NCCL_HIPRI", "1") != "0":
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        kw["pg_options"] = opts
+    dist.init_process_group(backend, **kw)
+
+
 def partition_bounds(n, world):
     """Contiguous slices, np.array_split sizes (the first n % world ranks get one more)."""
     sizes = [n // world + (1 if r < n % world else 0) for r in range(world)]

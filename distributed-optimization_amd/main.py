@@ -50,11 +50,12 @@ def _maybe_init_distributed():
 
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         import torch
-        import torch.distributed as dist
+
+        import distributed
 
         local = int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(local)
-        dist.init_process_group(os.environ.get("DOPT_BACKEND", "nccl"))
+        distributed.init_process_group(os.environ.get("DOPT_BACKEND", "nccl"))
 
 
 if __name__ == "__main__":
