@@ -95,6 +95,47 @@ def cpu_baseline(seconds, n_workers=64, d=1024, m=512, seed=11):
                       f"{m} rows x d={d}, {rounds} rounds, {dt:.1f} s, full-shard batches, metrics every round"}
 
 
+def pcie_leg(eng, top, n, d, m, b, lam, eta0, steps, dt_resident):
+    """Boundary cost when the caller hands over host buffers (Worker.local_data numpy arrays
+    -> dopt_load_shards): the device-generated shards are copied to host memory once
+    (untimed), then uploaded through the C ABI (timed: host -> HBM DMA + the convert kernel
+    into the padded layout), and the same `steps` rounds run on them.  Reported as the
+    PCIe-inclusive rate n*steps / (upload + rounds) next to the resident-input rate."""
+    import numpy as np
+    import torch
+
+    log("pcie leg: staging shards in host memory")
+    X = np.empty((n * m, d), dtype=np.float32)
+    y = np.empty(n * m, dtype=np.float32)
+    step = 256
+    for i0 in range(0, n, step):  # pull back by worker blocks (fp64 download path)
+        for i in range(i0, min(n, i0 + step)):
+            Xi, yi = eng.get_shard(i)
+            X[i * m:(i + 1) * m] = Xi
+            y[i * m:(i + 1) * m] = yi
+    off = np.arange(n + 1, dtype=np.int64) * m
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.load_shards("logistic", X, y, off)
+    torch.cuda.synchronize()
+    t_up = time.perf_counter() - t0
+    eng.set_topology(top.row_ptr, top.col, top.w)
+    eng.set_models(np.zeros((n, d)))
+    eng.set_profiling(False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.run_dsgd(steps, eta0, b, lam, lam, 0.0)
+    torch.cuda.synchronize()
+    t_run = time.perf_counter() - t0
+    nbytes = X.nbytes + y.nbytes
+    del X, y
+    return {"upload_s": t_up, "upload_GBps": nbytes / t_up / 1e9, "host_bytes": nbytes,
+            "rounds_s": t_run, "rounds_s_resident": dt_resident, "steps": steps,
+            "value_incl_upload": n * steps / (t_up + t_run), "unit": "worker-iters/s",
+            "note": "host float32 buffers (pageable numpy) through dopt_load_shards; rounds on the "
+                    "uploaded shards, same K; not the headline value (inputs resident in HBM)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -120,6 +161,10 @@ def main():
     ap.add_argument("--partition", default="spectral", choices=["spectral", "ranges"],
                     help="C3 at N > 1: workers -> GPUs by graph partition (recursive spectral bisection, "
                          "computed on rank 0 and broadcast) or by contiguous id ranges")
+    ap.add_argument("--pcie", action="store_true",
+                    help="C3, 1 GPU: after the timed region, hand the same shards over as host buffers "
+                         "(dopt_load_shards, the drop-in boundary) and report the PCIe-inclusive rate in a "
+                         "'pcie' object (never 'value')")
     ap.add_argument("--config", default="c3", choices=["c3", "c4", "c5"],
                     help="c3 (default, the metric's config); c4: 256x256 torus, 65536 workers total; "
                          "c5: quadratic, d=2^20, m=b=16, 1024 workers total, complete graph")
@@ -276,6 +321,8 @@ def main():
     if args.config != "c3":
         out["metric"] = f"worker-iters/sec ({args.config.upper()}, secondary config)"
         out["scaling"] = "strong"
+    if args.pcie and world == 1 and args.config == "c3":
+        out["pcie"] = pcie_leg(eng, top, n, d, m, b, lam, eta0, args.steps, dt)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
         log("cpu baseline")
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
