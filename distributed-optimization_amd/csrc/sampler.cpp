@@ -87,6 +87,10 @@ struct MT {
 // stream exactly as m-1 calls of interval(k) would.  Written as a branchless filter over
 // the buffered words (a word is kept when (w & mask) <= k, and then k moves on), so the
 // rejections cost no branch mispredictions; k < 2^32 (m < 2^31 is checked by the callers).
+// The mask only changes when k drops below a power of two, so the inner loop runs over
+// segments of constant mask: the loop-carried chain per word is compare + subtract, not
+// clz + shift + and + compare + subtract (this container, interleaved A/B: C2 8.5 -> 5.0-6.7
+// ns per draw, C3 b = 16 17.6 -> 11.5-14.1 ms per round of 4096 permutations).
 void draw_js(MT& mt, int64_t m, uint32_t* js) {
   uint32_t k = (uint32_t)(m - 1);
   uint32_t t = 0;
@@ -100,11 +104,14 @@ void draw_js(MT& mt, int64_t m, uint32_t* js) {
     int32_t q = mt.pos;
     while (q < kN && k >= 1) {
       const uint32_t mask = 0xffffffffu >> __builtin_clz(k);
-      const uint32_t v = mt.out[q++] & mask;
-      const uint32_t keep = v <= k;
-      js[t] = v;
-      t += keep;
-      k -= keep;
+      const uint32_t klo = mask >> 1;  // the mask holds while k > klo
+      while (q < kN && k > klo) {
+        const uint32_t v = mt.out[q++] & mask;
+        const uint32_t keep = v <= k;
+        js[t] = v;
+        t += keep;
+        k -= keep;
+      }
     }
     mt.pos = q;
   }
