@@ -115,6 +115,11 @@ hipError_t launch_split_dots(int dtype, int mode, const RoundArgs& a, int n_work
 hipError_t launch_split_coef(int dtype, int problem, int mode, const RoundArgs& a, int n_workers,
                              hipStream_t s);
 
+// Column sums of rows x[0:rows] in one launch when rows <= rpg (k_colsum_one), else the two
+// stages below; arguments as theirs (n = the mean's divisor).
+hipError_t launch_colsum(int dtype, const void* x, int64_t rows, int64_t ld, int32_t nchunks, int32_t rpg,
+                         double* part, uint64_t* stamp, int64_t n, void* out, const void* base, double eta,
+                         int mode, hipStream_t s, double* raw, const FoldArgs* fold);
 // Column sums of an [n x ld] matrix into fp64 partials [G x ld], G = ceil(n / rpg).
 hipError_t launch_colsum_partial(int dtype, const void* x, int64_t n, int64_t ld, int32_t nchunks,
                                  int32_t rpg, double* part, uint64_t* stamp, hipStream_t s);

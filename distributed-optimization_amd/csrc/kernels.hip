@@ -572,6 +572,23 @@ static hipError_t dispatch_mode(bool grad, bool met, const RoundArgs& a, int gro
     }
   }
   constexpr int DV = kr_default_var<CPL>();
+  if constexpr (CPL <= 4) {
+    // Fewer workers than CUs (C1 / C2 / main.py: 10-25 workers of 500 rows): a launch is
+    // one workgroup per worker streaming its rows, so its time is the per-row latency
+    // chain, not bandwidth: 16 waves (VAR bit 9), each with RB-row blocks in flight (the
+    // plain loop, not the 1-row software pipeline: bits 5 / 12 off) -- 4x the rows
+    // in flight per worker of the default.
+    static const bool wide_off = [] {
+      const char* v = getenv("DOPT_KR_FEW_WIDE");
+      return v && atoi(v) == 0;
+    }();
+    if (groups < 256 && !wide_off) {
+      constexpr int WV = (DV & ~(32 | 4096)) | 512;
+      if (grad && met && (a.flags & F_BIP)) return launch_round_t<T, CPL, PROB, true, true, WV | 64>(a, groups, s);
+      if (grad && met) return launch_round_t<T, CPL, PROB, true, true, WV>(a, groups, s);
+      if (grad) return launch_round_t<T, CPL, PROB, true, false, WV>(a, groups, s);
+    }
+  }
   if (grad && met && (a.flags & F_BIP)) return launch_round_t<T, CPL, PROB, true, true, DV | 64>(a, groups, s);
   if (grad && met) return launch_round_t<T, CPL, PROB, true, true, DV>(a, groups, s);
   if (grad) return launch_round_t<T, CPL, PROB, true, false, DV>(a, groups, s);
@@ -1108,6 +1125,98 @@ __global__ __launch_bounds__(NT) void k_colsum_final(const double* __restrict__ 
         out[col] = base[col] - (T)eta * (T)mean;  // trainer.py:57
     }
   }
+}
+
+// Both stages in one launch when the rows form a single group (n <= rpg: the small configs,
+// C1 / C2 / main.py's N = 25, where a round is launch-bound): workgroup cb sums all n rows
+// of its column block exactly as stage 1 does, then applies stage 2's epilogue to the one
+// partial (stage 2 adds it to 0.0 and three empty wave sums, repeated here, so the output
+// is bitwise the two-launch path's).  One extra block folds the history, as in stage 2.
+template <typename T>
+__global__ __launch_bounds__(NT) void k_colsum_one(const T* __restrict__ x, int64_t rows, int64_t ld, int nch,
+                                                   uint64_t* stamp, int64_t n, T* out, const T* base,
+                                                   double eta, int mode, double* raw, const FoldArgs fold) {
+  using V = typename VT<T>::v;
+  constexpr int VN = VT<T>::n;
+  __shared__ double red[NW][64 * VN];
+  if ((int)blockIdx.x == (nch + 63) / 64) {  // the fold block
+    fold_block<T>(fold, nch, red);
+    return;
+  }
+  if (stamp && blockIdx.x == 0 && threadIdx.x == 0) *stamp = wall_clock64();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  double acc[VN];
+#pragma unroll
+  for (int e = 0; e < VN; ++e) acc[e] = 0.0;
+  if (c < nch) {
+    int64_t r = wave;
+    for (; r + 3 * NW < rows; r += 4 * NW) {
+      V v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = *(const V*)(x + (r + k * NW) * ld + (int64_t)c * VN);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int e = 0; e < VN; ++e) acc[e] += (double)v[k][e];
+    }
+    for (; r < rows; r += NW) {
+      const V v = *(const V*)(x + r * ld + (int64_t)c * VN);
+#pragma unroll
+      for (int e = 0; e < VN; ++e) acc[e] += (double)v[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < VN; ++e) red[wave][lane * VN + e] = acc[e];
+  __syncthreads();
+  if (wave == 0 && c < nch) {
+#pragma unroll
+    for (int e = 0; e < VN; ++e) {
+      const int64_t col = (int64_t)c * VN + e;
+      double p = red[0][lane * VN + e];
+#pragma unroll
+      for (int q = 1; q < NW; ++q) p += red[q][lane * VN + e];
+      double s = 0.0;  // stage 2 over one group
+      s += p;
+      s = ((s + 0.0) + 0.0) + 0.0;
+      if (raw) {
+        raw[col] = s;
+        if (!out) continue;
+      }
+      const double mean = s / (double)n;
+      if (mode == 0)
+        out[col] = (T)mean;
+      else
+        out[col] = base[col] - (T)eta * (T)mean;
+    }
+  }
+}
+
+hipError_t launch_colsum(int dtype, const void* x, int64_t rows, int64_t ld, int32_t nchunks, int32_t rpg,
+                         double* part, uint64_t* stamp, int64_t n, void* out, const void* base, double eta,
+                         int mode, hipStream_t s, double* raw, const FoldArgs* fold) {
+  const int groups = (int)((rows + rpg - 1) / rpg);
+  static const bool two = [] {  // A/B knob DOPT_COLSUM_TWO=1: always the two-launch path
+    const char* v = getenv("DOPT_COLSUM_TWO");
+    return v && atoi(v) != 0;
+  }();
+  if (groups > 1 || two) {
+    hipError_t e = launch_colsum_partial(dtype, x, rows, ld, nchunks, rpg, part, stamp, s);
+    if (e != hipSuccess) return e;
+    return launch_colsum_final(dtype, part, groups > 0 ? groups : 1, n, ld, nchunks, out, base, eta, mode, s,
+                               raw, fold);
+  }
+  FoldArgs f;
+  memset(&f, 0, sizeof(f));
+  if (fold) f = *fold;
+  const dim3 grid((nchunks + 63) / 64 + (fold ? 1 : 0));
+  if (dtype == 0)
+    hipLaunchKernelGGL(k_colsum_one<float>, grid, dim3(NT), 0, s, (const float*)x, rows, ld, nchunks, stamp, n,
+                       (float*)out, (const float*)base, eta, mode, raw, f);
+  else
+    hipLaunchKernelGGL(k_colsum_one<double>, grid, dim3(NT), 0, s, (const double*)x, rows, ld, nchunks, stamp,
+                       n, (double*)out, (const double*)base, eta, mode, raw, f);
+  return hipGetLastError();
 }
 
 hipError_t launch_colsum_partial(int dtype, const void* x, int64_t n, int64_t ld, int32_t nchunks,

@@ -515,10 +515,8 @@ int64_t idx_chunk_rounds(dopt_ctx* c, int64_t T, int64_t b) {
 
 // xbar[xb] and S of the current iterates (run prologue).
 int colsum_current(dopt_ctx* c) {
-  HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur], c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part,
-                              nullptr, c->stream));
-  HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, n_div(c), c->ld, (int32_t)c->nch, c->xbar[c->xb], nullptr,
-                            0.0, 0, c->stream, c->S));
+  HIPOK(launch_colsum(c->dtype, c->xs[c->cur], c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part, nullptr,
+                      n_div(c), c->xbar[c->xb], nullptr, 0.0, 0, c->stream, c->S, nullptr));
   return refresh_sums_t(c);
 }
 
@@ -683,6 +681,14 @@ bool bip_possible(dopt_ctx* c, int64_t batch, const int32_t* idx) {
   const char* v = getenv("DOPT_BIP");
   if (v && v[0] == '0') return false;
   return idx && batch < c->max_m && c->max_m <= kMaxBipRows && !c->obj_sep && !c->split;
+}
+
+// Separate metrics pass for few logistic workers (dopt_run_dsgd).  DOPT_FEW_SPLIT=0 / 1
+// forces it off / on (A/B runs, tests).
+bool split_few_metrics(dopt_ctx* c) {
+  const char* v = getenv("DOPT_FEW_SPLIT");
+  if (v) return v[0] == '1' && !c->split && !c->obj_sep;
+  return c->n < 256 && c->problem == DOPT_LOGISTIC && !c->split && !c->obj_sep;
 }
 
 int check_run(dopt_ctx* c, int64_t T, int64_t batch, const int32_t* idx, bool need_topo) {
@@ -982,8 +988,13 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
   const bool want_obj = flags & DOPT_RUN_OBJECTIVE, want_cons = flags & DOPT_RUN_CONSENSUS;
   const bool metrics = want_obj || want_cons;
   const bool dev = !idx && batch < c->max_m;  // device sampler (check_run)
-  const bool bip = metrics && (dev ? !c->obj_sep : bip_possible(c, batch, idx));
-  const bool fused = (batch >= c->max_m || bip) && !c->obj_sep;
+  // Few logistic workers (C2: 10-25): one workgroup per worker puts a round on <= 25 CUs, and
+  // the fused objective (a second dot + exp / log per row) makes those CUs VALU-bound
+  // (fp64 C2: 55-62 us per round kernel vs 17 us without metrics and 7 us for the
+  // separate metrics pass over 64-row chunks on many CUs): take the metrics pass apart.
+  const bool few_split = split_few_metrics(c) && !dev;
+  const bool bip = metrics && (dev ? !c->obj_sep : !few_split && bip_possible(c, batch, idx));
+  const bool fused = ((batch >= c->max_m && !few_split) || bip) && !c->obj_sep;
   const int64_t CH = idx ? idx_chunk_rounds(c, T, batch) : 1;
   int& xb = c->xb;
   if (c->split) return run_dsgd_split(c, t0, T, eta0, batch, idx, lam_grad, lam_obj, f_opt, flags, obj_out,
@@ -1015,14 +1026,13 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
     HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, met || dev, a, (int)c->n, c->stream));
     if (c->prof && (rc = prof_event(c, true))) return rc;
     // xbar_{t+1} (trainer.py:182); the stamp marks the end of round t's update (trainer.py:181)
-    HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur ^ 1], c->n, c->ld, (int32_t)c->nch, kRowsPerGroup,
-                                c->part, c->stamps + h + 1, c->stream));
     // history[h-1] (this round's fused partials of x_h at xbar_h) rides the same launch
     double* hr = met ? c->hraw + 3 * (h - 1) : c->hraw;
     const FoldArgs fold = {want_cons ? c->slab_cons : nullptr, c->n, want_obj ? c->slab_loss : nullptr,
                            c->loss_groups, want_obj ? c->xbar[xb] : nullptr, hr, hr + 1, hr + 2};
-    HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, n_div(c), c->ld, (int32_t)c->nch, c->xbar[xb ^ 1],
-                              nullptr, 0.0, 0, c->stream, c->S, met ? &fold : nullptr));
+    HIPOK(launch_colsum(c->dtype, c->xs[c->cur ^ 1], c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part,
+                        c->stamps + h + 1, n_div(c), c->xbar[xb ^ 1], nullptr, 0.0, 0, c->stream, c->S,
+                        met ? &fold : nullptr));
     if ((rc = refresh_sums_t(c))) return rc;
     if (!met && !fused && metrics) {
       if ((rc = metrics_pass(c, c->xs[c->cur ^ 1], c->xbar[xb ^ 1], false, want_cons, want_obj))) return rc;
@@ -1074,11 +1084,9 @@ int dopt_run_centralized(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_
     HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, met, a, (int)c->n, c->stream));
     if (c->prof && (rc = prof_event(c, true))) return rc;
     // mean of the worker gradients and the step (trainer.py:53-57)
-    HIPOK(launch_colsum_partial(c->dtype, c->G, c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part,
-                                c->stamps + h + 1, c->stream));
-    HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nch,
-                              c->xg[c->gcur ^ 1], c->xg[c->gcur], eta0 / sqrt((double)(t + 1)), 1,
-                              c->stream));
+    HIPOK(launch_colsum(c->dtype, c->G, c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part, c->stamps + h + 1,
+                        c->n, c->xg[c->gcur ^ 1], c->xg[c->gcur], eta0 / sqrt((double)(t + 1)), 1, c->stream,
+                        nullptr, nullptr));
     if (met) {
       if ((rc = history(c, h - 1, c->xg[c->gcur], false, true, c->n))) return rc;
     } else if (!fused && want_obj) {

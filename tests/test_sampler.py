@@ -87,3 +87,29 @@ def test_rounds_leave_numpy_state_where_numpy_does(rows, b):
     ref = np.random.get_state()
     assert ours[2] == ref[2]
     np.testing.assert_array_equal(ours[1], ref[1])
+
+
+@pytest.mark.parametrize("b", [10 ** 6, 501, 16, 0])
+def test_trainer_index_chunks_advance_stream_like_choice(b):
+    """Trainer draws (full shards use b = 1 internally) leave numpy's global state exactly
+    where the reference's per-worker np.random.choice(m, min(b, m)) calls leave it
+    (worker.py:17-27), including empty shards and b far above m."""
+    from trainer import _index_chunks
+
+    class W:
+        def __init__(self, m):
+            self.n_local_samples, self.batch_size = m, b
+
+    rows = [500, 499, 0, 501]
+    np.random.seed(5)
+    chunks = list(_index_chunks([W(m) for m in rows], 37, {}))
+    key, pos = np.random.get_state()[1].copy(), np.random.get_state()[2]
+    np.random.seed(5)
+    for _ in range(37):
+        for m in rows:
+            if m > 0 and b > 0:
+                np.random.choice(m, min(b, m), replace=False)
+    np.testing.assert_array_equal(key, np.random.get_state()[1])
+    assert pos == np.random.get_state()[2]
+    assert sum(c[1] for c in chunks) == 37
+    assert (chunks[0][3] is None) == (b >= max(rows))
