@@ -17,20 +17,22 @@ import numpy as np  # noqa: E402
 
 import _dopt  # noqa: E402
 import main as M  # noqa: E402
-from trainer import DecentralizedTrainer  # noqa: E402
+from trainer import CentralizedTrainer, DecentralizedTrainer  # noqa: E402
 from utils import generate_and_preprocess_data  # noqa: E402
 from worker import Worker  # noqa: E402
 
 T = int(os.environ.get("C2_T", "10000"))
 
 
-def leg(name, cfg, shards, d, X, y):
+def leg(name, cfg, shards, d, X, y, central=False):
     workers = [Worker(i, shards[i], cfg["local_batch_size"], d, cfg) for i in range(cfg["n_workers"])]
-    tr = DecentralizedTrainer(workers, "ring", d, cfg)
+    tr = CentralizedTrainer(workers, d, cfg) if central else DecentralizedTrainer(workers, "ring", d, cfg)
     with contextlib.redirect_stdout(io.StringIO()):
         tr.run(50, X, y, 0.0)  # warm: engine, data upload, kernels
         for w in workers:
             w.x = np.zeros(d)
+        if central:
+            tr.x_global = np.zeros(d)
         t0 = time.perf_counter()
         tr.run(T, X, y, 0.0)
         dt = time.perf_counter() - t0
@@ -45,6 +47,7 @@ def main():
     leg("legacy sampler (exact)", cfg, shards, d, X, y)
     leg("device sampler", dict(cfg, sampling="device"), shards, d, X, y)
     leg("full shard (b = m)", dict(cfg, local_batch_size=10 ** 6), shards, d, X, y)
+    leg("centralized, legacy sampler", cfg, shards, d, X, y, central=True)
     rows = np.array([len(s["y"]) for s in shards])
     _dopt.mt_choice_rounds(1, rows, cfg["local_batch_size"])
     t0 = time.perf_counter()
