@@ -328,6 +328,7 @@ def test_minibatch_in_metrics_pass_matches_separate_pass(dtype, monkeypatch):
     np.random.seed(4)
     idx = _dopt.mt_choice_rounds(T, m_rows, b)
     runs = []
+    monkeypatch.setenv("DOPT_FEW_SPLIT", "0")  # 8 logistic workers: keep the fused paths under test
     for bip in ("1", "0"):
         monkeypatch.setenv("DOPT_BIP", bip)
         eng = _dopt.Engine(0, dtype)
@@ -336,6 +337,38 @@ def test_minibatch_in_metrics_pass_matches_separate_pass(dtype, monkeypatch):
         obj, cons, _ = eng.run_dsgd(T, 0.05, b, 1e-3, 1e-3, 0.0, idx=idx)
         runs.append((obj, cons, eng.get_models()))
         eng.close()
+    tol = 1e-12 if dtype == "float64" else 2e-6
+    for a_, b_ in zip(runs[0], runs[1]):
+        np.testing.assert_allclose(a_, b_, rtol=tol, atol=1e-14 if dtype == "float64" else 1e-7)
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+@pytest.mark.parametrize("batch", [8, 10 ** 6])
+def test_few_workers_separate_metrics_pass_matches_fused(dtype, batch, monkeypatch):
+    """Fewer than 256 logistic workers take the metrics pass apart from the round kernel
+    (runtime.cpp split_few_metrics, the C2 path); DOPT_FEW_SPLIT=0 keeps them fused into
+    the next round's pass (full shards) or the minibatch-in-pass round (b < m).  Only
+    summation orders differ: histories and iterates agree to rounding, ragged and empty
+    shards included."""
+    rng = np.random.default_rng(29)
+    m_rows = [40, 33, 0, 40, 17, 5, 40, 28]
+    n, d, T = len(m_rows), 45, 12
+    off = np.concatenate([[0], np.cumsum(m_rows)])
+    X = np.hstack([rng.standard_normal((off[-1], d - 1)), np.ones((off[-1], 1))])
+    y = rng.choice(np.array([-1.0, 1.0]), off[-1])
+    top = topology.ring(n)
+    np.random.seed(6)
+    idx = _dopt.mt_choice_rounds(T, m_rows, batch) if batch < max(m_rows) else None
+    runs = []
+    for split in ("1", "0"):
+        monkeypatch.setenv("DOPT_FEW_SPLIT", split)
+        eng = _dopt.Engine(0, dtype)
+        eng.load_shards("logistic", X, y, off)
+        eng.set_topology(top.row_ptr, top.col, top.w)
+        obj, cons, _ = eng.run_dsgd(T, 0.05, batch, 1e-3, 1e-3, 0.0, idx=idx)
+        runs.append((obj, cons, eng.get_models()))
+        eng.close()
+    assert len(runs[0][0]) == T and np.all(np.isfinite(runs[0][0]))
     tol = 1e-12 if dtype == "float64" else 2e-6
     for a_, b_ in zip(runs[0], runs[1]):
         np.testing.assert_allclose(a_, b_, rtol=tol, atol=1e-14 if dtype == "float64" else 1e-7)
