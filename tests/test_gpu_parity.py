@@ -421,3 +421,45 @@ def test_device_sampling_trainer_mode():
     assert np.all(np.isfinite(hist["objective"])) and hist["objective"][-1] < hist["objective"][0]
     with pytest.raises(NotImplementedError):
         _make_trainer("Centralized", shards, cfg).run(5, Xf, yf, meta["f_opt"])
+
+
+_COLSUM_SCRIPT = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import _dopt, topology
+rng = np.random.default_rng(31)
+m_rows = [40, 33, 0, 40, 17, 5, 40, 28, 12, 40]
+off = np.concatenate([[0], np.cumsum(m_rows)])
+d = 45
+X = np.hstack([rng.standard_normal((off[-1], d - 1)), np.ones((off[-1], 1))])
+y = rng.standard_normal(off[-1])
+top = topology.ring(len(m_rows))
+out = {}
+for dtype in ("float64", "float32"):
+    eng = _dopt.Engine(0, dtype)
+    eng.load_shards("quadratic", X, y, off)
+    eng.set_topology(top.row_ptr, top.col, top.w)
+    obj, cons, _ = eng.run_dsgd(15, 0.05, 10 ** 6, 1e-3, 1e-3, 0.0)
+    out[dtype + "_obj"], out[dtype + "_cons"], out[dtype + "_x"] = obj, cons, eng.get_models()
+    eng.close()
+np.savez(sys.argv[2], **out)
+"""
+
+
+def test_one_launch_column_sums_bitwise(tmp_path):
+    """<= 64 workers: the column sums (xbar, S, history fold) run as one launch
+    (k_colsum_one); DOPT_COLSUM_TWO=1 forces the two-stage kernels.  The launch choice is
+    read once per process, so each variant runs in its own process; the histories and
+    iterates must be bitwise equal."""
+    import subprocess
+    import sys
+
+    pkg = os.path.dirname(_dopt.__file__)
+    res = []
+    for two in ("0", "1"):
+        f = str(tmp_path / f"cs{two}.npz")
+        env = dict(os.environ, DOPT_COLSUM_TWO=two)
+        subprocess.run([sys.executable, "-c", _COLSUM_SCRIPT, pkg, f], env=env, check=True, timeout=120)
+        res.append(np.load(f))
+    for k in res[0].files:
+        np.testing.assert_array_equal(res[0][k], res[1][k], err_msg=k)
