@@ -308,6 +308,8 @@ def main():
                    "parallelism": (f"dp{world}: one graph of {n_global} workers, "
                                    f"{'graph-partitioned' if args.config == 'c3' and args.partition == 'spectral' else 'contiguous'} "
                                    f"slices per GPU, halo send/recv + all-reduce ({args.backend})") if world > 1
+                                  else ("single GPU: the multi-GPU phase path (lagged schedule, "
+                                        f"{args.backend} world 1)") if args.phase
                                   else "single GPU: fused round kernel, one launch per round"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
