@@ -992,9 +992,11 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
   // the fused objective (a second dot + exp / log per row) makes those CUs VALU-bound
   // (fp64 C2: 55-62 us per round kernel vs 17 us without metrics and 7 us for the
   // separate metrics pass over 64-row chunks on many CUs): take the metrics pass apart.
-  const bool few_split = split_few_metrics(c) && !dev;
-  const bool bip = metrics && (dev ? !c->obj_sep : !few_split && bip_possible(c, batch, idx));
-  const bool fused = ((batch >= c->max_m && !few_split) || bip) && !c->obj_sep;
+  // With the device sampler the round kernel still walks every row (the draw marks the
+  // batch rows in that pass) but computes only the batch rows: no metric work in it.
+  const bool few_split = split_few_metrics(c);
+  const bool bip = metrics && !few_split && (dev ? !c->obj_sep : bip_possible(c, batch, idx));
+  const bool fused = !few_split && (batch >= c->max_m || bip) && !c->obj_sep;
   const int64_t CH = idx ? idx_chunk_rounds(c, T, batch) : 1;
   int& xb = c->xb;
   if (c->split) return run_dsgd_split(c, t0, T, eta0, batch, idx, lam_grad, lam_obj, f_opt, flags, obj_out,

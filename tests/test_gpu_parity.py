@@ -343,7 +343,7 @@ def test_minibatch_in_metrics_pass_matches_separate_pass(dtype, monkeypatch):
 
 
 @pytest.mark.parametrize("dtype", ["float64", "float32"])
-@pytest.mark.parametrize("batch", [8, 10 ** 6])
+@pytest.mark.parametrize("batch", [8, 10 ** 6, "device"])
 def test_few_workers_separate_metrics_pass_matches_fused(dtype, batch, monkeypatch):
     """Fewer than 256 logistic workers take the metrics pass apart from the round kernel
     (runtime.cpp split_few_metrics, the C2 path); DOPT_FEW_SPLIT=0 keeps them fused into
@@ -358,12 +358,17 @@ def test_few_workers_separate_metrics_pass_matches_fused(dtype, batch, monkeypat
     y = rng.choice(np.array([-1.0, 1.0]), off[-1])
     top = topology.ring(n)
     np.random.seed(6)
-    idx = _dopt.mt_choice_rounds(T, m_rows, batch) if batch < max(m_rows) else None
+    dev = batch == "device"  # minibatches drawn on the GPU inside the pass over every row
+    if dev:
+        batch = 8
+    idx = _dopt.mt_choice_rounds(T, m_rows, batch) if batch < max(m_rows) and not dev else None
     runs = []
     for split in ("1", "0"):
         monkeypatch.setenv("DOPT_FEW_SPLIT", split)
         eng = _dopt.Engine(0, dtype)
         eng.load_shards("logistic", X, y, off)
+        if dev:
+            eng.set_sampler("device", seed=13)
         eng.set_topology(top.row_ptr, top.col, top.w)
         obj, cons, _ = eng.run_dsgd(T, 0.05, batch, 1e-3, 1e-3, 0.0, idx=idx)
         runs.append((obj, cons, eng.get_models()))
