@@ -116,10 +116,12 @@ hipError_t launch_split_coef(int dtype, int problem, int mode, const RoundArgs& 
                              hipStream_t s);
 
 // Column sums of rows x[0:rows] in one launch when rows <= rpg (k_colsum_one), else the two
-// stages below; arguments as theirs (n = the mean's divisor).
+// stages below; arguments as theirs (n = the mean's divisor).  cons_out (one-launch path
+// only, mode 0): per column block b, cons_out[b] = sum_i sum_{c in b} (x_ic - (T)xbar_c)^2.
 hipError_t launch_colsum(int dtype, const void* x, int64_t rows, int64_t ld, int32_t nchunks, int32_t rpg,
                          double* part, uint64_t* stamp, int64_t n, void* out, const void* base, double eta,
-                         int mode, hipStream_t s, double* raw, const FoldArgs* fold);
+                         int mode, hipStream_t s, double* raw, const FoldArgs* fold,
+                         double* cons_out = nullptr);
 // Column sums of an [n x ld] matrix into fp64 partials [G x ld], G = ceil(n / rpg).
 hipError_t launch_colsum_partial(int dtype, const void* x, int64_t n, int64_t ld, int32_t nchunks,
                                  int32_t rpg, double* part, uint64_t* stamp, hipStream_t s);

@@ -1135,10 +1135,13 @@ __global__ __launch_bounds__(NT) void k_colsum_final(const double* __restrict__ 
 template <typename T>
 __global__ __launch_bounds__(NT) void k_colsum_one(const T* __restrict__ x, int64_t rows, int64_t ld, int nch,
                                                    uint64_t* stamp, int64_t n, T* out, const T* base,
-                                                   double eta, int mode, double* raw, const FoldArgs fold) {
+                                                   double eta, int mode, double* raw, const FoldArgs fold,
+                                                   double* cons_out) {
   using V = typename VT<T>::v;
   constexpr int VN = VT<T>::n;
   __shared__ double red[NW][64 * VN];
+  __shared__ T xm[64 * VN];  // (T) xbar of this column block (cons_out)
+  __shared__ double cred[NW];
   if ((int)blockIdx.x == (nch + 63) / 64) {  // the fold block
     fold_block<T>(fold, nch, red);
     return;
@@ -1179,28 +1182,51 @@ __global__ __launch_bounds__(NT) void k_colsum_one(const T* __restrict__ x, int6
       double s = 0.0;  // stage 2 over one group
       s += p;
       s = ((s + 0.0) + 0.0) + 0.0;
+      const double mean = s / (double)n;
+      if (cons_out) xm[lane * VN + e] = (T)mean;
       if (raw) {
         raw[col] = s;
         if (!out) continue;
       }
-      const double mean = s / (double)n;
       if (mode == 0)
         out[col] = (T)mean;
       else
         out[col] = base[col] - (T)eta * (T)mean;
     }
   }
+  if (cons_out) {  // this block's share of sum_i ||x_i - xbar||^2 (trainer.py:183-186), xbar in T
+    __syncthreads();
+    double q = 0.0;
+    if (c < nch) {
+      V xv;
+#pragma unroll
+      for (int e = 0; e < VN; ++e) xv[e] = xm[lane * VN + e];
+      for (int64_t r = wave; r < rows; r += NW) {
+        const V dv = *(const V*)(x + r * ld + (int64_t)c * VN) - xv;
+        q += (double)hsum<T>(dv * dv);
+      }
+    }
+    q = wave_sum(q);
+    if (lane == 0) cred[wave] = q;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      for (int w = 0; w < NW; ++w) t += cred[w];
+      cons_out[blockIdx.x] = t;
+    }
+  }
 }
 
 hipError_t launch_colsum(int dtype, const void* x, int64_t rows, int64_t ld, int32_t nchunks, int32_t rpg,
                          double* part, uint64_t* stamp, int64_t n, void* out, const void* base, double eta,
-                         int mode, hipStream_t s, double* raw, const FoldArgs* fold) {
+                         int mode, hipStream_t s, double* raw, const FoldArgs* fold, double* cons_out) {
   const int groups = (int)((rows + rpg - 1) / rpg);
   static const bool two = [] {  // A/B knob DOPT_COLSUM_TWO=1: always the two-launch path
     const char* v = getenv("DOPT_COLSUM_TWO");
     return v && atoi(v) != 0;
   }();
   if (groups > 1 || two) {
+    if (cons_out) return hipErrorInvalidValue;  // one-launch path only (caller checks)
     hipError_t e = launch_colsum_partial(dtype, x, rows, ld, nchunks, rpg, part, stamp, s);
     if (e != hipSuccess) return e;
     return launch_colsum_final(dtype, part, groups > 0 ? groups : 1, n, ld, nchunks, out, base, eta, mode, s,
@@ -1212,10 +1238,10 @@ hipError_t launch_colsum(int dtype, const void* x, int64_t rows, int64_t ld, int
   const dim3 grid((nchunks + 63) / 64 + (fold ? 1 : 0));
   if (dtype == 0)
     hipLaunchKernelGGL(k_colsum_one<float>, grid, dim3(NT), 0, s, (const float*)x, rows, ld, nchunks, stamp, n,
-                       (float*)out, (const float*)base, eta, mode, raw, f);
+                       (float*)out, (const float*)base, eta, mode, raw, f, cons_out);
   else
     hipLaunchKernelGGL(k_colsum_one<double>, grid, dim3(NT), 0, s, (const double*)x, rows, ld, nchunks, stamp,
-                       n, (double*)out, (const double*)base, eta, mode, raw, f);
+                       n, (double*)out, (const double*)base, eta, mode, raw, f, cons_out);
   return hipGetLastError();
 }
 

@@ -459,9 +459,9 @@ void finalize_metrics(const double* raw, int64_t T, int problem, int64_t n, int6
   }
 }
 
-int history(dopt_ctx* c, int64_t h, const void* point, bool cons, bool loss, int64_t ng_unused) {
-  (void)ng_unused;
-  HIPOK(launch_history(c->dtype, cons ? c->slab_cons : nullptr, loss ? c->slab_loss : nullptr, c->n,
+// nc: valid consensus slab entries (c->n per-worker partials, or per column block)
+int history(dopt_ctx* c, int64_t h, const void* point, bool cons, bool loss, int64_t nc) {
+  HIPOK(launch_history(c->dtype, cons ? c->slab_cons : nullptr, loss ? c->slab_loss : nullptr, nc,
                        c->loss_groups, point, c->ld, (int32_t)c->nch, loss, c->hraw + 3 * h, c->stream));
   return DOPT_OK;
 }
@@ -997,6 +997,12 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
   const bool few_split = split_few_metrics(c);
   const bool bip = metrics && !few_split && (dev ? !c->obj_sep : bip_possible(c, batch, idx));
   const bool fused = !few_split && (batch >= c->max_m || bip) && !c->obj_sep;
+  // separate metrics with <= 64 workers: the consensus rides the one-launch column sums
+  // (per column block partials; one metrics launch less per round)
+  const int64_t cs_blocks = (c->nch + 63) / 64;
+  const char* two = getenv("DOPT_COLSUM_TWO");  // the two-stage column sums carry no consensus
+  const bool cons_cs = !fused && want_cons && c->n <= kRowsPerGroup && cs_blocks <= c->slab_cap && !c->split &&
+                       !(two && atoi(two) != 0);
   const int64_t CH = idx ? idx_chunk_rounds(c, T, batch) : 1;
   int& xb = c->xb;
   if (c->split) return run_dsgd_split(c, t0, T, eta0, batch, idx, lam_grad, lam_obj, f_opt, flags, obj_out,
@@ -1034,11 +1040,12 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
                            c->loss_groups, want_obj ? c->xbar[xb] : nullptr, hr, hr + 1, hr + 2};
     HIPOK(launch_colsum(c->dtype, c->xs[c->cur ^ 1], c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part,
                         c->stamps + h + 1, n_div(c), c->xbar[xb ^ 1], nullptr, 0.0, 0, c->stream, c->S,
-                        met ? &fold : nullptr));
+                        met ? &fold : nullptr, cons_cs ? c->slab_cons : nullptr));
     if ((rc = refresh_sums_t(c))) return rc;
     if (!met && !fused && metrics) {
-      if ((rc = metrics_pass(c, c->xs[c->cur ^ 1], c->xbar[xb ^ 1], false, want_cons, want_obj))) return rc;
-      if ((rc = history(c, h, c->xbar[xb ^ 1], want_cons, want_obj, c->n))) return rc;
+      if ((rc = metrics_pass(c, c->xs[c->cur ^ 1], c->xbar[xb ^ 1], false, want_cons && !cons_cs, want_obj)))
+        return rc;
+      if ((rc = history(c, h, c->xbar[xb ^ 1], want_cons, want_obj, cons_cs ? cs_blocks : c->n))) return rc;
     }
     c->cur ^= 1;
     xb ^= 1;
