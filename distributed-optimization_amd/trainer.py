@@ -178,6 +178,17 @@ def _set_objective_data(eng, workers, n_features, X_full, y_full):
     return True
 
 
+def _grad_reg(cfg, n_iterations, workers):
+    """Gradient regulariser (worker.py:36-42): lambda for logistic, mu for quadratic.  The
+    reference's Worker.compute_gradient reads BOTH keys on every call, so a run that takes
+    any gradient raises KeyError when either is missing, whatever the problem."""
+    if int(n_iterations) > 0 and len(workers) > 0:
+        lam, mu = cfg["l2_regularization_lambda"], cfg["strong_convexity_mu"]
+    else:
+        lam, mu = cfg.get("l2_regularization_lambda", 0.0), cfg.get("strong_convexity_mu", 0.0)
+    return lam if cfg["problem_type"] == "logistic" else mu
+
+
 def _batch_size(workers):
     bs = {int(w.batch_size) for w in workers}
     if len(bs) > 1:
@@ -263,7 +274,7 @@ class CentralizedTrainer:
         reg_param = self._get_regularization_param()
         self.total_floats_transmitted = 0
         cfg = self.config
-        lam_grad = cfg["l2_regularization_lambda"] if cfg["problem_type"] == "logistic" else cfg["strong_convexity_mu"]
+        lam_grad = _grad_reg(cfg, n_iterations, self.workers)
         info = _dist_info(cfg)
         if info is not None:
             return self._run_distributed(info, int(n_iterations), X_full, y_full, f_opt, lam_grad, reg_param,
@@ -362,7 +373,7 @@ class DecentralizedTrainer:
         reg_param = self._get_regularization_param()
         self.total_floats_transmitted = 0
         cfg = self.config
-        lam_grad = cfg["l2_regularization_lambda"] if cfg["problem_type"] == "logistic" else cfg["strong_convexity_mu"]
+        lam_grad = _grad_reg(cfg, n_iterations, self.workers)
         info = _dist_info(cfg)
         if info is not None:
             return self._run_distributed(info, int(n_iterations), X_full, y_full, f_opt, lam_grad, reg_param,

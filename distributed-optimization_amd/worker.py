@@ -38,8 +38,12 @@ class Worker:
         params = model_params if model_params is not None else self.x
         X_batch, y_batch = self.get_mini_batch()
         problem = self.config["problem_type"]
+        # worker.py:36-37 reads BOTH keys before dispatching: a config without either raises
+        # KeyError whatever the problem (after the draw, as in the reference)
+        lambda_reg = self.config["l2_regularization_lambda"]
+        mu_reg = self.config["strong_convexity_mu"]
         if problem == "logistic":
-            return logistic_stochastic_gradient(params, X_batch, y_batch, self.config["l2_regularization_lambda"])
+            return logistic_stochastic_gradient(params, X_batch, y_batch, lambda_reg)
         elif problem == "quadratic":
-            return quadratic_stochastic_gradient(params, X_batch, y_batch, self.config["strong_convexity_mu"])
+            return quadratic_stochastic_gradient(params, X_batch, y_batch, mu_reg)
         raise NotImplementedError(f"Wrong {problem}")

@@ -1,0 +1,150 @@
+"""Parity of the benchmarked kernel instances: >= 256 workers, multi-round, vs the oracle.
+
+The fixture trajectories of test_gpu_parity.py have N <= 25 and d <= 100, so they select
+the few-worker launch shapes (16-wave round kernel, separate metrics pass) and one chunk
+per lane.  The bench (config C3) runs other instances of `k_round` (kernels.hip):
+
+* >= 256 workers: the default 8-wave (CPL <= 4) or 4-wave (CPL 8 / 16) kernel with the
+  objective and the consensus FUSED into the next round's row pass (runtime.cpp
+  dopt_run_dsgd, `fused`), and the metrics-only pass after the last round;
+* float32 logistic: hardware exp / log / reciprocal for the row terms (VAR bit 13);
+* minibatches by index inside the pass over every row (F_BIP) and the device sampler;
+* CPL = 1, 2, 4, 8, 16 chunks per lane in both dtypes, and row lengths that are not a
+  multiple of the wave's 64 chunks (masked-lane loads: lanes past the row re-read its
+  last chunk, VAR bit 11) or of the 16-byte vector (zero padding).
+
+Every case runs T = 10 rounds of the reference's round (trainer.py:161-193) on a random
+4-regular graph and compares, against oracle/dsgd_oracle.run_decentralized on the same
+shards, indices and CSR order (mixing='sparse'):
+  float64: objective and consensus of every round and the final iterates, rtol 1e-9;
+  float32: vs the float32 oracle, objective rtol 1e-5, consensus 5e-5, iterates 1e-4
+           (of the largest entry); the bench's own instance also vs the float64 oracle,
+           objective 1e-4.
+"""
+import numpy as np
+import pytest
+
+import _dopt
+import device_sampler as DS
+import dsgd_oracle as O
+import topology
+
+pytestmark = pytest.mark.gpu
+
+N = 256
+T = 10
+
+
+def _shards(problem, n, d, m, seed):
+    rng = np.random.default_rng(seed)
+    wstar = rng.standard_normal(d) / np.sqrt(d)
+    X = np.hstack([rng.standard_normal((n * m, d - 1)), np.ones((n * m, 1))])
+    z = X @ wstar
+    if problem == "logistic":
+        y = np.where(z >= 0, 1.0, -1.0)
+        flip = rng.random(n * m) < 0.05
+        y[flip] = -y[flip]
+    else:
+        y = z + 0.5 * rng.standard_normal(n * m)
+    return X, y
+
+
+def _run(problem, dtype, d, m, b, seed=11, sampler="host", vs64=False):
+    X, y = _shards(problem, N, d, m, seed)
+    off = np.arange(N + 1, dtype=np.int64) * m
+    shards = [(X[i * m:(i + 1) * m], y[i * m:(i + 1) * m]) for i in range(N)]
+    top = topology.random_regular(N, 4, seed=3)
+    lam = 1e-4
+    eta0 = 0.05
+    cfg = {"problem_type": problem, "local_batch_size": b, "learning_rate_eta0": eta0,
+           "l2_regularization_lambda": lam, "strong_convexity_mu": lam}
+    idx = None
+    indices = None
+    if b < m and sampler == "host":
+        np.random.seed(seed)
+        idx = _dopt.mt_choice_rounds(T, [m] * N, b)  # worker.py:27, legacy stream
+        indices = [[idx[t, i].astype(np.int64) for i in range(N)] for t in range(T)]
+    elif b < m:
+        rep = DS.rounds(77, 0, T, [m] * N, b)
+        indices = [[rep[t, i][rep[t, i] >= 0].astype(np.int64) for i in range(N)] for t in range(T)]
+    else:
+        indices = [[np.arange(m)] * N] * T
+    eng = _dopt.Engine(0, dtype)
+    try:
+        eng.load_shards(problem, X, y, off)
+        eng.set_topology(top.row_ptr, top.col, top.w)
+        if sampler == "device":
+            eng.set_sampler("device", seed=77)
+        obj, cons, _ = eng.run_dsgd(T, eta0, b, lam, lam, 0.0, idx=idx)
+        x = eng.get_models()
+    finally:
+        eng.close()
+    W = top.dense_W()
+    npdt = np.float32 if dtype == "float32" else np.float64
+    h, _, xr, _ = O.run_decentralized(shards, W, T, cfg, X, y, 0.0, dtype=npdt, mixing="sparse", indices=indices)
+    h64 = None
+    if dtype == "float32" and vs64:
+        h64, _, _, _ = O.run_decentralized(shards, W, T, cfg, X, y, 0.0, mixing="sparse", indices=indices)
+    return (obj, cons, x), (h, xr), h64
+
+
+def _check(dtype, got, ref, h64):
+    (obj, cons, x), (h, xr) = got, ref
+    assert len(obj) == len(cons) == T
+    assert np.all(np.isfinite(obj)) and np.all(np.isfinite(cons))
+    if dtype == "float64":
+        np.testing.assert_allclose(obj, h["objective"], rtol=1e-9)
+        np.testing.assert_allclose(cons, h["consensus_error"], rtol=1e-9)
+        np.testing.assert_allclose(x, xr, rtol=1e-9, atol=1e-12 * np.abs(xr).max())
+    else:
+        np.testing.assert_allclose(obj, h["objective"], rtol=1e-5)
+        np.testing.assert_allclose(cons, h["consensus_error"], rtol=5e-5)
+        np.testing.assert_allclose(x, xr, rtol=1e-4, atol=1e-4 * np.abs(xr).max())
+        if h64 is not None:
+            np.testing.assert_allclose(obj, h64["objective"], rtol=1e-4)
+
+
+# (problem, dtype, d, m, b): the C3 shape (d = 1024, m = 512) in full-shard and b = 16 rounds
+C3_CASES = [
+    ("logistic", "float32", 1024, 512, 512),   # the bench's kernel: k_round<float,4,0,true,true,14627>
+    ("logistic", "float64", 1024, 512, 512),   # k_round<double,8,...>: the reference's precision
+    ("logistic", "float32", 1024, 512, 16),    # minibatch by index inside the pass over all rows
+    ("logistic", "float64", 1024, 512, 16),
+    ("quadratic", "float32", 1024, 512, 512),
+    ("quadratic", "float64", 1024, 512, 512),
+]
+
+
+@pytest.mark.parametrize("problem,dtype,d,m,b", C3_CASES)
+def test_c3_shape_trajectory_vs_oracle(problem, dtype, d, m, b):
+    got, ref, h64 = _run(problem, dtype, d, m, b, vs64=(problem, dtype, b) == ("logistic", "float32", 512))
+    _check(dtype, got, ref, h64)
+
+
+# Chunks per lane: float32 d <= 256 / 512 / 1024 / 2048 / 4096 -> CPL 1 / 2 / 4 / 8 / 16;
+# float64 d <= 128 / 256 / 512 / 1024 / 2048.  Rows that do not fill the last 64-chunk
+# stripe exercise the masked lanes; d % 4 != 0 (float32) the zero padding.
+CPL_CASES = [
+    ("float32", 200), ("float32", 300), ("float32", 1000), ("float32", 1001), ("float32", 2048), ("float32", 4000),
+    ("float64", 100), ("float64", 200), ("float64", 512), ("float64", 1000), ("float64", 2000),
+]
+
+
+@pytest.mark.parametrize("dtype,d", CPL_CASES)
+def test_chunks_per_lane_and_masked_rows_vs_oracle(dtype, d):
+    got, ref, h64 = _run("logistic", dtype, d, 64, 64, seed=d)
+    _check(dtype, got, ref, h64)
+
+
+@pytest.mark.parametrize("dtype", ["float32", "float64"])
+def test_quadratic_wide_rows_vs_oracle(dtype):
+    got, ref, h64 = _run("quadratic", dtype, 2000, 32, 32, seed=5)
+    _check(dtype, got, ref, h64)
+
+
+@pytest.mark.parametrize("dtype", ["float32", "float64"])
+def test_device_sampler_at_scale_vs_oracle(dtype):
+    """sampling='device' (Philox + Floyd on the GPU) at 256 workers: the host restatement
+    of the draw (oracle/device_sampler.py) fed to the oracle gives the same trajectory."""
+    got, ref, h64 = _run("logistic", dtype, 1024, 512, 16, sampler="device")
+    _check(dtype, got, ref, h64)
