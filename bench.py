@@ -146,6 +146,9 @@ def main():
     ap.add_argument("--d", type=int, default=1024)
     ap.add_argument("--m", type=int, default=512)
     ap.add_argument("--dtype", default="float32")
+    ap.add_argument("--data-dtype", default=None,
+                    help="shard storage (default: --dtype); float32 under --dtype float64 keeps every "
+                         "operation in float64 over float32-representable rows")
     ap.add_argument("--batch", type=int, default=0,
                     help="C3 minibatch per worker (0: the full shard, the metric's configuration); b < m "
                          "draws the minibatches on the device (sampling='device', Philox + Floyd)")
@@ -221,7 +224,7 @@ def main():
                                     np.zeros(world + 1, np.int64), None, None, None)
     n = plan.n_local
     log(f"rank {rank}/{world}: generating {plan.n_local} x {m} x {d} {args.dtype} shards on device {dev}")
-    eng = _dopt.Engine(dev, args.dtype)
+    eng = _dopt.Engine(dev, args.dtype, data_dtype=args.data_dtype)
     eng.generate_shards(problem, plan.n_local, d, m, seed=1000, flip=0.05, first_worker=plan.lo)
     lam = 1e-4
     b = args.batch if 0 < args.batch < m else m
@@ -273,18 +276,22 @@ def main():
         raise RuntimeError("non-finite metrics")
 
     esz = 4 if args.dtype in ("float32", "fp32", "f32") else 8
+    xesz = 4 if eng.data_dtype == _dopt.F32 else 8
     tname = "float" if esz == 4 else "double"
+    sname = "float" if xesz == 4 else "double"
     cpl = 1
-    while cpl * 64 < (d + (16 // esz) - 1) // (16 // esz):
+    while cpl * 64 < (d + (16 // xesz) - 1) // (16 // xesz):
         cpl *= 2
     if cpl <= 16:
         var = 14371 | 256 if cpl <= 4 else 14371  # kernels.hip: kr_default_var<CPL>()
-        kname = (f"void dopt::k_round<{tname}, {cpl}, {0 if problem == 'logistic' else 1}, true, true, {var}>"
+        if xesz != esz:
+            var = 14371
+        kname = (f"void dopt::k_round<{tname}, {sname}, {cpl}, {0 if problem == 'logistic' else 1}, true, true, {var}>"
                  "(dopt::RoundArgs)")
     else:
         kname = f"void dopt::k_split_step<{tname}, {4 if m <= 16 else 16}, true, true>(dopt::RoundArgs)"
     traffic, traffic_src = pmc_traffic(kname) if args.config == "c3" and n == 4096 and world == 1 else (None, None)
-    bytes_per_launch = esz * n * (m * d + m + 2 * d)  # X_b + y_b + x read + x write
+    bytes_per_launch = n * (xesz * (m * d + m) + esz * 2 * d)  # X_b + y_b + x read + x write
     avg_s = (kr_ms / launches) * 1e-3 if launches else float("nan")
     achieved = bytes_per_launch / avg_s / 1e9 if launches else None
     value = n_global * args.steps / dt

@@ -45,6 +45,8 @@ _SIGS = {
     "dopt_device_count": ([_P], ctypes.c_int),
     "dopt_create": ([ctypes.c_int, ctypes.c_int, _P], ctypes.c_int),
     "dopt_destroy": ([_P], ctypes.c_int),
+    "dopt_set_data_dtype": ([_P, ctypes.c_int], ctypes.c_int),
+    "dopt_get_data_dtype": ([_P, _P], ctypes.c_int),
     "dopt_load_shards": ([_P, ctypes.c_int, _I64, _I64, _P, _P, _P, ctypes.c_int], ctypes.c_int),
     "dopt_generate_shards": ([_P, ctypes.c_int, _I64, _I64, _I64, ctypes.c_uint64, _D, _D, _I64], ctypes.c_int),
     "dopt_load_objective_data": ([_P, _I64, _P, _P, ctypes.c_int], ctypes.c_int),
@@ -177,15 +179,24 @@ def mt_choice_rounds(T, shard_rows, b):
 
 # ---------------------------------------------------------------------------- device engine
 class Engine:
-    """One dopt context (one GPU): shards, topology and iterates resident in HBM."""
+    """One dopt context (one GPU): shards, topology and iterates resident in HBM.
 
-    def __init__(self, device=0, dtype="float64"):
+    dtype: iterates and arithmetic.  data_dtype: storage of the shard rows (default: dtype);
+    'float32' under dtype 'float64' keeps every operation in float64 and reads the rows as
+    float32 (exact for float32-representable data: half the HBM bytes per round)."""
+
+    def __init__(self, device=0, dtype="float64", data_dtype=None):
         self.dtype = DTYPES[dtype] if not isinstance(dtype, int) else dtype
         self.np_dtype = np.float32 if self.dtype == F32 else np.float64
         self.device = int(device)
         h = ctypes.c_void_p()
         check(lib().dopt_create(self.device, self.dtype, ctypes.byref(h)))
         self._h = h
+        self.data_dtype = self.dtype
+        if data_dtype is not None:
+            xd = DTYPES[data_dtype] if not isinstance(data_dtype, int) else data_dtype
+            check(lib().dopt_set_data_dtype(self._h, xd))
+            self.data_dtype = xd
         self.n = 0
         self.d = 0
         self.problem = None

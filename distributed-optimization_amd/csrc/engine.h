@@ -65,6 +65,8 @@ struct RoundArgs {
   int32_t groups;         // column-block groups = gridDim.y
   int32_t contig;         // column-blocked kernels: contiguous block range per group (set by the launcher)
   int32_t bip_rows;       // F_BIP: the largest shard (LDS byte map size)
+  int32_t defer_rows;     // k_round VAR bit 14: >= the rows of every workgroup of this launch (loss terms
+                          // buffered in LDS), or 0 when they do not all fit (the launch keeps them inline)
   // F_DEVSAMPLE: the minibatch of worker i in this round is a function of (seed, round, wid0 + i)
   uint64_t seed;
   int64_t round;
@@ -95,10 +97,20 @@ struct FoldArgs {
 };
 
 // Kernel launchers (kernels.hip).  dtype: 0 = float, 1 = double.
-// cpl = 16-byte chunks per lane (1, 2, 4, 8, 16); grad / met select the variant.
-hipError_t launch_round(int dtype, int problem, int cpl, bool grad, bool met, const RoundArgs& a,
+// k_round: dtype = iterates and arithmetic, xdtype = shard storage (equal, or float32 rows
+// under float64 arithmetic); cpl = 16-byte DATA chunks per lane (1, 2, 4, 8, 16); a.nchunks
+// counts data chunks.  The state-only kernels below take STATE chunks (nchunks, cpl).
+// grad / met select the variant.
+hipError_t launch_round(int dtype, int xdtype, int problem, int cpl, bool grad, bool met, const RoundArgs& a,
                         int n_groups, hipStream_t s);
-int max_chunks_per_lane();
+int max_chunks_per_lane(int dtype, int xdtype);
+// per element-type pair (round_f32.hip / round_f64.hip / round_x32.hip)
+hipError_t launch_round_f32(int problem, int cpl, bool grad, bool met, const RoundArgs& a, int n_groups,
+                            hipStream_t s);
+hipError_t launch_round_f64(int problem, int cpl, bool grad, bool met, const RoundArgs& a, int n_groups,
+                            hipStream_t s);
+hipError_t launch_round_x32(int problem, int cpl, bool grad, bool met, const RoundArgs& a, int n_groups,
+                            hipStream_t s);
 
 // ---- large d (column-blocked): one workgroup per (worker, group of 64-chunk column blocks)
 constexpr int kSplitMaxRows = 64;  // rows held in registers by a step workgroup (16 per wave)

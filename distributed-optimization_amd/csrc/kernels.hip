@@ -26,600 +26,22 @@
 //
 // No atomics anywhere: every reduction has a fixed order, so runs are bitwise
 // reproducible.
-#include <math.h>
-#include <stdlib.h>
-#include <string.h>
-
-#include <type_traits>
-
-#include "engine.h"
+#include "kcommon.h"
 
 namespace dopt {
 
-template <typename T>
-struct VT;
-template <>
-struct VT<float> {
-  static constexpr int n = 4;
-  typedef float v __attribute__((ext_vector_type(4)));
-};
-template <>
-struct VT<double> {
-  static constexpr int n = 2;
-  typedef double v __attribute__((ext_vector_type(2)));
-};
-
-constexpr int NW = 4;         // waves per workgroup
-constexpr int NT = NW * 64;   // threads per workgroup
-constexpr int MAX_CPL = 16;   // 16-byte chunks per lane: d <= 4096 (fp32) / 2048 (fp64)
-static_assert(NW == 4, "k_cons folds four wave sums");
-
-template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-// Wave-wide sum by DPP: quad swaps, row_shr 4/8, row_bcast 15/31 (GFX9-family DPP), then
-// one v_readlane of lane 63 -- the result lands in an SGPR (the coefficient is wave-uniform).
-template <int CTRL, int RM, int BM>
-__device__ __forceinline__ int dpp_i(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, RM, BM, false);
-}
-template <int CTRL, int RM, int BM>
-__device__ __forceinline__ float dpp_add(float v) {
-  return v + __builtin_bit_cast(float, dpp_i<CTRL, RM, BM>(__builtin_bit_cast(int, v)));
-}
-template <int CTRL, int RM, int BM>
-__device__ __forceinline__ double dpp_add(double v) {
-  const long long b = __builtin_bit_cast(long long, v);
-  const int lo = dpp_i<CTRL, RM, BM>((int)(b & 0xffffffffll));
-  const int hi = dpp_i<CTRL, RM, BM>((int)(b >> 32));
-  return v + __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
-}
-template <typename T>
-__device__ __forceinline__ T wave_sum_dpp(T v) {
-  v = dpp_add<0xb1, 0xf, 0xf>(v);   // quad_perm [1,0,3,2]
-  v = dpp_add<0x4e, 0xf, 0xf>(v);   // quad_perm [2,3,0,1]
-  v = dpp_add<0x114, 0xf, 0xe>(v);  // row_shr:4
-  v = dpp_add<0x118, 0xf, 0xc>(v);  // row_shr:8
-  v = dpp_add<0x142, 0xa, 0xf>(v);  // row_bcast:15
-  v = dpp_add<0x143, 0xc, 0xf>(v);  // row_bcast:31  -> lane 63 holds the sum
-  if constexpr (sizeof(T) == 4) {
-    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
-  } else {
-    const long long b = __builtin_bit_cast(long long, v);
-    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), 63);
-    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
-    return __builtin_bit_cast(T, ((long long)hi << 32) | (unsigned int)lo);
-  }
-}
-
-template <typename T, typename V>
-__device__ __forceinline__ T hsum(V v) {
-  T s = v[0];
-#pragma unroll
-  for (int e = 1; e < VT<T>::n; ++e) s += v[e];
-  return s;
-}
-
-// Philox4x32-10 (Salmon et al., SC'11): counter-based, so a worker's minibatch of a round
-// is a pure function of (seed, round, worker) -- no generator state anywhere.
-struct U4 {
-  uint32_t x, y, z, w;
-};
-__device__ __forceinline__ U4 philox4x32(U4 c, uint32_t k0, uint32_t k1) {
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
-    c = U4{(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0};
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
-  }
-  return c;
-}
-
-// Device minibatch (sampling = 'device', the non-parity throughput mode of SURVEY section 7):
-// Floyd's algorithm marks a uniform nb-subset of [0, m) in the LDS byte map; draw k is word
-// k % 4 of philox(counter = (k / 4, worker, round lo, round hi), key = seed), mapped to
-// [0, j] by a 32x32 multiply-high (bias <= m / 2^32).  oracle/device_sampler.py restates it.
-__device__ void floyd_sample(unsigned char* bmask, int64_t m, int64_t nb, uint64_t seed, int64_t round,
-                             int64_t worker) {
-  U4 r = {0, 0, 0, 0};
-  int64_t k = 0;
-  for (int64_t j = m - nb; j < m; ++j, ++k) {
-    if ((k & 3) == 0)
-      r = philox4x32(U4{(uint32_t)(k >> 2), (uint32_t)worker, (uint32_t)round, (uint32_t)((uint64_t)round >> 32)},
-                     (uint32_t)seed, (uint32_t)(seed >> 32));
-    const uint32_t u = (k & 3) == 0 ? r.x : (k & 3) == 1 ? r.y : (k & 3) == 2 ? r.z : r.w;
-    const int64_t t = (int64_t)(((uint64_t)u * (uint64_t)(j + 1)) >> 32);
-    if (bmask[t]) bmask[j] = 1;
-    else bmask[t] = 1;
-  }
-}
-
-// scipy.special.expit(x) = 1 / (1 + exp(-x)); the gradient needs expit(-y z).
-template <typename T>
-__device__ __forceinline__ T sigmoid_neg(T yz) {
-  return T(1) / (T(1) + exp(yz));
-}
-
-// Hardware transcendentals for float (v_exp_f32 / v_log_f32 / v_rcp_f32, ~1 ulp): the
-// library expf / logf / division add range reduction and Newton steps per row.
-__device__ __forceinline__ float sigmoid_neg_fast(float yz) {
-  return __builtin_amdgcn_rcpf(1.0f + __expf(yz));
-}
-__device__ __forceinline__ double row_loss_fast(float yv, float u) {
-  const float t = yv * u;
-  const float a = t < 0.f ? -t : t;
-  return (double)((t < 0.f ? -t : 0.f) + __logf(1.0f + __expf(-a)));
-}
-
-// obj_problems.py:5-7 (logistic, np.log(1 + exp(-|t|)) as written, not log1p)
-// and obj_problems.py:41-42 (quadratic, the 0.5 is applied once at the end).
-template <typename T, int PROB>
-__device__ __forceinline__ double row_loss(T yv, T u) {
-  if (PROB == 0) {
-    const T t = yv * u;
-    const T a = t < T(0) ? -t : t;
-    return (double)((t < T(0) ? -t : T(0)) + log(T(1) + exp(-a)));
-  } else {
-    const T e = u - yv;
-    return (double)(e * e);
-  }
-}
-
-// sum_j W_ij x_j for the 16-byte chunk c of worker i: CSR over local / halo rows, or, for the
-// complete graph (F_MEAN), w_off (S - x_i) + W_ii x_i from the column sums S (trainer.py:173).
-template <typename T>
-__device__ __forceinline__ typename VT<T>::v mix_chunk(const RoundArgs& a, int i, int c,
-                                                       typename VT<T>::v own) {
-  using V = typename VT<T>::v;
-  constexpr int VN = VT<T>::n;
-  V acc = V(0);
-  if (a.flags & F_MEAN) {
-    const double wii = (double)((const T*)a.wdiag)[i];
-    if (a.colsum_t) {  // sums rounded to T: one 16-byte load per chunk instead of VN doubles
-      const V sv = *(const V*)((const T*)a.colsum_t + (int64_t)c * VN);
-#pragma unroll
-      for (int e = 0; e < VN; ++e) {
-        const double x = (double)own[e];
-        acc[e] = (T)(a.w_off * ((double)sv[e] - x) + wii * x);
-      }
-      return acc;
-    }
-#pragma unroll
-    for (int e = 0; e < VN; ++e) {
-      const double x = (double)own[e];
-      acc[e] = (T)(a.w_off * (a.colsum[(int64_t)c * VN + e] - x) + wii * x);
-    }
-    return acc;
-  }
-  for (int64_t e = a.rp[i]; e < a.rp[i + 1]; ++e) {
-    const T wt = ((const T*)a.cw)[e];
-    const int col = a.ci[e];
-    const T* src = col < a.n_local ? (const T*)a.x_old + (int64_t)col * a.ld
-                                   : (const T*)a.halo + (int64_t)(col - a.n_local) * a.ld;
-    acc += wt * *(const V*)(src + (int64_t)c * VN);
-  }
-  return acc;
-}
-
 // ---------------------------------------------------------------------------- k_round
-// VAR: bit 0 nontemporal row loads (rows are read once per round: +11 % on MI355X,
-// 6.28 -> 7.15 TB/s on the bare access pattern, tools/bw_probe.hip), bit 1 DPP wave
-// reduction (readlane to an SGPR; ~0.5-1 %), bit 2 twice the rows in flight (no gain).
-// bit 3 persistent workgroups (-2 %: loses the dispatcher's dynamic balancing), bit 4 CSR
-// rows prefetched to LDS (null), bit 5 software-pipelined row loop (-0.9 %, adopted),
-// bit 6 minibatch inside the metrics pass (F_BIP), bit 8 8 waves per workgroup (-0.8 %,
-// adopted for <= 4 chunks per lane), bit 9 16 waves (no gain), bit 10 6 waves per SIMD
-// (spills: 2.7x slower), bit 11 branch-free row loads (lanes past the row re-read its last
-// chunk), bit 12 peeled pipelined loop -- with 11, the compiler's wait before a row's
-// arithmetic covers that row only (vmcnt(4) instead of vmcnt(0): the conditional and
-// lane-masked loads of the plain loop made it drain everything in flight; -0.6 %, won
-// 7 of 7 reps), bit 13 hardware exp / log / reciprocal for the float logistic row terms
-// (-0.3 %).  Not kept: ping-pong row buffers (loop unrolled by two by hand; the register
-// allocator still copies the refilled buffer at the latch behind a vmcnt(0): +1.3 %).
-// Default 14371 = NT + DPP + pipelined + branch-free + peeled + fast transcendentals
-// (| 256 for short rows); the others stay reachable through DOPT_KR_VARIANT for A/B runs
-// (tools/kr_variants.py).
-constexpr int KR_DEFAULT_VAR = 35 | 2048 | 4096 | 8192;
-// Rows of up to 4 chunks per lane (d <= 1024 fp32 / 512 fp64) also take VAR bit 8: 8 waves
-// per workgroup, so a workgroup lives half as long and the launch's last generation drains
-// sooner (C3: 1.2686 vs 1.2789 ms, won 7 of 7 interleaved reps); longer rows keep 4 waves
-// (their 2x VGPRs would not fit 2 waves per SIMD per workgroup).
-template <int CPL>
-constexpr int kr_default_var() { return CPL <= 4 ? (KR_DEFAULT_VAR | 256) : KR_DEFAULT_VAR; }
-template <typename T, int CPL, int PROB, bool GRAD, bool MET, int VAR = KR_DEFAULT_VAR>
-__global__ __launch_bounds__((VAR & 512) ? 4 * NT : (VAR & 256) ? 2 * NT : NT)
-__attribute__((amdgpu_waves_per_eu((VAR & 1024) ? 6 : 1))) void k_round(const RoundArgs a) {
-  // VAR bit 8: 8 waves per workgroup (half the workgroup duration, twice the generations);
-  // bit 9: 16 waves (one workgroup per CU)
-  constexpr int KW = (VAR & 512) ? 4 * NW : (VAR & 256) ? 2 * NW : NW;
-  constexpr int KT = KW * 64;
-  constexpr size_t KSRED = 3 * KW * 8;
-  using V = typename VT<T>::v;
-  constexpr int VN = VT<T>::n;
-  constexpr int RB = (CPL >= 8 ? 1 : 8 / CPL) * ((VAR & 4) ? 2 : 1);  // rows in flight per wave
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // VAR bit 3: persistent workgroups, each walking workers blockIdx.x + k * gridDim.x
-  const int i_end = (VAR & 8) ? a.n_local : (int)blockIdx.x + 1;
-  const int i_step = (VAR & 8) ? (int)gridDim.x : 1;
-  for (int i = blockIdx.x; i < i_end; i += i_step) {
-  const int flags = a.flags;
-  const int nch = a.nchunks;
-  const int64_t ld = a.ld;
-  const int64_t row0 = a.off[i];
-  const int64_t m = a.off[i + 1] - row0;
-  const bool dev_sample = (flags & F_DEVSAMPLE) != 0;
-  const int64_t nb = (GRAD && (a.idx || dev_sample)) ? (a.b < m ? a.b : m) : m;
-  const T* __restrict__ X = (const T*)a.X;
-  const T* __restrict__ Y = (const T*)a.y;
-  const T* wsrc = (flags & F_SHARED) ? (const T*)a.w_shared : (const T*)a.x_old + (int64_t)i * ld;
-  // VAR bit 4: the CSR rows of the mix (x_old, fixed during the round) go to LDS right away,
-  // overlapping the row stream, so the epilogue touches no global memory but the store.
-  constexpr bool PRE = (VAR & 16) != 0;
-  V* nbuf = (V*)(smem + (size_t)KW * nch * 16 + KSRED);  // after red + sred
-  const int64_t pe0 = a.rp ? a.rp[i] : 0, pe1 = a.rp ? a.rp[i + 1] : 0;
-  const bool pre = PRE && GRAD && (flags & F_STEP) && !(flags & F_MEAN) && (pe1 - pe0) <= a.pre_rows;
-  if (pre) {
-    for (int64_t e = pe0; e < pe1; ++e) {
-      const int col = a.ci[e];
-      const T* src = col < a.n_local ? (const T*)a.x_old + (int64_t)col * ld
-                                     : (const T*)a.halo + (int64_t)(col - a.n_local) * ld;
-      for (int c = threadIdx.x; c < nch; c += KT) nbuf[(e - pe0) * nch + c] = *(const V*)(src + (int64_t)c * VN);
-    }
-  }
-  // VAR bit 6 (minibatch in the metrics pass): the objective needs every row of the shard at
-  // xbar anyway, so the pass streams all m rows and the minibatch rows (marked in an LDS byte
-  // map) also feed the gradient -- one pass over the shard per round for every batch size.
-  constexpr bool BIP = GRAD && MET && (VAR & 64) != 0;
-  const int64_t nrow = BIP ? m : nb;
-  unsigned char* bmask = (unsigned char*)(smem + (size_t)KW * nch * 16 + KSRED + (PRE ? (size_t)a.pre_rows * nch * 16 : 0));
-  if (BIP) {
-    for (int64_t r = threadIdx.x; r < m; r += KT) bmask[r] = 0;
-    __syncthreads();
-    if (dev_sample) {
-      if (threadIdx.x == 0) floyd_sample(bmask, m, nb, a.seed, a.round, a.wid0 + i);
-    } else {
-      for (int64_t k = threadIdx.x; k < nb; k += KT) bmask[a.idx[(int64_t)i * a.b + k]] = 1;
-    }
-    __syncthreads();
-  }
-
-  const bool loss_from_z = (flags & F_LOSS_FROM_Z) != 0;
-  const bool want_loss = MET && (flags & F_LOSS);
-  const bool want_cons = MET && (flags & F_CONS);
-  // F_LOSS2 (metrics-only passes): a second objective at w_shared from z, next to the one at xbar
-  const bool want_loss2 = MET && !GRAD && (flags & F_LOSS2);
-  const bool compute_z = GRAD || (want_loss && loss_from_z) || want_loss2;
-  const bool compute_u = want_loss && !loss_from_z;
-  const bool need_w = compute_z || want_cons;
-  const bool need_xb = compute_u || want_cons;
-
-  V w[CPL], xb[CPL], g[CPL];
-#pragma unroll
-  for (int j = 0; j < CPL; ++j) {
-    const int c = lane + 64 * j;
-    const bool in = c < nch;
-    w[j] = (need_w && in) ? *(const V*)(wsrc + (int64_t)c * VN) : V(0);
-    xb[j] = (need_xb && in) ? *(const V*)((const T*)a.xbar + (int64_t)c * VN) : V(0);
-    g[j] = V(0);
-  }
-  double loss = 0.0, loss2 = 0.0;
-
-  // VAR bit 5: software-pipelined row loop -- row k+1's loads are issued before row k's
-  // dot / reduction / accumulate, so a wave never sits with nothing in flight (same
-  // two row buffers of registers as the default RB = 2 loop).
-  constexpr bool PIPE = (VAR & 32) != 0 && CPL <= 4;  // same registers as RB = 2 only there
-  if (PIPE && (compute_z || compute_u)) {
-    auto load_row = [&](int64_t rr, V (&dst)[CPL], T& yd) {
-      int64_t lr = rr;
-      if (GRAD && a.idx && !BIP) lr = a.idx[(int64_t)i * a.b + rr];
-      const T* xp = X + (row0 + lr) * ld;
-      yd = Y[row0 + lr];
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) {
-        const int c = lane + 64 * j;
-        if (VAR & 2048) {  // branch-free: lanes past the row re-read its last chunk (w, xb are 0 there)
-          const int cc = c < nch ? c : nch - 1;
-          dst[j] = (VAR & 1) ? __builtin_nontemporal_load((const V*)(xp + (int64_t)cc * VN))
-                             : *(const V*)(xp + (int64_t)cc * VN);
-        } else {
-          dst[j] = c < nch ? ((VAR & 1) ? __builtin_nontemporal_load((const V*)(xp + (int64_t)c * VN))
-                                        : *(const V*)(xp + (int64_t)c * VN))
-                           : V(0);
-        }
-      }
-    };
-    V cur[CPL], nxt[CPL];
-    T ycur = T(0), ynxt = T(0);
-    // VAR bit 13: hardware exp / log / reciprocal for the float logistic row terms
-    constexpr bool FAST = (VAR & 8192) && std::is_same<T, float>::value && PROB == 0;
-    auto process =[&](const V (&rv)[CPL], T yv, int64_t rr) {
-      const bool g_row = !BIP || bmask[rr] != 0;  // wave-uniform
-      V az = V(0), au = V(0);
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) {
-        if (compute_z && g_row) az += rv[j] * w[j];
-        if (compute_u) au += rv[j] * xb[j];
-      }
-      T z = hsum<T>(az), u = hsum<T>(au);
-      if (compute_z && g_row) z = (VAR & 2) ? wave_sum_dpp(z) : wave_sum(z);
-      if (compute_u) u = (VAR & 2) ? wave_sum_dpp(u) : wave_sum(u);
-      if (GRAD && g_row) {
-        T coef;
-        if constexpr (FAST) coef = -yv * sigmoid_neg_fast(yv * z);
-        else coef = (PROB == 0) ? -yv * sigmoid_neg(yv * z) : z - yv;
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) g[j] += coef * rv[j];
-      }
-      if constexpr (FAST) {
-        if (want_loss) loss += row_loss_fast(yv, loss_from_z ? z : u);
-        if (want_loss2) loss2 += row_loss_fast(yv, z);
-      } else {
-        if (want_loss) loss += row_loss<T, PROB>(yv, loss_from_z ? z : u);
-        if (want_loss2) loss2 += row_loss<T, PROB>(yv, z);
-      }
-    };
-    int64_t r = wave;
-    if (r < nrow) load_row(r, cur, ycur);
-    if (VAR & 4096) {
-      // peeled: every iteration issues the next row's loads unconditionally, so the compiler's
-      // wait before the current row's arithmetic only covers the current row (with the
-      // conditional load of the plain loop, the merged path waits for everything in flight)
-      for (; r + KW < nrow; r += KW) {
-        load_row(r + KW, nxt, ynxt);
-        process(cur, ycur, r);
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) cur[j] = nxt[j];
-        ycur = ynxt;
-      }
-      if (r < nrow) process(cur, ycur, r);
-    } else {
-      for (; r < nrow; r += KW) {
-        if (r + KW < nrow) load_row(r + KW, nxt, ynxt);
-        process(cur, ycur, r);
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) cur[j] = nxt[j];
-        ycur = ynxt;
-      }
-    }
-  }
-  if (!PIPE && (compute_z || compute_u)) {
-    for (int64_t r0 = (int64_t)wave * RB; r0 < nrow; r0 += KW * RB) {
-      V xr[RB][CPL];
-      T yv[RB];
-      bool g_row[RB];
-#pragma unroll
-      for (int k = 0; k < RB; ++k) {
-        const int64_t rr = r0 + k;
-        const bool ok = rr < nrow;
-        g_row[k] = ok && (!BIP || bmask[rr] != 0);
-        int64_t lr = rr;
-        if (GRAD && a.idx && ok && !BIP) lr = a.idx[(int64_t)i * a.b + rr];
-        const T* xp = X + (row0 + lr) * ld;
-        yv[k] = ok ? Y[row0 + lr] : T(0);
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) {
-          const int c = lane + 64 * j;
-          if (VAR & 1)
-            xr[k][j] = (ok && c < nch) ? __builtin_nontemporal_load((const V*)(xp + (int64_t)c * VN)) : V(0);
-          else
-            xr[k][j] = (ok && c < nch) ? *(const V*)(xp + (int64_t)c * VN) : V(0);
-        }
-      }
-      T z[RB], u[RB];
-#pragma unroll
-      for (int k = 0; k < RB; ++k) {
-        V az = V(0), au = V(0);
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) {
-          if (compute_z && (!BIP || g_row[k])) az += xr[k][j] * w[j];
-          if (compute_u) au += xr[k][j] * xb[j];
-        }
-        z[k] = hsum<T>(az);
-        u[k] = hsum<T>(au);
-      }
-#pragma unroll
-      for (int k = 0; k < RB; ++k) {
-        if (compute_z && (!BIP || g_row[k])) z[k] = (VAR & 2) ? wave_sum_dpp(z[k]) : wave_sum(z[k]);
-        if (compute_u) u[k] = (VAR & 2) ? wave_sum_dpp(u[k]) : wave_sum(u[k]);
-      }
-#pragma unroll
-      for (int k = 0; k < RB; ++k) {
-        if (r0 + k < nrow) {
-          if (GRAD && (!BIP || g_row[k])) {
-            const T coef = (PROB == 0) ? -yv[k] * sigmoid_neg(yv[k] * z[k]) : z[k] - yv[k];
-#pragma unroll
-            for (int j = 0; j < CPL; ++j) g[j] += coef * xr[k][j];
-          }
-          if (want_loss) loss += row_loss<T, PROB>(yv[k], loss_from_z ? z[k] : u[k]);
-          if (want_loss2) loss2 += row_loss<T, PROB>(yv[k], z[k]);
-        }
-      }
-    }
-  }
-
-  V* red = (V*)smem;  // [KW][nch]
-  double* sred = (double*)(smem + (GRAD ? (size_t)KW * nch * 16 : 0));  // 3*KW doubles (KSRED bytes)
-  if (GRAD) {
-#pragma unroll
-    for (int j = 0; j < CPL; ++j) {
-      const int c = lane + 64 * j;
-      if (c < nch) red[wave * nch + c] = g[j];
-    }
-  }
-  if (MET) {
-    double cons = 0.0;
-    if (want_cons && wave == 0) {  // every wave holds the whole iterate: count it once
-      V dv = V(0);
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) {
-        const V t = w[j] - xb[j];
-        dv += t * t;
-      }
-      cons = wave_sum((double)hsum<T>(dv));
-    }
-    if (lane == 0) {
-      sred[wave] = cons;
-      sred[KW + wave] = loss;
-      sred[2 * KW + wave] = loss2;
-    }
-  }
-  __syncthreads();
-
-  if (GRAD) {
-    const T inv_eta = (T)a.eta;
-    const T lam = (T)a.lam;
-    for (int c = threadIdx.x; c < nch; c += KT) {
-      V s = red[c];
-#pragma unroll
-      for (int q = 1; q < KW; ++q) s += red[q * nch + c];  // fixed order
-      const V wc = *(const V*)(wsrc + (int64_t)c * VN);
-      const V gc = (flags & F_GSUM) ? s : ((nb > 0) ? (s / (T)nb + lam * wc) : V(0));
-      if (flags & F_STEP) {
-        V acc = V(0);
-        if (pre) {
-          for (int64_t e = pe0; e < pe1; ++e) acc += ((const T*)a.cw)[e] * nbuf[(e - pe0) * nch + c];
-        } else {
-          acc = mix_chunk<T>(a, i, c, wc);
-        }
-        *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = acc - inv_eta * gc;
-      } else if (flags & F_GOUT) {
-        *(V*)((T*)a.g_out + (int64_t)i * ld + (int64_t)c * VN) = gc;
-      }
-    }
-  }
-  if (MET && threadIdx.x == 0) {
-    double cs = 0.0, ls = 0.0, l2 = 0.0;
-#pragma unroll
-    for (int q = 0; q < KW; ++q) {
-      cs += sred[q];
-      ls += sred[KW + q];
-      l2 += sred[2 * KW + q];
-    }
-    if (want_cons) a.slab_cons[i] = cs;
-    if (want_loss) a.slab_loss[i] = ls;
-    if (want_loss2) a.slab_loss2[i] = l2;
-  }
-  if (VAR & 8) __syncthreads();  // LDS of this worker's epilogue is reused by the next
-  }
-}
-
-template <typename T, int CPL, int PROB, bool GRAD, bool MET, int VAR = KR_DEFAULT_VAR>
-static hipError_t launch_round_t(const RoundArgs& a, int groups, hipStream_t s) {
-  const size_t pre = (VAR & 16) ? (size_t)a.pre_rows * a.nchunks * 16 : 0;
-  const size_t bip = (VAR & 64) ? ((size_t)a.bip_rows + 15) / 16 * 16 : 0;  // minibatch byte map
-  constexpr int KW = (VAR & 512) ? 4 * NW : (VAR & 256) ? 2 * NW : NW;
-  constexpr size_t KSRED = 3 * KW * 8;
-  const size_t lds = (GRAD ? (size_t)KW * a.nchunks * 16 + KSRED + pre + bip : KSRED);
-  static bool attr_set = false;
-  if (!attr_set) {
-    const size_t max_lds = 160 * 1024;
-    hipError_t e = hipFuncSetAttribute((const void*)k_round<T, CPL, PROB, GRAD, MET, VAR>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  const int grid = (VAR & 8) ? (groups < 1024 ? groups : 1024) : groups;  // 4 workgroups per CU
-  hipLaunchKernelGGL((k_round<T, CPL, PROB, GRAD, MET, VAR>), dim3(grid), dim3(KW * 64), lds, s, a);
-  return hipGetLastError();
-}
-
-// Tuning variants of the C3 kernel (float, 4 chunks per lane, logistic), selected by
-// DOPT_KR_VARIANT for in-process A/B runs (tools/kr_variants.py).
-template <bool GRAD, bool MET>
-static hipError_t dispatch_variant(int var, const RoundArgs& a, int groups, hipStream_t s) {
-  switch (var) {
-    case 1: return launch_round_t<float, 4, 0, GRAD, MET, 1>(a, groups, s);
-    case 2: return launch_round_t<float, 4, 0, GRAD, MET, 2>(a, groups, s);
-    case 3: return launch_round_t<float, 4, 0, GRAD, MET, 3>(a, groups, s);
-    case 4: return launch_round_t<float, 4, 0, GRAD, MET, 4>(a, groups, s);
-    case 6: return launch_round_t<float, 4, 0, GRAD, MET, 6>(a, groups, s);
-    case 7: return launch_round_t<float, 4, 0, GRAD, MET, 7>(a, groups, s);
-    case 11: return launch_round_t<float, 4, 0, GRAD, MET, 11>(a, groups, s);
-    case 19: return launch_round_t<float, 4, 0, GRAD, MET, 19>(a, groups, s);
-    case 0: return launch_round_t<float, 4, 0, GRAD, MET, 0>(a, groups, s);
-    case 35: return launch_round_t<float, 4, 0, GRAD, MET, 35>(a, groups, s);
-    case 291: return launch_round_t<float, 4, 0, GRAD, MET, 291>(a, groups, s);
-    case 547: return launch_round_t<float, 4, 0, GRAD, MET, 547>(a, groups, s);
-    case 2339: return launch_round_t<float, 4, 0, GRAD, MET, 2339>(a, groups, s);
-    case 2083: return launch_round_t<float, 4, 0, GRAD, MET, 2083>(a, groups, s);
-    case 4387: return launch_round_t<float, 4, 0, GRAD, MET, 4387>(a, groups, s);
-    case 6435: return launch_round_t<float, 4, 0, GRAD, MET, 6435>(a, groups, s);
-    case 14627: return launch_round_t<float, 4, 0, GRAD, MET, 14627>(a, groups, s);
-    default: return launch_round_t<float, 4, 0, GRAD, MET>(a, groups, s);
-  }
-}
-
-static int kr_variant() {  // -1: the default build
-  const char* v = getenv("DOPT_KR_VARIANT");
-  return v ? atoi(v) : -1;
-}
-
-template <typename T, int CPL, int PROB>
-static hipError_t dispatch_mode(bool grad, bool met, const RoundArgs& a, int groups, hipStream_t s) {
-  if constexpr (std::is_same<T, float>::value && CPL == 4 && PROB == 0) {
-    const int var = kr_variant();
-    if (var >= 0 && var != kr_default_var<CPL>()) {
-      if (grad && met) return dispatch_variant<true, true>(var, a, groups, s);
-      if (grad) return dispatch_variant<true, false>(var, a, groups, s);
-    }
-  }
-  constexpr int DV = kr_default_var<CPL>();
-  if constexpr (CPL <= 4) {
-    // Fewer workers than CUs (C1 / C2 / main.py: 10-25 workers of 500 rows): a launch is
-    // one workgroup per worker streaming its rows, so its time is the per-row latency
-    // chain, not bandwidth: 16 waves (VAR bit 9), each with RB-row blocks in flight (the
-    // plain loop, not the 1-row software pipeline: bits 5 / 12 off) -- 4x the rows
-    // in flight per worker of the default.
-    static const bool wide_off = [] {
-      const char* v = getenv("DOPT_KR_FEW_WIDE");
-      return v && atoi(v) == 0;
-    }();
-    if (groups < 256 && !wide_off) {
-      constexpr int WV = (DV & ~(32 | 4096)) | 512;
-      if (grad && met && (a.flags & F_BIP)) return launch_round_t<T, CPL, PROB, true, true, WV | 64>(a, groups, s);
-      if (grad && met) return launch_round_t<T, CPL, PROB, true, true, WV>(a, groups, s);
-      if (grad) return launch_round_t<T, CPL, PROB, true, false, WV>(a, groups, s);
-    }
-  }
-  if (grad && met && (a.flags & F_BIP)) return launch_round_t<T, CPL, PROB, true, true, DV | 64>(a, groups, s);
-  if (grad && met) return launch_round_t<T, CPL, PROB, true, true, DV>(a, groups, s);
-  if (grad) return launch_round_t<T, CPL, PROB, true, false, DV>(a, groups, s);
-  if (met) return launch_round_t<T, CPL, PROB, false, true, DV>(a, groups, s);
-  return hipErrorInvalidValue;
-}
-
-template <typename T, int PROB>
-static hipError_t dispatch_cpl(int cpl, bool grad, bool met, const RoundArgs& a, int groups,
-                               hipStream_t s) {
-  switch (cpl) {
-    case 1: return dispatch_mode<T, 1, PROB>(grad, met, a, groups, s);
-    case 2: return dispatch_mode<T, 2, PROB>(grad, met, a, groups, s);
-    case 4: return dispatch_mode<T, 4, PROB>(grad, met, a, groups, s);
-    case 8: return dispatch_mode<T, 8, PROB>(grad, met, a, groups, s);
-    case 16: return dispatch_mode<T, 16, PROB>(grad, met, a, groups, s);
-  }
-  return hipErrorInvalidValue;
-}
-
-hipError_t launch_round(int dtype, int problem, int cpl, bool grad, bool met, const RoundArgs& a,
+// The fused round kernel lives in k_round.inc (one translation unit per element-type pair).
+hipError_t launch_round(int dtype, int xdtype, int problem, int cpl, bool grad, bool met, const RoundArgs& a,
                         int n_groups, hipStream_t s) {
   if (n_groups <= 0) return hipSuccess;
-  if (dtype == 0)
-    return problem == 0 ? dispatch_cpl<float, 0>(cpl, grad, met, a, n_groups, s)
-                        : dispatch_cpl<float, 1>(cpl, grad, met, a, n_groups, s);
-  return problem == 0 ? dispatch_cpl<double, 0>(cpl, grad, met, a, n_groups, s)
-                      : dispatch_cpl<double, 1>(cpl, grad, met, a, n_groups, s);
+  if (dtype == 0) return launch_round_f32(problem, cpl, grad, met, a, n_groups, s);
+  if (xdtype == 0) return launch_round_x32(problem, cpl, grad, met, a, n_groups, s);
+  return launch_round_f64(problem, cpl, grad, met, a, n_groups, s);
 }
 
-int max_chunks_per_lane() { return MAX_CPL; }
+int max_chunks_per_lane(int dtype, int xdtype) { return (dtype == 1 && xdtype == 0) ? 8 : MAX_CPL; }
+
 
 
 // ---------------------------------------------------------------------------- large d
@@ -761,7 +183,7 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
       if (gout) {
         if (wave == 0 && in) *(V*)((T*)a.g_out + (int64_t)i * ld + (int64_t)c * VN) = g;
       } else if (in) {
-        xn = mix_chunk<T>(a, i, c, own[j]) - inv_eta * g;
+        xn = mix_chunk<T, T>(a, i, c, own[j]) - inv_eta * g;
         if (wave == 0) *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = xn;
       }
       if (ZNEXT) {
@@ -1410,7 +832,7 @@ __global__ __launch_bounds__(NT) void k_mix(const RoundArgs a, const T* __restri
   if (a.flags & F_MEAN) {
 #pragma unroll
     for (int j = 0; j < CPL; ++j)
-      if (lane + 64 * j < nch) acc[j] = mix_chunk<T>(a, i, lane + 64 * j, own[j]);
+      if (lane + 64 * j < nch) acc[j] = mix_chunk<T, T>(a, i, lane + 64 * j, own[j]);
   } else {
     const int64_t e0 = a.rp[i], e1 = a.rp[i + 1];
     auto row_of = [&](int64_t e) {

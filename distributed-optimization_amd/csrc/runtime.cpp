@@ -66,14 +66,17 @@ int fail(int code, const char* fmt, ...) {
 constexpr size_t kStaging = 64ull << 20;  // host->device staging chunk
 constexpr int kRowsPerGroup = 64;         // column-sum partial group height (16 rows per wave)
 constexpr int64_t kLossChunk = 64;        // objective rows per workgroup in a separate metrics pass
+constexpr int64_t kDeferRows = 1024;      // rows per workgroup whose loss terms k_round may defer (LDS)
 
 }  // namespace
 
 struct dopt_ctx {
   int device = 0;
-  int dtype = DOPT_F64;
+  int dtype = DOPT_F64;   // iterates and arithmetic
   size_t esz = 8;
-  int vn = 2;  // elements per 16-byte vector
+  int xdtype = DOPT_F64;  // shard storage (dopt_set_data_dtype): float32 rows under float64 arithmetic
+  size_t xesz = 8;
+  int vn = 2;  // data elements per 16-byte vector (a "chunk"; the state chunk has as many elements)
   hipStream_t stream = nullptr;      // the stream every launch goes to
   hipStream_t own_stream = nullptr;  // created by dopt_create; dopt_set_stream may override
   double clock_hz = 1e8;
@@ -83,6 +86,8 @@ struct dopt_ctx {
   int problem = DOPT_LOGISTIC;
   int64_t n = 0, d = 0, ld = 0, nch = 0, rows = 0, max_m = 0;
   int cpl = 1;
+  int64_t nchs = 0;  // 16-byte chunks of a STATE row (= nch unless float32 data under float64 state)
+  int cpls = 1;      // ... and per lane (k_mix)
   bool split = false;  // d too long for the row-resident kernel: column-blocked rounds
   int split_groups = 1;
   void* X = nullptr;
@@ -252,16 +257,17 @@ int upload_rows(dopt_ctx* c, int dtype, const void* src, int src_f32, void* dst,
 }
 
 // Device T [rows x ld] -> host float64 [rows x d].
-int download_rows(dopt_ctx* c, const void* src, double* dst, int64_t rows, int64_t d, int64_t ld) {
+int download_rows(dopt_ctx* c, int edtype, const void* src, double* dst, int64_t rows, int64_t d, int64_t ld) {
   if (rows == 0) return DOPT_OK;
-  std::vector<char> tmp((size_t)(rows * ld) * c->esz);
+  const size_t esz = edtype == DOPT_F32 ? 4 : 8;
+  std::vector<char> tmp((size_t)(rows * ld) * esz);
   HIPOK(hipMemcpyAsync(tmp.data(), src, tmp.size(), hipMemcpyDeviceToHost, c->stream));
   HIPOK(hipStreamSynchronize(c->stream));
   for (int64_t r = 0; r < rows; ++r)
     for (int64_t k = 0; k < d; ++k) {
       const int64_t s = r * ld + k;
-      dst[r * d + k] = c->dtype == DOPT_F32 ? (double)((const float*)tmp.data())[s]
-                                            : ((const double*)tmp.data())[s];
+      dst[r * d + k] = edtype == DOPT_F32 ? (double)((const float*)tmp.data())[s]
+                                          : ((const double*)tmp.data())[s];
     }
   return DOPT_OK;
 }
@@ -324,7 +330,10 @@ int set_layout(dopt_ctx* c, int problem, int64_t n, int64_t d) {
   const int64_t ld = (d + c->vn - 1) / c->vn * c->vn;
   const int64_t nch = ld / c->vn;
   const int cpl = cpl_for(nch);
-  c->split = cpl > max_chunks_per_lane();
+  c->split = cpl > max_chunks_per_lane(c->dtype, c->xdtype);
+  if (c->split && c->xdtype != c->dtype)
+    return fail(DOPT_ERR_UNSUPPORTED, "float32 shard storage under float64 arithmetic: rows of at most %d "
+                "elements (d = %lld); store the rows as float64", 64 * 8 * c->vn, (long long)d);
   if (c->split) {  // enough workgroups to fill 256 CUs several times over
     const int64_t nblk = (nch + 63) / 64;
     const char* gw = getenv("DOPT_SPLIT_WGS");  // A/B knob: target workgroups per column-blocked launch
@@ -339,6 +348,8 @@ int set_layout(dopt_ctx* c, int problem, int64_t n, int64_t d) {
   c->ld = ld;
   c->nch = nch;
   c->cpl = cpl;
+  c->nchs = ld * (int64_t)c->esz / 16;
+  c->cpls = cpl_for(c->nchs);
   c->have_topo = false;
   c->obj_sep = false;
   c->n_global = c->rows_global = 0;
@@ -404,6 +415,8 @@ RoundArgs base_args(dopt_ctx* c) {
   a.pre_rows = (c->max_row_nnz <= 6 && !c->mean_mix) ? c->max_row_nnz : 0;
   a.groups = c->split_groups;
   a.bip_rows = (int32_t)std::min<int64_t>(c->max_m, kMaxBipRows);
+  // worker launches: every workgroup holds one shard (launches over 64-row chunks set kLossChunk)
+  a.defer_rows = (c->max_m > 0 && c->max_m <= kDeferRows) ? (int32_t)c->max_m : 0;
   return a;
 }
 
@@ -422,8 +435,9 @@ int metrics_pass(dopt_ctx* c, const void* x_state, const void* point, bool share
     a.off = c->obj_sep ? c->choff_o : c->choff;
     a.w_shared = point;
     a.flags |= F_LOSS | F_SHARED | F_LOSS_FROM_Z;
+    a.defer_rows = (int32_t)kLossChunk;  // 64-row chunks
     const int64_t nc = c->obj_sep ? c->n_chunks_o : c->n_chunks;
-    HIPOK(launch_round(c->dtype, c->problem, c->cpl, false, true, a, (int)nc, c->stream));
+    HIPOK(launch_round(c->dtype, c->xdtype, c->problem, c->cpl, false, true, a, (int)nc, c->stream));
     c->loss_groups = nc;
   }
   if (cons) {
@@ -431,7 +445,7 @@ int metrics_pass(dopt_ctx* c, const void* x_state, const void* point, bool share
     a.x_old = x_state;
     a.xbar = point;
     a.flags |= F_CONS;
-    HIPOK(launch_round(c->dtype, c->problem, c->cpl, false, true, a, (int)c->n, c->stream));
+    HIPOK(launch_round(c->dtype, c->xdtype, c->problem, c->cpl, false, true, a, (int)c->n, c->stream));
   }
   return DOPT_OK;
 }
@@ -462,7 +476,7 @@ void finalize_metrics(const double* raw, int64_t T, int problem, int64_t n, int6
 // nc: valid consensus slab entries (c->n per-worker partials, or per column block)
 int history(dopt_ctx* c, int64_t h, const void* point, bool cons, bool loss, int64_t nc) {
   HIPOK(launch_history(c->dtype, cons ? c->slab_cons : nullptr, loss ? c->slab_loss : nullptr, nc,
-                       c->loss_groups, point, c->ld, (int32_t)c->nch, loss, c->hraw + 3 * h, c->stream));
+                       c->loss_groups, point, c->ld, (int32_t)c->nchs, loss, c->hraw + 3 * h, c->stream));
   return DOPT_OK;
 }
 
@@ -515,7 +529,7 @@ int64_t idx_chunk_rounds(dopt_ctx* c, int64_t T, int64_t b) {
 
 // xbar[xb] and S of the current iterates (run prologue).
 int colsum_current(dopt_ctx* c) {
-  HIPOK(launch_colsum(c->dtype, c->xs[c->cur], c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part, nullptr,
+  HIPOK(launch_colsum(c->dtype, c->xs[c->cur], c->n, c->ld, (int32_t)c->nchs, kRowsPerGroup, c->part, nullptr,
                       n_div(c), c->xbar[c->xb], nullptr, 0.0, 0, c->stream, c->S, nullptr));
   return refresh_sums_t(c);
 }
@@ -608,9 +622,9 @@ int run_dsgd_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batc
       q.idx = nullptr;
       HIPOK(launch_split_coef(c->dtype, c->problem, (full ? 1 : 0) | (met ? 2 : 0), q, (int)c->n, c->stream));
     }
-    HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur ^ 1], c->n, c->ld, (int32_t)c->nch, kRowsPerGroup,
+    HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur ^ 1], c->n, c->ld, (int32_t)c->nchs, kRowsPerGroup,
                                 c->part, c->stamps + h + 1, c->stream));
-    HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, n_div(c), c->ld, (int32_t)c->nch, c->xbar[xb ^ 1],
+    HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, n_div(c), c->ld, (int32_t)c->nchs, c->xbar[xb ^ 1],
                               nullptr, 0.0, 0, c->stream, c->S));
     if ((rc = refresh_sums_t(c))) return rc;
     if (met) {
@@ -661,9 +675,9 @@ int run_centralized_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64
     if (c->prof && (rc = prof_event(c, false))) return rc;
     HIPOK(launch_split_step(c->dtype, false, false, a, (int)c->n, c->stream));
     if (c->prof && (rc = prof_event(c, true))) return rc;
-    HIPOK(launch_colsum_partial(c->dtype, c->G, c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part,
+    HIPOK(launch_colsum_partial(c->dtype, c->G, c->n, c->ld, (int32_t)c->nchs, kRowsPerGroup, c->part,
                                 c->stamps + h + 1, c->stream));
-    HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nch, c->xg[c->gcur ^ 1],
+    HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nchs, c->xg[c->gcur ^ 1],
                               c->xg[c->gcur], eta0 / sqrt((double)(t + 1)), 1, c->stream));
     if (want_obj) {
       if ((rc = split_metrics(c, nullptr, c->xg[c->gcur ^ 1], true, false, true))) return rc;
@@ -735,6 +749,8 @@ int dopt_create(int device, int dtype, dopt_ctx** out) {
   c->device = device;
   c->dtype = dtype;
   c->esz = dtype == DOPT_F32 ? 4 : 8;
+  c->xdtype = dtype;
+  c->xesz = c->esz;
   c->vn = dtype == DOPT_F32 ? 4 : 2;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
@@ -747,6 +763,25 @@ int dopt_create(int device, int dtype, dopt_ctx** out) {
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
     c->clock_hz = (double)khz * 1e3;
   *out = c;
+  return DOPT_OK;
+}
+
+int dopt_set_data_dtype(dopt_ctx* c, int xdtype) {
+  CHECK_ARG(c, "ctx is NULL");
+  CHECK_ARG(xdtype == c->dtype || (c->dtype == DOPT_F64 && xdtype == DOPT_F32),
+            "data dtype %d with compute dtype %d: the shards are stored in the compute dtype, or as float32 "
+            "under float64 arithmetic", xdtype, c->dtype);
+  c->xdtype = xdtype;
+  c->xesz = xdtype == DOPT_F32 ? 4 : 8;
+  c->vn = (int)(16 / c->xesz);
+  c->have_data = false;  // the layout changes: load / generate the shards again
+  c->have_topo = false;
+  return DOPT_OK;
+}
+
+int dopt_get_data_dtype(dopt_ctx* c, int* xdtype) {
+  CHECK_ARG(c && xdtype, "NULL argument");
+  *xdtype = c->xdtype;
   return DOPT_OK;
 }
 
@@ -804,12 +839,12 @@ int dopt_load_shards(dopt_ctx* c, int problem, int64_t n_workers, int64_t d, con
   c->rows = rows;
   c->max_m = max_m;
   c->off_h.assign(off, off + n_workers + 1);
-  if ((rc = dalloc(&c->X, (size_t)rows * c->ld * c->esz))) return rc;
-  if ((rc = dalloc(&c->y, (size_t)rows * c->esz))) return rc;
+  if ((rc = dalloc(&c->X, (size_t)rows * c->ld * c->xesz))) return rc;
+  if ((rc = dalloc(&c->y, (size_t)rows * c->xesz))) return rc;
   if ((rc = dalloc_t(&c->off, (size_t)(n_workers + 1) * sizeof(int64_t)))) return rc;
   HIPOK(hipMemcpy(c->off, off, (size_t)(n_workers + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
-  if ((rc = upload_rows(c, c->dtype, X, src_f32, c->X, rows, d, c->ld))) return rc;
-  if ((rc = upload_rows(c, c->dtype, y, src_f32, c->y, rows, 1, 1))) return rc;
+  if ((rc = upload_rows(c, c->xdtype, X, src_f32, c->X, rows, d, c->ld))) return rc;
+  if ((rc = upload_rows(c, c->xdtype, y, src_f32, c->y, rows, 1, 1))) return rc;
   if ((rc = alloc_state(c))) return rc;
   c->have_data = true;
   return DOPT_OK;
@@ -828,13 +863,13 @@ int dopt_generate_shards(dopt_ctx* c, int problem, int64_t n_workers, int64_t d,
   c->max_m = rpw;
   c->off_h.resize((size_t)n_workers + 1);
   for (int64_t i = 0; i <= n_workers; ++i) c->off_h[(size_t)i] = i * rpw;
-  if ((rc = dalloc(&c->X, (size_t)rows * c->ld * c->esz))) return rc;
-  if ((rc = dalloc(&c->y, (size_t)rows * c->esz))) return rc;
+  if ((rc = dalloc(&c->X, (size_t)rows * c->ld * c->xesz))) return rc;
+  if ((rc = dalloc(&c->y, (size_t)rows * c->xesz))) return rc;
   if ((rc = dalloc_t(&c->off, (size_t)(n_workers + 1) * sizeof(int64_t)))) return rc;
   HIPOK(hipMemcpy(c->off, c->off_h.data(), (size_t)(n_workers + 1) * sizeof(int64_t),
                   hipMemcpyHostToDevice));
   CHECK_ARG(first_worker >= 0, "first_worker must be >= 0");
-  HIPOK(launch_generate(c->dtype, problem, c->X, c->y, rows, d, c->ld, seed, flip, noise, first_worker * rpw,
+  HIPOK(launch_generate(c->xdtype, problem, c->X, c->y, rows, d, c->ld, seed, flip, noise, first_worker * rpw,
                         c->stream));
   HIPOK(hipStreamSynchronize(c->stream));
   if ((rc = alloc_state(c))) return rc;
@@ -849,10 +884,10 @@ int dopt_load_objective_data(dopt_ctx* c, int64_t n_rows, const void* X, const v
   CHECK_ARG(n_rows == 0 || (X && y), "X / y are NULL");
   int rc;
   if ((rc = set_device(c))) return rc;
-  if ((rc = dalloc(&c->Xo, (size_t)n_rows * c->ld * c->esz))) return rc;
-  if ((rc = dalloc(&c->yo, (size_t)n_rows * c->esz))) return rc;
-  if ((rc = upload_rows(c, c->dtype, X, src_f32, c->Xo, n_rows, c->d, c->ld))) return rc;
-  if ((rc = upload_rows(c, c->dtype, y, src_f32, c->yo, n_rows, 1, 1))) return rc;
+  if ((rc = dalloc(&c->Xo, (size_t)n_rows * c->ld * c->xesz))) return rc;
+  if ((rc = dalloc(&c->yo, (size_t)n_rows * c->xesz))) return rc;
+  if ((rc = upload_rows(c, c->xdtype, X, src_f32, c->Xo, n_rows, c->d, c->ld))) return rc;
+  if ((rc = upload_rows(c, c->xdtype, y, src_f32, c->yo, n_rows, 1, 1))) return rc;
   // split the objective rows over the N metric workgroups (array_split sizes)
   std::vector<int64_t> o((size_t)c->n + 1);
   const int64_t q = n_rows / c->n, r = n_rows % c->n;
@@ -881,9 +916,9 @@ int dopt_get_shard(dopt_ctx* c, int64_t worker, double* X_out, double* y_out) {
   int rc;
   if ((rc = set_device(c))) return rc;
   const int64_t r0 = c->off_h[(size_t)worker], nr = c->off_h[(size_t)worker + 1] - r0;
-  if (X_out && (rc = download_rows(c, (const char*)c->X + r0 * c->ld * (int64_t)c->esz, X_out, nr, c->d, c->ld)))
+  if (X_out && (rc = download_rows(c, c->xdtype, (const char*)c->X + r0 * c->ld * (int64_t)c->xesz, X_out, nr, c->d, c->ld)))
     return rc;
-  if (y_out && (rc = download_rows(c, (const char*)c->y + r0 * (int64_t)c->esz, y_out, nr, 1, 1))) return rc;
+  if (y_out && (rc = download_rows(c, c->xdtype, (const char*)c->y + r0 * (int64_t)c->xesz, y_out, nr, 1, 1))) return rc;
   return DOPT_OK;
 }
 
@@ -957,7 +992,7 @@ int dopt_get_models(dopt_ctx* c, double* x) {
   if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");
   int rc;
   if ((rc = set_device(c))) return rc;
-  return download_rows(c, c->xs[c->cur], x, c->n, c->d, c->ld);
+  return download_rows(c, c->dtype, c->xs[c->cur], x, c->n, c->d, c->ld);
 }
 
 int dopt_set_global(dopt_ctx* c, const double* x) {
@@ -973,7 +1008,7 @@ int dopt_get_global(dopt_ctx* c, double* x) {
   if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");
   int rc;
   if ((rc = set_device(c))) return rc;
-  return download_rows(c, c->xg[c->gcur], x, 1, c->d, c->ld);
+  return download_rows(c, c->dtype, c->xg[c->gcur], x, 1, c->d, c->ld);
 }
 
 int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch, const int32_t* idx,
@@ -999,10 +1034,11 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
   const bool fused = !few_split && (batch >= c->max_m || bip) && !c->obj_sep;
   // separate metrics with <= 64 workers: the consensus rides the one-launch column sums
   // (per column block partials; one metrics launch less per round)
-  const int64_t cs_blocks = (c->nch + 63) / 64;
+  const int64_t cs_blocks = (c->nchs + 63) / 64;
   const char* two = getenv("DOPT_COLSUM_TWO");  // the two-stage column sums carry no consensus
+  const char* ccs = getenv("DOPT_CONS_CS");     // A/B knob: 0 = consensus from the metrics pass instead
   const bool cons_cs = !fused && want_cons && c->n <= kRowsPerGroup && cs_blocks <= c->slab_cap && !c->split &&
-                       !(two && atoi(two) != 0);
+                       !(two && atoi(two) != 0) && !(ccs && ccs[0] == '0');
   const int64_t CH = idx ? idx_chunk_rounds(c, T, batch) : 1;
   int& xb = c->xb;
   if (c->split) return run_dsgd_split(c, t0, T, eta0, batch, idx, lam_grad, lam_obj, f_opt, flags, obj_out,
@@ -1031,14 +1067,14 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
     a.wid0 = c->sample_wid0;
     if (a.flags & F_LOSS) c->loss_groups = c->n;  // per-worker loss slabs
     if (c->prof && (rc = prof_event(c, false))) return rc;
-    HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, met || dev, a, (int)c->n, c->stream));
+    HIPOK(launch_round(c->dtype, c->xdtype, c->problem, c->cpl, true, met || dev, a, (int)c->n, c->stream));
     if (c->prof && (rc = prof_event(c, true))) return rc;
     // xbar_{t+1} (trainer.py:182); the stamp marks the end of round t's update (trainer.py:181)
     // history[h-1] (this round's fused partials of x_h at xbar_h) rides the same launch
     double* hr = met ? c->hraw + 3 * (h - 1) : c->hraw;
     const FoldArgs fold = {want_cons ? c->slab_cons : nullptr, c->n, want_obj ? c->slab_loss : nullptr,
                            c->loss_groups, want_obj ? c->xbar[xb] : nullptr, hr, hr + 1, hr + 2};
-    HIPOK(launch_colsum(c->dtype, c->xs[c->cur ^ 1], c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part,
+    HIPOK(launch_colsum(c->dtype, c->xs[c->cur ^ 1], c->n, c->ld, (int32_t)c->nchs, kRowsPerGroup, c->part,
                         c->stamps + h + 1, n_div(c), c->xbar[xb ^ 1], nullptr, 0.0, 0, c->stream, c->S,
                         met ? &fold : nullptr, cons_cs ? c->slab_cons : nullptr));
     if ((rc = refresh_sums_t(c))) return rc;
@@ -1090,10 +1126,10 @@ int dopt_run_centralized(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_
     a.flags |= F_GOUT | F_SHARED | (met ? (F_LOSS | F_LOSS_FROM_Z) : 0);
     if (a.flags & F_LOSS) c->loss_groups = c->n;  // per-worker loss slabs
     if (c->prof && (rc = prof_event(c, false))) return rc;
-    HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, met, a, (int)c->n, c->stream));
+    HIPOK(launch_round(c->dtype, c->xdtype, c->problem, c->cpl, true, met, a, (int)c->n, c->stream));
     if (c->prof && (rc = prof_event(c, true))) return rc;
     // mean of the worker gradients and the step (trainer.py:53-57)
-    HIPOK(launch_colsum(c->dtype, c->G, c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part, c->stamps + h + 1,
+    HIPOK(launch_colsum(c->dtype, c->G, c->n, c->ld, (int32_t)c->nchs, kRowsPerGroup, c->part, c->stamps + h + 1,
                         c->n, c->xg[c->gcur ^ 1], c->xg[c->gcur], eta0 / sqrt((double)(t + 1)), 1, c->stream,
                         nullptr, nullptr));
     if (met) {
@@ -1125,7 +1161,7 @@ int eval_common(dopt_ctx* c, int problem, int64_t rows, int64_t d, const double*
   const int vn = 2;  // float64
   const int64_t ld = (d + vn - 1) / vn * vn, nch = ld / vn;
   const int cpl = cpl_for(nch);
-  if (cpl > max_chunks_per_lane())
+  if (cpl > max_chunks_per_lane(DOPT_F64, DOPT_F64))
     return fail(DOPT_ERR_UNSUPPORTED, "d = %lld exceeds the row-resident kernel limit", (long long)d);
   // objective: split rows over workgroups; gradient: one workgroup (one worker)
   const int64_t groups = grad ? 1 : std::max<int64_t>(1, std::min<int64_t>(4096, (rows + 255) / 256));
@@ -1167,14 +1203,14 @@ int eval_common(dopt_ctx* c, int problem, int64_t rows, int64_t d, const double*
   a.slab_loss = dslab;
   if (grad) {
     a.flags = F_GOUT | F_SHARED;
-    HIPOK(launch_round(DOPT_F64, problem, cpl, true, false, a, 1, c->stream));
+    HIPOK(launch_round(DOPT_F64, DOPT_F64, problem, cpl, true, false, a, 1, c->stream));
     std::vector<double> g((size_t)ld);
     HIPOK(hipMemcpyAsync(g.data(), dg, (size_t)ld * 8, hipMemcpyDeviceToHost, c->stream));
     HIPOK(hipStreamSynchronize(c->stream));
     memcpy(out, g.data(), (size_t)d * sizeof(double));
   } else {
     a.flags = F_SHARED | F_LOSS | F_LOSS_FROM_Z;
-    HIPOK(launch_round(DOPT_F64, problem, cpl, false, true, a, (int)groups, c->stream));
+    HIPOK(launch_round(DOPT_F64, DOPT_F64, problem, cpl, false, true, a, (int)groups, c->stream));
     HIPOK(launch_history(DOPT_F64, nullptr, dslab, 1, groups, dw, ld, (int32_t)nch, true, dout, c->stream));
     double raw[3];
     HIPOK(hipMemcpyAsync(raw, dout, sizeof(raw), hipMemcpyDeviceToHost, c->stream));
@@ -1209,19 +1245,20 @@ int dopt_eval_full(dopt_ctx* c, const double* w, double reg, double* f_out, doub
     a.X = c->Xo;
     a.y = c->yo;
     a.off = c->offo;
+    a.defer_rows = 0;  // rows per workgroup of the objective split, not of the shards
   }
   a.w_shared = c->xg[c->gcur ^ 1];
   a.g_out = c->G;
   a.flags = F_GOUT | F_GSUM | F_SHARED | F_LOSS | F_LOSS_FROM_Z;
-  HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, true, a, (int)c->n, c->stream));
+  HIPOK(launch_round(c->dtype, c->xdtype, c->problem, c->cpl, true, true, a, (int)c->n, c->stream));
   c->loss_groups = c->n;  // per-worker loss slabs
-  HIPOK(launch_colsum_partial(c->dtype, c->G, c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part, nullptr,
+  HIPOK(launch_colsum_partial(c->dtype, c->G, c->n, c->ld, (int32_t)c->nchs, kRowsPerGroup, c->part, nullptr,
                               c->stream));
   if ((rc = history(c, 0, a.w_shared, false, true, c->n))) return rc;
   std::vector<double> colsum((size_t)c->ld), raw(3);
   double* dsum = nullptr;
   if ((rc = dalloc_t(&dsum, (size_t)c->ld * sizeof(double)))) return rc;
-  hipError_t e = launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nch, nullptr, nullptr,
+  hipError_t e = launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nchs, nullptr, nullptr,
                                      0.0, 0, c->stream, dsum);
   if (e == hipSuccess) e = hipMemcpyAsync(colsum.data(), dsum, (size_t)c->ld * sizeof(double), hipMemcpyDeviceToHost,
                                           c->stream);
@@ -1339,7 +1376,7 @@ int dopt_phase_gather(dopt_ctx* c) {
   CHECK_ARG(c, "ctx is NULL");
   if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
   if (c->send_fresh) return DOPT_OK;  // the last mix wrote these rows already
-  HIPOK(launch_gather_rows(c->dtype, c->xs[c->cur], c->send_ids, c->n_send, c->ld, (int32_t)c->nch, c->send,
+  HIPOK(launch_gather_rows(c->dtype, c->xs[c->cur], c->send_ids, c->n_send, c->ld, (int32_t)c->nchs, c->send,
                            c->stream));
   return DOPT_OK;
 }
@@ -1404,7 +1441,7 @@ int dopt_phase_grad(dopt_ctx* c, int64_t batch, const int32_t* idx, double lam_g
   a.wid0 = c->sample_wid0;
   if (a.flags & F_LOSS) c->loss_groups = c->slab_n[0] = c->n;  // per-worker loss slabs
   if (c->prof && (rc = prof_event(c, false))) return rc;
-  HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, cons || loss || dev, a, (int)c->n, c->stream));
+  HIPOK(launch_round(c->dtype, c->xdtype, c->problem, c->cpl, true, cons || loss || dev, a, (int)c->n, c->stream));
   if (c->prof && (rc = prof_event(c, true))) return rc;
   return DOPT_OK;
 }
@@ -1443,7 +1480,8 @@ int dopt_phase_mix(dopt_ctx* c, int64_t t, double eta0) {
       a.sslot = c->sslot;
       a.send = c->send;
     }
-    HIPOK(launch_mix(c->dtype, c->cpl, a, c->G, (int)c->n, c->stream));
+    a.nchunks = (int32_t)c->nchs;  // k_mix walks state chunks
+    HIPOK(launch_mix(c->dtype, c->cpls, a, c->G, (int)c->n, c->stream));
     c->send_fresh = c->n_send > 0;
   }
   c->cur ^= 1;
@@ -1479,7 +1517,7 @@ int dopt_phase_grad_shared(dopt_ctx* c, int64_t batch, const int32_t* idx, doubl
     return DOPT_OK;
   }
   if (c->prof && (rc = prof_event(c, false))) return rc;
-  HIPOK(launch_round(c->dtype, c->problem, c->cpl, true, fuse_loss != 0, a, (int)c->n, c->stream));
+  HIPOK(launch_round(c->dtype, c->xdtype, c->problem, c->cpl, true, fuse_loss != 0, a, (int)c->n, c->stream));
   if (c->prof && (rc = prof_event(c, true))) return rc;
   return DOPT_OK;
 }
@@ -1487,16 +1525,16 @@ int dopt_phase_grad_shared(dopt_ctx* c, int64_t batch, const int32_t* idx, doubl
 int dopt_phase_colsum_grad(dopt_ctx* c, double* sum_dev) {
   CHECK_ARG(c && sum_dev, "NULL argument");
   if (!c->G) return fail(DOPT_ERR_STATE, "no gradient phase yet");
-  HIPOK(launch_colsum_partial(c->dtype, c->G, c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part, nullptr,
+  HIPOK(launch_colsum_partial(c->dtype, c->G, c->n, c->ld, (int32_t)c->nchs, kRowsPerGroup, c->part, nullptr,
                               c->stream));
-  HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nch, nullptr, nullptr, 0.0, 0,
+  HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nchs, nullptr, nullptr, 0.0, 0,
                             c->stream, sum_dev));
   return DOPT_OK;
 }
 
 int dopt_phase_central_step(dopt_ctx* c, const double* sum_dev, int64_t t, double eta0) {
   CHECK_ARG(c && sum_dev, "NULL argument");
-  HIPOK(launch_colsum_final(c->dtype, sum_dev, 1, n_div(c), c->ld, (int32_t)c->nch, c->xg[c->gcur ^ 1],
+  HIPOK(launch_colsum_final(c->dtype, sum_dev, 1, n_div(c), c->ld, (int32_t)c->nchs, c->xg[c->gcur ^ 1],
                             c->xg[c->gcur], eta0 / sqrt((double)(t + 1)), 1, c->stream));
   c->gcur ^= 1;
   return DOPT_OK;
@@ -1515,22 +1553,22 @@ int dopt_phase_metrics_pass_shared(dopt_ctx* c) {
 int dopt_phase_metrics_shared(dopt_ctx* c, int include_xnorm, double* out_dev) {
   CHECK_ARG(c && out_dev, "NULL argument");
   HIPOK(launch_history(c->dtype, nullptr, c->slab_loss, c->n, c->loss_groups, c->xg[c->gcur], c->ld,
-                       (int32_t)c->nch, include_xnorm != 0, out_dev, c->stream));
+                       (int32_t)c->nchs, include_xnorm != 0, out_dev, c->stream));
   return DOPT_OK;
 }
 
 int dopt_phase_colsum(dopt_ctx* c, double* sum_dev) {
   CHECK_ARG(c && sum_dev, "NULL argument");
-  HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur], c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part,
+  HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur], c->n, c->ld, (int32_t)c->nchs, kRowsPerGroup, c->part,
                               nullptr, c->stream));
-  HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nch, nullptr, nullptr, 0.0, 0,
+  HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nchs, nullptr, nullptr, 0.0, 0,
                             c->stream, sum_dev));
   return DOPT_OK;
 }
 
 int dopt_phase_xbar(dopt_ctx* c, const double* sum_dev) {
   CHECK_ARG(c && sum_dev, "NULL argument");
-  HIPOK(launch_colsum_final(c->dtype, sum_dev, 1, n_div(c), c->ld, (int32_t)c->nch, c->xbar[c->xb ^ 1], nullptr,
+  HIPOK(launch_colsum_final(c->dtype, sum_dev, 1, n_div(c), c->ld, (int32_t)c->nchs, c->xbar[c->xb ^ 1], nullptr,
                             0.0, 0, c->stream));
   c->xb ^= 1;
   c->S_ext = sum_dev;  // the complete-graph mix of the next round uses the global sums
@@ -1540,7 +1578,7 @@ int dopt_phase_xbar(dopt_ctx* c, const double* sum_dev) {
 int dopt_phase_cons(dopt_ctx* c) {
   CHECK_ARG(c, "ctx is NULL");
   if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
-  HIPOK(launch_cons(c->dtype, c->xs[c->cur], c->xbar[c->xb], c->n, c->ld, (int32_t)c->nch, c->slab_cons,
+  HIPOK(launch_cons(c->dtype, c->xs[c->cur], c->xbar[c->xb], c->n, c->ld, (int32_t)c->nchs, c->slab_cons,
                     c->stream));
   c->cons_n = (c->n + 63) / 64;
   return DOPT_OK;
@@ -1550,19 +1588,19 @@ int dopt_phase_fold(dopt_ctx* c, double* cons_out, double* xnorm_out, double* lo
   CHECK_ARG(c, "ctx is NULL");
   CHECK_ARG(slab == 0 || slab == 1, "slab must be 0 or 1");
   HIPOK(launch_fold(c->dtype, c->slab_cons, c->cons_n, slab ? c->slab_loss_b : c->slab_loss, c->slab_n[slab],
-                    c->xbar[c->xb], c->ld, (int32_t)c->nch, cons_out, loss_out, xnorm_out, c->stream));
+                    c->xbar[c->xb], c->ld, (int32_t)c->nchs, cons_out, loss_out, xnorm_out, c->stream));
   return DOPT_OK;
 }
 
 int dopt_phase_colsum_fold(dopt_ctx* c, double* sum_dev, double* cons_out, double* xnorm_out, double* loss_out) {
   CHECK_ARG(c && sum_dev, "NULL argument");
   if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
-  HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur], c->n, c->ld, (int32_t)c->nch, kRowsPerGroup, c->part,
+  HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur], c->n, c->ld, (int32_t)c->nchs, kRowsPerGroup, c->part,
                               nullptr, c->stream));
   const FoldArgs fold = {c->slab_cons, c->cons_n, c->slab_loss, c->slab_n[0], c->xbar[c->xb], cons_out, loss_out,
                          xnorm_out};
   const bool any = cons_out || xnorm_out || loss_out;
-  HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nch, nullptr, nullptr, 0.0, 0,
+  HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nchs, nullptr, nullptr, 0.0, 0,
                             c->stream, sum_dev, any ? &fold : nullptr));
   return DOPT_OK;
 }
@@ -1586,9 +1624,10 @@ int dopt_phase_mix_lagged(dopt_ctx* c, int64_t t, double eta0, const double* sum
   a.xbar_out = c->xbar[c->xb ^ 1];
   a.slab_cons = consensus ? c->slab_cons : nullptr;
   if (c->n > 0) {
-    HIPOK(launch_mix(c->dtype, c->cpl, a, c->G, (int)c->n, c->stream));
+    a.nchunks = (int32_t)c->nchs;  // k_mix walks state chunks
+    HIPOK(launch_mix(c->dtype, c->cpls, a, c->G, (int)c->n, c->stream));
   } else {  // no worker here: the average still has to be written
-    HIPOK(launch_colsum_final(c->dtype, sum_dev, 1, n_div(c), c->ld, (int32_t)c->nch, c->xbar[c->xb ^ 1], nullptr,
+    HIPOK(launch_colsum_final(c->dtype, sum_dev, 1, n_div(c), c->ld, (int32_t)c->nchs, c->xbar[c->xb ^ 1], nullptr,
                               0.0, 0, c->stream));
   }
   if (consensus) c->cons_n = c->n;
@@ -1607,6 +1646,7 @@ int dopt_phase_loss_pass(dopt_ctx* c, int two_points) {
   a.X = c->obj_sep ? c->Xo : c->X;
   a.y = c->obj_sep ? c->yo : c->y;
   a.off = c->obj_sep ? c->choff_o : c->choff;
+  a.defer_rows = (int32_t)kLossChunk;  // 64-row chunks
   const int64_t nc = c->obj_sep ? c->n_chunks_o : c->n_chunks;
   a.w_shared = c->xbar[c->xb];  // current average: z -> slab B
   if (two_points) {
@@ -1620,7 +1660,7 @@ int dopt_phase_loss_pass(dopt_ctx* c, int two_points) {
     a.flags |= F_LOSS | F_SHARED | F_LOSS_FROM_Z;
   }
   c->slab_n[1] = nc;
-  HIPOK(launch_round(c->dtype, c->problem, c->cpl, false, true, a, (int)nc, c->stream));
+  HIPOK(launch_round(c->dtype, c->xdtype, c->problem, c->cpl, false, true, a, (int)nc, c->stream));
   return DOPT_OK;
 }
 
@@ -1640,7 +1680,7 @@ int dopt_phase_metrics(dopt_ctx* c, uint32_t flags, int include_xnorm, double* o
   CHECK_ARG(c && out_dev, "NULL argument");
   const bool cons = flags & DOPT_RUN_CONSENSUS, loss = flags & DOPT_RUN_OBJECTIVE;
   HIPOK(launch_history(c->dtype, cons ? c->slab_cons : nullptr, loss ? c->slab_loss : nullptr, c->n,
-                       c->loss_groups, c->xbar[c->xb], c->ld, (int32_t)c->nch, loss && include_xnorm, out_dev,
+                       c->loss_groups, c->xbar[c->xb], c->ld, (int32_t)c->nchs, loss && include_xnorm, out_dev,
                        c->stream));
   return DOPT_OK;
 }

@@ -34,6 +34,7 @@ all-reduces over RCCL) and every rank ends with the same history and iterates.
 """
 import os
 import time
+from contextlib import closing
 
 import numpy as np
 
@@ -94,8 +95,49 @@ def _pack(workers, n_features):
     return X, y, off
 
 
-def _data_key(workers):
-    return tuple((id(w.X_local), w.X_local.shape, id(w.y_local)) for w in workers)
+def _fingerprint(arrays):
+    """Content hash of arrays (dtype, shape and bytes; xxh3 when available, ~7 GB/s).  The
+    engine cache compares data by content, not by id(): ids of freed arrays are reused by
+    CPython, and shards edited in place keep their ids."""
+    try:
+        import xxhash
+
+        h = xxhash.xxh3_128()
+    except ImportError:  # pragma: no cover - xxhash ships in this image
+        import hashlib
+
+        h = hashlib.blake2b(digest_size=16)
+    for a in arrays:
+        a = np.ascontiguousarray(a)
+        h.update(repr((a.dtype.str, a.shape)).encode())
+        if a.size:
+            h.update(memoryview(a.reshape(-1).view(np.uint8)))
+    return h.hexdigest()
+
+
+def _f32_exact(arrays):
+    """True when every value is exactly representable in float32 (so float32 storage under
+    float64 arithmetic changes nothing; dopt_set_data_dtype)."""
+    for a in arrays:
+        if a is None:
+            continue
+        a = np.asarray(a, dtype=np.float64)
+        if a.size and not np.array_equal(a.astype(np.float32).astype(np.float64), a):
+            return False
+    return True
+
+
+def _data_dtype(config, d, arrays):
+    """Shard storage: config 'data_dtype' = 'auto' (default: float32 when dtype is float64,
+    the rows fit the row-resident kernel and every value -- shards and a separate X_full --
+    is exactly float32; the arithmetic stays float64), 'float32' or 'float64'."""
+    dtype = config.get("dtype", "float64")
+    want = config.get("data_dtype", "auto")
+    if _dopt.DTYPES[dtype] == _dopt.F32:
+        return dtype
+    if want == "auto":
+        return "float32" if 0 < d <= 2048 and _f32_exact(arrays) else "float64"
+    return want
 
 
 def _same_rows(A, ya, B, yb):
@@ -116,23 +158,29 @@ def _same_rows(A, ya, B, yb):
 
 
 _ENGINES = {}
+_WARNED_CENTRAL_DEVICE = False
 
 
-def _engine(workers, n_features, config, lo=0, hi=None):
-    """One resident engine per (device, dtype, problem, shard set, slice), reused by the
-    four trainers Simulator.run_all builds over the same worker data.  [lo, hi) is the
-    slice of workers this process holds (multi-process mode)."""
+def _engine(workers, n_features, config, lo=0, hi=None, X_full=None, y_full=None):
+    """One resident engine per (device, dtype), holding one data set: reused by the four
+    trainers Simulator.run_all builds over the same worker data.  [lo, hi) is the slice of
+    workers this process holds (multi-process mode).  Reuse is decided by CONTENT (a hash
+    of the slice's shards), so freed-and-reallocated or edited-in-place arrays reload."""
     hi = len(workers) if hi is None else hi
-    key = (_device(config), config.get("dtype", "float64"), config["problem_type"], _data_key(workers), lo, hi)
-    eng = _ENGINES.get(key)
-    if eng is None:
-        for k in [k for k in _ENGINES if k[:2] == key[:2]]:
-            _ENGINES.pop(k).close()  # free the previous data set's HBM
-        eng = _dopt.Engine(key[0], key[1])
+    arrays = [a for w in workers[lo:hi] for a in (w.X_local, w.y_local)]
+    dev, dtype = _device(config), config.get("dtype", "float64")
+    xdt = _data_dtype(config, n_features, arrays + [X_full, y_full])
+    key = (config["problem_type"], xdt, lo, hi, _fingerprint(arrays))
+    eng = _ENGINES.get((dev, dtype))
+    if eng is None or eng.data_key != key:
+        if eng is not None:
+            _ENGINES.pop((dev, dtype)).close()  # free the previous data set's HBM
+        eng = _dopt.Engine(dev, dtype, data_dtype=xdt)
         X, y, off = _pack(workers[lo:hi], n_features)
         eng.load_shards(config["problem_type"], X, y, off)
         eng.obj_key = None
-        _ENGINES[key] = eng
+        eng.data_key = key
+        _ENGINES[(dev, dtype)] = eng
     device_sampling = config.get("sampling", "legacy") == "device"
     eng.set_sampler("device" if device_sampling else "host", seed=int(config.get("sampling_seed", 0)), first_worker=lo)
     return eng
@@ -154,7 +202,7 @@ def _dist_objective(eng, workers, n_features, X_full, y_full, rank, world):
     yf = np.asarray(y_full, dtype=np.float64).reshape(-1)
     parts = np.array_split(np.arange(Xf.shape[0]), world)[rank]
     eng.load_objective_data(Xf[parts], yf[parts])
-    eng.obj_key = ("dist", id(X_full))
+    eng.obj_key = ("dist", _fingerprint([X_full, y_full]))
     return True, Xf.shape[0], True
 
 
@@ -167,7 +215,7 @@ def _set_objective_data(eng, workers, n_features, X_full, y_full):
             eng.clear_objective_data()
             eng.obj_key = None
         return False
-    key = (id(X_full), np.shape(X_full), id(y_full))
+    key = _fingerprint([X_full, y_full])  # by content: ids are reused once arrays are freed
     if eng.obj_key != key:
         X, y, _ = _pack(workers, n_features)
         if _same_rows(X_full, y_full, X, y):
@@ -228,18 +276,35 @@ def _index_chunks(workers, T, config):
 
 def _one_ahead(gen):
     """Items of `gen`, each produced on a worker thread while the caller consumes the
-    previous one.  Exactly the items of gen are produced (no draw past the end)."""
+    previous one.  Exactly the items of gen are produced (no draw past the end).
+
+    The draws advance numpy's global legacy stream.  If the consumer stops early (the
+    device run of a chunk raised, or the loop was left), the chunk drawn ahead was never
+    used: numpy's state goes back to where the last CONSUMED chunk left it, so a later
+    trainer in the process continues the reference's stream (trainer.py:166, worker.py:27)."""
     from concurrent.futures import ThreadPoolExecutor
 
     done = object()
     with ThreadPoolExecutor(max_workers=1) as ex:
         fut = ex.submit(next, gen, done)
-        while True:
-            item = fut.result()
-            if item is done:
-                return
-            fut = ex.submit(next, gen, done)
-            yield item
+        finished = False
+        try:
+            while True:
+                item = fut.result()
+                if item is done:
+                    finished = True
+                    return
+                consumed = np.random.get_state()  # the stream after the chunk handed out now
+                fut = ex.submit(next, gen, done)
+                yield item
+        finally:
+            if not finished:
+                try:
+                    fut.result()  # let the in-flight draw finish, then undo it
+                except Exception:
+                    pass
+                if "consumed" in locals():
+                    np.random.set_state(consumed)
 
 
 # ---------------------------------------------------------------------------- centralized
@@ -274,50 +339,60 @@ class CentralizedTrainer:
         reg_param = self._get_regularization_param()
         self.total_floats_transmitted = 0
         cfg = self.config
+        if cfg.get("sampling", "legacy") == "device":
+            # the device sampler draws inside the D-SGD row pass only; the centralized trainer
+            # (which Simulator.run_all runs first) takes the reference's legacy stream instead
+            global _WARNED_CENTRAL_DEVICE
+            if not _WARNED_CENTRAL_DEVICE:
+                _say("Note: sampling='device' applies to D-SGD; the centralized trainer draws its "
+                     "minibatches from numpy's legacy stream (sampling='legacy')", cfg)
+                _WARNED_CENTRAL_DEVICE = True
+            cfg = dict(cfg, sampling="legacy")
         lam_grad = _grad_reg(cfg, n_iterations, self.workers)
         info = _dist_info(cfg)
         if info is not None:
             return self._run_distributed(info, int(n_iterations), X_full, y_full, f_opt, lam_grad, reg_param,
-                                         start_time)
-        eng = _engine(self.workers, self.n_features, cfg)
+                                         start_time, cfg)
+        eng = _engine(self.workers, self.n_features, cfg, X_full=X_full, y_full=y_full)
         want_obj = _set_objective_data(eng, self.workers, self.n_features, X_full, y_full)
         eng.set_global(self.x_global)
-        for t0, n, b, idx in _index_chunks(self.workers, int(n_iterations), cfg):
-            t_host = time.time() - start_time
-            obj, tim = eng.run_centralized(n, cfg["learning_rate_eta0"], b, lam_grad, reg_param, f_opt, idx=idx,
-                                           t0=t0, objective=want_obj)
-            if want_obj:
-                self.history["objective"].extend(list(obj))
-            self.history["time"].extend((tim + t_host).tolist())
-            # trainer.py:50,60-61: N*d up + N*d down per round (Python ints)
-            self.total_floats_transmitted += n * (self.n_workers * self.n_features * 2)
+        with closing(_index_chunks(self.workers, int(n_iterations), cfg)) as chunks:
+            for t0, n, b, idx in chunks:
+                t_host = time.time() - start_time
+                obj, tim = eng.run_centralized(n, cfg["learning_rate_eta0"], b, lam_grad, reg_param, f_opt, idx=idx,
+                                               t0=t0, objective=want_obj)
+                if want_obj:
+                    self.history["objective"].extend(list(obj))
+                self.history["time"].extend((tim + t_host).tolist())
+                # trainer.py:50,60-61: N*d up + N*d down per round (Python ints)
+                self.total_floats_transmitted += n * (self.n_workers * self.n_features * 2)
         self.x_global = eng.get_global()
         _warn_nonfinite(self.history, self.config)
         print(f"C-SGD training finished. Time: {time.time() - start_time:.2f}sseconds")
         return self.history, self.x_global
 
-    def _run_distributed(self, info, T, X_full, y_full, f_opt, lam_grad, reg_param, start_time):
+    def _run_distributed(self, info, T, X_full, y_full, f_opt, lam_grad, reg_param, start_time, cfg):
         import distributed
 
         rank, world, _ = info
-        cfg = self.config
         bounds = distributed.partition_bounds(self.n_workers, world)
         lo, hi = int(bounds[rank]), int(bounds[rank + 1])
-        eng = _engine(self.workers, self.n_features, cfg, lo, hi)
+        eng = _engine(self.workers, self.n_features, cfg, lo, hi, X_full=X_full, y_full=y_full)
         want_obj, rows_global, sep = _dist_objective(eng, self.workers, self.n_features, X_full, y_full, rank, world)
         plan = distributed.HaloPlan(rank, world, bounds, lo, hi, np.zeros(0, np.int64), np.zeros(world + 1, np.int64),
                                     np.zeros(0, np.int32), np.zeros(world + 1, np.int64), None, None, None)
         runner = distributed.DistributedCentralized(eng, plan, self.n_workers, rows_global, device=_device(cfg),
                                                     obj_sep=sep)
         eng.set_global(self.x_global)
-        for t0, n, b, idx in _index_chunks(self.workers, T, cfg):
-            t_host = time.time() - start_time
-            obj = runner.run(n, cfg["learning_rate_eta0"], b, lam_grad, reg_param, f_opt, t0=t0, objective=want_obj,
-                             idx=None if idx is None else idx[:, lo:hi])
-            if want_obj:
-                self.history["objective"].extend(list(obj))
-            self.history["time"].extend(list(np.linspace(t_host, time.time() - start_time, n + 1)[1:]))
-            self.total_floats_transmitted += n * (self.n_workers * self.n_features * 2)
+        with closing(_index_chunks(self.workers, T, cfg)) as chunks:
+            for t0, n, b, idx in chunks:
+                t_host = time.time() - start_time
+                obj = runner.run(n, cfg["learning_rate_eta0"], b, lam_grad, reg_param, f_opt, t0=t0, objective=want_obj,
+                                 idx=None if idx is None else idx[:, lo:hi])
+                if want_obj:
+                    self.history["objective"].extend(list(obj))
+                self.history["time"].extend(list(np.linspace(t_host, time.time() - start_time, n + 1)[1:]))
+                self.total_floats_transmitted += n * (self.n_workers * self.n_features * 2)
         self.x_global = eng.get_global()
         _warn_nonfinite(self.history, self.config)
         _say(f"C-SGD training finished. Time: {time.time() - start_time:.2f}sseconds", cfg)
@@ -378,7 +453,7 @@ class DecentralizedTrainer:
         if info is not None:
             return self._run_distributed(info, int(n_iterations), X_full, y_full, f_opt, lam_grad, reg_param,
                                          start_time)
-        eng = _engine(self.workers, self.n_features, cfg)
+        eng = _engine(self.workers, self.n_features, cfg, X_full=X_full, y_full=y_full)
         want_obj = _set_objective_data(eng, self.workers, self.n_features, X_full, y_full)
         t = self._topo
         uni = t.uniform_offdiag() if self.n_workers >= cfg.get("mean_mixing_min", MEAN_MIX_MIN) else None
@@ -388,16 +463,17 @@ class DecentralizedTrainer:
             eng.set_topology(t.row_ptr, t.col, t.w)
         eng.set_models(np.stack([np.asarray(w.x, dtype=np.float64) for w in self.workers]))
         iteration_transmission = np.sum(self.degrees) * self.n_features  # trainer.py:169
-        for t0, n, b, idx in _index_chunks(self.workers, int(n_iterations), cfg):
-            t_host = time.time() - start_time
-            obj, cons, tim = eng.run_dsgd(n, cfg["learning_rate_eta0"], b, lam_grad, reg_param, f_opt, idx=idx,
-                                          t0=t0, objective=want_obj, consensus=True)
-            self.history["consensus_error"].extend(list(cons))
-            if want_obj:
-                self.history["objective"].extend(list(obj))
-            self.history["time"].extend((tim + t_host).tolist())
-            for _ in range(n):
-                self.total_floats_transmitted += iteration_transmission
+        with closing(_index_chunks(self.workers, int(n_iterations), cfg)) as chunks:
+            for t0, n, b, idx in chunks:
+                t_host = time.time() - start_time
+                obj, cons, tim = eng.run_dsgd(n, cfg["learning_rate_eta0"], b, lam_grad, reg_param, f_opt, idx=idx,
+                                              t0=t0, objective=want_obj, consensus=True)
+                self.history["consensus_error"].extend(list(cons))
+                if want_obj:
+                    self.history["objective"].extend(list(obj))
+                self.history["time"].extend((tim + t_host).tolist())
+                for _ in range(n):
+                    self.total_floats_transmitted += iteration_transmission
         models = eng.get_models()
         for i, worker in enumerate(self.workers):  # trainer.py:178-179: row views
             worker.x = models[i, :]
@@ -414,24 +490,25 @@ class DecentralizedTrainer:
         t = self._topo
         uni = t.uniform_offdiag() if self.n_workers >= cfg.get("mean_mixing_min", MEAN_MIX_MIN) else None
         plan = distributed.build_plan(t, world, rank)
-        eng = _engine(self.workers, self.n_features, cfg, plan.lo, plan.hi)
+        eng = _engine(self.workers, self.n_features, cfg, plan.lo, plan.hi, X_full=X_full, y_full=y_full)
         want_obj, rows_global, sep = _dist_objective(eng, self.workers, self.n_features, X_full, y_full, rank, world)
         eng.set_models(np.stack([np.asarray(w.x, dtype=np.float64) for w in self.workers[plan.lo:plan.hi]]))
         runner = distributed.DistributedDSGD(eng, plan, self.n_workers, rows_global, device=_device(cfg),
                                              mean=None if uni is None else (uni[0], uni[1][plan.lo:plan.hi]),
                                              obj_sep=sep)
         iteration_transmission = np.sum(self.degrees) * self.n_features  # trainer.py:169
-        for t0, n, b, idx in _index_chunks(self.workers, T, cfg):
-            t_host = time.time() - start_time
-            obj, cons = runner.run(n, cfg["learning_rate_eta0"], b, lam_grad, reg_param, f_opt, t0=t0,
-                                   objective=want_obj, consensus=True,
-                                   idx=None if idx is None else idx[:, plan.lo:plan.hi])
-            self.history["consensus_error"].extend(list(cons))
-            if want_obj:
-                self.history["objective"].extend(list(obj))
-            self.history["time"].extend(list(np.linspace(t_host, time.time() - start_time, n + 1)[1:]))
-            for _ in range(n):
-                self.total_floats_transmitted += iteration_transmission
+        with closing(_index_chunks(self.workers, T, cfg)) as chunks:
+            for t0, n, b, idx in chunks:
+                t_host = time.time() - start_time
+                obj, cons = runner.run(n, cfg["learning_rate_eta0"], b, lam_grad, reg_param, f_opt, t0=t0,
+                                       objective=want_obj, consensus=True,
+                                       idx=None if idx is None else idx[:, plan.lo:plan.hi])
+                self.history["consensus_error"].extend(list(cons))
+                if want_obj:
+                    self.history["objective"].extend(list(obj))
+                self.history["time"].extend(list(np.linspace(t_host, time.time() - start_time, n + 1)[1:]))
+                for _ in range(n):
+                    self.total_floats_transmitted += iteration_transmission
         models = runner.gather_models()
         for i, worker in enumerate(self.workers):
             worker.x = models[i, :]

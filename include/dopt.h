@@ -79,6 +79,18 @@ int dopt_device_count(int *count);
 int dopt_create(int device, int dtype, dopt_ctx **out);
 int dopt_destroy(dopt_ctx *ctx);
 
+/* Storage type of the shard rows (Worker.X_local / y_local, worker.py:7-8) on the device.
+ * Default: the compute dtype.  With compute dtype DOPT_F64, DOPT_F32 stores the rows as
+ * float32 while the iterates, every product, sum and transcendental stay float64
+ * (trainer.py:161-193 evaluated as the reference evaluates it): rows are widened exactly
+ * to float64 as they are loaded, so on data that is exactly float32-representable the
+ * round is the reference's float64 round at half the HBM bytes per row.  Other values
+ * are rounded to float32 on upload (the drop-in trainers only choose DOPT_F32 storage
+ * when that rounding is the identity).  Row-resident contexts only (d <= 2048 here).
+ * Call before loading / generating the shards; it drops the loaded data. */
+int dopt_set_data_dtype(dopt_ctx *ctx, int data_dtype);
+int dopt_get_data_dtype(dopt_ctx *ctx, int *data_dtype);
+
 /* Load the worker shards (utils.py:38-43 layout, Worker.X_local / y_local,
  * worker.py:7-10).  X is n_rows x d float64 (src_f32 = 0) or float32
  * (src_f32 = 1), host memory.  problem: DOPT_LOGISTIC / DOPT_QUADRATIC. */

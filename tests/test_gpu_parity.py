@@ -414,7 +414,8 @@ def test_device_sampler_matches_host_replay(dtype):
 
 def test_device_sampling_trainer_mode():
     """The drop-in trainer with config sampling='device': D-SGD runs without touching
-    numpy's stream; the centralized trainer reports the mode as unsupported."""
+    numpy's stream; the centralized trainer (run first by Simulator.run_all) falls back to
+    the legacy stream, so it reproduces the reference fixture exactly."""
     meta, z = _load("c2")
     cfg = dict(meta["config"], sampling="device", sampling_seed=4)
     shards, Xf, yf = _shards(meta, z)
@@ -424,8 +425,11 @@ def test_device_sampling_trainer_mode():
     assert np.random.get_state()[2] == pos
     assert len(hist["objective"]) == len(hist["consensus_error"]) == 200
     assert np.all(np.isfinite(hist["objective"])) and hist["objective"][-1] < hist["objective"][0]
-    with pytest.raises(NotImplementedError):
-        _make_trainer("Centralized", shards, cfg).run(5, Xf, yf, meta["f_opt"])
+    j = meta["labels"].index("Centralized")
+    np.random.set_state(_state(z, j))
+    T = 300
+    hc, _ = _make_trainer("Centralized", shards, cfg).run(T, Xf, yf, meta["f_opt"])
+    _close(hc["objective"], z[f"L{j}_objective"][:T], RTOL64)
 
 
 _COLSUM_SCRIPT = r"""
@@ -468,3 +472,69 @@ def test_one_launch_column_sums_bitwise(tmp_path):
         res.append(np.load(f))
     for k in res[0].files:
         np.testing.assert_array_equal(res[0][k], res[1][k], err_msg=k)
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+@pytest.mark.parametrize("problem,batch", [("logistic", 8), ("logistic", 10 ** 6), ("quadratic", 8)])
+def test_consensus_in_column_sums_matches_metrics_pass(dtype, problem, batch, monkeypatch):
+    """<= 64 workers with a separate metrics pass (few logistic workers, or minibatches):
+    the consensus rides the one-launch column sums (runtime.cpp cons_cs, per column block).
+    DOPT_CONS_CS=0 takes it from the metrics pass instead; only the summation order differs."""
+    rng = np.random.default_rng(41)
+    m_rows = [40, 33, 0, 40, 17, 5, 40, 28, 12, 40]
+    n, d, T = len(m_rows), 45, 12
+    off = np.concatenate([[0], np.cumsum(m_rows)])
+    X = np.hstack([rng.standard_normal((off[-1], d - 1)), np.ones((off[-1], 1))])
+    y = rng.choice(np.array([-1.0, 1.0]), off[-1]) if problem == "logistic" else rng.standard_normal(off[-1])
+    top = topology.ring(n)
+    np.random.seed(3)
+    idx = _dopt.mt_choice_rounds(T, m_rows, batch) if batch < max(m_rows) else None
+    runs = []
+    for knob in ("1", "0"):
+        monkeypatch.setenv("DOPT_CONS_CS", knob)
+        monkeypatch.setenv("DOPT_BIP", "0")  # minibatches: separate metrics pass (the cons_cs case)
+        eng = _dopt.Engine(0, dtype)
+        eng.load_shards(problem, X, y, off)
+        eng.set_topology(top.row_ptr, top.col, top.w)
+        obj, cons, _ = eng.run_dsgd(T, 0.05, batch, 1e-3, 1e-3, 0.0, idx=idx)
+        runs.append((obj, cons, eng.get_models()))
+        eng.close()
+    tol = 1e-12 if dtype == "float64" else 2e-6
+    np.testing.assert_array_equal(runs[0][0], runs[1][0])  # the objective path is untouched
+    np.testing.assert_allclose(runs[0][1], runs[1][1], rtol=tol)
+    np.testing.assert_array_equal(runs[0][2], runs[1][2])
+
+
+def test_engine_cache_keys_on_content():
+    """trainer._engine reuses the resident shards only for the same CONTENT: a second data
+    set of the same shape built after the first was freed (ids get reused), and shards
+    edited in place (ids unchanged), must both be reloaded."""
+    import gc
+
+    cfg = {"problem_type": "logistic", "local_batch_size": 50, "learning_rate_eta0": 0.05,
+           "l2_regularization_lambda": 1e-4, "strong_convexity_mu": 1e-4, "sampling": "full"}
+    n, d, m, T = 6, 12, 50, 20
+
+    def data(seed):
+        rng = np.random.default_rng(seed)
+        return [(np.hstack([rng.standard_normal((m, d - 1)), np.ones((m, 1))]), rng.choice([-1.0, 1.0], m))
+                for _ in range(n)]
+
+    def run(shards):
+        ws = [Worker(i, {"X": X, "y": y}, m, d, cfg) for i, (X, y) in enumerate(shards)]
+        Xf = np.vstack([s[0] for s in shards])
+        yf = np.concatenate([s[1] for s in shards])
+        h, _ = DecentralizedTrainer(ws, "ring", d, cfg).run(T, Xf, yf, 0.0)
+        ref, _, _, _ = O.run_decentralized(shards, topology.ring(n).dense_W(), T, cfg, Xf, yf, 0.0,
+                                           indices=[[np.arange(m)] * n] * T)
+        _close(h["objective"], ref["objective"], RTOL64)
+        return h
+
+    a = data(1)
+    run(a)
+    del a
+    gc.collect()
+    b = data(2)
+    run(b)
+    b[3][0][7, 2] += 1.5  # in place: same array object, same id
+    run(b)

@@ -9,6 +9,8 @@ per lane.  The bench (config C3) runs other instances of `k_round` (kernels.hip)
   dopt_run_dsgd, `fused`), and the metrics-only pass after the last round;
 * float32 logistic: hardware exp / log / reciprocal for the row terms (VAR bit 13);
 * minibatches by index inside the pass over every row (F_BIP) and the device sampler;
+* float64 iterates and arithmetic over float32-stored rows (dopt_set_data_dtype; the data
+  is made float32-representable, so the stored rows are exactly the reference's rows);
 * CPL = 1, 2, 4, 8, 16 chunks per lane in both dtypes, and row lengths that are not a
   multiple of the wave's 64 chunks (masked-lane loads: lanes past the row re-read its
   last chunk, VAR bit 11) or of the 16-byte vector (zero padding).
@@ -16,7 +18,8 @@ per lane.  The bench (config C3) runs other instances of `k_round` (kernels.hip)
 Every case runs T = 10 rounds of the reference's round (trainer.py:161-193) on a random
 4-regular graph and compares, against oracle/dsgd_oracle.run_decentralized on the same
 shards, indices and CSR order (mixing='sparse'):
-  float64: objective and consensus of every round and the final iterates, rtol 1e-9;
+  float64 (either storage): objective and consensus of every round and the final
+           iterates, rtol 1e-9;
   float32: vs the float32 oracle, objective rtol 1e-5, consensus 5e-5, iterates 1e-4
            (of the largest entry); the bench's own instance also vs the float64 oracle,
            objective 1e-4.
@@ -51,6 +54,10 @@ def _shards(problem, n, d, m, seed):
 
 def _run(problem, dtype, d, m, b, seed=11, sampler="host", vs64=False):
     X, y = _shards(problem, N, d, m, seed)
+    mixed = dtype == "float64/x32"  # float64 arithmetic over float32-stored rows
+    if mixed:  # data exactly representable in float32: the stored rows ARE the reference's rows
+        X, y = X.astype(np.float32).astype(np.float64), y.astype(np.float32).astype(np.float64)
+        dtype = "float64"
     off = np.arange(N + 1, dtype=np.int64) * m
     shards = [(X[i * m:(i + 1) * m], y[i * m:(i + 1) * m]) for i in range(N)]
     top = topology.random_regular(N, 4, seed=3)
@@ -69,7 +76,7 @@ def _run(problem, dtype, d, m, b, seed=11, sampler="host", vs64=False):
         indices = [[rep[t, i][rep[t, i] >= 0].astype(np.int64) for i in range(N)] for t in range(T)]
     else:
         indices = [[np.arange(m)] * N] * T
-    eng = _dopt.Engine(0, dtype)
+    eng = _dopt.Engine(0, dtype, data_dtype="float32" if mixed else None)
     try:
         eng.load_shards(problem, X, y, off)
         eng.set_topology(top.row_ptr, top.col, top.w)
@@ -90,6 +97,7 @@ def _run(problem, dtype, d, m, b, seed=11, sampler="host", vs64=False):
 
 def _check(dtype, got, ref, h64):
     (obj, cons, x), (h, xr) = got, ref
+    dtype = "float64" if dtype == "float64/x32" else dtype
     assert len(obj) == len(cons) == T
     assert np.all(np.isfinite(obj)) and np.all(np.isfinite(cons))
     if dtype == "float64":
@@ -112,6 +120,10 @@ C3_CASES = [
     ("logistic", "float64", 1024, 512, 16),
     ("quadratic", "float32", 1024, 512, 512),
     ("quadratic", "float64", 1024, 512, 512),
+    # float64 iterates / arithmetic over float32-stored rows of float32-representable data
+    ("logistic", "float64/x32", 1024, 512, 512),
+    ("logistic", "float64/x32", 1024, 512, 16),
+    ("quadratic", "float64/x32", 1024, 512, 512),
 ]
 
 
@@ -127,6 +139,7 @@ def test_c3_shape_trajectory_vs_oracle(problem, dtype, d, m, b):
 CPL_CASES = [
     ("float32", 200), ("float32", 300), ("float32", 1000), ("float32", 1001), ("float32", 2048), ("float32", 4000),
     ("float64", 100), ("float64", 200), ("float64", 512), ("float64", 1000), ("float64", 2000),
+    ("float64/x32", 200), ("float64/x32", 300), ("float64/x32", 1001), ("float64/x32", 2048),
 ]
 
 
@@ -142,9 +155,35 @@ def test_quadratic_wide_rows_vs_oracle(dtype):
     _check(dtype, got, ref, h64)
 
 
-@pytest.mark.parametrize("dtype", ["float32", "float64"])
+@pytest.mark.parametrize("dtype", ["float32", "float64", "float64/x32"])
 def test_device_sampler_at_scale_vs_oracle(dtype):
     """sampling='device' (Philox + Floyd on the GPU) at 256 workers: the host restatement
     of the draw (oracle/device_sampler.py) fed to the oracle gives the same trajectory."""
     got, ref, h64 = _run("logistic", dtype, 1024, 512, 16, sampler="device")
     _check(dtype, got, ref, h64)
+
+
+def test_float32_storage_matches_float64_storage():
+    """On float32-representable data the float64 engine gives the same trajectory whether
+    the rows are stored as float64 or as float32 (only the lane order of the row dots
+    differs: 2 vs 4 elements per 16-byte chunk), and rows that are NOT representable are
+    rounded on upload -- the API stores what it is asked to store."""
+    n, d, m, b = 300, 1000, 64, 64
+    X, y = _shards("logistic", n, d, m, 2)
+    X = X.astype(np.float32).astype(np.float64)
+    off = np.arange(n + 1, dtype=np.int64) * m
+    top = topology.random_regular(n, 4, seed=1)
+    runs = []
+    for xd in (None, "float32"):
+        eng = _dopt.Engine(0, "float64", data_dtype=xd)
+        eng.load_shards("logistic", X, y, off)
+        eng.set_topology(top.row_ptr, top.col, top.w)
+        obj, cons, _ = eng.run_dsgd(8, 0.05, b, 1e-4, 1e-4, 0.0)
+        Xi, yi = eng.get_shard(5)
+        np.testing.assert_array_equal(Xi, X[5 * m:6 * m])
+        runs.append((obj, cons, eng.get_models()))
+        eng.close()
+    for a_, b_ in zip(runs[0], runs[1]):
+        np.testing.assert_allclose(a_, b_, rtol=1e-12, atol=1e-15)
+    with pytest.raises(ValueError):
+        _dopt.Engine(0, "float32", data_dtype="float64")

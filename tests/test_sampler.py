@@ -113,3 +113,30 @@ def test_trainer_index_chunks_advance_stream_like_choice(b):
     assert pos == np.random.get_state()[2]
     assert sum(c[1] for c in chunks) == 37
     assert (chunks[0][3] is None) == (b >= max(rows))
+
+
+def test_prefetched_draw_is_undone_when_the_run_stops_early():
+    """trainer._one_ahead draws the next chunk of legacy-MT19937 indices on a helper thread.
+    When the consumer stops after the first chunk (e.g. the device run raised), numpy's
+    global stream must be where the CONSUMED chunk left it, not one chunk further."""
+    from contextlib import closing
+
+    import trainer
+
+    class W:
+        def __init__(self, m):
+            self.n_local_samples, self.batch_size = m, 4
+
+    ws = [W(30), W(17), W(30)]
+    rows = [30, 17, 30]
+    np.random.seed(11)
+    expect_first = _dopt.mt_choice_rounds(trainer.IDX_CHUNK_ROUNDS, rows, 4)
+    expect_state = np.random.get_state()
+    np.random.seed(11)
+    with closing(trainer._index_chunks(ws, 3 * trainer.IDX_CHUNK_ROUNDS, {})) as chunks:
+        t0, n, b, idx = next(chunks)
+    assert (t0, n, b) == (0, trainer.IDX_CHUNK_ROUNDS, 4)
+    np.testing.assert_array_equal(idx, expect_first)
+    st = np.random.get_state()
+    assert st[2] == expect_state[2]
+    np.testing.assert_array_equal(st[1], expect_state[1])

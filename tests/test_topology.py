@@ -59,3 +59,18 @@ def test_large_torus_sparse_only():
     np.testing.assert_allclose(np.add.reduceat(t.w, t.row_ptr[:-1]), 1.0)
     diag = t.w[t.col == np.repeat(np.arange(t.n), 5)]
     assert diag.shape == (t.n,) and np.all(diag == 1.0 - np.sum(np.full(4, 0.2)))
+
+
+@pytest.mark.parametrize("name,n", [("ring", 4097), ("grid", 6400), ("random_regular", 4100), ("random_regular", 4098)])
+def test_lanczos_spectral_gap_matches_dense(name, n):
+    """trainer.py:133-135 computes 1 - (second largest |eigenvalue|) with dense eigvalsh;
+    above 4096 workers Topology.spectral_gap switches to Lanczos (scipy eigsh on the CSR
+    W).  Just past the crossover, both must agree: on the ring (gap ~ 1e-6, nearly
+    degenerate top eigenvalues), the 80 x 80 torus (4-fold degenerate lambda_2) and
+    random 4-regular expanders."""
+    t = T.build(name, n, {"regular_degree": 4, "topology_seed": 2})
+    assert t.n > 4096
+    dense = 1.0 - np.sort(np.abs(np.linalg.eigvalsh(t.dense_W())))[-2]
+    lanczos = t.spectral_gap()
+    np.testing.assert_allclose(lanczos, dense, rtol=1e-6, atol=1e-9)
+    assert round(lanczos, 4) == round(dense, 4)  # the value trainer.py:135 prints

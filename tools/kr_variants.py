@@ -4,6 +4,9 @@ interleaved rounds in ONE process, median and min reported).  Each variant's
 histories must match variant 0 (fp32 tolerance) -- a faster wrong kernel is not a win.
 
   python tools/kr_variants.py [--variants 0,1,2,3,4,6,7] [--reps 5] [--rounds 10]
+  python tools/kr_variants.py --mode x32 --variants -1,30755,129059   (float64 over float32 rows)
+
+Variant -1 is the default build (env knob unset).
 """
 import argparse
 import json
@@ -26,9 +29,13 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--workers", type=int, default=4096)
+    ap.add_argument("--mode", default="f32", choices=["f32", "x32"],
+                    help="f32: float32 engine (DOPT_KR_VARIANT); x32: float64 arithmetic over float32 rows "
+                         "(DOPT_KRX_VARIANT)")
     args = ap.parse_args()
     n, d, m = args.workers, 1024, 512
-    eng = _dopt.Engine(0, "float32")
+    knob = "DOPT_KR_VARIANT" if args.mode == "f32" else "DOPT_KRX_VARIANT"
+    eng = _dopt.Engine(0, "float32") if args.mode == "f32" else _dopt.Engine(0, "float64", data_dtype="float32")
     eng.generate_shards("logistic", n, d, m, seed=1000, flip=0.05)
     top = topology.random_regular(n, 4, seed=0)
     eng.set_topology(top.row_ptr, top.col, top.w)
@@ -36,10 +43,13 @@ def main():
     variants = [int(v) for v in args.variants.split(",")]
     times = {v: [] for v in variants}
     ref = None
-    bytes_per = 4 * n * (m * d + m + 2 * d)
+    bytes_per = 4 * n * (m * d + m) + (4 if args.mode == "f32" else 8) * n * 2 * d
     for rep in range(args.reps):
         for v in variants:
-            os.environ["DOPT_KR_VARIANT"] = str(v)
+            if v < 0:
+                os.environ.pop(knob, None)
+            else:
+                os.environ[knob] = str(v)
             eng.set_models(np.zeros((n, d)))
             eng.kernel_stats()
             obj, cons, _ = eng.run_dsgd(args.rounds, 0.05, m, 1e-4, 1e-4, 0.0, want_time=False)
@@ -48,8 +58,9 @@ def main():
             if ref is None:
                 ref = (obj, cons)
             else:
-                np.testing.assert_allclose(obj, ref[0], rtol=2e-5)
-                np.testing.assert_allclose(cons, ref[1], rtol=2e-4)
+                tol = (2e-5, 2e-4) if args.mode == "f32" else (1e-11, 1e-9)
+                np.testing.assert_allclose(obj, ref[0], rtol=tol[0])
+                np.testing.assert_allclose(cons, ref[1], rtol=tol[1])
         print(f"rep {rep}: " + " ".join(f"v{v}={times[v][-1]:.4f}ms" for v in variants), file=sys.stderr, flush=True)
     out = {}
     for v in variants:
