@@ -3,9 +3,18 @@
 
 Workload (BASELINE.json config C3, the metric's configuration): logistic regression,
 N = 4096 workers per GPU, d = 1024 (incl. bias), m = 512 rows per worker, full-shard
-batches (b = m), random 4-regular topology with Metropolis-Hastings weights, fp32,
+batches (b = m), random 4-regular topology with Metropolis-Hastings weights,
 objective + consensus recorded EVERY round (as trainer.py:182-191 does).
 A step = one D-SGD round over every worker (gradient, mix, step, metrics).
+
+Precision (the reference computes in float64, obj_problems.py / trainer.py:173): the
+headline `value` runs every product, sum and transcendental in float64 with float64
+iterates, over shards whose values are exactly float32-representable and are therefore
+stored as float32 (dopt_set_data_dtype: the stored rows ARE the float64 rows, at half the
+bytes).  Secondary legs at N=1: the same round with float64-stored rows ('f64_storage'),
+the float32 engine ('f32'), the device f(x*) solver (final suboptimality, as
+trainer.py:189-191 reports objective - f_opt), and the drop-in DecentralizedTrainer at C3
+with the reference's legacy RNG stream ('dropin').
 
 Multi-GPU (`--gpus N` under torch.distributed.run): ONE random 4-regular graph over
 4096 x N workers (weak scaling), each rank owning a contiguous slice; halo rows of
@@ -92,7 +101,10 @@ def cpu_baseline(seconds, n_workers=64, d=1024, m=512, seed=11):
     dt = time.perf_counter() - t0
     return {"value": n_workers * rounds / dt, "unit": "worker-iters/s", "cores": int(threads), "kind": "port",
             "sample": f"oracle (numpy float64 restatement of trainer.py:161-193) on {n_workers} workers x "
-                      f"{m} rows x d={d}, {rounds} rounds, {dt:.1f} s, full-shard batches, metrics every round"}
+                      f"{m} rows x d={d}, {rounds} rounds, {dt:.1f} s, full-shard batches, metrics every round; "
+                      f"extrapolated per worker to C3's 4096 (its dense W @ X, 0.08-0.14 s of a 9.25 s reference "
+                      f"round at N=4096 (SURVEY.md 3.3), is under 2 % of the per-worker work, so the "
+                      f"extrapolation flatters the CPU by at most that much)"}
 
 
 def pcie_leg(eng, top, n, d, m, b, lam, eta0, steps, dt_resident):
@@ -136,6 +148,145 @@ def pcie_leg(eng, top, n, d, m, b, lam, eta0, steps, dt_resident):
                     "uploaded shards, same K; not the headline value (inputs resident in HBM)"}
 
 
+def _chunks_per_lane(d, xesz):
+    nch = (d + (16 // xesz) - 1) // (16 // xesz)
+    cpl = 1
+    while cpl * 64 < nch:
+        cpl *= 2
+    return cpl
+
+
+def kernel_name(eng, problem, d, m, b):
+    """Name of the round kernel instance run_dsgd launches for this context (the dispatch of
+    k_round.inc: default variant per element-type pair, deferred loss terms and F_BIP)."""
+    import _dopt
+
+    esz = 4 if eng.dtype == _dopt.F32 else 8
+    xesz = 4 if eng.data_dtype == _dopt.F32 else 8
+    tname, sname = ("float" if esz == 4 else "double"), ("float" if xesz == 4 else "double")
+    cpl = _chunks_per_lane(d, xesz)
+    if cpl > 16 or (esz != xesz and cpl > 8):
+        return f"void dopt::k_split_step<{tname}, {4 if m <= 16 else 16}, true, true, false, 1>(dopt::RoundArgs)"
+    base = 35 | 2048 | 4096 | 8192
+    if esz != xesz:
+        var = base | 131072 | (16384 if 0 < m <= 1024 else 0)
+    else:
+        var = base | 256 if cpl <= 4 else base
+    if b < m:
+        var |= 64
+    return f"void dopt::k_round<{tname}, {sname}, {cpl}, {0 if problem == 'logistic' else 1}, true, true, {var}>(dopt::RoundArgs)"
+
+
+def bytes_per_round(eng, n, d, m):
+    """shard rows + labels read once, own iterate read + new iterate written
+    (neighbour rows hit L2 / MALL): n * (xesz * (m*d + m) + esz * 2d)."""
+    import _dopt
+
+    esz = 4 if eng.dtype == _dopt.F32 else 8
+    xesz = 4 if eng.data_dtype == _dopt.F32 else 8
+    return n * (xesz * (m * d + m) + esz * 2 * d)
+
+
+def timed_leg(eng, rounds, steps, warmup, n_models, d, barrier, event_every):
+    """Warmup, reset, then `steps` rounds bracketed by barrier + device sync, with HIP events
+    around every `event_every`-th round kernel (at least 10 sampled launches)."""
+    import numpy as np
+
+    if warmup > 0:
+        rounds(warmup)
+    eng.set_models(np.zeros((n_models, d)))
+    eng.kernel_stats()  # reset the event window
+    every = event_every if event_every > 0 else max(1, steps // 10)
+    eng.set_profiling(True, every=every)
+    barrier()
+    t0 = time.perf_counter()
+    obj, cons = rounds(steps)
+    barrier()
+    dt = time.perf_counter() - t0
+    launches, kr_ms = eng.kernel_stats()
+    eng.set_profiling(False)
+    if not all(map(math.isfinite, list(obj) + list(cons))):
+        raise RuntimeError("non-finite metrics")
+    return dt, launches, kr_ms, every, obj, cons
+
+
+def secondary_leg(dev, dtype, data_dtype, top, n, d, m, steps, warmup, lam, eta0, barrier, event_every):
+    """The C3 round with another storage / compute dtype on a fresh context (same generated data)."""
+    import _dopt
+
+    eng = _dopt.Engine(dev, dtype, data_dtype=data_dtype)
+    try:
+        eng.generate_shards("logistic", n, d, m, seed=1000, flip=0.05)
+        eng.set_topology(top.row_ptr, top.col, top.w)
+
+        def rounds(k):
+            obj, cons, _ = eng.run_dsgd(k, eta0, m, lam, lam, 0.0)
+            return obj, cons
+
+        dt, launches, kr_ms, every, obj, cons = timed_leg(eng, rounds, steps, warmup, n, d, barrier, event_every)
+        bpl = bytes_per_round(eng, n, d, m)
+        avg = kr_ms / launches * 1e-3
+        return {"value": n * steps / dt, "unit": "worker-iters/s", "ms_per_step": dt / steps * 1e3,
+                "dtype": "f32" if eng.dtype == _dopt.F32 else "f64",
+                "storage": "f32" if eng.data_dtype == _dopt.F32 else "f64",
+                "kernel": kernel_name(eng, "logistic", d, m, m), "kernel_avg_ms": avg * 1e3,
+                "kernel_launches_timed": launches, "bytes_per_launch": bpl,
+                "roofline_frac": bpl / avg / 1e9 / HBM_PEAK_GBS, "final_objective": float(obj[-1])}
+    finally:
+        eng.close()
+
+
+def suboptimality(eng, lam, final_objective):
+    """f_opt of the C3 problem by the device L-BFGS solver (solver.py over dopt_eval_full, one
+    pass over the shards per evaluation, float64), and the reference's reported quantity
+    objective - f_opt (trainer.py:189-191, f_opt from simulator.py:32-69)."""
+    import solver
+
+    t0 = time.perf_counter()
+    f_opt, _, info = solver.reference_optimum(eng, lam, gtol=1e-9, max_iter=500)
+    return {"f_opt": f_opt, "final_suboptimality": final_objective - f_opt, "solver_s": time.perf_counter() - t0,
+            "solver_evaluations": info["evaluations"], "solver_grad_norm": info["grad_norm"],
+            "note": "device L-BFGS on the full-data objective (replaces sklearn saga at sizes it cannot run)"}
+
+
+def dropin_leg(eng, n, d, m, lam, eta0, rounds=40):
+    """The drop-in DecentralizedTrainer (trainer.py API) on the same C3 shards as host arrays,
+    sampling='legacy': every round draws the reference's numpy legacy-MT19937 stream
+    (4096 permutations of 512 per round, worker.py:27) on the host before the device runs
+    it.  Timed: a second run() on the warm engine; the fixed per-run cost (data hash and
+    checks) is measured by a 0-round run and reported apart."""
+    import numpy as np
+
+    from trainer import DecentralizedTrainer
+    from worker import Worker
+
+    X = np.empty((n * m, d), dtype=np.float32)
+    y = np.empty(n * m, dtype=np.float32)
+    for i in range(n):  # the headline's shards (exactly float32)
+        Xi, yi = eng.get_shard(i)
+        X[i * m:(i + 1) * m] = Xi
+        y[i * m:(i + 1) * m] = yi
+    cfg = {"problem_type": "logistic", "local_batch_size": m, "learning_rate_eta0": eta0,
+           "l2_regularization_lambda": lam, "strong_convexity_mu": lam, "dtype": "float64",
+           "sampling": "legacy", "regular_degree": 4, "topology_seed": 0, "spectral_gap": False}
+    ws = [Worker(i, {"X": X[i * m:(i + 1) * m], "y": y[i * m:(i + 1) * m]}, m, d, cfg) for i in range(n)]
+    tr = DecentralizedTrainer(ws, "random_regular", d, cfg)
+    np.random.seed(203)
+    tr.run(2, X, y)  # loads the engine
+    walls = []
+    for T in (0, rounds):
+        tr = DecentralizedTrainer(ws, "random_regular", d, cfg)
+        t0 = time.perf_counter()
+        hist, _ = tr.run(T, X, y)
+        walls.append(time.perf_counter() - t0)
+    per_round = (walls[1] - walls[0]) / rounds
+    return {"value": n / per_round, "unit": "worker-iters/s", "rounds": rounds, "run_wall_s": walls[1],
+            "fixed_per_run_s": walls[0], "ms_per_round": per_round * 1e3,
+            "final_objective": float(hist["objective"][-1]),
+            "note": "trainer.DecentralizedTrainer, sampling='legacy' (numpy's stream, drawn on the host one "
+                    "chunk ahead of the device); per-round rate excludes the fixed per-run cost"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -145,20 +296,22 @@ def main():
     ap.add_argument("--workers", type=int, default=4096, help="workers per GPU")
     ap.add_argument("--d", type=int, default=1024)
     ap.add_argument("--m", type=int, default=512)
-    ap.add_argument("--dtype", default="float32")
-    ap.add_argument("--data-dtype", default=None,
-                    help="shard storage (default: --dtype); float32 under --dtype float64 keeps every "
-                         "operation in float64 over float32-representable rows")
+    ap.add_argument("--dtype", default="float64", help="iterates and arithmetic (the reference: float64)")
+    ap.add_argument("--data-dtype", default="float32",
+                    help="shard storage: float32 (default; the synthetic values are exactly float32, so the "
+                         "float64 round reads them at half the bytes) or float64")
     ap.add_argument("--batch", type=int, default=0,
                     help="C3 minibatch per worker (0: the full shard, the metric's configuration); b < m "
                          "draws the minibatches on the device (sampling='device', Philox + Floyd)")
     ap.add_argument("--degree", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="N=1: skip the f64-storage / f32 legs, the f(x*) solver and the drop-in trainer leg")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (gloo: 1-GPU rehearsal)")
-    ap.add_argument("--event-every", type=int, default=10,
-                    help="bracket every k-th round kernel with a HIP event pair (0: none). A pair costs ~30 us "
-                         "of round time, so the default samples 1 launch in 10 of the timed region")
+    ap.add_argument("--event-every", type=int, default=0,
+                    help="bracket every k-th round kernel with a HIP event pair (0: steps // 10, i.e. 10 "
+                         "sampled launches whatever --steps is). A pair costs ~4-30 us of round time")
     ap.add_argument("--phase", action="store_true",
                     help="drive the multi-GPU phase path even on one GPU (measures its per-rank overhead)")
     ap.add_argument("--partition", default="spectral", choices=["spectral", "ranges"],
@@ -223,8 +376,12 @@ def main():
                                     np.zeros(0, np.int64), np.zeros(world + 1, np.int64), np.zeros(0, np.int32),
                                     np.zeros(world + 1, np.int64), None, None, None)
     n = plan.n_local
-    log(f"rank {rank}/{world}: generating {plan.n_local} x {m} x {d} {args.dtype} shards on device {dev}")
-    eng = _dopt.Engine(dev, args.dtype, data_dtype=args.data_dtype)
+    data_dtype = args.data_dtype
+    if args.dtype in ("float32", "fp32", "f32") or _chunks_per_lane(d, 4) > 8:
+        data_dtype = None  # float32 engine, or rows beyond the mixed kernel (C5): storage = compute dtype
+    log(f"rank {rank}/{world}: generating {plan.n_local} x {m} x {d} shards ({args.dtype} arithmetic, "
+        f"{data_dtype or args.dtype} storage) on device {dev}")
+    eng = _dopt.Engine(dev, args.dtype, data_dtype=data_dtype)
     eng.generate_shards(problem, plan.n_local, d, m, seed=1000, flip=0.05, first_worker=plan.lo)
     lam = 1e-4
     b = args.batch if 0 < args.batch < m else m
@@ -233,10 +390,18 @@ def main():
             raise SystemExit("--batch < m: C3 only (device sampling)")
         eng.set_sampler("device", seed=7, first_worker=plan.lo)
         workload = workload.replace(f"m=b={m}", f"m={m}, b={b} (device-drawn minibatches)")
+    comm = None
     if world > 1 or args.phase:
         mean_local = None if mean is None else (mean[0], mean[1][plan.lo:plan.hi])
         runner = distributed.DistributedDSGD(eng, plan, n_global, n_global * m, device=dev, mean=mean_local)
-        log(f"halo: {plan.n_halo} rows in, {len(plan.send_ids)} rows out per round")
+        ld, esz_state = eng.layout()
+        comm = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                "halo_rows_in": int(plan.n_halo), "send_rows_out": int(len(plan.send_ids)),
+                "halo_bytes_in_per_round": int(plan.n_halo) * ld * esz_state,
+                "send_bytes_out_per_round": int(len(plan.send_ids)) * ld * esz_state,
+                "peers": [int(p) for p in runner._peers],
+                "allreduce_bytes_per_round": ld * 8}
+        log(f"comm: {comm}")
 
         def rounds(k):
             return runner.run(k, eta0, b, lam, lam, 0.0)
@@ -249,52 +414,30 @@ def main():
         def rounds(k):
             obj, cons, _ = eng.run_dsgd(k, eta0, b, lam, lam, 0.0)
             return obj, cons
-    log("warmup")
-    if args.warmup > 0:
-        rounds(args.warmup)
-    eng.set_models(np.zeros((plan.n_local, d)))
-    eng.kernel_stats()  # reset the event window
 
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    eng.set_profiling(args.event_every > 0, every=max(1, args.event_every))
-    barrier()
-    log(f"timing {args.steps} rounds")
-    t0 = time.perf_counter()
-    obj, cons = rounds(args.steps)
-    barrier()
-    dt = time.perf_counter() - t0
+    log(f"warmup {args.warmup}, timing {args.steps} rounds")
+    dt, launches, kr_ms, every, obj, cons = timed_leg(eng, rounds, args.steps, args.warmup, plan.n_local, d, barrier,
+                                                      args.event_every)
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}" if args.backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-    launches, kr_ms = eng.kernel_stats()
-    if not all(map(math.isfinite, list(obj) + list(cons))):
-        raise RuntimeError("non-finite metrics")
 
-    esz = 4 if args.dtype in ("float32", "fp32", "f32") else 8
+    esz = 4 if eng.dtype == _dopt.F32 else 8
     xesz = 4 if eng.data_dtype == _dopt.F32 else 8
-    tname = "float" if esz == 4 else "double"
-    sname = "float" if xesz == 4 else "double"
-    cpl = 1
-    while cpl * 64 < (d + (16 // xesz) - 1) // (16 // xesz):
-        cpl *= 2
-    if cpl <= 16:
-        var = 14371 | 256 if cpl <= 4 else 14371  # kernels.hip: kr_default_var<CPL>()
-        if xesz != esz:
-            var = 14371
-        kname = (f"void dopt::k_round<{tname}, {sname}, {cpl}, {0 if problem == 'logistic' else 1}, true, true, {var}>"
-                 "(dopt::RoundArgs)")
-    else:
-        kname = f"void dopt::k_split_step<{tname}, {4 if m <= 16 else 16}, true, true>(dopt::RoundArgs)"
+    kname = kernel_name(eng, problem, d, m, b)
     traffic, traffic_src = pmc_traffic(kname) if args.config == "c3" and n == 4096 and world == 1 else (None, None)
-    bytes_per_launch = n * (xesz * (m * d + m) + esz * 2 * d)  # X_b + y_b + x read + x write
+    bytes_per_launch = bytes_per_round(eng, n, d, m)
     avg_s = (kr_ms / launches) * 1e-3 if launches else float("nan")
     achieved = bytes_per_launch / avg_s / 1e9 if launches else None
     value = n_global * args.steps / dt
+    storage = ("float32 (every value exactly float32-representable; rows widened exactly to float64 as they "
+               "are loaded)" if xesz == 4 and esz == 8 else ("float32" if esz == 4 else "float64"))
     out = {
         "metric": METRIC,
         "value": value,
@@ -307,8 +450,10 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32" if esz == 4 else "f64",
-        "data": "synthetic (device-generated X~N(0,1)+bias, planted-w* labels, 5% flips)",
-        "config": {"workload": workload,
+        "data": "synthetic (device-generated X~N(0,1) rounded to float32 + bias column, planted-w* labels, "
+                "5% flips)",
+        "config": {"workload": workload, "arithmetic": "float64" if esz == 8 else "float32",
+                   "iterates": "float64" if esz == 8 else "float32", "shard_storage": storage,
                    "workers_per_gpu": n, "d": d, "rows_per_worker": m, "batch": b, "topology": top.name,
                    "degree": args.degree if args.config == "c3" else None,
                    "halo_rows_per_gpu": int(plan.n_halo),
@@ -322,22 +467,41 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
                      "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                      "kernel": kname, "kernel_avg_ms": avg_s * 1e3 if launches else None,
-                     "kernel_launches_timed": launches, "event_every": args.event_every,
+                     "kernel_launches_timed": launches, "event_every": every,
                      "bytes_per_launch": bytes_per_launch},
         "final_objective": float(obj[-1]),
         "final_consensus": float(cons[-1]),
     }
+    if comm is not None:
+        out["comm"] = comm
     if args.config != "c3":
         out["metric"] = f"worker-iters/sec ({args.config.upper()}, secondary config)"
         out["scaling"] = "strong"
+    secondary = rank == 0 and world == 1 and not args.phase and args.config == "c3" and not args.no_secondary
+    if secondary and b == m:
+        log("f(x*): device L-BFGS")
+        out["suboptimality"] = suboptimality(eng, lam, float(obj[-1]))
+        log("drop-in trainer leg (legacy RNG stream)")
+        out["dropin"] = dropin_leg(eng, n, d, m, lam, eta0)
     if args.pcie and world == 1 and args.config == "c3":
         out["pcie"] = pcie_leg(eng, top, n, d, m, b, lam, eta0, args.steps, dt)
+    eng.close()
+    if secondary and b == m:
+        legs = {}
+        if not (esz == 8 and xesz == 8):
+            log("leg: float64 storage")
+            legs["f64_storage"] = secondary_leg(dev, "float64", None, top, n, d, m, args.steps, args.warmup, lam,
+                                                eta0, barrier, args.event_every)
+        if esz == 8:
+            log("leg: float32 engine")
+            legs["f32"] = secondary_leg(dev, "float32", None, top, n, d, m, args.steps, args.warmup, lam, eta0,
+                                        barrier, args.event_every)
+        out["legs"] = legs
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
         log("cpu baseline")
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    eng.close()
     if world > 1 or args.phase:
         dist.destroy_process_group()
 

@@ -83,16 +83,24 @@ def _device(config):
     return int(config.get("device", os.environ.get("LOCAL_RANK", os.environ.get("DOPT_DEVICE", 0))))
 
 
-def _pack(workers, n_features):
+def _pack(workers, n_features, f32=False):
+    """Shards back to back (utils.py:38-43 order) + row offsets.  f32: pack as float32 (the
+    engine stores float32 rows: exact values, or a float32 engine) -- half the host bytes."""
     rows = np.array([w.X_local.shape[0] for w in workers], dtype=np.int64)
     off = np.zeros(len(workers) + 1, dtype=np.int64)
     np.cumsum(rows, out=off[1:])
+    dt = np.float32 if f32 else np.float64
     if off[-1] > 0:
-        X = np.concatenate([np.asarray(w.X_local, dtype=np.float64).reshape(-1, n_features) for w in workers])
-        y = np.concatenate([np.asarray(w.y_local, dtype=np.float64).reshape(-1) for w in workers])
+        X = np.concatenate([np.asarray(w.X_local, dtype=dt).reshape(-1, n_features) for w in workers])
+        y = np.concatenate([np.asarray(w.y_local, dtype=dt).reshape(-1) for w in workers])
     else:
-        X, y = np.zeros((0, n_features)), np.zeros(0)
+        X, y = np.zeros((0, n_features), dtype=dt), np.zeros(0, dtype=dt)
     return X, y, off
+
+
+def _all_f32(workers):
+    return all(np.asarray(w.X_local).dtype == np.float32 and np.asarray(w.y_local).dtype == np.float32
+               for w in workers)
 
 
 def _fingerprint(arrays):
@@ -121,6 +129,9 @@ def _f32_exact(arrays):
     for a in arrays:
         if a is None:
             continue
+        a = np.asarray(a)
+        if a.dtype == np.float32:
+            continue
         a = np.asarray(a, dtype=np.float64)
         if a.size and not np.array_equal(a.astype(np.float32).astype(np.float64), a):
             return False
@@ -142,8 +153,10 @@ def _data_dtype(config, d, arrays):
 
 def _same_rows(A, ya, B, yb):
     """True when (A, ya) and (B, yb) hold the same multiset of (row, label) pairs."""
-    A = np.asarray(A, dtype=np.float64)
-    B = np.asarray(B, dtype=np.float64)
+    A, B = np.asarray(A), np.asarray(B)
+    if A.dtype != B.dtype or A.dtype.kind != "f":
+        A = np.asarray(A, dtype=np.float64)
+        B = np.asarray(B, dtype=np.float64)
     ya = np.asarray(ya, dtype=np.float64).reshape(-1)
     yb = np.asarray(yb, dtype=np.float64).reshape(-1)
     if A.shape != B.shape or ya.shape[0] != A.shape[0] or yb.shape[0] != B.shape[0]:
@@ -176,7 +189,7 @@ def _engine(workers, n_features, config, lo=0, hi=None, X_full=None, y_full=None
         if eng is not None:
             _ENGINES.pop((dev, dtype)).close()  # free the previous data set's HBM
         eng = _dopt.Engine(dev, dtype, data_dtype=xdt)
-        X, y, off = _pack(workers[lo:hi], n_features)
+        X, y, off = _pack(workers[lo:hi], n_features, f32=eng.data_dtype == _dopt.F32)
         eng.load_shards(config["problem_type"], X, y, off)
         eng.obj_key = None
         eng.data_key = key
@@ -193,7 +206,7 @@ def _dist_objective(eng, workers, n_features, X_full, y_full, rank, world):
         eng.clear_objective_data()
         eng.obj_key = None
         return False, 1, False
-    X, y, _ = _pack(workers, n_features)
+    X, y, _ = _pack(workers, n_features, f32=_all_f32(workers))
     if _same_rows(X_full, y_full, X, y):
         eng.clear_objective_data()
         eng.obj_key = None
@@ -217,7 +230,7 @@ def _set_objective_data(eng, workers, n_features, X_full, y_full):
         return False
     key = _fingerprint([X_full, y_full])  # by content: ids are reused once arrays are freed
     if eng.obj_key != key:
-        X, y, _ = _pack(workers, n_features)
+        X, y, _ = _pack(workers, n_features, f32=_all_f32(workers))
         if _same_rows(X_full, y_full, X, y):
             eng.clear_objective_data()
         else:

@@ -538,3 +538,32 @@ def test_engine_cache_keys_on_content():
     run(b)
     b[3][0][7, 2] += 1.5  # in place: same array object, same id
     run(b)
+
+
+def test_trainer_stores_float32_representable_shards_as_float32():
+    """data_dtype='auto' (trainer default): shards whose values are all exactly float32 are
+    stored as float32 under float64 arithmetic -- same trajectory as the reference (rtol
+    1e-9 against the float64 oracle); other data stays float64-stored."""
+    import trainer as TR
+
+    rng = np.random.default_rng(8)
+    n, d, m, T = 12, 40, 30, 25
+    shards = [(np.hstack([rng.standard_normal((m, d - 1)), np.ones((m, 1))]).astype(np.float32).astype(np.float64),
+               rng.choice([-1.0, 1.0], m)) for _ in range(n)]
+    cfg = {"problem_type": "logistic", "local_batch_size": 8, "learning_rate_eta0": 0.05,
+           "l2_regularization_lambda": 1e-4, "strong_convexity_mu": 1e-4}
+    Xf = np.vstack([s[0] for s in shards])
+    yf = np.concatenate([s[1] for s in shards])
+    for exact in (True, False):
+        sh = shards if exact else [(X + 1e-9, y) for X, y in shards]
+        Xs = Xf if exact else Xf + 1e-9
+        np.random.seed(5)
+        st = np.random.get_state()
+        ws = [Worker(i, {"X": X, "y": y}, 8, d, cfg) for i, (X, y) in enumerate(sh)]
+        tr = DecentralizedTrainer(ws, "ring", d, cfg)
+        hist, _ = tr.run(T, Xs, yf, 0.0)
+        eng = TR._ENGINES[(TR._device(cfg), "float64")]
+        assert eng.data_dtype == (_dopt.F32 if exact else _dopt.F64)
+        h, _, _, _ = O.run_decentralized(sh, topology.ring(n).dense_W(), T, cfg, Xs, yf, 0.0, rng_state=st)
+        _close(hist["objective"], h["objective"], RTOL64)
+        _close(hist["consensus_error"], h["consensus_error"], RTOL64)
