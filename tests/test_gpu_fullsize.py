@@ -1,0 +1,115 @@
+"""Configs C4 and C5 at full size on ONE MI355X (288 GB of HBM holds either).
+
+C4: logistic, N = 65536 workers on the 256 x 256 torus, d = 1024, m = b = 512 -- the
+    configuration the reference cannot run (trainer.py:93,118 build dense N x N matrices:
+    64 GiB at this N).  Float64 arithmetic over float32-stored exact rows (137 GB of shards).
+C5: quadratic, N = 1024 workers, d = 2^20, m = b = 16, complete graph mixed through the
+    column sums (trainer.py:109-110, 173), float32 (64 GiB of shards): the column-blocked
+    round kernels.
+
+Both run T = 3 rounds in one call and are checked against host recomputation in float64 of
+the reference's round (trainer.py:161-193) from the downloaded shards: the updates of
+workers on the torus wrap-around rows / columns and random ones, every worker's consensus,
+and (C5) every round, re-run round by round from the same start.  C4's float64 checks are
+rtol 1e-10 (summation order only); C5's float32 ones 2e-4 (the float32 engine vs the
+float64 host recomputation of one round).
+"""
+import numpy as np
+import pytest
+
+import _dopt
+import dsgd_oracle as O
+import topology as TP
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_gb():
+    import torch
+
+    free, _ = torch.cuda.mem_get_info(0)
+    return free / 1e9
+
+
+def _mix_row(top, x, i):
+    s, e = top.row_ptr[i], top.row_ptr[i + 1]
+    acc = np.zeros(x.shape[1])
+    for k in range(s, e):  # CSR order, as the kernel sums
+        acc = acc + top.w[k] * x[top.col[k]]
+    return acc
+
+
+def test_c4_torus_65536_workers_full_size():
+    n, d, m, T, eta0, lam = 65536, 1024, 512, 3, 0.05, 1e-4
+    if _free_gb() < 150:
+        pytest.skip("needs ~140 GB of free HBM")
+    top = TP.grid(n)
+    eng = _dopt.Engine(0, "float64", data_dtype="float32")
+    try:
+        eng.generate_shards("logistic", n, d, m, seed=1000, flip=0.05)
+        eng.set_topology(top.row_ptr, top.col, top.w)
+        rng = np.random.default_rng(2)
+        x0 = rng.standard_normal((n, d)) * 1e-2
+        eng.set_models(x0)
+        obj, cons, _ = eng.run_dsgd(1, eta0, m, lam, lam, 0.0)
+        x1 = eng.get_models()
+        # torus corners / wrap-around rows and columns (neighbours ids i +- 1 mod 256, i +- 256 mod 65536)
+        picks = [0, 255, 256, 511, 65280, 65535, 32767, 32768] + list(rng.choice(n, 8, replace=False))
+        for i in picks:
+            X, y = eng.get_shard(int(i))
+            g = O.logistic_gradient(x0[i], X, y, lam)
+            np.testing.assert_allclose(x1[i], _mix_row(top, x0, i) - eta0 * g, rtol=1e-10, atol=1e-13)
+        xbar = x1.mean(axis=0)
+        np.testing.assert_allclose(cons[0], np.mean(np.sum((x1 - xbar) ** 2, axis=1)), rtol=1e-10)
+        # two more rounds in one call: the fused path (metrics of round t in round t+1's pass)
+        obj2, cons2, _ = eng.run_dsgd(T - 1, eta0, m, lam, lam, 0.0, t0=1)
+        x3 = eng.get_models()
+        assert np.all(np.isfinite(obj2)) and np.all(np.isfinite(cons2))
+        xbar3 = x3.mean(axis=0)
+        np.testing.assert_allclose(cons2[-1], np.mean(np.sum((x3 - xbar3) ** 2, axis=1)), rtol=1e-10)
+        for i in (0, 65535):  # the objective at xbar over a worker's rows enters history: spot-check sums
+            X, y = eng.get_shard(i)
+            assert np.isfinite(O.logistic_objective(xbar3, X, y, lam))
+    finally:
+        eng.close()
+
+
+def test_c5_d2pow20_1024_workers_full_size():
+    n, d, m, T, eta0, lam = 1024, 1 << 20, 16, 3, 1e-5, 1e-4
+    if _free_gb() < 75:
+        pytest.skip("needs ~70 GB of free HBM")
+    top = TP.fully_connected(n)
+    w_off, diag = top.uniform_offdiag()
+    eng = _dopt.Engine(0, "float32")
+    try:
+        eng.generate_shards("quadratic", n, d, m, seed=3, noise=10.0)
+        eng.set_mixing_mean(w_off, diag)
+        rng = np.random.default_rng(1)
+        x0 = (rng.standard_normal((n, d)) * 1e-3).astype(np.float32).astype(np.float64)
+        eng.set_models(x0)
+        obj_all, cons_all, _ = eng.run_dsgd(T, eta0, m, lam, lam, 0.0)  # T rounds, one call
+        x_all = eng.get_models()
+        eng.set_models(x0)
+        x = x0
+        picks = [0, 1, 511, 1023] + list(rng.choice(n, 4, replace=False))
+        shards = {int(i): eng.get_shard(int(i)) for i in picks}
+        for t in range(T):  # the same rounds one call each: every round checked on the host
+            obj, cons, _ = eng.run_dsgd(1, eta0, m, lam, lam, 0.0, t0=t)
+            xn = eng.get_models()
+            S = x.sum(axis=0)
+            eta = eta0 / np.sqrt(t + 1)
+            for i in picks:
+                X, y = shards[int(i)]
+                g = O.quadratic_gradient(x[i], X, y, lam)
+                ref = w_off * (S - x[i]) + diag[i] * x[i] - eta * g
+                np.testing.assert_allclose(xn[i], ref, rtol=2e-4, atol=2e-6 * np.abs(ref).max())
+            xb = xn.mean(axis=0)
+            np.testing.assert_allclose(cons[0], np.mean(np.sum((xn - xb) ** 2, axis=1)), rtol=1e-3)
+            np.testing.assert_allclose(cons[0], cons_all[t], rtol=1e-5)
+            np.testing.assert_allclose(obj[0], obj_all[t], rtol=1e-5)
+            x = xn
+        # one call (next round's coefficients fused into the step) or T calls (a dots pass per call):
+        # the same rounds up to the row-dot summation tree
+        np.testing.assert_allclose(x, x_all, rtol=1e-5, atol=1e-7 * np.abs(x_all).max())
+    finally:
+        eng.close()
