@@ -20,6 +20,7 @@ enum : int32_t {
   F_LOSS2 = 256,       // metrics-only pass: also the objective at w_shared (from z) into slab_loss2
   F_BIP = 512,         // minibatch gradient inside the metrics pass over all rows (k_round VAR bit 6)
   F_DEVSAMPLE = 1024,  // with F_BIP: the minibatch is drawn on the device (Philox + Floyd), not from idx
+  F_EARLYMIX = 2048,   // k_split_step: sum_j W_ij x_j of a block before the block's barrier (set by the launcher)
 };
 constexpr int64_t kMaxBipRows = 65536;  // shard rows the F_BIP byte map holds in LDS
 

@@ -60,6 +60,15 @@ __device__ __forceinline__ typename VT<T>::v ld_nt(const T* p) {
 // CPB = 16-byte chunks per lane per column block (a block is 64 * CPB chunks of every row).
 // One barrier per block: the waves' gradient partials go to a double-buffered LDS
 // slot, every wave folds them and forms the new block itself (wave 0 stores it).
+// Round 2 (C5, float32, interleaved A/B, tools/split_ab.py): the block's mix before its
+// barrier 14.93 -> 14.60 ms; all of the next block's loads in flight through the barrier
+// (PF, unrolled by two over fixed register sets, branch-free loads so the compiler's waits
+// stay partial) 14.60 -> 14.24; 1/16 as a multiply 14.24 -> ~14.0 (5.5 TB/s, 69 %).
+// Little's law says why it stops there: 4 waves / SIMD x 4 KB ahead per wave = 64 KB in
+// flight per CU, where ~90 KB are needed at the loaded latency (the dots-only kernel, 32
+// VGPRs, 8 waves / SIMD, streams the same rows at 85 %).  Not kept: 2 chunks per lane with
+// PF (166 VGPRs, 13.90 vs 13.99), a column-per-wave kernel without barriers that re-reads
+// the rows from L2 for the dots (k_split_colwave, DOPT_SPLIT_COLWAVE: 17.6 ms).
 // CPB > 1 keeps 2-4x the bytes in flight per wave between two barriers but costs
 // occupancy (C5: CPB 1 / 2 / 4 = 85 / 115 / 169 VGPRs, 15.1 / 15.5 / 16.7 ms): default 1,
 // DOPT_SPLIT_CPB selects 2 or 4 for A/B runs.  Not kept either: own / xbar / column sums
@@ -123,49 +132,88 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
   }
   double cacc = 0.0;
   const T inv_eta = (T)a.eta, lam = (T)a.lam;
-  int buf = 0;
-  V rn[RPW][CPB];  // PF: the next block's row segments, loaded one block ahead
-  if (PF) {
+  // 1 / nb when nb is a power of two (C5: 16): a multiply instead of an IEEE division per element
+  const bool pow2 = nb > 0 && (nb & (nb - 1)) == 0;
+  const T inv_nb = nb > 0 ? T(1) / (T)nb : T(0);
+  // PF: everything block cb + st needs -- its column sums (complete-graph mix), own and xbar
+  // chunks, then its row segments -- is loaded while block cb is processed.  The loop is
+  // unrolled by two over register sets A / B with fixed roles (stage B, process A, stage A,
+  // process B), so no loaded register is copied: a copy needs its load complete, and the
+  // compiler's wait for it would drain the whole next group (vmcnt counts in issue order).
+  // The block's barrier is LDS-only.  Mixes other than the column-sum one read their
+  // neighbour rows inside the block, as without PF.
+  const bool mean = (a.flags & F_MEAN) != 0;
+  const T* sums = (sizeof(T) == 8 && !a.colsum_t) ? (const T*)(const void*)a.colsum : (const T*)a.colsum_t;
+  // PF launches are complete-graph D-SGD steps with the sums in T (launch_split_step checks):
+  // the mix is formed from prefetched column sums, never from neighbour rows
+  constexpr bool pf_mix = PF;
+  (void)mean;
+  (void)pf_mix;
+  double wii = mean ? (double)((const T*)a.wdiag)[i] : 0.0;
+  asm volatile("" : "+v"(wii));  // loaded here, once: a load sunk into the block loop would wait for the prefetch
+  const bool early = (a.flags & F_EARLYMIX) != 0 && !gout;
+  struct Set {
+    V rw[RPW][CPB], own[CPB], xb[CPB], sv[CPB];
+  };
+  auto stage = [&](Set& S, int cbn) {  // small loads first, then the rows
+    if (PF) {
+      // branch-free: every load is issued (a block past the walk re-reads its last block, lanes
+      // past the row its last chunk, absent rows the worker's first row -- all unused), so the
+      // compiler's count of loads in flight is exact and the waits for the older set stay partial
+      const int cbc = cbn < bw.b1 ? cbn : bw.b1 - 1;
+#pragma unroll
+      for (int j = 0; j < CPB; ++j) {
+        const int c0 = cbc * BC + j * 64 + lane;
+        const int c = c0 < nch ? c0 : nch - 1;
+        S.sv[j] = *(const V*)(sums + (int64_t)c * VN);
+        S.own[j] = *(const V*)(own_p + (int64_t)c * VN);
+        if (MET) S.xb[j] = *(const V*)((const T*)a.xbar + (int64_t)c * VN);
+      }
+#pragma unroll
+      for (int j = 0; j < CPB; ++j) {
+        const int c0 = cbc * BC + j * 64 + lane;
+        const int c = c0 < nch ? c0 : nch - 1;
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) S.rw[r][j] = ld_nt<T>(X + (rowp[r] >= 0 ? rowp[r] : row0 * ld) + (int64_t)c * VN);
+      }
+      return;
+    }
+    const bool blk = cbn < bw.b1;
 #pragma unroll
     for (int j = 0; j < CPB; ++j) {
-      const int c = bw.b0 * BC + j * 64 + lane;
-#pragma unroll
-      for (int r = 0; r < RPW; ++r)
-        rn[r][j] = (bw.b0 < bw.b1 && rowp[r] >= 0 && c < nch) ? ld_nt<T>(X + rowp[r] + (int64_t)c * VN) : V(0);
+      const int c = cbn * BC + j * 64 + lane;
+      const bool in = blk && c < nch;
+      S.own[j] = in ? *(const V*)(own_p + (int64_t)c * VN) : V(0);
+      S.xb[j] = (MET && in) ? *(const V*)((const T*)a.xbar + (int64_t)c * VN) : V(0);
     }
-  }
-  for (int cb = bw.b0; cb < bw.b1; cb += bw.st, buf ^= 1) {
-    V rv[RPW][CPB];
-    if (PF) {
 #pragma unroll
-      for (int j = 0; j < CPB; ++j) {
-        const int cn = (cb + bw.st) * BC + j * 64 + lane;
-        const bool nin = cb + bw.st < bw.b1 && cn < nch;
+    for (int j = 0; j < CPB; ++j) {
+      const int c = cbn * BC + j * 64 + lane;
+      const bool in = blk && c < nch;
 #pragma unroll
-        for (int r = 0; r < RPW; ++r) {
-          rv[r][j] = rn[r][j];
-          rn[r][j] = (nin && rowp[r] >= 0) ? ld_nt<T>(X + rowp[r] + (int64_t)cn * VN) : V(0);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < CPB; ++j) {
-        const int c = cb * BC + j * 64 + lane;
-#pragma unroll
-        for (int r = 0; r < RPW; ++r)
-          rv[r][j] = (rowp[r] >= 0 && c < nch) ? ld_nt<T>(X + rowp[r] + (int64_t)c * VN) : V(0);
-      }
+      for (int r = 0; r < RPW; ++r) S.rw[r][j] = (in && rowp[r] >= 0) ? ld_nt<T>(X + rowp[r] + (int64_t)c * VN) : V(0);
     }
-    V own[CPB], xb[CPB];
+  };
+  auto process = [&](Set& S, int cb, int buf) {
+    V mixv[CPB];
 #pragma unroll
     for (int j = 0; j < CPB; ++j) {
       const int c = cb * BC + j * 64 + lane;
       const bool in = c < nch;
-      own[j] = in ? *(const V*)(own_p + (int64_t)c * VN) : V(0);
-      xb[j] = (MET && in) ? *(const V*)((const T*)a.xbar + (int64_t)c * VN) : V(0);
+      if constexpr (PF) {  // mix_chunk's column-sum form, from the prefetched sums (same arithmetic)
+#pragma unroll
+        for (int e = 0; e < VN; ++e) {
+          const double x = (double)S.own[j][e];
+          mixv[j][e] = (T)(a.w_off * ((double)S.sv[j][e] - x) + wii * x);
+        }
+      } else {
+        // the mix does not depend on the gradient: with F_EARLYMIX its loads (column sums or the
+        // neighbour rows) are issued before the block's barrier instead of after it
+        mixv[j] = (early && in) ? mix_chunk<T, T>(a, i, c, S.own[j]) : V(0);
+      }
       V gp = V(0);
 #pragma unroll
-      for (int r = 0; r < RPW; ++r) gp += coef[r] * rv[r][j];
+      for (int r = 0; r < RPW; ++r) gp += coef[r] * S.rw[r][j];  // absent rows: coef 0
       gred[buf][wave][j * 64 + lane] = gp;
     }
     if (PF)
@@ -178,26 +226,48 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
       const bool in = c < nch;
       const int q = j * 64 + lane;
       V g = V(0);
-      if (nb > 0) g = (gred[buf][0][q] + gred[buf][1][q] + gred[buf][2][q] + gred[buf][3][q]) / (T)nb + lam * own[j];
+      if (nb > 0) {
+        const V gs = gred[buf][0][q] + gred[buf][1][q] + gred[buf][2][q] + gred[buf][3][q];
+        g = (pow2 ? gs * inv_nb : gs / (T)nb) + lam * S.own[j];  // x * 2^-k == x / 2^k exactly
+      }
       V xn = V(0);
       if (gout) {
         if (wave == 0 && in) *(V*)((T*)a.g_out + (int64_t)i * ld + (int64_t)c * VN) = g;
       } else if (in) {
-        xn = mix_chunk<T, T>(a, i, c, own[j]) - inv_eta * g;
+        if constexpr (PF) xn = mixv[j] - inv_eta * g;
+        else xn = (early ? mixv[j] : mix_chunk<T, T>(a, i, c, S.own[j])) - inv_eta * g;
         if (wave == 0) *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = xn;
       }
       if (ZNEXT) {
 #pragma unroll
-        for (int r = 0; r < RPW; ++r) zacc[r] += (double)hsum<T>(rv[r][j] * xn);
+        for (int r = 0; r < RPW; ++r) zacc[r] += (double)hsum<T>(S.rw[r][j] * xn);
       }
-      if (MET) {
+      if (MET && in) {  // (PF: lanes past the row hold re-read chunks)
 #pragma unroll
-        for (int r = 0; r < RPW; ++r) uacc[r] += (double)hsum<T>(rv[r][j] * xb[j]);
+        for (int r = 0; r < RPW; ++r) uacc[r] += (double)hsum<T>(S.rw[r][j] * S.xb[j]);
         if (wave == 0) {
-          const V dv = own[j] - xb[j];
+          const V dv = S.own[j] - S.xb[j];
           cacc += (double)hsum<T>(dv * dv);
         }
       }
+    }
+  };
+  if (PF) {
+    Set A, B;
+    stage(A, bw.b0);
+    for (int cb = bw.b0; cb < bw.b1; cb += 2 * bw.st) {
+      stage(B, cb + bw.st);
+      process(A, cb, 0);
+      if (cb + bw.st >= bw.b1) break;
+      stage(A, cb + 2 * bw.st);
+      process(B, cb + bw.st, 1);
+    }
+  } else {
+    Set A;
+    int buf = 0;
+    for (int cb = bw.b0; cb < bw.b1; cb += bw.st, buf ^= 1) {
+      stage(A, cb);
+      process(A, cb, buf);
     }
   }
 #pragma unroll
@@ -217,6 +287,128 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
     const double cs = wave_sum_dpp(cacc);
     if (lane == 0) a.cpart[(int64_t)i * G + grp] = cs;
   }
+}
+
+// Column-per-wave form of the column-blocked step (DOPT_SPLIT_COLWAVE, <= 16 rows per worker):
+// every wave owns whole 64-chunk blocks of the workgroup's walk (wave w takes every NW-th
+// block) and ALL of the worker's rows.  Pass 1 streams the rows (cached loads) into the
+// gradient chunk, the wave forms and stores x_i' itself; pass 2 re-reads the same rows --
+// just fetched, so L2 hits -- for the next round's dots and the metric dots.  No barrier and
+// no cross-wave exchange per block, no mix / division repeated by four waves; the waves'
+// per-row dot partials meet in LDS once, after the walk.
+template <typename T, bool ZNEXT, bool MET>
+__global__ __launch_bounds__(NT) void k_split_colwave(const RoundArgs a) {
+  using V = typename VT<T>::v;
+  constexpr int VN = VT<T>::n;
+  constexpr int R = 16;  // rows per worker (host-checked)
+  constexpr int RB = 4;  // row loads in flight per wave and pass step
+  __shared__ double dred[NW][2][R];
+  __shared__ double cred[NW];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int i = blockIdx.x, grp = blockIdx.y, G = gridDim.y;
+  const int nch = a.nchunks, nblk = (nch + 63) / 64;
+  const BlockWalk bw(a, grp, G, nblk);
+  const int64_t ld = a.ld;
+  const int64_t row0 = a.off[i], m = a.off[i + 1] - row0;
+  const int nb = (int)(a.idx ? (a.b < m ? a.b : m) : m);  // <= R
+  const T* __restrict__ X = (const T*)a.X;
+  const bool shared = (a.flags & F_SHARED) != 0;
+  const bool gout = (a.flags & F_GOUT) != 0;
+  const T* own_p = shared ? (const T*)a.w_shared : (const T*)a.x_old + (int64_t)i * ld;
+  int64_t rowp[R];
+  T coef[R];
+  double zacc[R], uacc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const bool ok = r < nb;
+    const int lr = ok ? (a.idx ? a.idx[(int64_t)i * a.b + r] : r) : 0;
+    // wave-uniform: kept in SGPRs (the VGPRs go to the per-row dot accumulators)
+    rowp[r] = (row0 + __builtin_amdgcn_readfirstlane(lr)) * ld;  // absent rows: row 0, coefficient 0
+    const T cf = ok ? ((const T*)a.coef)[(int64_t)i * a.bcap + r] : T(0);
+    if constexpr (sizeof(T) == 4) {
+      coef[r] = __builtin_bit_cast(T, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, cf)));
+    } else {
+      coef[r] = readlane_t(cf, 0);
+    }
+    zacc[r] = 0.0;
+    uacc[r] = 0.0;
+  }
+  double cacc = 0.0;
+  const T inv_eta = (T)a.eta, lam = (T)a.lam;
+  // 1 / nb when nb is a power of two: x * 2^-k is x / 2^k exactly (one rounding of the same value)
+  const bool pow2 = nb > 0 && (nb & (nb - 1)) == 0;
+  const T inv_nb = nb > 0 ? T(1) / (T)nb : T(0);
+  for (int cb = bw.b0 + wave * bw.st; cb < bw.b1; cb += NW * bw.st) {
+    const int c0 = cb * 64 + lane;
+    const bool in = c0 < nch;
+    const int c = in ? c0 : nch - 1;
+    const V own = *(const V*)(own_p + (int64_t)c * VN);
+    V xb = V(0);
+    if (MET) xb = *(const V*)((const T*)a.xbar + (int64_t)c * VN);
+    V g = V(0);
+#pragma unroll
+    for (int r0 = 0; r0 < R; r0 += RB) {
+      if (r0 >= nb) break;
+      V x[RB];
+#pragma unroll
+      for (int k = 0; k < RB; ++k) x[k] = *(const V*)(X + rowp[r0 + k] + (int64_t)c * VN);
+#pragma unroll
+      for (int k = 0; k < RB; ++k) g += coef[r0 + k] * x[k];
+    }
+    if (nb > 0) g = (pow2 ? g * inv_nb : g / (T)nb) + lam * own;
+    V xn = V(0);
+    if (gout) {
+      if (in) *(V*)((T*)a.g_out + (int64_t)i * ld + (int64_t)c * VN) = g;
+    } else {
+      xn = mix_chunk<T, T>(a, i, c, own) - inv_eta * g;
+      if (in) *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = xn;
+    }
+    if (!in) {
+      xn = V(0);
+      xb = V(0);
+    }
+    if (ZNEXT || MET) {
+#pragma unroll
+      for (int r0 = 0; r0 < R; r0 += RB) {
+        if (r0 >= nb) break;
+        V x[RB];
+#pragma unroll
+        for (int k = 0; k < RB; ++k) x[k] = ld_nt<T>(X + rowp[r0 + k] + (int64_t)c * VN);
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+          if (ZNEXT) zacc[r0 + k] += (double)hsum<T>(x[k] * xn);
+          if (MET) uacc[r0 + k] += (double)hsum<T>(x[k] * xb);
+        }
+      }
+    }
+    if (MET && in) {
+      const V dv = own - xb;
+      cacc += (double)hsum<T>(dv * dv);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    double z = 0.0, u = 0.0;
+    if (ZNEXT) z = wave_sum_dpp(zacc[r]);
+    if (MET) u = wave_sum_dpp(uacc[r]);
+    if (lane == 0) {
+      dred[wave][0][r] = z;
+      dred[wave][1][r] = u;
+    }
+  }
+  if (MET) {
+    const double cs = wave_sum_dpp(cacc);
+    if (lane == 0) cred[wave] = cs;
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < nb) {
+    const int r = threadIdx.x;
+    const int64_t slot = ((int64_t)i * a.bcap + r) * G + grp;
+    if (ZNEXT) a.zpart[slot] = ((dred[0][0][r] + dred[1][0][r]) + dred[2][0][r]) + dred[3][0][r];
+    if (MET) a.upart[slot] = ((dred[0][1][r] + dred[1][1][r]) + dred[2][1][r]) + dred[3][1][r];
+  }
+  if (MET && threadIdx.x == 0) a.cpart[(int64_t)i * G + grp] = ((cred[0] + cred[1]) + cred[2]) + cred[3];
 }
 
 template <typename T, int MODE, int RPW>
@@ -327,14 +519,33 @@ hipError_t launch_split_step(int dtype, bool znext, bool met, const RoundArgs& a
   const bool small = a.b_rows <= 4 * NW;  // rows per worker this step touches
   RoundArgs a2 = a;
   a2.contig = split_contig();
-  // A/B knob (tools/split_ab.py): next-block prefetch measured 1 % slower on C5, so off
+  {  // A/B knob DOPT_SPLIT_EARLYMIX (tools/split_ab.py): the block's mix before its barrier
+    const char* em = getenv("DOPT_SPLIT_EARLYMIX");
+    if (!(em && em[0] == '0')) a2.flags |= F_EARLYMIX;
+  }
+  // A/B knob DOPT_SPLIT_PREFETCH (tools/split_ab.py): the next block's loads in flight through
+  // the block's barrier; complete-graph D-SGD steps with the column sums in T only
+  // (default on: C5 14.60 -> 14.24 ms, and 13.99 with the exact 1/16, interleaved A/B)
   const char* ev = getenv("DOPT_SPLIT_PREFETCH");
-  const bool pf = ev && ev[0] == '1';
+  const bool pf = !(ev && ev[0] == '0') && (a.flags & F_MEAN) && !(a.flags & F_GOUT) &&
+                  (dtype == 1 ? a.colsum != nullptr : a.colsum_t != nullptr);
   // 2 or 4 chunks per lane per block for <= 16 rows when every group still walks >= 2
   // blocks (the slab layout [n][bcap][G] does not depend on the block size)
   const char* cv = getenv("DOPT_SPLIT_CPB");
   int cpb = cv ? atoi(cv) : 1;
-  if (!small || pf || (a.nchunks + 64 * cpb - 1) / (64 * cpb) < 2 * a.groups) cpb = 1;
+  if (!small || (pf && cpb > 2) || (a.nchunks + 64 * cpb - 1) / (64 * cpb) < 2 * a.groups) cpb = 1;
+  // A/B knob DOPT_SPLIT_COLWAVE (tools/split_ab.py): the column-per-wave kernel for <= 16 rows
+  const char* cw = getenv("DOPT_SPLIT_COLWAVE");
+  if (small && cw && cw[0] == '1') {
+#define COLWAVE(T_)                                                                                       \
+  if (znext && met) hipLaunchKernelGGL((k_split_colwave<T_, true, true>), grid, dim3(NT), 0, s, a2);       \
+  else if (znext) hipLaunchKernelGGL((k_split_colwave<T_, true, false>), grid, dim3(NT), 0, s, a2);        \
+  else if (met) hipLaunchKernelGGL((k_split_colwave<T_, false, true>), grid, dim3(NT), 0, s, a2);          \
+  else hipLaunchKernelGGL((k_split_colwave<T_, false, false>), grid, dim3(NT), 0, s, a2);
+    if (dtype == 0) { COLWAVE(float) } else { COLWAVE(double) }
+#undef COLWAVE
+    return hipGetLastError();
+  }
 #define SPLIT_STEP2(T_, R_, P_, C_)                                                                              \
   if (znext && met) hipLaunchKernelGGL((k_split_step<T_, R_, true, true, P_, C_>), grid, dim3(NT), 0, s, a2);     \
   else if (znext) hipLaunchKernelGGL((k_split_step<T_, R_, true, false, P_, C_>), grid, dim3(NT), 0, s, a2);      \
@@ -343,6 +554,7 @@ hipError_t launch_split_step(int dtype, bool znext, bool met, const RoundArgs& a
 #define SPLIT_STEP(T_, R_) if (pf) { SPLIT_STEP2(T_, R_, true, 1) } else { SPLIT_STEP2(T_, R_, false, 1) }
 #define SPLIT_SMALL(T_)                           \
   if (cpb == 4) { SPLIT_STEP2(T_, 4, false, 4) }  \
+  else if (cpb == 2 && pf) { SPLIT_STEP2(T_, 4, true, 2) } \
   else if (cpb == 2) { SPLIT_STEP2(T_, 4, false, 2) } \
   else { SPLIT_STEP(T_, 4) }
   if (dtype == 0) {
