@@ -169,6 +169,12 @@ hipError_t launch_gather_rows(int dtype, const void* x, const int32_t* ids, int6
 hipError_t launch_generate(int dtype, int problem, void* X, void* y, int64_t rows, int64_t d,
                            int64_t ld, uint64_t seed, double flip, double noise, int64_t row_base,
                            hipStream_t s);
+// Single float64 evaluation for rows too long for the row-resident kernel (obj_problems.py
+// API): part[rows x G] partial dots, rowbuf[rows] coefficients (grad) or loss terms
+// (objective), g_out[d] the gradient (grad).  Fixed reduction orders.
+hipError_t launch_wide_eval(const double* X, const double* y, const double* w, int64_t rows, int64_t d, int64_t ld,
+                            int problem, bool grad, double reg, double* part, int G, double* rowbuf, double* g_out,
+                            hipStream_t s);
 // One thread writes the constant-rate wall clock (trainer.py:181 timestamps).
 hipError_t launch_stamp(uint64_t* out, hipStream_t s);
 // float64 host data -> T rows padded to ld (zero padding).

@@ -600,6 +600,61 @@ hipError_t launch_split_coef(int dtype, int problem, int mode, const RoundArgs& 
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------- wide single evaluations
+// The obj_problems.py API (dopt_eval_gradient / dopt_eval_objective) for rows too long for
+// the row-resident kernel, float64: k_wide_dots -> per-row partial dots over column ranges,
+// k_wide_rows -> per row z = sum of partials (fixed order) -> gradient coefficient
+// (obj_problems.py:16-17 / :49-50) or loss term (:5-7 / :41-42), k_wide_colsum -> g_c =
+// sum_k coef_k x_kc in row order (fixed), / b + reg w_c (:18-19 / :51-52).  Not a hot path.
+__global__ __launch_bounds__(NT) void k_wide_dots(const double* __restrict__ X, const double* __restrict__ w,
+                                                  int64_t ld, int64_t d, int G, double* __restrict__ part) {
+  __shared__ double red[NW];
+  const int64_t r = blockIdx.x;
+  const int g = blockIdx.y;
+  const int64_t per = (d + G - 1) / G, c0 = g * per, c1 = c0 + per < d ? c0 + per : d;
+  double acc = 0.0;
+  for (int64_t c = c0 + threadIdx.x; c < c1; c += NT) acc += X[r * ld + c] * w[c];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[r * G + g] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+__global__ __launch_bounds__(NT) void k_wide_rows(const double* __restrict__ part, int G, const double* __restrict__ y,
+                                                  int64_t rows, int problem, int grad, double* __restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (r >= rows) return;
+  double z = 0.0;
+  for (int g = 0; g < G; ++g) z += part[r * G + g];
+  const double yv = y[r];
+  if (grad) out[r] = problem == 0 ? -yv * sigmoid_neg(yv * z) : z - yv;
+  else out[r] = problem == 0 ? row_loss<double, 0>(yv, z) : row_loss<double, 1>(yv, z);
+}
+
+__global__ __launch_bounds__(NT) void k_wide_colsum(const double* __restrict__ X, const double* __restrict__ coef,
+                                                    int64_t ld, int64_t d, int64_t rows, const double* __restrict__ w,
+                                                    double reg, double* __restrict__ g) {
+  const int64_t c = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (c >= d) return;
+  double acc = 0.0;
+  for (int64_t r = 0; r < rows; ++r) acc += coef[r] * X[r * ld + c];
+  g[c] = rows > 0 ? acc / (double)rows + reg * w[c] : 0.0;
+}
+
+hipError_t launch_wide_eval(const double* X, const double* y, const double* w, int64_t rows, int64_t d, int64_t ld,
+                            int problem, bool grad, double reg, double* part, int G, double* rowbuf, double* g_out,
+                            hipStream_t s) {
+  if (rows > 0) {
+    hipLaunchKernelGGL(k_wide_dots, dim3((unsigned)rows, G), dim3(NT), 0, s, X, w, ld, d, G, part);
+    hipLaunchKernelGGL(k_wide_rows, dim3((unsigned)((rows + NT - 1) / NT)), dim3(NT), 0, s, part, G, y, rows,
+                       problem, grad ? 1 : 0, rowbuf);
+  }
+  if (grad)
+    hipLaunchKernelGGL(k_wide_colsum, dim3((unsigned)((d + NT - 1) / NT)), dim3(NT), 0, s, X, rowbuf, ld, d, rows, w,
+                       reg, g_out);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------- column sums
 // Stage 1: workgroup (g, cb) sums rows [g*rpg, (g+1)*rpg) of the 64-chunk column block cb;
 // lane = chunk in the block, the 4 waves split the rows and meet in LDS (fixed order).

@@ -1149,6 +1149,49 @@ int dopt_run_centralized(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_
 
 // ---------------------------------------------------------------------------- single evaluations
 namespace {
+// Rows longer than the row-resident kernel holds (d > 2048 in float64): dots over column
+// ranges, per-row coefficient / loss, column sums of coef * row (kernels.hip k_wide_*).
+int eval_wide(dopt_ctx* c, int problem, int64_t rows, int64_t d, const double* w, const double* X, const double* y,
+              bool grad, double reg, double* out) {
+  const int64_t ld = (d + 1) / 2 * 2, nch = ld / 2;
+  const int G = (int)std::max<int64_t>(1, std::min<int64_t>(64, d / 8192));
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t bX = al((size_t)rows * ld * 8), by = al((size_t)rows * 8 + 8), bw = al((size_t)ld * 8),
+               bp = al((size_t)rows * G * 8 + 8), br = al((size_t)rows * 8 + 8), bg = al((size_t)ld * 8),
+               bout = al(3 * 8);
+  const size_t need = bX + by + bw + bp + br + bg + bout;
+  int rc;
+  if (need > c->sx_cap) {
+    if ((rc = dalloc(&c->sx, need))) return rc;
+    c->sx_cap = need;
+  }
+  char* base = (char*)c->sx;
+  double* dX = (double*)base;
+  double* dy = (double*)(base + bX);
+  double* dw = (double*)(base + bX + by);
+  double* dpart = (double*)(base + bX + by + bw);
+  double* drow = (double*)(base + bX + by + bw + bp);
+  double* dg = (double*)(base + bX + by + bw + bp + br);
+  double* dout = (double*)(base + bX + by + bw + bp + br + bg);
+  if ((rc = upload_rows(c, DOPT_F64, X, 0, dX, rows, d, ld))) return rc;
+  if ((rc = upload_rows(c, DOPT_F64, y, 0, dy, rows, 1, 1))) return rc;
+  if ((rc = upload_rows(c, DOPT_F64, w, 0, dw, 1, d, ld))) return rc;
+  HIPOK(launch_wide_eval(dX, dy, dw, rows, d, ld, problem, grad, reg, dpart, G, drow, dg, c->stream));
+  if (grad) {
+    std::vector<double> g((size_t)d);
+    HIPOK(hipMemcpyAsync(g.data(), dg, (size_t)d * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPOK(hipStreamSynchronize(c->stream));
+    memcpy(out, g.data(), (size_t)d * sizeof(double));
+    return DOPT_OK;
+  }
+  HIPOK(launch_fold(DOPT_F64, nullptr, 0, drow, rows, dw, ld, (int32_t)nch, nullptr, dout + 1, dout + 2, c->stream));
+  double raw[3] = {0.0, 0.0, 0.0};
+  HIPOK(hipMemcpyAsync(raw + 1, dout + 1, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPOK(hipStreamSynchronize(c->stream));
+  finalize_metrics(raw, 1, problem, 1, rows, reg, 0.0, out, nullptr);
+  return DOPT_OK;
+}
+
 int eval_common(dopt_ctx* c, int problem, int64_t rows, int64_t d, const double* w, const double* X,
                 const double* y, bool grad, double reg, double* out) {
   CHECK_ARG(c, "ctx is NULL");
@@ -1161,8 +1204,7 @@ int eval_common(dopt_ctx* c, int problem, int64_t rows, int64_t d, const double*
   const int vn = 2;  // float64
   const int64_t ld = (d + vn - 1) / vn * vn, nch = ld / vn;
   const int cpl = cpl_for(nch);
-  if (cpl > max_chunks_per_lane(DOPT_F64, DOPT_F64))
-    return fail(DOPT_ERR_UNSUPPORTED, "d = %lld exceeds the row-resident kernel limit", (long long)d);
+  if (cpl > max_chunks_per_lane(DOPT_F64, DOPT_F64)) return eval_wide(c, problem, rows, d, w, X, y, grad, reg, out);
   // objective: split rows over workgroups; gradient: one workgroup (one worker)
   const int64_t groups = grad ? 1 : std::max<int64_t>(1, std::min<int64_t>(4096, (rows + 255) / 256));
   // scratch layout (bytes, 16-aligned): X | y | w | g | off | slab | out

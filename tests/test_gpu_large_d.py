@@ -104,3 +104,28 @@ def test_c5_shape_round_spot_check():
     np.testing.assert_allclose(cons[0], np.mean(np.sum((x1 - xbar) ** 2, axis=1)), rtol=1e-3)
     assert np.isfinite(obj[0])
     eng.close()
+
+
+@pytest.mark.parametrize("d", [2100, 5000])
+def test_single_evaluations_wide_rows_vs_oracle(d):
+    """The obj_problems.py API for rows beyond the row-resident kernel (d > 2048 in float64):
+    k_wide_* kernels, rtol 1e-12 against the oracle -- the Simulator's f(x*) evaluation
+    (simulator.py:32-69 calls the objectives) must work at any n_features."""
+    import obj_problems as P
+
+    rng = np.random.default_rng(d)
+    w = rng.standard_normal(d) * 0.05
+    for rows in (1, 13, 700):
+        X = np.hstack([rng.standard_normal((rows, d - 1)), np.ones((rows, 1))])
+        yl = rng.choice([-1.0, 1.0], rows)
+        yq = rng.standard_normal(rows) * 3
+        gl, gq = O.logistic_gradient(w, X, yl, 1e-3), O.quadratic_gradient(w, X, yq, 2e-3)
+        # atol: entries that cancel to ~0 carry the rounding of the others (summation order only)
+        np.testing.assert_allclose(P.logistic_stochastic_gradient(w, X, yl, 1e-3), gl, rtol=1e-12,
+                                   atol=1e-13 * np.abs(gl).max())
+        np.testing.assert_allclose(P.quadratic_stochastic_gradient(w, X, yq, 2e-3), gq, rtol=1e-12,
+                                   atol=1e-13 * np.abs(gq).max())
+        np.testing.assert_allclose(P.logistic_objective(w, X, yl, 1e-3), O.logistic_objective(w, X, yl, 1e-3),
+                                   rtol=1e-12)
+        np.testing.assert_allclose(P.quadratic_objective(w, X, yq, 2e-3), O.quadratic_objective(w, X, yq, 2e-3),
+                                   rtol=1e-12)

@@ -187,3 +187,36 @@ def test_float32_storage_matches_float64_storage():
         np.testing.assert_allclose(a_, b_, rtol=1e-12, atol=1e-15)
     with pytest.raises(ValueError):
         _dopt.Engine(0, "float32", data_dtype="float64")
+
+
+@pytest.mark.parametrize("problem", ["logistic", "quadratic"])
+def test_device_optimum_at_1024_workers(problem):
+    """f(x*) by the device L-BFGS solver (solver.py over dopt_eval_full) at
+    1024 workers: the returned point is stationary for the ORACLE's full gradient
+    (obj_problems.py:22-36 / :55-69 restated), no perturbation improves it, and the float64
+    engine over float32-stored exact rows finds the same optimum."""
+    import solver
+
+    n, d, m, lam = 1024, 256, 32, 1e-3
+    X, y = _shards(problem, n, d, m, 21)
+    X = X.astype(np.float32).astype(np.float64)
+    y = y.astype(np.float32).astype(np.float64)
+    off = np.arange(n + 1, dtype=np.int64) * m
+    shards = [(X[i * m:(i + 1) * m], y[i * m:(i + 1) * m]) for i in range(n)]
+    res = []
+    for xd in (None, "float32"):
+        eng = _dopt.Engine(0, "float64", data_dtype=xd)
+        try:
+            eng.load_shards(problem, X, y, off)
+            res.append(solver.reference_optimum(eng, lam, gtol=1e-10))
+        finally:
+            eng.close()
+    (f_opt, w_opt, info), (f2, w2, _) = res
+    g = O.full_gradient(problem, w_opt, shards, lam)
+    assert np.linalg.norm(g) < 1e-7 * max(1.0, np.linalg.norm(w_opt))
+    f_ref = O.objective(problem, w_opt, X, y, lam)
+    np.testing.assert_allclose(f_opt, f_ref, rtol=1e-12)
+    rng = np.random.default_rng(0)
+    for _ in range(3):
+        assert O.objective(problem, w_opt + 1e-3 * rng.standard_normal(d), X, y, lam) > f_ref
+    np.testing.assert_allclose(f2, f_opt, rtol=1e-10)
