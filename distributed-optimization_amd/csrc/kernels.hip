@@ -75,6 +75,15 @@ __device__ __forceinline__ typename VT<T>::v ld_nt(const T* p) {
 // loaded once per workgroup and shared through LDS instead of by every wave (15.22 vs
 // 15.14 ms).  The kernel waits on memory 78 % of its wave cycles (SQ_WAIT_ANY) at 42 %
 // VALU issue per SIMD.
+// Where the rest goes (round 2, C5, timing-only builds interleaved with this one, same box):
+// WITHOUT the x' store the kernel runs 11.3-11.7 ms instead of 13.3-14.5 (reads alone at
+// 6.4-6.6 TB/s) -- the 4.2 GB of writes cost 1.8-2.8 ms, ~2x what a copy kernel's write share
+// predicts.  Unchanged by: which wave stores (one wave / round robin), nt / sc1 / sc0 sc1
+// stores, a block-major x' layout (each generation writing one contiguous region), a
+// rotated block walk per worker, removing the block barrier (13.8), and more bytes in flight
+// (k_split_glds: 2-3 blocks per wave by LDS-DMA, 15.0-15.2; the no-prefetch kernel capped at
+// 6 / 8 waves per SIMD: 15.3 / 24.8 with spills).  So this kernel is bound by HBM write
+// turnaround, not by latency.
 // LDS-only workgroup barrier: waits for this wave's LDS traffic, not for its global loads
 // (__syncthreads() also drains vmcnt, which would cancel the next block's prefetch).
 __device__ __forceinline__ void lds_barrier() {
@@ -270,6 +279,190 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
       process(A, cb, buf);
     }
   }
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int k = wave + NW * r;
+    const int64_t slot = ((int64_t)i * a.bcap + k) * G + grp;
+    if (ZNEXT) {
+      const double z = wave_sum_dpp(zacc[r]);
+      if (lane == 0 && k < nb) a.zpart[slot] = z;
+    }
+    if (MET) {
+      const double u = wave_sum_dpp(uacc[r]);
+      if (lane == 0 && k < nb) a.upart[slot] = u;
+    }
+  }
+  if (MET && wave == 0) {
+    const double cs = wave_sum_dpp(cacc);
+    if (lane == 0) a.cpart[(int64_t)i * G + grp] = cs;
+  }
+}
+
+// LDS-DMA form of the prefetching step (DOPT_SPLIT_GLDS = D, complete-graph D-SGD steps with
+// the column sums in T, <= 16 rows per worker).  Every load of the block walk is a
+// global_load_lds_dwordx4 (1 KiB per wave instruction, no VGPR destination), so D blocks ahead
+// stay in flight per wave without costing registers: each wave streams its 4 rows' segments
+// into a private D-slot LDS ring; the own-iterate, column-sum and xbar segments go to a
+// workgroup ring of D + 1 slots, one piece per wave (waves 0 / 1 / 2), read by all after the
+// block's barrier.  The waits are counted by hand (s_waitcnt vmcnt(N), N = the loads and stores
+// this wave issued after the block's own; no ordinary global load is in the loop, so hipcc adds
+// no wait of its own), and the block barrier is LDS-only.  Arithmetic is the prefetching
+// kernel's, operation for operation (bitwise the same iterates and partial dots; tested).
+// Measured slower than the register-prefetch kernel at C5 (D = 2 / 3: 15.16 / 15.03 vs 13.32
+// ms, 3 / 2 workgroups per CU by LDS): kept as the A/B knob the write-bound finding rests on.
+__device__ __forceinline__ void vm_wait(int n) {  // s_waitcnt vmcnt(n), n wave-uniform
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;  // never less safe
+  }
+}
+
+// One global_load_lds_dwordx4 (nt: the bytes are read once) into LDS at lds_base + 16 * lane, in
+// inline asm: the builtin form makes hipcc wait vmcnt(0) before every LDS read it cannot prove
+// disjoint from a DMA in flight (all of them, with ring slots indexed at run time).  M0 is set
+// and restored in the same statement (the compiler does not preserve it around asm).
+template <typename V>
+__device__ __forceinline__ void glds16(const V* src, V* lds_base) {
+  const unsigned dst = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds_base;
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(dst)
+               : "memory");
+}
+
+template <typename T, bool ZNEXT, bool MET, int D>
+__global__ __launch_bounds__(NT) void k_split_glds(const RoundArgs a) {
+  using V = typename VT<T>::v;
+  constexpr int VN = VT<T>::n;
+  constexpr int RPW = 4;
+  constexpr int NSM = MET ? 3 : 2;  // workgroup pieces per block: own, column sums (, xbar)
+  __shared__ V rws[NW][D][RPW][64];  // per-wave ring: this wave's rows' segments
+  __shared__ V sml[D + 1][NSM][64];  // workgroup ring: own / sums / xbar segments
+  __shared__ V gred[2][NW][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int i = blockIdx.x, grp = blockIdx.y, G = gridDim.y;
+  const int nch = a.nchunks, nblk = (nch + 63) / 64;
+  const BlockWalk bw(a, grp, G, nblk);
+  const int nloc = bw.b1 > bw.b0 ? (bw.b1 - bw.b0 + bw.st - 1) / bw.st : 0;
+  const int64_t ld = a.ld;
+  const int64_t row0 = a.off[i], m = a.off[i + 1] - row0;
+  const int64_t nb = a.idx ? (a.b < m ? a.b : m) : m;  // <= NW * RPW (host-checked)
+  const T* __restrict__ X = (const T*)a.X;
+  const T* own_p = (const T*)a.x_old + (int64_t)i * ld;
+  const T* sums = (sizeof(T) == 8 && !a.colsum_t) ? (const T*)(const void*)a.colsum : (const T*)a.colsum_t;
+  const T* piece = wave == 0 ? own_p : wave == 1 ? sums : (const T*)a.xbar;  // waves < NSM
+  int64_t rowp[RPW];
+  T coef[RPW];
+  double zacc[RPW], uacc[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int k = wave + NW * r;
+    const bool ok = k < nb;
+    const int64_t lr = ok ? (a.idx ? (int64_t)a.idx[(int64_t)i * a.b + k] : (int64_t)k) : 0;
+    // wave-uniform values read into SGPRs here: the wait for their loads lands before the first
+    // LDS-DMA (hipcc drains every DMA in flight at the first use of an ordinary load's result)
+    rowp[r] = readlane_t<int64_t>((row0 + lr) * ld, 0);  // absent rows re-read the first row (coef 0)
+    coef[r] = readlane_t<T>(ok ? ((const T*)a.coef)[(int64_t)i * a.bcap + k] : T(0), 0);
+    zacc[r] = 0.0;
+    uacc[r] = 0.0;
+  }
+  double cacc = 0.0;
+  const T inv_eta = (T)a.eta, lam = (T)a.lam;
+  const bool pow2 = nb > 0 && (nb & (nb - 1)) == 0;
+  const T inv_nb = nb > 0 ? T(1) / (T)nb : T(0);
+  const double wii = readlane_t<double>((double)((const T*)a.wdiag)[i], 0);
+  // branch-free issue: a block past the walk re-reads the last block, lanes past the row the
+  // row's last chunk, so every wave issues the same loads each block and the counts are static
+  auto chunk_of = [&](int j) {
+    const int cb = bw.b0 + j * bw.st;
+    const int cbc = cb < bw.b1 ? cb : bw.b1 - 1;
+    const int c0 = cbc * 64 + lane;
+    return (int64_t)(c0 < nch ? c0 : nch - 1) * VN;
+  };
+  auto issue_rows = [&](int j) {
+    const int64_t off = chunk_of(j);
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) glds16<V>((const V*)(X + rowp[r] + off), &rws[wave][j % D][r][0]);
+  };
+  auto issue_small = [&](int j) {
+    if (wave < NSM) glds16<V>((const V*)(piece + chunk_of(j)), &sml[j % (D + 1)][wave][0]);
+  };
+  const int s_cnt = wave < NSM ? 1 : 0;  // this wave's loads / stores per block
+  const int t_cnt = wave == 0 ? 1 : 0;
+  if (nloc > 0) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      issue_rows(j);
+      issue_small(j);
+    }
+  }
+  for (int j = 0; j < nloc; ++j) {
+    const int cb = bw.b0 + j * bw.st;
+    const int c = cb * 64 + lane;
+    const bool in = c < nch;
+    // issued after block j's loads: blocks j+1 .. j+D-1 (RPW + s each) and the stores of blocks
+    // j-D+1 .. j-1 that exist
+    vm_wait((D - 1) * (RPW + s_cnt) + t_cnt * (j < D - 1 ? j : D - 1));
+    V rw[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) rw[r] = rws[wave][j % D][r][lane];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read: refill it
+    issue_rows(j + D);
+    V gp = V(0);
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) gp += coef[r] * rw[r];  // absent rows: coef 0
+    gred[j & 1][wave][lane] = gp;
+    lds_barrier();  // every wave's pieces of block j have landed (each waited for its own)
+    const int sl = j % (D + 1);
+    const V own = sml[sl][0][lane];
+    const V sv = sml[sl][1][lane];
+    V xb = V(0);
+    if (MET) xb = sml[sl][2][lane];
+    V g = V(0);
+    if (nb > 0) {
+      const V gs = gred[j & 1][0][lane] + gred[j & 1][1][lane] + gred[j & 1][2][lane] + gred[j & 1][3][lane];
+      g = (pow2 ? gs * inv_nb : gs / (T)nb) + lam * own;
+    }
+    V mixv;
+#pragma unroll
+    for (int e = 0; e < VN; ++e) {
+      const double x = (double)own[e];
+      mixv[e] = (T)(a.w_off * ((double)sv[e] - x) + wii * x);
+    }
+    const V xn = mixv - inv_eta * g;
+    if (wave == 0) {  // every block: the store count stays static (lanes past the row rewrite nothing)
+      if (in) *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = xn;
+    }
+    // slot (j + D) % (D + 1) held block j - 1, which every wave finished reading before this barrier
+    issue_small(j + D);
+    if (ZNEXT && in) {
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) zacc[r] += (double)hsum<T>(rw[r] * xn);
+    }
+    if (MET && in) {
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) uacc[r] += (double)hsum<T>(rw[r] * xb);
+      if (wave == 0) {
+        const V dv = own - xb;
+        cacc += (double)hsum<T>(dv * dv);
+      }
+    }
+  }
+  vm_wait(0);  // no LDS-DMA may land after the workgroup's LDS is handed to the next one
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
     const int k = wave + NW * r;
@@ -531,6 +724,22 @@ hipError_t launch_split_step(int dtype, bool znext, bool met, const RoundArgs& a
                   (dtype == 1 ? a.colsum != nullptr : a.colsum_t != nullptr);
   // 2 or 4 chunks per lane per block for <= 16 rows when every group still walks >= 2
   // blocks (the slab layout [n][bcap][G] does not depend on the block size)
+  // A/B knob DOPT_SPLIT_GLDS = D (2 or 3): the LDS-DMA kernel with D blocks in flight per wave,
+  // where the prefetching kernel would run with <= 16 rows
+  const char* gv = getenv("DOPT_SPLIT_GLDS");
+  const int glds = gv ? atoi(gv) : 0;
+  if (pf && small && (glds == 2 || glds == 3)) {
+#define GLDS2(T_, D_)                                                                                 \
+  if (znext && met) hipLaunchKernelGGL((k_split_glds<T_, true, true, D_>), grid, dim3(NT), 0, s, a2); \
+  else if (znext) hipLaunchKernelGGL((k_split_glds<T_, true, false, D_>), grid, dim3(NT), 0, s, a2);  \
+  else if (met) hipLaunchKernelGGL((k_split_glds<T_, false, true, D_>), grid, dim3(NT), 0, s, a2);    \
+  else hipLaunchKernelGGL((k_split_glds<T_, false, false, D_>), grid, dim3(NT), 0, s, a2);
+#define GLDS(T_) if (glds == 2) { GLDS2(T_, 2) } else { GLDS2(T_, 3) }
+    if (dtype == 0) { GLDS(float) } else { GLDS(double) }
+#undef GLDS
+#undef GLDS2
+    return hipGetLastError();
+  }
   const char* cv = getenv("DOPT_SPLIT_CPB");
   int cpb = cv ? atoi(cv) : 1;
   if (!small || (pf && cpb > 2) || (a.nchunks + 64 * cpb - 1) / (64 * cpb) < 2 * a.groups) cpb = 1;

@@ -62,6 +62,30 @@ def test_split_rounds_vs_oracle(problem, topo, batch, mean, m):
     eng.close()
 
 
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+def test_split_glds_kernel_bitwise_equals_prefetch_kernel(dtype, monkeypatch):
+    """k_split_glds (LDS-DMA ring, DOPT_SPLIT_GLDS = 2 / 3 blocks in flight) does the prefetching
+    kernel's arithmetic operation for operation: iterates and history bitwise equal.  Two
+    column-block groups per worker, so each walks 8-18 blocks (the ring wraps); d = 2100
+    float64 ends in a partial column block."""
+    n, m, T = 9, 12, 5
+    d = 2100 if dtype == "float64" else 9000
+    monkeypatch.setenv("DOPT_SPLIT_WGS", "18")  # read when the layout is set: 2 groups per worker
+    shards = _data(n, d, m, 5, "quadratic")
+    eng = _engine(shards, "quadratic", dtype)
+    eng.set_mixing_mean(*TP.fully_connected(n).uniform_offdiag())
+    out = {}
+    for v in ("0", "2", "3"):
+        monkeypatch.setenv("DOPT_SPLIT_GLDS", v)
+        eng.set_models(np.zeros((n, d)))
+        obj, cons, _ = eng.run_dsgd(T, 0.05, m, 2e-3, 2e-3, 0.1)
+        out[v] = (np.asarray(obj), np.asarray(cons), eng.get_models())
+    for v in ("2", "3"):
+        for a, b in zip(out[v], out["0"]):
+            assert np.array_equal(a, b), v
+    eng.close()
+
+
 def test_split_centralized_vs_oracle():
     n, d, m, T, b = 5, 2100, 10, 4, 3
     shards = _data(n, d, m, 2, "logistic")

@@ -29,13 +29,14 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--workers", type=int, default=4096)
-    ap.add_argument("--mode", default="f32", choices=["f32", "x32"],
+    ap.add_argument("--mode", default="f32", choices=["f32", "x32", "f64"],
                     help="f32: float32 engine (DOPT_KR_VARIANT); x32: float64 arithmetic over float32 rows "
-                         "(DOPT_KRX_VARIANT)")
+                         "(DOPT_KRX_VARIANT); f64: float64 rows (DOPT_KRD_VARIANT)")
     args = ap.parse_args()
     n, d, m = args.workers, 1024, 512
-    knob = "DOPT_KR_VARIANT" if args.mode == "f32" else "DOPT_KRX_VARIANT"
-    eng = _dopt.Engine(0, "float32") if args.mode == "f32" else _dopt.Engine(0, "float64", data_dtype="float32")
+    knob = {"f32": "DOPT_KR_VARIANT", "x32": "DOPT_KRX_VARIANT", "f64": "DOPT_KRD_VARIANT"}[args.mode]
+    eng = {"f32": lambda: _dopt.Engine(0, "float32"), "x32": lambda: _dopt.Engine(0, "float64", data_dtype="float32"),
+           "f64": lambda: _dopt.Engine(0, "float64")}[args.mode]()
     eng.generate_shards("logistic", n, d, m, seed=1000, flip=0.05)
     top = topology.random_regular(n, 4, seed=0)
     eng.set_topology(top.row_ptr, top.col, top.w)
@@ -43,7 +44,8 @@ def main():
     variants = [int(v) for v in args.variants.split(",")]
     times = {v: [] for v in variants}
     ref = None
-    bytes_per = 4 * n * (m * d + m) + (4 if args.mode == "f32" else 8) * n * 2 * d
+    xs = 8 if args.mode == "f64" else 4
+    bytes_per = xs * n * (m * d + m) + (4 if args.mode == "f32" else 8) * n * 2 * d
     for rep in range(args.reps):
         for v in variants:
             if v < 0:
