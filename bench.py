@@ -156,25 +156,12 @@ def _chunks_per_lane(d, xesz):
     return cpl
 
 
-def kernel_name(eng, problem, d, m, b):
-    """Name of the round kernel instance run_dsgd launches for this context (the dispatch of
-    k_round.inc: default variant per element-type pair, deferred loss terms and F_BIP)."""
+def kernel_name():
+    """Instance name (rocprofv3's spelling) of the gradient-round kernel the runtime launched last
+    (dopt_last_round_kernel: recorded by the launcher, not re-derived here)."""
     import _dopt
 
-    esz = 4 if eng.dtype == _dopt.F32 else 8
-    xesz = 4 if eng.data_dtype == _dopt.F32 else 8
-    tname, sname = ("float" if esz == 4 else "double"), ("float" if xesz == 4 else "double")
-    cpl = _chunks_per_lane(d, xesz)
-    if cpl > 16 or (esz != xesz and cpl > 8):
-        return f"void dopt::k_split_step<{tname}, {4 if m <= 16 else 16}, true, true, false, 1>(dopt::RoundArgs)"
-    base = 35 | 2048 | 4096 | 8192
-    if esz != xesz:
-        var = base | 131072 | (16384 if 0 < m <= 1024 else 0)
-    else:
-        var = base | 256 if cpl <= 4 else base
-    if b < m:
-        var |= 64
-    return f"void dopt::k_round<{tname}, {sname}, {cpl}, {0 if problem == 'logistic' else 1}, true, true, {var}>(dopt::RoundArgs)"
+    return _dopt.last_round_kernel() or "unknown"
 
 
 def bytes_per_round(eng, n, d, m):
@@ -229,7 +216,7 @@ def secondary_leg(dev, dtype, data_dtype, top, n, d, m, steps, warmup, lam, eta0
         return {"value": n * steps / dt, "unit": "worker-iters/s", "ms_per_step": dt / steps * 1e3,
                 "dtype": "f32" if eng.dtype == _dopt.F32 else "f64",
                 "storage": "f32" if eng.data_dtype == _dopt.F32 else "f64",
-                "kernel": kernel_name(eng, "logistic", d, m, m), "kernel_avg_ms": avg * 1e3,
+                "kernel": kernel_name(), "kernel_avg_ms": avg * 1e3,
                 "kernel_launches_timed": launches, "bytes_per_launch": bpl,
                 "roofline_frac": bpl / avg / 1e9 / HBM_PEAK_GBS, "final_objective": float(obj[-1])}
     finally:
@@ -430,7 +417,7 @@ def main():
 
     esz = 4 if eng.dtype == _dopt.F32 else 8
     xesz = 4 if eng.data_dtype == _dopt.F32 else 8
-    kname = kernel_name(eng, problem, d, m, b)
+    kname = kernel_name()
     traffic, traffic_src = pmc_traffic(kname) if args.config == "c3" and n == 4096 and world == 1 else (None, None)
     bytes_per_launch = bytes_per_round(eng, n, d, m)
     avg_s = (kr_ms / launches) * 1e-3 if launches else float("nan")

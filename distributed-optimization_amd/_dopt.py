@@ -42,6 +42,8 @@ _SIGS = {
     "dopt_last_error": ([], ctypes.c_char_p),
     "dopt_mt_choice": ([_P, _P, _I64, _I64, _P], ctypes.c_int),
     "dopt_mt_choice_rounds": ([_P, _P, _I64, _I64, _P, _I64, _P], ctypes.c_int),
+    "dopt_mt_advance_rounds": ([_P, _P, _I64, _I64, _P], ctypes.c_int),
+    "dopt_last_round_kernel": ([], ctypes.c_char_p),
     "dopt_device_count": ([_P], ctypes.c_int),
     "dopt_create": ([ctypes.c_int, ctypes.c_int, _P], ctypes.c_int),
     "dopt_destroy": ([_P], ctypes.c_int),
@@ -175,6 +177,20 @@ def mt_choice_rounds(T, shard_rows, b):
                                       int(b), _ptr(out)))
     _set_np_state(st, key, pos)
     return out
+
+
+def last_round_kernel():
+    """Instance name of the last gradient-round kernel launched in this process ('' before any)."""
+    return lib().dopt_last_round_kernel().decode()
+
+
+def mt_advance_rounds(T, shard_rows):
+    """Advance numpy's global legacy state as T rounds x N workers of choice() draws would
+    (full-shard batches: the indices are discarded, worker.py:27)."""
+    st, key, pos = _get_np_state()
+    rows = np.ascontiguousarray(shard_rows, dtype=np.int64)
+    check(lib().dopt_mt_advance_rounds(_ptr(key), ctypes.byref(pos), int(T), len(rows), _ptr(rows)))
+    _set_np_state(st, key, pos)
 
 
 # ---------------------------------------------------------------------------- device engine

@@ -104,6 +104,9 @@ struct FoldArgs {
 // grad / met select the variant.
 hipError_t launch_round(int dtype, int xdtype, int problem, int cpl, bool grad, bool met, const RoundArgs& a,
                         int n_groups, hipStream_t s);
+// The instance name (rocprofv3's spelling) of the last gradient-round kernel launched --
+// k_round or the column-blocked step -- for reports (dopt_last_round_kernel).
+void note_round_kernel(const char* name);
 int max_chunks_per_lane(int dtype, int xdtype);
 // per element-type pair (round_f32.hip / round_f64.hip / round_x32.hip)
 hipError_t launch_round_f32(int problem, int cpl, bool grad, bool met, const RoundArgs& a, int n_groups,

@@ -4,7 +4,10 @@
 #pragma once
 #include <math.h>
 #include <stdlib.h>
+#include <stdio.h>
 #include <string.h>
+
+#include <string>
 
 #include <type_traits>
 

@@ -705,9 +705,17 @@ static int split_contig() {
   return v ? atoi(v) != 0 : 0;
 }
 
+static void note_split(const char* kernel, int dtype, const char* params) {
+  char buf[160];
+  snprintf(buf, sizeof(buf), "void dopt::%s<%s, %s>(dopt::RoundArgs)", kernel, dtype == 0 ? "float" : "double", params);
+  note_round_kernel(buf);
+}
+static const char* tf(bool b) { return b ? "true" : "false"; }
+
 hipError_t launch_split_step(int dtype, bool znext, bool met, const RoundArgs& a, int n_workers,
                              hipStream_t s) {
   if (n_workers <= 0) return hipSuccess;
+  char params[96];
   const dim3 grid(n_workers, a.groups);
   const bool small = a.b_rows <= 4 * NW;  // rows per worker this step touches
   RoundArgs a2 = a;
@@ -734,6 +742,8 @@ hipError_t launch_split_step(int dtype, bool znext, bool met, const RoundArgs& a
   else if (znext) hipLaunchKernelGGL((k_split_glds<T_, true, false, D_>), grid, dim3(NT), 0, s, a2);  \
   else if (met) hipLaunchKernelGGL((k_split_glds<T_, false, true, D_>), grid, dim3(NT), 0, s, a2);    \
   else hipLaunchKernelGGL((k_split_glds<T_, false, false, D_>), grid, dim3(NT), 0, s, a2);
+    snprintf(params, sizeof(params), "%s, %s, %d", tf(znext), tf(met), glds);
+    note_split("k_split_glds", dtype, params);
 #define GLDS(T_) if (glds == 2) { GLDS2(T_, 2) } else { GLDS2(T_, 3) }
     if (dtype == 0) { GLDS(float) } else { GLDS(double) }
 #undef GLDS
@@ -746,6 +756,8 @@ hipError_t launch_split_step(int dtype, bool znext, bool met, const RoundArgs& a
   // A/B knob DOPT_SPLIT_COLWAVE (tools/split_ab.py): the column-per-wave kernel for <= 16 rows
   const char* cw = getenv("DOPT_SPLIT_COLWAVE");
   if (small && cw && cw[0] == '1') {
+    snprintf(params, sizeof(params), "%s, %s", tf(znext), tf(met));
+    note_split("k_split_colwave", dtype, params);
 #define COLWAVE(T_)                                                                                       \
   if (znext && met) hipLaunchKernelGGL((k_split_colwave<T_, true, true>), grid, dim3(NT), 0, s, a2);       \
   else if (znext) hipLaunchKernelGGL((k_split_colwave<T_, true, false>), grid, dim3(NT), 0, s, a2);        \
@@ -766,6 +778,9 @@ hipError_t launch_split_step(int dtype, bool znext, bool met, const RoundArgs& a
   else if (cpb == 2 && pf) { SPLIT_STEP2(T_, 4, true, 2) } \
   else if (cpb == 2) { SPLIT_STEP2(T_, 4, false, 2) } \
   else { SPLIT_STEP(T_, 4) }
+  snprintf(params, sizeof(params), "%d, %s, %s, %s, %d", small ? 4 : 16, tf(znext), tf(met),
+           tf(small ? (cpb == 4 ? false : pf) : pf), small ? cpb : 1);
+  note_split("k_split_step", dtype, params);
   if (dtype == 0) {
     if (small) { SPLIT_SMALL(float) } else { SPLIT_STEP(float, 16) }
   } else {

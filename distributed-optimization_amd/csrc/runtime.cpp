@@ -724,11 +724,15 @@ int check_run(dopt_ctx* c, int64_t T, int64_t batch, const int32_t* idx, bool ne
 
 }  // namespace
 
+static std::string g_round_kernel;
+void dopt::note_round_kernel(const char* name) { g_round_kernel = name; }
+
 // ============================================================================ C ABI
 extern "C" {
 
 int dopt_abi_version(void) { return DOPT_ABI_VERSION; }
 const char* dopt_last_error(void) { return g_err.c_str(); }
+const char* dopt_last_round_kernel(void) { return g_round_kernel.c_str(); }
 
 int dopt_device_count(int* count) {
   CHECK_ARG(count, "count is NULL");

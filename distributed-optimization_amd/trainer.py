@@ -273,16 +273,19 @@ def _index_chunks(workers, T, config):
             yield t, min(ch, T - t), b, None
         return
     # Full shards: the indices are discarded but the stream must still advance (every
-    # choice() is a whole permutation of m_i, whatever b is), so draw with b = 1 -- the
-    # same stream consumption without writing b (possibly >> m) indices per worker.
-    b_draw = min(b, 1) if full else b
+    # choice() is a whole permutation of m_i, whatever b is): advance it without making them.
+    b_draw = 1 if full else b
     ch = max(1, min(IDX_CHUNK_ROUNDS, IDX_CHUNK_ELEMS // max(1, len(workers) * max(b_draw, 1))))
 
     def draws():
         for t in range(0, T, ch):
             n = min(ch, T - t)
-            idx = _dopt.mt_choice_rounds(n, rows, b_draw)  # advances np.random exactly like the reference
-            yield t, n, b, (None if full else idx)
+            if full:  # the stream advance alone (dopt_mt_advance_rounds): no indices are made
+                _dopt.mt_advance_rounds(n, rows)
+                yield t, n, b, None
+            else:
+                idx = _dopt.mt_choice_rounds(n, rows, b_draw)  # advances np.random exactly like the reference
+                yield t, n, b, idx
 
     yield from _one_ahead(draws())
 

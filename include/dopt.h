@@ -55,6 +55,9 @@ typedef struct dopt_ctx dopt_ctx;
 
 int dopt_abi_version(void);
 const char *dopt_last_error(void);
+/* Instance name (rocprofv3's spelling) of the last gradient-round kernel launched in this
+ * process -- the fused round kernel or the column-blocked step -- or "" (reports only). */
+const char *dopt_last_round_kernel(void);
 
 /* ------------------------------------------------------------------ host only
  * Legacy-MT19937 minibatch sampler: bit-exact with np.random.choice(m, b,
@@ -70,6 +73,13 @@ int dopt_mt_choice(uint32_t key[624], int32_t *pos, int64_t m, int64_t b, int64_
  * [T][N][b] int32 local row ids; entries past min(b, m_i) are set to -1. */
 int dopt_mt_choice_rounds(uint32_t key[624], int32_t *pos, int64_t T, int64_t n_workers,
                           const int64_t *shard_rows, int64_t b, int32_t *out);
+
+/* The same stream advance without the indices: what T rounds x N workers of
+ * Worker.get_mini_batch consume when every draw's result is discarded (full-shard
+ * batches: each np.random.choice is a whole permutation of m_i whatever b is,
+ * worker.py:27).  Replaces the draws of trainer.py:166 when local_batch_size >= m. */
+int dopt_mt_advance_rounds(uint32_t key[624], int32_t *pos, int64_t T, int64_t n_workers,
+                           const int64_t *shard_rows);
 
 /* ------------------------------------------------------------------ device */
 int dopt_device_count(int *count);

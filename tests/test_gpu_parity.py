@@ -567,3 +567,20 @@ def test_trainer_stores_float32_representable_shards_as_float32():
         h, _, _, _ = O.run_decentralized(sh, topology.ring(n).dense_W(), T, cfg, Xs, yf, 0.0, rng_state=st)
         _close(hist["objective"], h["objective"], RTOL64)
         _close(hist["consensus_error"], h["consensus_error"], RTOL64)
+
+
+def test_last_round_kernel_names_the_launched_instance():
+    """dopt_last_round_kernel (what bench.py reports as the timed kernel) names the instance the
+    dispatcher picked: float64 fused round kernel, and the column-blocked step for long rows."""
+    rng = np.random.default_rng(3)
+    for d, want in ((50, "void dopt::k_round<double, double, 1, 1, true, true, "),
+                    (2100, "void dopt::k_split_step<double, 4, true, true, ")):
+        n, m = 4, 8
+        X = rng.standard_normal((n * m, d))
+        eng = _dopt.Engine(0, "float64")
+        eng.load_shards("quadratic", X, rng.standard_normal(n * m), np.arange(0, n * m + 1, m))
+        top = topology.build("ring", n)
+        eng.set_topology(top.row_ptr, top.col, top.w)
+        eng.run_dsgd(2, 0.05, m, 1e-3, 1e-3, 0.0)
+        assert _dopt.last_round_kernel().startswith(want), _dopt.last_round_kernel()
+        eng.close()

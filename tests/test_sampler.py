@@ -140,3 +140,44 @@ def test_prefetched_draw_is_undone_when_the_run_stops_early():
     st = np.random.get_state()
     assert st[2] == expect_state[2]
     np.testing.assert_array_equal(st[1], expect_state[1])
+
+
+@pytest.mark.parametrize("start_draws", [0, 1, 313])
+def test_rounds_long_stream_through_the_block_ring(start_draws):
+    """Many more MT19937 blocks than the generator thread's ring holds (BlockRing::kSlots = 64),
+    starting mid-block: indices and the state left behind equal numpy's, call by call."""
+    rows, T, b = [300, 0, 1, 257, 300, 31], 40, 7
+    np.random.seed(19)
+    np.random.randint(0, 2 ** 16, size=start_draws)  # leaves pos mid-block
+    st0 = np.random.get_state()
+    out = _dopt.mt_choice_rounds(T, rows, b)
+    st_ours = np.random.get_state()
+    np.random.set_state(st0)
+    for t in range(T):
+        for i, m in enumerate(rows):
+            eb = 0 if m == 0 else min(b, m)
+            if eb:
+                np.testing.assert_array_equal(out[t, i, :eb], np.random.choice(m, eb, replace=False))
+    st = np.random.get_state()
+    assert st[2] == st_ours[2]
+    np.testing.assert_array_equal(st[1], st_ours[1])
+
+
+@pytest.mark.parametrize("rows", [[512] * 64, [0, 1, 2, 999, 5000]])
+def test_advance_rounds_leaves_numpy_state_where_numpy_does(rows):
+    """dopt_mt_advance_rounds (full-shard batches: indices discarded) consumes exactly what
+    T x N np.random.choice calls consume (trainer.py:166, worker.py:27)."""
+    T = 12
+    np.random.seed(23)
+    np.random.randint(0, 10, size=5)
+    st0 = np.random.get_state()
+    _dopt.mt_advance_rounds(T, rows)
+    st_ours = np.random.get_state()
+    np.random.set_state(st0)
+    for _ in range(T):
+        for m in rows:
+            if m:
+                np.random.choice(m, m, replace=False)
+    st = np.random.get_state()
+    assert st[2] == st_ours[2]
+    np.testing.assert_array_equal(st[1], st_ours[1])
