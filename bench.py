@@ -404,7 +404,10 @@ def main():
 
     def barrier():
         if world > 1:
-            dist.barrier()
+            if args.backend == "nccl":
+                dist.barrier(device_ids=[dev])  # this rank's GPU, not one guessed from the rank
+            else:
+                dist.barrier()
         torch.cuda.synchronize(dev)
 
     log(f"warmup {args.warmup}, timing {args.steps} rounds")

@@ -257,20 +257,32 @@ def _batch_size(workers):
     return bs.pop() if bs else 0
 
 
-def _index_chunks(workers, T, config):
-    """Yield (t_start, n_rounds, idx or None): minibatch indices drawn on the host in
-    trainer order (trainer.py:47-50 / :166), `None` when every batch is the full shard.
-    The legacy MT19937 stream is sequential, so the draw runs one chunk AHEAD on a host
-    thread (the C sampler releases the GIL) while the device runs the current chunk."""
+def _index_chunks(workers, T, config, t_begin=0, max_chunk=0):
+    """Yield (t_start, n_rounds, b, idx or None, rng_state): minibatch indices drawn on the
+    host in trainer order (trainer.py:47-50 / :166), `None` when every batch is the full
+    shard; rng_state = numpy's legacy state right after this chunk's draws (what a
+    checkpoint taken after the chunk records).  Rounds t_begin .. T-1; chunks of at most
+    max_chunk rounds (0: no limit) starting at multiples of it.  The legacy MT19937 stream
+    is sequential, so the draw runs one chunk AHEAD on a host thread (the C sampler
+    releases the GIL) while the device runs the current chunk."""
     b = _batch_size(workers)
     rows = np.array([w.n_local_samples for w in workers], dtype=np.int64)
     full = b >= (rows.max() if len(rows) else 0)
     mode = config.get("sampling", "legacy")
     skip_rng = (full and mode == "full") or mode == "device"  # device: the GPU draws the minibatches
+
+    def bounds(ch):  # chunks of <= ch rounds that never cross a multiple of max_chunk
+        t = t_begin
+        while t < T:
+            n = min(ch, T - t)
+            if max_chunk > 0:
+                n = min(n, max_chunk - t % max_chunk)
+            yield t, n
+            t += n
+
     if skip_rng:
-        ch = max(1, T)
-        for t in range(0, T, ch):
-            yield t, min(ch, T - t), b, None
+        for t, n in bounds(max(1, T)):
+            yield t, n, b, None, np.random.get_state()
         return
     # Full shards: the indices are discarded but the stream must still advance (every
     # choice() is a whole permutation of m_i, whatever b is): advance it without making them.
@@ -278,16 +290,74 @@ def _index_chunks(workers, T, config):
     ch = max(1, min(IDX_CHUNK_ROUNDS, IDX_CHUNK_ELEMS // max(1, len(workers) * max(b_draw, 1))))
 
     def draws():
-        for t in range(0, T, ch):
-            n = min(ch, T - t)
+        for t, n in bounds(ch):
             if full:  # the stream advance alone (dopt_mt_advance_rounds): no indices are made
                 _dopt.mt_advance_rounds(n, rows)
-                yield t, n, b, None
+                yield t, n, b, None, np.random.get_state()
             else:
                 idx = _dopt.mt_choice_rounds(n, rows, b_draw)  # advances np.random exactly like the reference
-                yield t, n, b, idx
+                yield t, n, b, idx, np.random.get_state()
 
     yield from _one_ahead(draws())
+
+
+class _Checkpoint:
+    """Checkpoint / resume (the reference keeps its state in memory only):
+    config 'checkpoint_path' + 'checkpoint_every' (rounds; 0 = at the end of run only) save,
+    after every such round, the iterates (N x d, or the global model), the round count t,
+    the history so far, floats transmitted and numpy's legacy RNG state as of the last
+    consumed draw; config 'resume_from' restarts run(n_iterations) at round t of that file.
+    A resumed run continues bit for bit: the iterates, the learning-rate schedule
+    (eta0 / sqrt(t+1), trainer.py:138-140) and the minibatch stream pick up where they were.
+    The file is an .npz (no pickles) written to a temporary name and renamed."""
+
+    def __init__(self, cfg, kind, trainer, rank=0):
+        self.path = cfg.get("checkpoint_path")
+        self.every = int(cfg.get("checkpoint_every", 0) or 0)
+        self.resume = cfg.get("resume_from")
+        self.kind, self.tr, self.rank = kind, trainer, rank
+        self.meta = {"kind": kind, "n_workers": trainer.n_workers, "n_features": trainer.n_features,
+                     "problem_type": cfg["problem_type"], "topology": getattr(trainer, "topology", "")}
+
+    def max_chunk(self):
+        return self.every if self.path and self.every > 0 else 0
+
+    def due(self, t_done, T):
+        return bool(self.path) and ((self.every > 0 and t_done % self.every == 0) or t_done == T)
+
+    def load(self, T):
+        """(t, state array, time offset) from 'resume_from', history / floats / RNG restored,
+        or (0, None, 0.0) without one."""
+        if not self.resume:
+            return 0, None, 0.0
+        with np.load(self.resume, allow_pickle=False) as z:
+            got = {k: (str(z[k]) if z[k].dtype.kind == "U" else int(z[k])) for k in self.meta}
+            if got != self.meta:
+                raise ValueError(f"checkpoint {self.resume} does not match this trainer: {got} vs {self.meta}")
+            t = int(z["t"])
+            if t > T:
+                raise ValueError(f"checkpoint {self.resume} is at round {t} > n_iterations = {T}")
+            for key in self.tr.history:
+                self.tr.history[key] = list(z[f"history_{key}"])
+            self.tr.total_floats_transmitted = int(z["floats"])
+            np.random.set_state(("MT19937", z["rng_key"], int(z["rng_pos"]), int(z["rng_has_gauss"]),
+                                 float(z["rng_gauss"])))
+            state = np.array(z["state"])
+            offset = float(self.tr.history["time"][-1]) if self.tr.history["time"] else 0.0
+        return t, state, offset
+
+    def save(self, t, state, rng_state):
+        if self.rank != 0:
+            return
+        arrays = {k: np.array(v) for k, v in self.meta.items()}
+        arrays.update({f"history_{k}": np.asarray(v, dtype=np.float64) for k, v in self.tr.history.items()})
+        arrays.update(t=np.int64(t), state=np.asarray(state, dtype=np.float64),
+                      floats=np.int64(self.tr.total_floats_transmitted),
+                      rng_key=np.asarray(rng_state[1], dtype=np.uint32), rng_pos=np.int64(rng_state[2]),
+                      rng_has_gauss=np.int64(rng_state[3]), rng_gauss=np.float64(rng_state[4]))
+        tmp = self.path + ".tmp.npz"
+        np.savez(tmp, **arrays)
+        os.replace(tmp, self.path)
 
 
 def _one_ahead(gen):
@@ -371,10 +441,15 @@ class CentralizedTrainer:
                                          start_time, cfg)
         eng = _engine(self.workers, self.n_features, cfg, X_full=X_full, y_full=y_full)
         want_obj = _set_objective_data(eng, self.workers, self.n_features, X_full, y_full)
+        T = int(n_iterations)
+        ck = _Checkpoint(cfg, "centralized", self)
+        t_begin, state, t_off = ck.load(T)
+        if state is not None:
+            self.x_global = state
         eng.set_global(self.x_global)
-        with closing(_index_chunks(self.workers, int(n_iterations), cfg)) as chunks:
-            for t0, n, b, idx in chunks:
-                t_host = time.time() - start_time
+        with closing(_index_chunks(self.workers, T, cfg, t_begin, ck.max_chunk())) as chunks:
+            for t0, n, b, idx, rng in chunks:
+                t_host = time.time() - start_time + t_off
                 obj, tim = eng.run_centralized(n, cfg["learning_rate_eta0"], b, lam_grad, reg_param, f_opt, idx=idx,
                                                t0=t0, objective=want_obj)
                 if want_obj:
@@ -382,6 +457,8 @@ class CentralizedTrainer:
                 self.history["time"].extend((tim + t_host).tolist())
                 # trainer.py:50,60-61: N*d up + N*d down per round (Python ints)
                 self.total_floats_transmitted += n * (self.n_workers * self.n_features * 2)
+                if ck.due(t0 + n, T):
+                    ck.save(t0 + n, eng.get_global(), rng)
         self.x_global = eng.get_global()
         _warn_nonfinite(self.history, self.config)
         print(f"C-SGD training finished. Time: {time.time() - start_time:.2f}sseconds")
@@ -399,16 +476,22 @@ class CentralizedTrainer:
                                     np.zeros(0, np.int32), np.zeros(world + 1, np.int64), None, None, None)
         runner = distributed.DistributedCentralized(eng, plan, self.n_workers, rows_global, device=_device(cfg),
                                                     obj_sep=sep)
+        ck = _Checkpoint(cfg, "centralized", self, rank)
+        t_begin, state, t_off = ck.load(T)
+        if state is not None:
+            self.x_global = state
         eng.set_global(self.x_global)
-        with closing(_index_chunks(self.workers, T, cfg)) as chunks:
-            for t0, n, b, idx in chunks:
-                t_host = time.time() - start_time
+        with closing(_index_chunks(self.workers, T, cfg, t_begin, ck.max_chunk())) as chunks:
+            for t0, n, b, idx, rng in chunks:
+                t_host = time.time() - start_time + t_off
                 obj = runner.run(n, cfg["learning_rate_eta0"], b, lam_grad, reg_param, f_opt, t0=t0, objective=want_obj,
                                  idx=None if idx is None else idx[:, lo:hi])
                 if want_obj:
                     self.history["objective"].extend(list(obj))
-                self.history["time"].extend(list(np.linspace(t_host, time.time() - start_time, n + 1)[1:]))
+                self.history["time"].extend(list(np.linspace(t_host, time.time() - start_time + t_off, n + 1)[1:]))
                 self.total_floats_transmitted += n * (self.n_workers * self.n_features * 2)
+                if ck.due(t0 + n, T):
+                    ck.save(t0 + n, eng.get_global(), rng)  # every rank holds the same global model
         self.x_global = eng.get_global()
         _warn_nonfinite(self.history, self.config)
         _say(f"C-SGD training finished. Time: {time.time() - start_time:.2f}sseconds", cfg)
@@ -477,11 +560,15 @@ class DecentralizedTrainer:
             eng.set_mixing_mean(*uni)
         else:
             eng.set_topology(t.row_ptr, t.col, t.w)
-        eng.set_models(np.stack([np.asarray(w.x, dtype=np.float64) for w in self.workers]))
+        T = int(n_iterations)
+        ck = _Checkpoint(cfg, "decentralized", self)
+        t_begin, state, t_off = ck.load(T)
+        eng.set_models(state if state is not None else np.stack([np.asarray(w.x, dtype=np.float64)
+                                                                 for w in self.workers]))
         iteration_transmission = np.sum(self.degrees) * self.n_features  # trainer.py:169
-        with closing(_index_chunks(self.workers, int(n_iterations), cfg)) as chunks:
-            for t0, n, b, idx in chunks:
-                t_host = time.time() - start_time
+        with closing(_index_chunks(self.workers, T, cfg, t_begin, ck.max_chunk())) as chunks:
+            for t0, n, b, idx, rng in chunks:
+                t_host = time.time() - start_time + t_off
                 obj, cons, tim = eng.run_dsgd(n, cfg["learning_rate_eta0"], b, lam_grad, reg_param, f_opt, idx=idx,
                                               t0=t0, objective=want_obj, consensus=True)
                 self.history["consensus_error"].extend(list(cons))
@@ -490,6 +577,8 @@ class DecentralizedTrainer:
                 self.history["time"].extend((tim + t_host).tolist())
                 for _ in range(n):
                     self.total_floats_transmitted += iteration_transmission
+                if ck.due(t0 + n, T):
+                    ck.save(t0 + n, eng.get_models(), rng)
         models = eng.get_models()
         for i, worker in enumerate(self.workers):  # trainer.py:178-179: row views
             worker.x = models[i, :]
@@ -508,23 +597,28 @@ class DecentralizedTrainer:
         plan = distributed.build_plan(t, world, rank)
         eng = _engine(self.workers, self.n_features, cfg, plan.lo, plan.hi, X_full=X_full, y_full=y_full)
         want_obj, rows_global, sep = _dist_objective(eng, self.workers, self.n_features, X_full, y_full, rank, world)
-        eng.set_models(np.stack([np.asarray(w.x, dtype=np.float64) for w in self.workers[plan.lo:plan.hi]]))
+        ck = _Checkpoint(cfg, "decentralized", self, rank)
+        t_begin, state, t_off = ck.load(T)
+        x0 = state if state is not None else np.stack([np.asarray(w.x, dtype=np.float64) for w in self.workers])
+        eng.set_models(np.ascontiguousarray(x0[plan.lo:plan.hi]))
         runner = distributed.DistributedDSGD(eng, plan, self.n_workers, rows_global, device=_device(cfg),
                                              mean=None if uni is None else (uni[0], uni[1][plan.lo:plan.hi]),
                                              obj_sep=sep)
         iteration_transmission = np.sum(self.degrees) * self.n_features  # trainer.py:169
-        with closing(_index_chunks(self.workers, T, cfg)) as chunks:
-            for t0, n, b, idx in chunks:
-                t_host = time.time() - start_time
+        with closing(_index_chunks(self.workers, T, cfg, t_begin, ck.max_chunk())) as chunks:
+            for t0, n, b, idx, rng in chunks:
+                t_host = time.time() - start_time + t_off
                 obj, cons = runner.run(n, cfg["learning_rate_eta0"], b, lam_grad, reg_param, f_opt, t0=t0,
                                        objective=want_obj, consensus=True,
                                        idx=None if idx is None else idx[:, plan.lo:plan.hi])
                 self.history["consensus_error"].extend(list(cons))
                 if want_obj:
                     self.history["objective"].extend(list(obj))
-                self.history["time"].extend(list(np.linspace(t_host, time.time() - start_time, n + 1)[1:]))
+                self.history["time"].extend(list(np.linspace(t_host, time.time() - start_time + t_off, n + 1)[1:]))
                 for _ in range(n):
                     self.total_floats_transmitted += iteration_transmission
+                if ck.due(t0 + n, T):
+                    ck.save(t0 + n, runner.gather_models(), rng)  # collective: every rank gathers, rank 0 writes
         models = runner.gather_models()
         for i, worker in enumerate(self.workers):
             worker.x = models[i, :]

@@ -134,7 +134,7 @@ def test_prefetched_draw_is_undone_when_the_run_stops_early():
     expect_state = np.random.get_state()
     np.random.seed(11)
     with closing(trainer._index_chunks(ws, 3 * trainer.IDX_CHUNK_ROUNDS, {})) as chunks:
-        t0, n, b, idx = next(chunks)
+        t0, n, b, idx, _ = next(chunks)
     assert (t0, n, b) == (0, trainer.IDX_CHUNK_ROUNDS, 4)
     np.testing.assert_array_equal(idx, expect_first)
     st = np.random.get_state()
@@ -181,3 +181,38 @@ def test_advance_rounds_leaves_numpy_state_where_numpy_does(rows):
     st = np.random.get_state()
     assert st[2] == st_ours[2]
     np.testing.assert_array_equal(st[1], st_ours[1])
+
+
+@pytest.mark.parametrize("batch,max_chunk,t_begin", [(4, 7, 0), (4, 7, 10), (10 ** 6, 5, 3), (4, 0, 0)])
+def test_index_chunks_boundaries_and_rng_states(batch, max_chunk, t_begin):
+    """trainer._index_chunks (host side of checkpoint / resume): chunks cover rounds
+    t_begin .. T-1 in order, never cross a multiple of max_chunk, and each carries numpy's
+    state right after its own draws (the state a checkpoint after that chunk records)."""
+    from contextlib import closing
+
+    from trainer import _index_chunks
+
+    class W:
+        def __init__(self, m):
+            self.n_local_samples, self.batch_size = m, batch
+
+    ws = [W(m) for m in (30, 30, 17)]
+    T = 23
+    np.random.seed(4)
+    st0 = np.random.get_state()
+    with closing(_index_chunks(ws, T, {"sampling": "legacy"}, t_begin, max_chunk)) as chunks:
+        got = [(t0, n, idx, st) for t0, n, _, idx, st in chunks]
+    assert [g[0] for g in got] == list(np.cumsum([t_begin] + [g[1] for g in got[:-1]]))
+    assert got[-1][0] + got[-1][1] == T
+    if max_chunk:
+        assert all((t0 % max_chunk) + n <= max_chunk for t0, n, _, _ in got)
+    np.random.set_state(st0)
+    for t0, n, idx, st in got:
+        for t in range(n):
+            for i, w in enumerate(ws):
+                eb = min(batch, w.n_local_samples)
+                want = np.random.choice(w.n_local_samples, eb, replace=False)
+                if idx is not None:
+                    np.testing.assert_array_equal(idx[t, i, :eb], want)
+        now = np.random.get_state()
+        assert now[2] == st[2] and np.array_equal(now[1], st[1])
