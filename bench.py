@@ -174,14 +174,23 @@ def bytes_per_round(eng, n, d, m):
     return n * (xesz * (m * d + m) + esz * 2 * d)
 
 
-def timed_leg(eng, rounds, steps, warmup, n_models, d, barrier, event_every):
+def timed_leg(eng, rounds, steps, warmup, n_models, d, barrier, event_every, flush=None):
     """Warmup, reset, then `steps` rounds bracketed by barrier + device sync, with HIP events
-    around every `event_every`-th round kernel (at least 10 sampled launches)."""
+    around every `event_every`-th round kernel (at least 10 sampled launches).
+
+    flush: the rounds are PIPELINED runs (dopt_run_dsgd_pipelined): then the warmup runs from
+    the reset iterate and leaves the metrics of its last iterate owed, the timed call takes
+    them in (its first pass) and leaves its own last ones owed, and flush() computes those
+    after the timed region -- so the timed region holds exactly `steps` fused rounds and
+    `steps` metric evaluations, the steady state of a long run (a lone dopt_run_dsgd of
+    `steps` rounds adds one unfused metrics-only pass over the shards: 1/steps more work)."""
     import numpy as np
 
-    if warmup > 0:
+    if flush is None and warmup > 0:
         rounds(warmup)
     eng.set_models(np.zeros((n_models, d)))
+    if flush is not None:
+        rounds(max(1, warmup))
     eng.kernel_stats()  # reset the event window
     every = event_every if event_every > 0 else max(1, steps // 10)
     eng.set_profiling(True, every=every)
@@ -192,6 +201,11 @@ def timed_leg(eng, rounds, steps, warmup, n_models, d, barrier, event_every):
     dt = time.perf_counter() - t0
     launches, kr_ms = eng.kernel_stats()
     eng.set_profiling(False)
+    if flush is not None:
+        if len(obj) != steps:
+            raise RuntimeError(f"pipelined timed call wrote {len(obj)} metric entries for {steps} rounds")
+        fo, fc = flush()  # the metrics of the final iterate (untimed)
+        obj, cons = np.concatenate([obj, fo]), np.concatenate([cons, fc])
     if not all(map(math.isfinite, list(obj) + list(cons))):
         raise RuntimeError("non-finite metrics")
     return dt, launches, kr_ms, every, obj, cons
@@ -207,10 +221,13 @@ def secondary_leg(dev, dtype, data_dtype, top, n, d, m, steps, warmup, lam, eta0
         eng.set_topology(top.row_ptr, top.col, top.w)
 
         def rounds(k):
-            obj, cons, _ = eng.run_dsgd(k, eta0, m, lam, lam, 0.0)
-            return obj, cons
+            return eng.run_dsgd_pipelined(k, eta0, m, lam, lam, 0.0)
 
-        dt, launches, kr_ms, every, obj, cons = timed_leg(eng, rounds, steps, warmup, n, d, barrier, event_every)
+        def flush():
+            return eng.run_dsgd_pipelined(0, eta0, m, lam, lam, 0.0)
+
+        dt, launches, kr_ms, every, obj, cons = timed_leg(eng, rounds, steps, warmup, n, d, barrier, event_every,
+                                                          flush)
         bpl = bytes_per_round(eng, n, d, m)
         avg = kr_ms / launches * 1e-3
         return {"value": n * steps / dt, "unit": "worker-iters/s", "ms_per_step": dt / steps * 1e3,
@@ -392,15 +409,19 @@ def main():
 
         def rounds(k):
             return runner.run(k, eta0, b, lam, lam, 0.0)
+
+        flush = None
     else:
         if mean is not None:
             eng.set_mixing_mean(*mean)
         else:
             eng.set_topology(top.row_ptr, top.col, top.w)
 
-        def rounds(k):
-            obj, cons, _ = eng.run_dsgd(k, eta0, b, lam, lam, 0.0)
-            return obj, cons
+        def rounds(k):  # metrics pipelined across calls (dopt_run_dsgd_pipelined; timed_leg)
+            return eng.run_dsgd_pipelined(k, eta0, b, lam, lam, 0.0)
+
+        def flush():
+            return eng.run_dsgd_pipelined(0, eta0, b, lam, lam, 0.0)
 
     def barrier():
         if world > 1:
@@ -412,7 +433,7 @@ def main():
 
     log(f"warmup {args.warmup}, timing {args.steps} rounds")
     dt, launches, kr_ms, every, obj, cons = timed_leg(eng, rounds, args.steps, args.warmup, plan.n_local, d, barrier,
-                                                      args.event_every)
+                                                      args.event_every, flush)
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}" if args.backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)

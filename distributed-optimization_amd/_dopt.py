@@ -61,6 +61,8 @@ _SIGS = {
     "dopt_set_global": ([_P, _P], ctypes.c_int),
     "dopt_get_global": ([_P, _P], ctypes.c_int),
     "dopt_run_dsgd": ([_P, _I64, _I64, _D, _I64, _P, _D, _D, _D, ctypes.c_uint32, _P, _P, _P], ctypes.c_int),
+    "dopt_run_dsgd_pipelined": ([_P, _I64, _I64, _D, _I64, _P, _D, _D, _D, ctypes.c_uint32, _P, _P, _P],
+                                ctypes.c_int),
     "dopt_run_centralized": ([_P, _I64, _I64, _D, _I64, _P, _D, _D, _D, ctypes.c_uint32, _P, _P], ctypes.c_int),
     "dopt_eval_gradient": ([_P, ctypes.c_int, _I64, _I64, _P, _P, _P, _D, _P], ctypes.c_int),
     "dopt_eval_objective": ([_P, ctypes.c_int, _I64, _I64, _P, _P, _P, _D, _P], ctypes.c_int),
@@ -307,6 +309,23 @@ class Engine:
         check(lib().dopt_run_dsgd(self._h, int(t0), T, float(eta0), int(batch), _ptr(idx), float(lam_grad),
                                   float(lam_obj), float(f_opt), flags, _ptr(obj), _ptr(cons), _ptr(tim)))
         return obj, cons, tim
+
+    def run_dsgd_pipelined(self, T, eta0, batch, lam_grad, lam_obj, f_opt=0.0, idx=None, t0=0,
+                           objective=True, consensus=True):
+        """dopt_run_dsgd_pipelined: the metrics of the last iterate are owed to the next such
+        call (entry 0 of its output); returns (objective, consensus) of the entries written."""
+        T = int(T)
+        obj = np.zeros(T + 1) if objective else None
+        cons = np.zeros(T + 1) if consensus else None
+        if idx is not None:
+            idx = np.ascontiguousarray(idx, dtype=np.int32)
+        flags = (RUN_OBJECTIVE if objective else 0) | (RUN_CONSENSUS if consensus else 0)
+        n = ctypes.c_int64(0)
+        check(lib().dopt_run_dsgd_pipelined(self._h, int(t0), T, float(eta0), int(batch), _ptr(idx),
+                                            float(lam_grad), float(lam_obj), float(f_opt), flags, _ptr(obj),
+                                            _ptr(cons), ctypes.byref(n)))
+        k = n.value
+        return (None if obj is None else obj[:k]), (None if cons is None else cons[:k])
 
     def run_centralized(self, T, eta0, batch, lam_grad, lam_obj, f_opt=0.0, idx=None, t0=0,
                         objective=True, want_time=True):

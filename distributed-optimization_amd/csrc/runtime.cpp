@@ -90,6 +90,10 @@ struct dopt_ctx {
   int cpls = 1;      // ... and per lane (k_mix)
   bool split = false;  // d too long for the row-resident kernel: column-blocked rounds
   int split_groups = 1;
+  // dopt_run_dsgd_pipelined: the metrics of the current iterate (at xbar[xb]) are still owed
+  // by the last pipelined run and ride the next pipelined run's first pass
+  bool carry_pending = false;
+  uint32_t carry_flags = 0;
   void* X = nullptr;
   void* y = nullptr;
   int64_t* off = nullptr;
@@ -323,6 +327,7 @@ int alloc_state(dopt_ctx* c) {
 }
 
 int set_layout(dopt_ctx* c, int problem, int64_t n, int64_t d) {
+  c->carry_pending = false;
   if (problem != DOPT_LOGISTIC && problem != DOPT_QUADRATIC)
     return fail(DOPT_ERR_UNSUPPORTED, "unknown problem %d", problem);
   CHECK_ARG(n >= 1 && d >= 1, "n_workers (%lld) and d (%lld) must be >= 1", (long long)n, (long long)d);
@@ -983,7 +988,7 @@ int dopt_set_mixing_mean(dopt_ctx* c, int64_t n_workers, double w_off, const dou
 }
 
 int dopt_set_models(dopt_ctx* c, const double* x) {
-  if (c) c->send_fresh = false;
+  if (c) c->send_fresh = c->carry_pending = false;
   CHECK_ARG(c && x, "NULL argument");
   if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");
   int rc;
@@ -1015,14 +1020,19 @@ int dopt_get_global(dopt_ctx* c, double* x) {
   return download_rows(c, c->dtype, c->xg[c->gcur], x, 1, c->d, c->ld);
 }
 
-int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch, const int32_t* idx,
-                  double lam_grad, double lam_obj, double f_opt, uint32_t flags, double* obj_out,
-                  double* cons_out, double* time_out) {
+static int run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch, const int32_t* idx,
+                    double lam_grad, double lam_obj, double f_opt, uint32_t flags, double* obj_out,
+                    double* cons_out, double* time_out, bool pipelined, int64_t* n_out) {
   CHECK_ARG(c, "ctx is NULL");
   int rc;
   if ((rc = check_run(c, T, batch, idx, true))) return rc;
   if ((rc = set_device(c))) return rc;
-  if ((rc = ensure_hist(c, T))) return rc;
+  if ((rc = ensure_hist(c, T + 1))) return rc;
+  const bool carry_in = pipelined && c->carry_pending;
+  c->carry_pending = false;
+  if (carry_in && c->carry_flags != (flags & (DOPT_RUN_OBJECTIVE | DOPT_RUN_CONSENSUS)))
+    return fail(DOPT_ERR_INVALID, "pipelined run: metrics flags %u differ from the pending metrics' %u", flags,
+                c->carry_flags);
   c->send_fresh = false;
   const bool want_obj = flags & DOPT_RUN_OBJECTIVE, want_cons = flags & DOPT_RUN_CONSENSUS;
   const bool metrics = want_obj || want_cons;
@@ -1045,9 +1055,16 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
                        !(two && atoi(two) != 0) && !(ccs && ccs[0] == '0');
   const int64_t CH = idx ? idx_chunk_rounds(c, T, batch) : 1;
   int& xb = c->xb;
-  if (c->split) return run_dsgd_split(c, t0, T, eta0, batch, idx, lam_grad, lam_obj, f_opt, flags, obj_out,
-                                      cons_out, time_out);
-  if ((rc = colsum_current(c))) return rc;  // xbar and S of the starting iterates
+  if (c->split) {
+    if (n_out) *n_out = T;
+    return run_dsgd_split(c, t0, T, eta0, batch, idx, lam_grad, lam_obj, f_opt, flags, obj_out, cons_out,
+                          time_out);
+  }
+  // pipelined: the last round's metrics stay owed (its pass would be the only unfused one)
+  const bool carry_out = pipelined && fused && metrics;
+  const int64_t lag = (carry_in && fused && metrics) ? 1 : 0;  // output entry of round h's fused metrics: h - 1 + lag
+  if (carry_in && !lag) return fail(DOPT_ERR_INVALID, "pipelined run: the pending metrics need a fused run");
+  if (!carry_in && (rc = colsum_current(c))) return rc;  // xbar and S of the starting iterates (carried: current)
   HIPOK(launch_stamp(c->stamps, c->stream));
 
   for (int64_t h = 0; h < T; ++h) {
@@ -1063,7 +1080,7 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
     a.xbar = c->xbar[xb];
     a.eta = eta0 / sqrt((double)(t + 1));  // trainer.py:138-140
     a.lam = lam_grad;
-    const bool met = fused && metrics && h > 0;
+    const bool met = fused && metrics && (h > 0 || lag);
     a.flags |= F_STEP | (met && want_cons ? F_CONS : 0) | (met && want_obj ? F_LOSS : 0) |
                ((met && bip) || dev ? F_BIP : 0) | (dev ? F_DEVSAMPLE : 0);
     a.seed = c->sample_seed;
@@ -1075,7 +1092,7 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
     if (c->prof && (rc = prof_event(c, true))) return rc;
     // xbar_{t+1} (trainer.py:182); the stamp marks the end of round t's update (trainer.py:181)
     // history[h-1] (this round's fused partials of x_h at xbar_h) rides the same launch
-    double* hr = met ? c->hraw + 3 * (h - 1) : c->hraw;
+    double* hr = met ? c->hraw + 3 * (h - 1 + lag) : c->hraw;
     const FoldArgs fold = {want_cons ? c->slab_cons : nullptr, c->n, want_obj ? c->slab_loss : nullptr,
                            c->loss_groups, want_obj ? c->xbar[xb] : nullptr, hr, hr + 1, hr + 2};
     HIPOK(launch_colsum(c->dtype, c->xs[c->cur ^ 1], c->n, c->ld, (int32_t)c->nchs, kRowsPerGroup, c->part,
@@ -1090,18 +1107,40 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
     c->cur ^= 1;
     xb ^= 1;
   }
-  if (fused && metrics && T > 0) {  // history[T-1]: one metrics pass over x_T
+  int64_t nh = T + lag;  // history entries this call produces
+  if (carry_out && T > 0) {
+    nh -= 1;  // history of x_T: owed to the next pipelined run
+    c->carry_pending = true;
+    c->carry_flags = flags & (DOPT_RUN_OBJECTIVE | DOPT_RUN_CONSENSUS);
+  } else if (fused && metrics && (T > 0 || lag)) {  // one metrics pass over x_T
     if ((rc = metrics_pass(c, c->xs[c->cur], c->xbar[xb], false, want_cons, want_obj))) return rc;
-    if ((rc = history(c, T - 1, c->xbar[xb], want_cons, want_obj, c->n))) return rc;
+    if ((rc = history(c, nh - 1, c->xbar[xb], want_cons, want_obj, c->n))) return rc;
   }
-  return finish_run(c, T, T, lam_obj, f_opt, want_obj ? obj_out : nullptr, want_cons ? cons_out : nullptr,
-                    time_out);
+  if (n_out) *n_out = nh;
+  return finish_run(c, nh, T, lam_obj, f_opt, want_obj ? obj_out : nullptr, want_cons ? cons_out : nullptr,
+                    pipelined ? nullptr : time_out);
+}
+
+int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch, const int32_t* idx,
+                  double lam_grad, double lam_obj, double f_opt, uint32_t flags, double* obj_out,
+                  double* cons_out, double* time_out) {
+  return run_dsgd(c, t0, T, eta0, batch, idx, lam_grad, lam_obj, f_opt, flags, obj_out, cons_out, time_out, false,
+                  nullptr);
+}
+
+int dopt_run_dsgd_pipelined(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch, const int32_t* idx,
+                            double lam_grad, double lam_obj, double f_opt, uint32_t flags, double* obj_out,
+                            double* cons_out, int64_t* n_out) {
+  CHECK_ARG(n_out, "n_out is NULL");
+  return run_dsgd(c, t0, T, eta0, batch, idx, lam_grad, lam_obj, f_opt, flags, obj_out, cons_out, nullptr, true,
+                  n_out);
 }
 
 int dopt_run_centralized(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch,
                          const int32_t* idx, double lam_grad, double lam_obj, double f_opt,
                          uint32_t flags, double* obj_out, double* time_out) {
   CHECK_ARG(c, "ctx is NULL");
+  c->carry_pending = false;
   int rc;
   if ((rc = check_run(c, T, batch, idx, false))) return rc;
   if (!idx && batch < c->max_m) return fail(DOPT_ERR_UNSUPPORTED, "device sampling: D-SGD rounds only");
@@ -1429,6 +1468,7 @@ int dopt_phase_gather(dopt_ctx* c) {
 
 int dopt_phase_begin(dopt_ctx* c, int64_t batch) {
   CHECK_ARG(c, "ctx is NULL");
+  c->carry_pending = false;
   if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
   c->send_fresh = false;  // the iterates may have been set since the last mix
   int rc;

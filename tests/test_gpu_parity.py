@@ -584,3 +584,39 @@ def test_last_round_kernel_names_the_launched_instance():
         eng.run_dsgd(2, 0.05, m, 1e-3, 1e-3, 0.0)
         assert _dopt.last_round_kernel().startswith(want), _dopt.last_round_kernel()
         eng.close()
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float64/x32", "float32"])
+def test_pipelined_runs_equal_one_run(dtype):
+    """dopt_run_dsgd_pipelined (bench.py's steady-state timing): chained calls whose last
+    iterate's metrics ride the next call's first pass give, concatenated, exactly the history
+    and iterates of one dopt_run_dsgd over all their rounds -- every round's metrics computed
+    once, by the same kernels.  256 logistic workers: the benchmarked 8-wave instances."""
+    n, d, m = 256, 1024, 24
+    if dtype == "float64/x32":
+        eng = _dopt.Engine(0, "float64", data_dtype="float32")
+    else:
+        eng = _dopt.Engine(0, dtype)
+    eng.generate_shards("logistic", n, d, m, seed=5, flip=0.05)
+    top = topology.random_regular(n, 4, seed=1)
+    eng.set_topology(top.row_ptr, top.col, top.w)
+    eng.set_models(np.zeros((n, d)))
+    obj_ref, cons_ref, _ = eng.run_dsgd(12, 0.05, m, 1e-3, 1e-3, 0.0)
+    x_ref = eng.get_models()
+    eng.set_models(np.zeros((n, d)))
+    objs, conss, t0 = [], [], 0
+    for k in (5, 1, 4, 2, 0):
+        o, c = eng.run_dsgd_pipelined(k, 0.05, m, 1e-3, 1e-3, 0.0, t0=t0)
+        assert len(o) == (k - 1 if t0 == 0 else (k if k else 1))
+        objs.append(o)
+        conss.append(c)
+        t0 += k
+    assert np.array_equal(np.concatenate(objs), obj_ref)
+    assert np.array_equal(np.concatenate(conss), cons_ref)
+    assert np.array_equal(eng.get_models(), x_ref)
+    # anything else in between drops the owed entry: a fresh chain starts with T - 1 entries
+    eng.run_dsgd_pipelined(3, 0.05, m, 1e-3, 1e-3, 0.0)
+    eng.set_models(np.zeros((n, d)))
+    o, _ = eng.run_dsgd_pipelined(3, 0.05, m, 1e-3, 1e-3, 0.0)
+    assert len(o) == 2
+    eng.close()
