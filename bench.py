@@ -190,7 +190,7 @@ def timed_leg(eng, rounds, steps, warmup, n_models, d, barrier, event_every, flu
         rounds(warmup)
     eng.set_models(np.zeros((n_models, d)))
     if flush is not None:
-        rounds(max(1, warmup))
+        rounds(max(3, warmup))  # the multi-GPU lagged schedule completes history[t] 3 rounds later
     eng.kernel_stats()  # reset the event window
     every = event_every if event_every > 0 else max(1, steps // 10)
     eng.set_profiling(True, every=every)
@@ -407,10 +407,17 @@ def main():
                 "allreduce_bytes_per_round": ld * 8}
         log(f"comm: {comm}")
 
-        def rounds(k):
-            return runner.run(k, eta0, b, lam, lam, 0.0)
+        if runner._lagged_ok:  # the lagged schedule continued across calls (as on one GPU: timed_leg)
+            def rounds(k):
+                return runner.run_pipelined(k, eta0, b, lam, lam, 0.0)
 
-        flush = None
+            def flush():
+                return runner.run_pipelined(0, eta0, b, lam, lam, 0.0)
+        else:
+            def rounds(k):
+                return runner.run(k, eta0, b, lam, lam, 0.0)
+
+            flush = None
     else:
         if mean is not None:
             eng.set_mixing_mean(*mean)

@@ -71,6 +71,7 @@ _SIGS = {
     "dopt_set_partition": ([_P, _I64, _I64], ctypes.c_int),
     "dopt_set_halo": ([_P, _I64, _P, _I64, _P, _P], ctypes.c_int),
     "dopt_phase_begin": ([_P, _I64], ctypes.c_int),
+    "dopt_phase_chain": ([_P, ctypes.c_int, _P], ctypes.c_int),
     "dopt_phase_gather": ([_P], ctypes.c_int),
     "dopt_phase_grad_shared": ([_P, _I64, _P, _D, ctypes.c_int], ctypes.c_int),
     "dopt_phase_colsum_grad": ([_P, _P], ctypes.c_int),
@@ -375,6 +376,13 @@ class Engine:
         ids = np.ascontiguousarray(send_ids, dtype=np.int32)
         check(lib().dopt_set_halo(self._h, int(n_halo), ctypes.c_void_p(halo_ptr) if halo_ptr else None, len(ids),
                                   ctypes.c_void_p(send_ptr) if send_ptr else None, _ptr(ids)))
+
+    def phase_chain(self, mark):
+        """dopt_phase_chain: whether the last pipelined phase run left its schedule open (and
+        nothing has touched the context since); then set (mark) or clear the mark."""
+        was = ctypes.c_int(0)
+        check(lib().dopt_phase_chain(self._h, 1 if mark else 0, ctypes.byref(was)))
+        return bool(was.value)
 
     def phase_begin(self, batch):
         check(lib().dopt_phase_begin(self._h, int(batch)))

@@ -1028,7 +1028,7 @@ static int run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t bat
   if ((rc = check_run(c, T, batch, idx, true))) return rc;
   if ((rc = set_device(c))) return rc;
   if ((rc = ensure_hist(c, T + 1))) return rc;
-  const bool carry_in = pipelined && c->carry_pending;
+  const bool carry_in = pipelined && c->carry_pending && c->carry_flags != 0;
   c->carry_pending = false;
   if (carry_in && c->carry_flags != (flags & (DOPT_RUN_OBJECTIVE | DOPT_RUN_CONSENSUS)))
     return fail(DOPT_ERR_INVALID, "pipelined run: metrics flags %u differ from the pending metrics' %u", flags,
@@ -1463,6 +1463,14 @@ int dopt_phase_gather(dopt_ctx* c) {
   if (c->send_fresh) return DOPT_OK;  // the last mix wrote these rows already
   HIPOK(launch_gather_rows(c->dtype, c->xs[c->cur], c->send_ids, c->n_send, c->ld, (int32_t)c->nchs, c->send,
                            c->stream));
+  return DOPT_OK;
+}
+
+int dopt_phase_chain(dopt_ctx* c, int mark, int* was_pending) {
+  CHECK_ARG(c && was_pending, "NULL argument");
+  *was_pending = c->carry_pending ? 1 : 0;
+  c->carry_pending = mark != 0;
+  c->carry_flags = 0;
   return DOPT_OK;
 }
 

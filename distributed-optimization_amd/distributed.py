@@ -347,63 +347,112 @@ class DistributedDSGD:
         obj, cons = _dopt.finalize_metrics(self.eng.problem, raw, self.n_global, self.rows_global, lam_obj, f_opt)
         return (obj if objective else None), (cons if consensus else None)
 
-    def _run_lagged(self, T, eta0, batch, lam_grad, lam_obj, f_opt, t0, objective, consensus, idx=None):
+    def run_pipelined(self, T, eta0, batch, lam_grad, lam_obj, f_opt=0.0, t0=0, objective=True, consensus=True,
+                      idx=None):
+        """The lagged schedule continued across calls (steady-state timing, bench.py; the
+        multi-GPU counterpart of Engine.run_dsgd_pipelined).  A chain of such calls is one
+        long lagged run: no call ends with the tail of _run_lagged (xbar_T, the consensus of
+        x_T and a pass for the last losses); T = 0 runs that tail and closes the chain.  Each
+        call returns the GLOBAL (objective, consensus) entries that became complete during it
+        -- T of them in the steady state (history[t] is complete once the loss at xbar_t has
+        been folded, three rounds later).  Rounds use learning-rate index t0 + h per call.
+        Any other run or dopt_set_models ends a chain (dopt_phase_chain)."""
+        rows = self.eng.shard_rows
+        bip = (idx is not None and not self.obj_sep and rows is not None and len(rows) > 0 and
+               batch < int(rows.max()) <= _dopt.MAX_BIP_ROWS and os.environ.get("DOPT_BIP", "1") != "0")
+        if not ((idx is None and not self.obj_sep) or bip) or not (objective or consensus) or not self._lagged_ok:
+            raise NotImplementedError("pipelined runs: the lagged schedule only (CSR mixing, fused metrics)")
+        return self._run_lagged(T, eta0, batch, lam_grad, lam_obj, f_opt, t0, objective, consensus, idx,
+                                pipelined=True)
+
+    def _run_lagged(self, T, eta0, batch, lam_grad, lam_obj, f_opt, t0, objective, consensus, idx=None,
+                    pipelined=False):
         """Rounds with CSR mixing whose metrics ride the gradient pass (full shards, or
         minibatches taken inside a pass over every row); history[t] = metrics of x_{t+1}.
-        Round h, all on the engine stream except the two transfers:
+        Round g (counted from the start of the chain; one call = one chain unless pipelined),
+        all on the engine stream except the two transfers:
 
-          P2P(send rows of x_h) -----------------------------------------------.
-          colsum(x_h) [+ fold of history[h-2] / loss of history[h-3]] -> all-reduce --.
-          grad(x_h) + loss of every row at xbar_{h-1} ------------------------------+-+-> mix
-                                                      mix: xbar_h, consensus of x_h, x_{h+1},
-                                                           send rows of x_{h+1}
+          P2P(send rows of x_g) -----------------------------------------------.
+          colsum(x_g) [+ fold of history[g-2] / loss of history[g-3]] -> all-reduce --.
+          grad(x_g) + loss of every row at xbar_{g-1} ------------------------------+-+-> mix
+                                                      mix: xbar_g, consensus of x_g, x_{g+1},
+                                                           send rows of x_{g+1}
 
-        Four kernels per round and no collective between two of them; after the last
-        round xbar_T, the consensus of x_T and one pass for the losses at xbar_{T-1}, xbar_T."""
+        Four kernels per round and no collective between two of them; after the last round
+        of a chain (the tail) xbar_T, the consensus of x_T and one pass for the losses at
+        xbar_{T-1}, xbar_T."""
         torch, eng = self.torch, self.eng
         xnorm = self.plan.rank == 0  # ||xbar||^2 is global already: count it once
         obj_f = _dopt.RUN_OBJECTIVE if objective else 0
-        if T == 0:
-            return (np.zeros(0) if objective else None), (np.zeros(0) if consensus else None)
+        flags = (objective, consensus)
+        # every rank makes the same calls, so all see the same chain state
+        cont = pipelined and eng.phase_chain(False) and getattr(self, "_chain", None) is not None \
+            and self._chain["flags"] == flags
+        if not cont:
+            if not pipelined and T == 0:
+                return (np.zeros(0) if objective else None), (np.zeros(0) if consensus else None)
+            self._chain = {"g": 0, "done": 0, "flags": flags, "hist": None}
+        ch = self._chain
+        G0, G1 = ch["g"], ch["g"] + T
+        tail = not pipelined or T == 0
         with torch.cuda.stream(self.stream):
-            partials = torch.zeros((T, 3), dtype=torch.float64, device=self.dev)
+            cap = max(1, G1)
+            if ch["hist"] is None or ch["hist"].shape[0] < cap:  # history rows by global entry, grown by doubling
+                new = torch.zeros((max(cap, 2 * (0 if ch["hist"] is None else ch["hist"].shape[0])), 3),
+                                  dtype=torch.float64, device=self.dev)
+                if ch["hist"] is not None:
+                    new[:ch["hist"].shape[0]].copy_(ch["hist"])
+                ch["hist"] = new
+            partials = ch["hist"]
             base = partials.data_ptr()
 
-            def at(h, k, want=True):  # device address of partials[h, k], or None
-                return base + (3 * h + k) * 8 if want and 0 <= h < T else None
+            def at(e, k, want=True):  # device address of history row e, column k, or None
+                return base + (3 * e + k) * 8 if want and 0 <= e < G1 else None
 
-            def colsum_fold(h):  # column sums of x_h; history[h-2] (consensus, ||xbar||^2), [h-3] (loss)
-                eng.phase_colsum_fold(self.sum.data_ptr(), at(h - 2, 0, consensus), at(h - 2, 2, objective and xnorm),
-                                      at(h - 3, 1, objective))
+            def colsum_fold(g):  # column sums of x_g; history[g-2] (consensus, ||xbar||^2), [g-3] (loss)
+                eng.phase_colsum_fold(self.sum.data_ptr(), at(g - 2, 0, consensus), at(g - 2, 2, objective and xnorm),
+                                      at(g - 3, 1, objective))
 
-            eng.phase_begin(batch)
-            eng.phase_gather()  # send rows of x_0; later rounds get them from the mix kernel
-            for h in range(T):
+            if not cont:
+                eng.phase_begin(batch)
+                eng.phase_gather()  # send rows of x_0; later rounds get them from the mix kernel
+            for g in range(G0, G1):
+                h = g - G0
                 pending = self._start_exchange()
-                colsum_fold(h)
+                colsum_fold(g)
                 ar = self._all_reduce_start(self.sum)
                 eng.phase_set_round(t0 + h)  # the device sampler's counter (sampling='device')
-                eng.phase_grad(batch, lam_grad, obj_f if h >= 2 else 0,  # loss at xbar_{h-1}
+                eng.phase_grad(batch, lam_grad, obj_f if g >= 2 else 0,  # loss at xbar_{g-1}
                                idx=None if idx is None else idx[h])
                 if ar is not None:
                     ar.wait()
                 self._finish_exchange(pending)
                 eng.phase_mix_lagged(t0 + h, eta0, self.sum.data_ptr(), consensus)
-            colsum_fold(T)
-            ar = self._all_reduce_start(self.sum)
-            if ar is not None:
-                ar.wait()
-            eng.phase_xbar(self.sum.data_ptr())  # xbar_T
-            if consensus:
-                eng.phase_cons()
-            if objective:  # losses at xbar_T (history[T-1]) and xbar_{T-1} (history[T-2])
-                eng.phase_loss_pass(T >= 2)
-            eng.phase_fold(at(T - 1, 0, consensus), at(T - 1, 2, objective and xnorm), at(T - 1, 1, objective), 1)
-            if objective and T >= 2:
-                eng.phase_fold(None, None, at(T - 2, 1), 0)
-            self._all_reduce(partials)
-            raw = partials.cpu().numpy()
+            if tail and G1 > 0:
+                colsum_fold(G1)
+                ar = self._all_reduce_start(self.sum)
+                if ar is not None:
+                    ar.wait()
+                eng.phase_xbar(self.sum.data_ptr())  # xbar_T
+                if consensus:
+                    eng.phase_cons()
+                if objective:  # losses at xbar_T (history[T-1]) and xbar_{T-1} (history[T-2])
+                    eng.phase_loss_pass(G1 >= 2)
+                eng.phase_fold(at(G1 - 1, 0, consensus), at(G1 - 1, 2, objective and xnorm),
+                               at(G1 - 1, 1, objective), 1)
+                if objective and G1 >= 2:
+                    eng.phase_fold(None, None, at(G1 - 2, 1), 0)
+            upto = G1 if tail else max(ch["done"], G1 - 3)  # history rows complete on every rank
+            done = ch["done"]
+            if upto > done:
+                self._all_reduce(partials[done:upto])
+            raw = partials[done:upto].cpu().numpy()
         self.stream.synchronize()
+        ch["g"], ch["done"] = G1, upto
+        if tail:
+            self._chain = None
+        else:
+            eng.phase_chain(True)
         obj, cons = _dopt.finalize_metrics(self.eng.problem, raw, self.n_global, self.rows_global, lam_obj, f_opt)
         return (obj if objective else None), (cons if consensus else None)
 

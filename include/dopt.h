@@ -228,6 +228,12 @@ int dopt_set_partition(dopt_ctx *ctx, int64_t n_global, int64_t rows_global);
  * before dopt_set_topology (the local CSR indexes local + halo rows). */
 int dopt_set_halo(dopt_ctx *ctx, int64_t n_halo, void *halo_dev, int64_t n_send, void *send_dev,
                   const int32_t *send_ids);
+/* Pipelined multi-GPU runs (distributed.py DistributedDSGD.run_pipelined): *was_pending =
+ * whether the previous pipelined phase run on this context left its lagged schedule open
+ * (nothing else -- dopt_set_models, new data, any other run, dopt_phase_begin -- has
+ * touched the context since); then the mark is set (mark = 1: this run leaves it open) or
+ * cleared. */
+int dopt_phase_chain(dopt_ctx *ctx, int mark, int *was_pending);
 /* Start of a run of phases: column-blocked contexts (large d) compute the
  * coefficients of the starting iterates here (full-shard batches). */
 int dopt_phase_begin(dopt_ctx *ctx, int64_t batch);

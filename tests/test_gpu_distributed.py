@@ -55,7 +55,19 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
     run = Dm.DistributedDSGD(eng, plan, N, N * M, device=0,
                              mean=None if uni is None else (uni[0], uni[1][plan.lo:plan.hi]))
     which = os.environ.get("DOPT_TEST_METRICS", "both")
-    obj, cons = run.run(T, 0.05, B, 1e-3, 1e-3, 0.25, objective=which != "cons", consensus=which != "obj")
+    if os.environ.get("DOPT_TEST_PIPE") == "1":  # a chain of pipelined calls covering T rounds, then the tail
+        parts, t = [], 0
+        for k in [2, 1, 3, 1, T]:
+            k = min(k, T - t)
+            parts.append(run.run_pipelined(k, 0.05, B, 1e-3, 1e-3, 0.25, t0=t, objective=which != "cons",
+                                           consensus=which != "obj"))
+            t += k
+        parts.append(run.run_pipelined(0, 0.05, B, 1e-3, 1e-3, 0.25, objective=which != "cons",
+                                       consensus=which != "obj"))
+        obj = None if which == "cons" else np.concatenate([p[0] for p in parts])
+        cons = None if which == "obj" else np.concatenate([p[1] for p in parts])
+    else:
+        obj, cons = run.run(T, 0.05, B, 1e-3, 1e-3, 0.25, objective=which != "cons", consensus=which != "obj")
     obj = np.zeros(0) if obj is None else obj
     cons = np.zeros(0) if cons is None else cons
     x = run.gather_models()
@@ -246,3 +258,19 @@ def test_column_blocked_ranks_match_single_context(tmp_path, mean):
                        nprocs=2, join=True, start_method="spawn")
     got = np.load(tmp_path / "dist.npz")
     _compare_single(got, "float64", mean, t, n, d, m, exact=False)
+
+
+@pytest.mark.parametrize("world,backend,dtype", [(2, "gloo", "float64"), (3, "gloo", "float64/x32"),
+                                                 (1, "nccl", "float64")])
+def test_pipelined_chain_matches_single_context(tmp_path, monkeypatch, world, backend, dtype):
+    """DistributedDSGD.run_pipelined (bench.py's multi-GPU timing): a chain of calls of 2, 1,
+    3, 1 and the rest of 9 rounds, then the closing call, returns exactly the history of one
+    run and ends on the same iterates as one context (bitwise)."""
+    import torch.multiprocessing as mp
+
+    monkeypatch.setenv("DOPT_TEST_PIPE", "1")
+    mp.start_processes(_rank_main, args=(world, _free_port(), dtype, str(tmp_path), False, 9, "1", N, D, M, backend),
+                       nprocs=world, join=True, start_method="spawn")
+    got = np.load(tmp_path / "dist.npz")
+    assert len(got["obj"]) == len(got["cons"]) == 9
+    _compare_single(got, dtype, False, 9)
