@@ -253,7 +253,7 @@ def suboptimality(eng, lam, final_objective):
             "note": "device L-BFGS on the full-data objective (replaces sklearn saga at sizes it cannot run)"}
 
 
-def dropin_leg(eng, n, d, m, lam, eta0, rounds=40):
+def dropin_leg(eng, n, d, m, lam, eta0, rounds=128):
     """The drop-in DecentralizedTrainer (trainer.py API) on the same C3 shards as host arrays,
     sampling='legacy': every round draws the reference's numpy legacy-MT19937 stream
     (4096 permutations of 512 per round, worker.py:27) on the host before the device runs

@@ -61,7 +61,7 @@ _SIGS = {
     "dopt_set_global": ([_P, _P], ctypes.c_int),
     "dopt_get_global": ([_P, _P], ctypes.c_int),
     "dopt_run_dsgd": ([_P, _I64, _I64, _D, _I64, _P, _D, _D, _D, ctypes.c_uint32, _P, _P, _P], ctypes.c_int),
-    "dopt_run_dsgd_pipelined": ([_P, _I64, _I64, _D, _I64, _P, _D, _D, _D, ctypes.c_uint32, _P, _P, _P],
+    "dopt_run_dsgd_pipelined": ([_P, _I64, _I64, _D, _I64, _P, _D, _D, _D, ctypes.c_uint32, _P, _P, _P, _P],
                                 ctypes.c_int),
     "dopt_run_centralized": ([_P, _I64, _I64, _D, _I64, _P, _D, _D, _D, ctypes.c_uint32, _P, _P], ctypes.c_int),
     "dopt_eval_gradient": ([_P, ctypes.c_int, _I64, _I64, _P, _P, _P, _D, _P], ctypes.c_int),
@@ -312,21 +312,24 @@ class Engine:
         return obj, cons, tim
 
     def run_dsgd_pipelined(self, T, eta0, batch, lam_grad, lam_obj, f_opt=0.0, idx=None, t0=0,
-                           objective=True, consensus=True):
+                           objective=True, consensus=True, want_time=False):
         """dopt_run_dsgd_pipelined: the metrics of the last iterate are owed to the next such
-        call (entry 0 of its output); returns (objective, consensus) of the entries written."""
+        call (entry 0 of its output); returns (objective, consensus) of the entries written,
+        and with want_time also the end-of-round times of this call's T rounds."""
         T = int(T)
         obj = np.zeros(T + 1) if objective else None
         cons = np.zeros(T + 1) if consensus else None
+        tim = np.zeros(T) if want_time else None
         if idx is not None:
             idx = np.ascontiguousarray(idx, dtype=np.int32)
         flags = (RUN_OBJECTIVE if objective else 0) | (RUN_CONSENSUS if consensus else 0)
         n = ctypes.c_int64(0)
         check(lib().dopt_run_dsgd_pipelined(self._h, int(t0), T, float(eta0), int(batch), _ptr(idx),
                                             float(lam_grad), float(lam_obj), float(f_opt), flags, _ptr(obj),
-                                            _ptr(cons), ctypes.byref(n)))
+                                            _ptr(cons), _ptr(tim), ctypes.byref(n)))
         k = n.value
-        return (None if obj is None else obj[:k]), (None if cons is None else cons[:k])
+        res = (None if obj is None else obj[:k]), (None if cons is None else cons[:k])
+        return res + (tim,) if want_time else res
 
     def run_centralized(self, T, eta0, batch, lam_grad, lam_obj, f_opt=0.0, idx=None, t0=0,
                         objective=True, want_time=True):

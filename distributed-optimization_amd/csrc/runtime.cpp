@@ -510,7 +510,9 @@ int prof_event(dopt_ctx* c, bool stop) {
   return DOPT_OK;
 }
 
-int finish_run(dopt_ctx* c, int64_t T, int64_t launches, double lam_obj, double f_opt, double* obj_out,
+// T history entries (metrics) and `rounds` end-of-round time stamps (they differ only for
+// pipelined runs).
+int finish_run(dopt_ctx* c, int64_t T, int64_t rounds, double lam_obj, double f_opt, double* obj_out,
                double* cons_out, double* time_out) {
   HIPOK(hipStreamSynchronize(c->stream));
   if ((obj_out || cons_out) && T > 0) {
@@ -518,12 +520,11 @@ int finish_run(dopt_ctx* c, int64_t T, int64_t launches, double lam_obj, double 
     HIPOK(hipMemcpy(raw.data(), c->hraw, raw.size() * sizeof(double), hipMemcpyDeviceToHost));
     finalize_metrics(raw.data(), T, c->problem, n_div(c), obj_rows(c), lam_obj, f_opt, obj_out, cons_out);
   }
-  if (time_out && T > 0) {
-    std::vector<uint64_t> st((size_t)T + 1);
+  if (time_out && rounds > 0) {
+    std::vector<uint64_t> st((size_t)rounds + 1);
     HIPOK(hipMemcpy(st.data(), c->stamps, st.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    for (int64_t h = 0; h < T; ++h) time_out[h] = (double)(st[(size_t)h + 1] - st[0]) / c->clock_hz;
+    for (int64_t h = 0; h < rounds; ++h) time_out[h] = (double)(st[(size_t)h + 1] - st[0]) / c->clock_hz;
   }
-  (void)launches;
   return DOPT_OK;
 }
 
@@ -1025,6 +1026,10 @@ static int run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t bat
                     double* cons_out, double* time_out, bool pipelined, int64_t* n_out) {
   CHECK_ARG(c, "ctx is NULL");
   int rc;
+  if (T == 0) {  // no round: at most the owed metrics pass, which does not depend on the batch
+    batch = c->max_m;
+    idx = nullptr;
+  }
   if ((rc = check_run(c, T, batch, idx, true))) return rc;
   if ((rc = set_device(c))) return rc;
   if ((rc = ensure_hist(c, T + 1))) return rc;
@@ -1033,6 +1038,10 @@ static int run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t bat
   if (carry_in && c->carry_flags != (flags & (DOPT_RUN_OBJECTIVE | DOPT_RUN_CONSENSUS)))
     return fail(DOPT_ERR_INVALID, "pipelined run: metrics flags %u differ from the pending metrics' %u", flags,
                 c->carry_flags);
+  if (T == 0 && !carry_in) {  // nothing to run, nothing owed
+    if (n_out) *n_out = 0;
+    return DOPT_OK;
+  }
   c->send_fresh = false;
   const bool want_obj = flags & DOPT_RUN_OBJECTIVE, want_cons = flags & DOPT_RUN_CONSENSUS;
   const bool metrics = want_obj || want_cons;
@@ -1118,7 +1127,7 @@ static int run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t bat
   }
   if (n_out) *n_out = nh;
   return finish_run(c, nh, T, lam_obj, f_opt, want_obj ? obj_out : nullptr, want_cons ? cons_out : nullptr,
-                    pipelined ? nullptr : time_out);
+                    time_out);
 }
 
 int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch, const int32_t* idx,
@@ -1130,9 +1139,9 @@ int dopt_run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch
 
 int dopt_run_dsgd_pipelined(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch, const int32_t* idx,
                             double lam_grad, double lam_obj, double f_opt, uint32_t flags, double* obj_out,
-                            double* cons_out, int64_t* n_out) {
+                            double* cons_out, double* time_out, int64_t* n_out) {
   CHECK_ARG(n_out, "n_out is NULL");
-  return run_dsgd(c, t0, T, eta0, batch, idx, lam_grad, lam_obj, f_opt, flags, obj_out, cons_out, nullptr, true,
+  return run_dsgd(c, t0, T, eta0, batch, idx, lam_grad, lam_obj, f_opt, flags, obj_out, cons_out, time_out, true,
                   n_out);
 }
 

@@ -47,6 +47,7 @@ MEAN_MIX_MIN = 128          # complete graphs from this size mix through the col
 IDX_CHUNK_ELEMS = 1 << 24   # host index buffer per device call (64 MiB of int32)
 IDX_CHUNK_ROUNDS = 512      # rounds per device call when indices are drawn (the next chunk's draw
                             # runs on a host thread while the device runs this one)
+IDX_CHUNK_DRAWS = 1 << 24   # pipelined D-SGD: draws per chunk (~25 ms of host stream at 1.4 ns; C3: 8 rounds)
 
 
 # ---------------------------------------------------------------------------- shared helpers
@@ -257,14 +258,17 @@ def _batch_size(workers):
     return bs.pop() if bs else 0
 
 
-def _index_chunks(workers, T, config, t_begin=0, max_chunk=0):
+def _index_chunks(workers, T, config, t_begin=0, max_chunk=0, overlap=False):
     """Yield (t_start, n_rounds, b, idx or None, rng_state): minibatch indices drawn on the
     host in trainer order (trainer.py:47-50 / :166), `None` when every batch is the full
     shard; rng_state = numpy's legacy state right after this chunk's draws (what a
     checkpoint taken after the chunk records).  Rounds t_begin .. T-1; chunks of at most
     max_chunk rounds (0: no limit) starting at multiples of it.  The legacy MT19937 stream
     is sequential, so the draw runs one chunk AHEAD on a host thread (the C sampler
-    releases the GIL) while the device runs the current chunk."""
+    releases the GIL) while the device runs the current chunk.  overlap: chunks of about
+    IDX_CHUNK_DRAWS stream words, so the device starts after a short first draw and the
+    draw of chunk k+1 overlaps the device run of chunk k even in short runs (callers whose
+    chunk calls carry no extra metrics pass: pipelined D-SGD runs)."""
     b = _batch_size(workers)
     rows = np.array([w.n_local_samples for w in workers], dtype=np.int64)
     full = b >= (rows.max() if len(rows) else 0)
@@ -288,6 +292,9 @@ def _index_chunks(workers, T, config, t_begin=0, max_chunk=0):
     # choice() is a whole permutation of m_i, whatever b is): advance it without making them.
     b_draw = 1 if full else b
     ch = max(1, min(IDX_CHUNK_ROUNDS, IDX_CHUNK_ELEMS // max(1, len(workers) * max(b_draw, 1))))
+    if overlap:  # every choice() draws a whole permutation: about m_i - 1 words per worker
+        per_round = max(1, int(np.sum(np.maximum(rows - 1, 0))))
+        ch = max(1, min(ch, IDX_CHUNK_DRAWS // per_round))
 
     def draws():
         for t, n in bounds(ch):
@@ -566,11 +573,21 @@ class DecentralizedTrainer:
         eng.set_models(state if state is not None else np.stack([np.asarray(w.x, dtype=np.float64)
                                                                  for w in self.workers]))
         iteration_transmission = np.sum(self.degrees) * self.n_features  # trainer.py:169
-        with closing(_index_chunks(self.workers, T, cfg, t_begin, ck.max_chunk())) as chunks:
+        eta0 = cfg["learning_rate_eta0"]
+        # chunks run as one pipelined chain (dopt_run_dsgd_pipelined: each chunk's last metrics ride
+        # the next chunk's first pass), closed where the history must be complete: at a
+        # checkpoint and at the end -- the same values as one run_dsgd over all the rounds
+        with closing(_index_chunks(self.workers, T, cfg, t_begin, ck.max_chunk(), overlap=True)) as chunks:
             for t0, n, b, idx, rng in chunks:
                 t_host = time.time() - start_time + t_off
-                obj, cons, tim = eng.run_dsgd(n, cfg["learning_rate_eta0"], b, lam_grad, reg_param, f_opt, idx=idx,
-                                              t0=t0, objective=want_obj, consensus=True)
+                obj, cons, tim = eng.run_dsgd_pipelined(n, eta0, b, lam_grad, reg_param, f_opt, idx=idx, t0=t0,
+                                                        objective=want_obj, consensus=True, want_time=True)
+                end = t0 + n == T or ck.due(t0 + n, T)
+                if end:  # the owed metrics of the last iterate
+                    o2, c2 = eng.run_dsgd_pipelined(0, eta0, b, lam_grad, reg_param, f_opt, objective=want_obj,
+                                                    consensus=True)
+                    cons = np.concatenate([cons, c2])
+                    obj = np.concatenate([obj, o2]) if want_obj else obj
                 self.history["consensus_error"].extend(list(cons))
                 if want_obj:
                     self.history["objective"].extend(list(obj))

@@ -184,10 +184,12 @@ int dopt_run_dsgd(dopt_ctx *ctx, int64_t t0, int64_t T, double eta0, int64_t bat
  * fused round and each round's metrics are still computed exactly once.  *n_out = the
  * entries written: T - 1 (nothing owed before) or T (owed metrics taken in); T = 0 with
  * metrics owed computes them alone (1 entry).  Any other run, dopt_set_models or new data
- * drops an owed entry; the column-blocked path runs as dopt_run_dsgd.  time_out: none. */
+ * drops an owed entry; the column-blocked path runs as dopt_run_dsgd.  obj_out / cons_out:
+ * [T + 1] or NULL; time_out: [T] (the end of each of this call's rounds) or NULL. */
 int dopt_run_dsgd_pipelined(dopt_ctx *ctx, int64_t t0, int64_t T, double eta0, int64_t batch,
                             const int32_t *idx, double lam_grad, double lam_obj, double f_opt,
-                            uint32_t flags, double *obj_out, double *cons_out, int64_t *n_out);
+                            uint32_t flags, double *obj_out, double *cons_out, double *time_out,
+                            int64_t *n_out);
 
 /* T rounds of CentralizedTrainer.run (trainer.py:41-71): every worker's
  * gradient at the shared iterate, their mean, one step; objective at the
