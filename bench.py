@@ -99,7 +99,15 @@ def cpu_baseline(seconds, n_workers=64, d=1024, m=512, seed=11):
     t0 = time.perf_counter()
     O.run_decentralized(shards, W, rounds, cfg, Xf, yf, 0.0)
     dt = time.perf_counter() - t0
+    cpu_model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), cpu_model)
+    except OSError:
+        pass
     return {"value": n_workers * rounds / dt, "unit": "worker-iters/s", "cores": int(threads), "kind": "port",
+            "cpu_model": cpu_model, "nproc": os.cpu_count(),
+            "blas_threads": int(threads),
             "sample": f"oracle (numpy float64 restatement of trainer.py:161-193) on {n_workers} workers x "
                       f"{m} rows x d={d}, {rounds} rounds, {dt:.1f} s, full-shard batches, metrics every round; "
                       f"extrapolated per worker to C3's 4096 (its dense W @ X, 0.08-0.14 s of a 9.25 s reference "

@@ -1299,22 +1299,33 @@ hipError_t launch_cons(int dtype, const void* x, const void* xbar, int64_t n, in
 // All loads of the worker (own row, gradient, up to MAXE neighbour rows) are issued before
 // the first use, so a wave has ~30 16-byte loads in flight instead of one dependent chain
 // per chunk.
-template <typename T, int CPL>
+// k_mix: the multi-GPU phase path's mix + step (and the lagged schedule's xbar, consensus and
+// send rows).  WPW waves per worker, each holding CPL 16-byte chunks per lane of its slice
+// of the row: rows of 8-16 chunks per lane run as 2-4 waves of 4, so every CSR entry's loads
+// of a wave are in flight at once (one latency per wave instead of one per entry; C3 float64
+// rows, 4 neighbours: 37.3 us per round with one wave of 8 chunks per worker).
+template <typename T, int CPL, int WPW = 1>
 __global__ __launch_bounds__(NT) void k_mix(const RoundArgs a, const T* __restrict__ G, int n) {
   using V = typename VT<T>::v;
   constexpr int VN = VT<T>::n;
   constexpr int MAXE = CPL <= 4 ? 6 : 0;  // CSR entries held in registers (deg + 1 <= 5 for ring / torus / 4-regular)
+  static_assert(NW % WPW == 0, "a worker's waves share one workgroup");
+  __shared__ double cred[NW];
   const int lane = threadIdx.x & 63;
-  const int i = blockIdx.x * NW + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (i >= n) return;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int i = (blockIdx.x * NW + wave) / WPW;
+  const int c0 = (wave % WPW) * 64 * CPL;  // first chunk of this wave's slice
+  const bool live = i < n;
   const int64_t ld = a.ld;
   const int nch = a.nchunks;
   const T eta = (T)a.eta;
+  V dv = V(0);  // consensus term of x_old[i] (a.xsum): formed as k_round's F_CONS forms it
+  if (live) {
   const T* xo = (const T*)a.x_old + (int64_t)i * ld;
   V own[CPL], gc[CPL], acc[CPL];
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
-    const int c = lane + 64 * j;
+    const int c = c0 + lane + 64 * j;
     const bool in = c < nch;
     own[j] = in ? *(const V*)(xo + (int64_t)c * VN) : V(0);
     gc[j] = in ? *(const V*)(G + (int64_t)i * ld + (int64_t)c * VN) : V(0);
@@ -1323,7 +1334,7 @@ __global__ __launch_bounds__(NT) void k_mix(const RoundArgs a, const T* __restri
   if (a.flags & F_MEAN) {
 #pragma unroll
     for (int j = 0; j < CPL; ++j)
-      if (lane + 64 * j < nch) acc[j] = mix_chunk<T, T>(a, i, lane + 64 * j, own[j]);
+      if (c0 + lane + 64 * j < nch) acc[j] = mix_chunk<T, T>(a, i, c0 + lane + 64 * j, own[j]);
   } else {
     const int64_t e0 = a.rp[i], e1 = a.rp[i + 1];
     auto row_of = [&](int64_t e) {
@@ -1339,7 +1350,7 @@ __global__ __launch_bounds__(NT) void k_mix(const RoundArgs a, const T* __restri
           const T* src = row_of(e0 + k);
 #pragma unroll
           for (int j = 0; j < CPL; ++j) {
-            const int c = lane + 64 * j;
+            const int c = c0 + lane + 64 * j;
             r[k][j] = c < nch ? *(const V*)(src + (int64_t)c * VN) : V(0);
           }
         }
@@ -1358,17 +1369,16 @@ __global__ __launch_bounds__(NT) void k_mix(const RoundArgs a, const T* __restri
         const T* src = row_of(e);
 #pragma unroll
         for (int j = 0; j < CPL; ++j) {
-          const int c = lane + 64 * j;
+          const int c = c0 + lane + 64 * j;
           if (c < nch) acc[j] += wt * *(const V*)(src + (int64_t)c * VN);
         }
       }
     }
   }
-  V dv = V(0);  // consensus term of x_old[i] (a.xsum): formed exactly as k_round's F_CONS forms it
   const int64_t s0 = a.sptr ? a.sptr[i] : 0, s1 = a.sptr ? a.sptr[i + 1] : 0;
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
-    const int c = lane + 64 * j;
+    const int c = c0 + lane + 64 * j;
     if (c >= nch) continue;
     if (a.xsum) {  // xbar = (T)(column sum / n) of the iterates being mixed, as k_colsum_final rounds it
       V xb;
@@ -1383,15 +1393,37 @@ __global__ __launch_bounds__(NT) void k_mix(const RoundArgs a, const T* __restri
     for (int64_t q = s0; q < s1; ++q)  // rows peers read next round: the send buffer is refreshed here
       *(V*)((T*)a.send + (int64_t)a.sslot[q] * ld + (int64_t)c * VN) = xn;
   }
+  }
   if (a.xsum && a.slab_cons) {
     const double cs = wave_sum((double)hsum<T>(dv));
-    if (lane == 0) a.slab_cons[i] = cs;
+    if constexpr (WPW == 1) {
+      if (live && lane == 0) a.slab_cons[i] = cs;
+    } else {  // the worker's waves meet in LDS, summed in slice order
+      if (lane == 0) cred[wave] = cs;
+      __syncthreads();
+      if (live && lane == 0 && wave % WPW == 0) {
+        double t = cred[wave];
+#pragma unroll
+        for (int q = 1; q < WPW; ++q) t += cred[wave + q];
+        a.slab_cons[i] = t;
+      }
+    }
   }
 }
 
 template <typename T>
 static hipError_t launch_mix_t(int cpl, const RoundArgs& a, const T* G, int n, hipStream_t s) {
+  // A/B knob DOPT_MIX_ONEWAVE=1: one wave per worker for rows of 8 / 16 chunks per lane
+  const char* ov = getenv("DOPT_MIX_ONEWAVE");
+  const bool one = ov && ov[0] == '1';
   const dim3 grid((n + NW - 1) / NW);
+  if (!one && (cpl == 8 || cpl == 16)) {
+    const int wpw = cpl / 4;
+    const dim3 g2(((int64_t)n * wpw + NW - 1) / NW);
+    if (wpw == 2) hipLaunchKernelGGL((k_mix<T, 4, 2>), g2, dim3(NT), 0, s, a, G, n);
+    else hipLaunchKernelGGL((k_mix<T, 4, 4>), g2, dim3(NT), 0, s, a, G, n);
+    return hipGetLastError();
+  }
   switch (cpl) {
     case 1: hipLaunchKernelGGL((k_mix<T, 1>), grid, dim3(NT), 0, s, a, G, n); break;
     case 2: hipLaunchKernelGGL((k_mix<T, 2>), grid, dim3(NT), 0, s, a, G, n); break;
