@@ -19,7 +19,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DOPT_LIB", os.path.join(_HERE, "libdopt.so"))
 
-OK, ERR_INVALID, ERR_HIP, ERR_STATE, ERR_UNSUPPORTED, ERR_COMM = 0, -1, -2, -3, -4, -5
+OK, ERR_INVALID, ERR_HIP, ERR_STATE, ERR_UNSUPPORTED, ERR_COMM, ERR_NOMEM, ERR_RUNTIME = 0, -1, -2, -3, -4, -5, -6, -7
 LOGISTIC, QUADRATIC = 0, 1
 F32, F64 = 0, 1
 RUN_OBJECTIVE, RUN_CONSENSUS = 1, 2
@@ -136,6 +136,10 @@ def check(rc):
         raise ValueError(msg)
     if rc == ERR_UNSUPPORTED:
         raise NotImplementedError(msg)
+    if rc == ERR_NOMEM:
+        raise MemoryError("libdopt: host memory exhausted")
+    if rc == ERR_RUNTIME:
+        raise RuntimeError("libdopt: host failure (a helper thread could not start)")
     raise RuntimeError(f"libdopt error {rc}: {msg}")
 
 

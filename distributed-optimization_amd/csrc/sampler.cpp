@@ -279,9 +279,13 @@ class ShufflePool {
       : n_(n), rows_(rows), b_(b), out_(out), stride_(max_m), njobs_(T * n),
         B_(std::max<int64_t>(1, (int64_t(1) << 15) / max_m)), nbatch_((njobs_ + B_ - 1) / B_),
         js_((size_t)(kSlots * B_ * stride_)) {
-    for (int h = 0; h < kThreads; ++h) {
-      done_[h].v.store(0, std::memory_order_relaxed);
-      th_[h] = std::thread([this, h] { run(h); });
+    try {
+      for (int h = 0; h < kThreads; ++h) th_[h] = std::thread([this, h] { run(h); });
+    } catch (...) {  // a thread that would not start: release the started ones, then report
+      abort_.store(true, std::memory_order_release);
+      for (auto& t : th_)
+        if (t.joinable()) t.join();
+      throw;
     }
   }
   ~ShufflePool() {
@@ -309,7 +313,10 @@ class ShufflePool {
     std::vector<int64_t> perm;
     int64_t mine = 0;
     for (int64_t k = h; k < nbatch_; k += kThreads) {
-      while (filtered_.v.load(std::memory_order_acquire) <= k) std::this_thread::yield();
+      while (filtered_.v.load(std::memory_order_acquire) <= k) {
+        if (abort_.load(std::memory_order_acquire)) return;
+        std::this_thread::yield();
+      }
       const uint32_t* js = js_.data() + (size_t)((k % kSlots) * B_ * stride_);
       for (int64_t q = k * B_; q < std::min(njobs_, (k + 1) * B_); ++q) {
         const int64_t i = q % n_;
@@ -330,11 +337,14 @@ class ShufflePool {
   std::vector<uint32_t> js_;
   Ctr filtered_;
   Ctr done_[kThreads];
+  std::atomic<bool> abort_{false};
   std::thread th_[kThreads];
 };
 
-extern "C" int dopt_mt_choice_rounds(uint32_t key[624], int32_t* pos, int64_t T, int64_t n_workers,
-                                     const int64_t* shard_rows, int64_t b, int32_t* out) {
+// The numpy state (key, pos) is written only when a call completes: a call that fails leaves
+// it where it was.
+static int choice_rounds(uint32_t key[624], int32_t* pos, int64_t T, int64_t n_workers, const int64_t* shard_rows,
+                         int64_t b, int32_t* out) {
   if (b < 0) return DOPT_ERR_INVALID;
   if (int rc = check_rounds(key, pos, T, n_workers, shard_rows)) return rc;
   if (T == 0 || n_workers == 0) return DOPT_OK;
@@ -378,8 +388,7 @@ extern "C" int dopt_mt_choice_rounds(uint32_t key[624], int32_t* pos, int64_t T,
   return DOPT_OK;
 }
 
-extern "C" int dopt_mt_advance_rounds(uint32_t key[624], int32_t* pos, int64_t T, int64_t n_workers,
-                                      const int64_t* shard_rows) {
+static int advance_rounds(uint32_t key[624], int32_t* pos, int64_t T, int64_t n_workers, const int64_t* shard_rows) {
   if (int rc = check_rounds(key, pos, T, n_workers, shard_rows)) return rc;
   if (T == 0 || n_workers == 0) return DOPT_OK;
   BlockRing ring(key, *pos);
@@ -394,4 +403,28 @@ extern "C" int dopt_mt_advance_rounds(uint32_t key[624], int32_t* pos, int64_t T
       if (shard_rows[i] > 0) st.draw(shard_rows[i], js.data());  // every choice() is a whole permutation
   st.save(key, pos);
   return DOPT_OK;
+}
+
+// Host threads or buffers that cannot be had (std::system_error / std::bad_alloc) come back as
+// error codes, not as exceptions through the C ABI.
+extern "C" int dopt_mt_choice_rounds(uint32_t key[624], int32_t* pos, int64_t T, int64_t n_workers,
+                                     const int64_t* shard_rows, int64_t b, int32_t* out) {
+  try {
+    return choice_rounds(key, pos, T, n_workers, shard_rows, b, out);
+  } catch (const std::bad_alloc&) {
+    return DOPT_ERR_NOMEM;
+  } catch (...) {
+    return DOPT_ERR_RUNTIME;
+  }
+}
+
+extern "C" int dopt_mt_advance_rounds(uint32_t key[624], int32_t* pos, int64_t T, int64_t n_workers,
+                                      const int64_t* shard_rows) {
+  try {
+    return advance_rounds(key, pos, T, n_workers, shard_rows);
+  } catch (const std::bad_alloc&) {
+    return DOPT_ERR_NOMEM;
+  } catch (...) {
+    return DOPT_ERR_RUNTIME;
+  }
 }

@@ -40,6 +40,8 @@ typedef struct dopt_ctx dopt_ctx;
 #define DOPT_ERR_STATE (-3)       /* call out of order (no data / topology loaded) */
 #define DOPT_ERR_UNSUPPORTED (-4) /* shape outside what this build handles (NotImplementedError) */
 #define DOPT_ERR_COMM (-5)        /* RCCL failure */
+#define DOPT_ERR_NOMEM (-6)       /* host memory exhausted */
+#define DOPT_ERR_RUNTIME (-7)     /* other host failure (e.g. a helper thread that cannot start) */
 
 /* problems: obj_problems.py:3-20 (logistic), obj_problems.py:39-53 (quadratic) */
 #define DOPT_LOGISTIC 0
