@@ -52,6 +52,41 @@ __global__ __launch_bounds__(W * 64) void k_shard_read_w(const f4* __restrict__ 
   if (acc.x == 1234.5f) { lds[threadIdx.x] = 1; out[0] = acc.y + acc.z + acc.w + lds[threadIdx.x ^ 1]; }
 }
 
+// C5's stream shape: every workgroup reads 17 rows' segments per 1 KiB column block and (WR)
+// writes one 1 KiB segment -- 94 % reads, 6 % writes interleaved -- vs the same reads alone.
+// x: [n_wg][17][cols] f4 rows, y: [n_wg][cols] f4.
+// WR = 2: the written segments are gathered in LDS and leave in 16 KiB bursts (16 blocks).
+template <int WR>
+__global__ __launch_bounds__(256) void k_c5_stream(const f4* __restrict__ x, f4* __restrict__ y, int cols,
+                                                   float* out) {
+  __shared__ f4 wbuf[16][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const f4* base = x + (size_t)blockIdx.x * 17 * cols;
+  f4 acc = f4(0);
+  for (int cb = 0; cb < cols; cb += 64) {
+    f4 v[5];
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {  // waves 0..3 read rows wave, wave+4, ... (17 rows; wave 0 the 17th)
+      const int row = wave + 4 * r;
+      const f4* p = base + (size_t)row * cols + cb + lane;
+      v[r] = row < 17 ? (WR >= 3 ? *p : __builtin_nontemporal_load(p)) : f4(0);
+    }
+#pragma unroll
+    for (int r = 0; r < 5; ++r) acc += v[r];
+    if ((WR == 1 || WR == 4) && wave == 0) y[(size_t)blockIdx.x * cols + cb + lane] = acc;
+    if (WR == 5 && wave == 0) __builtin_nontemporal_store(acc, y + (size_t)blockIdx.x * cols + cb + lane);
+    if (WR == 2 && wave == 0) {
+      const int k = (cb >> 6) & 15;
+      wbuf[k][lane] = acc;
+      if (k == 15 || cb + 64 >= cols) {
+        const int cb0 = cb - 64 * k;
+        for (int q = 0; q <= k; ++q) y[(size_t)blockIdx.x * cols + cb0 + 64 * q + lane] = wbuf[q][lane];
+      }
+    }
+  }
+  if (acc.x == 1234.5f) out[0] = acc.y + acc.z + acc.w;
+}
+
 __global__ __launch_bounds__(256) void k_grid_read(const f4* __restrict__ x, size_t n, float* out) {
   f4 acc = f4(0);
   const size_t stride = (size_t)gridDim.x * 256;
@@ -130,5 +165,30 @@ int main() {
   printf("8 waves, 2048 WGs x 1024 rows %.3f ms  %.0f GB/s\n", ms, gbs(ms, bytes));
   ms = timeit([&] { hipLaunchKernelGGL(k_copy, dim3(8192), dim3(256), 0, 0, x, y, n4 / 4); }, 5);
   printf("copy 2 GiB             %.3f ms  %.0f GB/s (read+write)\n", ms, gbs(ms, bytes / 2));
+  {  // C5's shape scaled to the 8 GiB buffer: 1024 workgroups x 17 rows x 480 KiB (+ 1 row written)
+    const int cols = (int)(bytes / 16 / 1024 / 17) / 64 * 64;
+    const size_t rbytes = (size_t)1024 * 17 * cols * 16, wbytes = (size_t)1024 * cols * 16;
+    ms = timeit([&] { hipLaunchKernelGGL((k_c5_stream<0>), dim3(1024), dim3(256), 0, 0, x, y, cols, out); }, 5);
+    printf("C5 shape, reads only   %.3f ms  %.0f GB/s\n", ms, gbs(ms, rbytes));
+    const double ms_r = ms;
+    ms = timeit([&] { hipLaunchKernelGGL((k_c5_stream<1>), dim3(1024), dim3(256), 0, 0, x, y, cols, out); }, 5);
+    printf("C5 shape, + 6%% writes  %.3f ms  %.0f GB/s (read+write); the writes cost %.3f ms = %.0f GB/s\n", ms,
+           gbs(ms, rbytes + wbytes), ms - ms_r, gbs(ms - ms_r, wbytes));
+    ms = timeit([&] { hipLaunchKernelGGL((k_c5_stream<2>), dim3(1024), dim3(256), 0, 0, x, y, cols, out); }, 5);
+    printf("  ... writes in 16 KiB bursts %.3f ms; the writes cost %.3f ms = %.0f GB/s\n", ms, ms - ms_r,
+           gbs(ms - ms_r, wbytes));
+    ms = timeit([&] { hipLaunchKernelGGL((k_c5_stream<3>), dim3(1024), dim3(256), 0, 0, x, y, cols, out); }, 5);
+    printf("  default-policy reads only %.3f ms\n", ms);
+    const double ms_d = ms;
+    ms = timeit([&] { hipLaunchKernelGGL((k_c5_stream<4>), dim3(1024), dim3(256), 0, 0, x, y, cols, out); }, 5);
+    printf("  default-policy reads + writes %.3f ms; the writes cost %.3f ms\n", ms, ms - ms_d);
+    ms = timeit([&] { hipLaunchKernelGGL((k_c5_stream<5>), dim3(1024), dim3(256), 0, 0, x, y, cols, out); }, 5);
+    printf("  default-policy reads + nt writes %.3f ms; the writes cost %.3f ms\n", ms, ms - ms_d);
+    ms = timeit([&] { hipLaunchKernelGGL((k_c5_stream<0>), dim3(4096), dim3(256), 0, 0, x, y, cols / 4, out); }, 5);
+    printf("  4096 WGs, reads only %.3f ms\n", ms);
+    const double ms_r4 = ms;
+    ms = timeit([&] { hipLaunchKernelGGL((k_c5_stream<1>), dim3(4096), dim3(256), 0, 0, x, y, cols / 4, out); }, 5);
+    printf("  4096 WGs, + writes   %.3f ms; the writes cost %.3f ms\n", ms, ms - ms_r4);
+  }
   return 0;
 }
