@@ -274,3 +274,71 @@ def test_pipelined_chain_matches_single_context(tmp_path, monkeypatch, world, ba
     got = np.load(tmp_path / "dist.npz")
     assert len(got["obj"]) == len(got["cons"]) == 9
     _compare_single(got, dtype, False, 9)
+
+
+def _ckpt_rank(rank, world, port, out):
+    import json
+
+    import torch  # noqa: F401
+    import torch.distributed as dist
+
+    import data as odata
+    from trainer import CentralizedTrainer, DecentralizedTrainer
+    from worker import Worker
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    meta = json.load(open(os.path.join(G, "traj_c2.json")))
+    z = np.load(os.path.join(G, "traj_c2.npz"))
+    shards, Xf, yf = odata.generate(dict(meta["config"]), order=z["order"])
+    res = {}
+    for label in ("D-SGD (Ring)", "Centralized"):
+        j = meta["labels"].index(label)
+        st = ("MT19937", z[f"state{j}_key"], int(z[f"state{j}_pos"]), 0, 0.0)
+        ck = os.path.join(out, f"ck_{j}.npz")  # every rank names the same file; rank 0 writes it
+
+        def make(cfg):
+            ws = [Worker(i, {"X": X, "y": y}, cfg["local_batch_size"], Xf.shape[1], cfg)
+                  for i, (X, y) in enumerate(shards)]
+            if label == "Centralized":
+                return CentralizedTrainer(ws, Xf.shape[1], cfg)
+            return DecentralizedTrainer(ws, "ring", Xf.shape[1], cfg)
+
+        cfg = dict(meta["config"])
+        np.random.set_state(st)
+        make(dict(cfg, checkpoint_path=ck, checkpoint_every=20)).run(20, Xf, yf, meta["f_opt"])
+        dist.barrier()  # the file is written before any rank resumes from it
+        np.random.seed(99)
+        tr = make(dict(cfg, resume_from=ck))
+        h, x = tr.run(50, Xf, yf, meta["f_opt"])
+        res[f"L{j}_objective"] = np.asarray(h["objective"])
+        if "consensus_error" in h:
+            res[f"L{j}_consensus"] = np.asarray(h["consensus_error"])
+        res[f"L{j}_pos"] = np.int64(np.random.get_state()[2])
+        res[f"L{j}_x"] = np.asarray(x)
+    if rank == 0:
+        np.savez(os.path.join(out, "ckpt.npz"), **res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_trainers_multiprocess_checkpoint_resume(tmp_path):
+    """Checkpoint / resume under a 2-rank job: rank 0 writes the file after 20 rounds (the
+    gathered iterates), both ranks resume from it; the 50-round history equals the
+    reference's C2 trajectory (rtol 1e-9), and every rank ends on the same RNG position as
+    one uninterrupted process would."""
+    import json
+
+    import torch.multiprocessing as mp
+
+    mp.start_processes(_ckpt_rank, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    got = np.load(tmp_path / "ckpt.npz")
+    G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    meta = json.load(open(os.path.join(G, "traj_c2.json")))
+    z = np.load(os.path.join(G, "traj_c2.npz"))
+    for label in ("D-SGD (Ring)", "Centralized"):
+        j = meta["labels"].index(label)
+        np.testing.assert_allclose(got[f"L{j}_objective"], z[f"L{j}_objective"][:50], rtol=1e-9)
+        if label != "Centralized":
+            np.testing.assert_allclose(got[f"L{j}_consensus"], z[f"L{j}_consensus"][:50], rtol=1e-9)
