@@ -576,9 +576,12 @@ int split_metrics(dopt_ctx* c, const void* x_state, const void* point, bool shar
 }
 
 // D-SGD rounds for rows longer than the row-resident kernel takes (config C5).
+// lag = 1: a pipelined run that owes the metrics of the current iterate (computed by this
+// call's first step; coefficients, S and xbar of that iterate are current); carry_out: leave
+// the metrics of the last iterate owed.  *nh = history entries written.
 int run_dsgd_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch, const int32_t* idx,
                    double lam_grad, double lam_obj, double f_opt, uint32_t flags, double* obj_out,
-                   double* cons_out, double* time_out) {
+                   double* cons_out, double* time_out, int64_t lag, bool carry_out, int64_t* nh_out) {
   int rc;
   const bool want_obj = flags & DOPT_RUN_OBJECTIVE, want_cons = flags & DOPT_RUN_CONSENSUS;
   const bool metrics = want_obj || want_cons;
@@ -591,10 +594,10 @@ int run_dsgd_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batc
   if ((rc = ensure_split(c))) return rc;
   const int64_t CH = idx ? idx_chunk_rounds(c, T, batch) : 1;
   int& xb = c->xb;
-  if ((rc = colsum_current(c))) return rc;
+  if (!lag && (rc = colsum_current(c))) return rc;
   RoundArgs p = base_args(c);
   p.x_old = c->xs[c->cur];
-  if (full) {  // prologue: coefficients of the starting iterates
+  if (full && !lag) {  // prologue: coefficients of the starting iterates (carried: the last step made them)
     HIPOK(launch_split_dots(c->dtype, 0, p, (int)c->n, c->stream));
     HIPOK(launch_split_coef(c->dtype, c->problem, 1, p, (int)c->n, c->stream));
   }
@@ -617,7 +620,7 @@ int run_dsgd_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batc
       HIPOK(launch_split_dots(c->dtype, 0, a, (int)c->n, c->stream));
       HIPOK(launch_split_coef(c->dtype, c->problem, 1, a, (int)c->n, c->stream));
     }
-    const bool met = fused_met && metrics && h > 0;
+    const bool met = fused_met && metrics && (h > 0 || lag);
     a.flags |= (met && want_cons ? F_CONS : 0) | (met && want_obj ? F_LOSS : 0);
     if (a.flags & F_LOSS) c->loss_groups = c->n;  // per-worker loss slabs
     if (c->prof && (rc = prof_event(c, false))) return rc;
@@ -634,7 +637,7 @@ int run_dsgd_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batc
                               nullptr, 0.0, 0, c->stream, c->S));
     if ((rc = refresh_sums_t(c))) return rc;
     if (met) {
-      if ((rc = history(c, h - 1, c->xbar[xb], want_cons, want_obj, c->n))) return rc;
+      if ((rc = history(c, h - 1 + lag, c->xbar[xb], want_cons, want_obj, c->n))) return rc;
     } else if (!fused_met && metrics) {
       if ((rc = split_metrics(c, c->xs[c->cur ^ 1], c->xbar[xb ^ 1], false, want_cons, want_obj))) return rc;
       if ((rc = history(c, h, c->xbar[xb ^ 1], want_cons, want_obj, c->n))) return rc;
@@ -642,11 +645,15 @@ int run_dsgd_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batc
     c->cur ^= 1;
     xb ^= 1;
   }
-  if (fused_met && metrics && T > 0) {
+  int64_t nh = T + lag;
+  if (carry_out && T > 0) {
+    nh -= 1;  // the metrics of x_T: owed to the next pipelined run
+  } else if (fused_met && metrics && (T > 0 || lag)) {
     if ((rc = split_metrics(c, c->xs[c->cur], c->xbar[xb], false, want_cons, want_obj))) return rc;
-    if ((rc = history(c, T - 1, c->xbar[xb], want_cons, want_obj, c->n))) return rc;
+    if ((rc = history(c, nh - 1, c->xbar[xb], want_cons, want_obj, c->n))) return rc;
   }
-  return finish_run(c, T, T, lam_obj, f_opt, want_obj ? obj_out : nullptr, want_cons ? cons_out : nullptr,
+  if (nh_out) *nh_out = nh;
+  return finish_run(c, nh, T, lam_obj, f_opt, want_obj ? obj_out : nullptr, want_cons ? cons_out : nullptr,
                     time_out);
 }
 
@@ -1064,10 +1071,19 @@ static int run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t bat
                        !(two && atoi(two) != 0) && !(ccs && ccs[0] == '0');
   const int64_t CH = idx ? idx_chunk_rounds(c, T, batch) : 1;
   int& xb = c->xb;
-  if (c->split) {
-    if (n_out) *n_out = T;
-    return run_dsgd_split(c, t0, T, eta0, batch, idx, lam_grad, lam_obj, f_opt, flags, obj_out, cons_out,
-                          time_out);
+  if (c->split) {  // the column-blocked rounds pipeline the same way (full-shard batches)
+    const bool sfused = batch >= c->max_m && !c->obj_sep && metrics;
+    if (carry_in && !sfused) return fail(DOPT_ERR_INVALID, "pipelined run: the pending metrics need a fused run");
+    int64_t nh = 0;
+    if ((rc = run_dsgd_split(c, t0, T, eta0, batch, idx, lam_grad, lam_obj, f_opt, flags, obj_out, cons_out,
+                             time_out, carry_in ? 1 : 0, pipelined && sfused, &nh)))
+      return rc;
+    if (pipelined && sfused && T > 0) {
+      c->carry_pending = true;
+      c->carry_flags = flags & (DOPT_RUN_OBJECTIVE | DOPT_RUN_CONSENSUS);
+    }
+    if (n_out) *n_out = nh;
+    return DOPT_OK;
   }
   // pipelined: the last round's metrics stay owed (its pass would be the only unfused one)
   const bool carry_out = pipelined && fused && metrics;

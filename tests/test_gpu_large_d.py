@@ -153,3 +153,32 @@ def test_single_evaluations_wide_rows_vs_oracle(d):
                                    rtol=1e-12)
         np.testing.assert_allclose(P.quadratic_objective(w, X, yq, 2e-3), O.quadratic_objective(w, X, yq, 2e-3),
                                    rtol=1e-12)
+
+
+@pytest.mark.parametrize("mean", [True, False])
+def test_split_pipelined_runs_equal_one_run(mean):
+    """Column-blocked rounds pipelined across calls (bench.py's C5 timing): the last step's
+    next-round coefficients, S and xbar carry over, the owed metrics ride the next call's
+    first step -- concatenated, exactly one run's history and iterates."""
+    n, d, m = 9, 2100, 12
+    shards = _data(n, d, m, 7, "quadratic")
+    eng = _engine(shards, "quadratic")
+    top = TP.build("fully_connected" if mean else "ring", n)
+    if mean:
+        eng.set_mixing_mean(*top.uniform_offdiag())
+    else:
+        eng.set_topology(top.row_ptr, top.col, top.w)
+    eng.set_models(np.zeros((n, d)))
+    obj_ref, cons_ref, _ = eng.run_dsgd(9, 0.05, m, 2e-3, 2e-3, 0.1)
+    x_ref = eng.get_models()
+    eng.set_models(np.zeros((n, d)))
+    objs, conss, t0 = [], [], 0
+    for k in (3, 1, 5, 0):
+        o, c = eng.run_dsgd_pipelined(k, 0.05, m, 2e-3, 2e-3, 0.1, t0=t0)
+        objs.append(o)
+        conss.append(c)
+        t0 += k
+    assert np.array_equal(np.concatenate(objs), obj_ref)
+    assert np.array_equal(np.concatenate(conss), cons_ref)
+    assert np.array_equal(eng.get_models(), x_ref)
+    eng.close()
