@@ -478,7 +478,12 @@ def main():
         "dtype": "f32" if esz == 4 else "f64",
         "data": "synthetic (device-generated X~N(0,1) rounded to float32 + bias column, planted-w* labels, "
                 "5% flips)",
-        "config": {"workload": workload, "arithmetic": "float64" if esz == 8 else "float32",
+        "config": {"workload": workload,
+                   "timing": ("pipelined calls: the timed call holds exactly `steps` fused rounds and `steps` "
+                              "metric evaluations (its first pass takes the warmup's last metrics, its last "
+                              "metrics are taken after the timed region; DESIGN.md section 7)"
+                              if flush is not None else "one call of `steps` rounds incl. its final metrics pass"),
+                   "arithmetic": "float64" if esz == 8 else "float32",
                    "iterates": "float64" if esz == 8 else "float32", "shard_storage": storage,
                    "workers_per_gpu": n, "d": d, "rows_per_worker": m, "batch": b, "topology": top.name,
                    "degree": args.degree if args.config == "c3" else None,
