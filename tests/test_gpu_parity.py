@@ -620,3 +620,39 @@ def test_pipelined_runs_equal_one_run(dtype):
     o, _ = eng.run_dsgd_pipelined(3, 0.05, m, 1e-3, 1e-3, 0.0)
     assert len(o) == 2
     eng.close()
+
+
+@pytest.mark.parametrize("case", ["few_logistic", "device_sampler", "host_minibatch"])
+def test_pipelined_runs_other_paths(case):
+    """Pipelined chains on the other round paths: few logistic workers (separate metrics
+    pass, nothing owed: every call returns all its entries), device-drawn minibatches inside
+    the metrics pass (owed like full shards; the Philox round counter follows t0) and host
+    minibatches (idx) -- concatenated, exactly one run."""
+    rng = np.random.default_rng(5)
+    n, d, m, T = (12, 40, 30, 8) if case == "few_logistic" else (300, 200, 40, 8)
+    eng = _dopt.Engine(0, "float64")
+    eng.generate_shards("logistic", n, d, m, seed=9, flip=0.05)
+    top = topology.random_regular(n, 4, seed=3)
+    eng.set_topology(top.row_ptr, top.col, top.w)
+    b, idx = m, None
+    if case == "device_sampler":
+        b = 7
+        eng.set_sampler("device", seed=11)
+    elif case == "host_minibatch":
+        b = 7
+        idx = np.stack([np.stack([rng.permutation(m)[:b] for _ in range(n)]) for _ in range(T)]).astype(np.int32)
+    eng.set_models(np.zeros((n, d)))
+    obj_ref, cons_ref, _ = eng.run_dsgd(T, 0.05, b, 1e-3, 1e-3, 0.0, idx=idx)
+    x_ref = eng.get_models()
+    eng.set_models(np.zeros((n, d)))
+    objs, conss, t0 = [], [], 0
+    for k in (3, 2, 3, 0):
+        o, c = eng.run_dsgd_pipelined(k, 0.05, b, 1e-3, 1e-3, 0.0, t0=t0,
+                                      idx=None if idx is None or k == 0 else idx[t0:t0 + k])
+        objs.append(o)
+        conss.append(c)
+        t0 += k
+    np.testing.assert_array_equal(np.concatenate(objs), obj_ref)
+    np.testing.assert_array_equal(np.concatenate(conss), cons_ref)
+    np.testing.assert_array_equal(eng.get_models(), x_ref)
+    eng.close()
