@@ -172,13 +172,17 @@ def kernel_name():
     return _dopt.last_round_kernel() or "unknown"
 
 
-def bytes_per_round(eng, n, d, m):
+def bytes_per_round(eng, n, d, m, kname=""):
     """shard rows + labels read once, own iterate read + new iterate written
-    (neighbour rows hit L2 / MALL): n * (xesz * (m*d + m) + esz * 2d)."""
+    (neighbour rows hit L2 / MALL): n * (xesz * (m*d + m) + esz * 2d).  The row-space pass
+    (C5, k_rs_pass: iterates held as Z + X_i^T beta_i) reads the rows and one
+    float64 coefficient per row and writes no iterate: n * m * (xesz * d + 8)."""
     import _dopt
 
     esz = 4 if eng.dtype == _dopt.F32 else 8
     xesz = 4 if eng.data_dtype == _dopt.F32 else 8
+    if "k_rs_pass" in kname:
+        return n * m * (xesz * d + 8)
     return n * (xesz * (m * d + m) + esz * 2 * d)
 
 
@@ -458,7 +462,7 @@ def main():
     xesz = 4 if eng.data_dtype == _dopt.F32 else 8
     kname = kernel_name()
     traffic, traffic_src = pmc_traffic(kname) if args.config == "c3" and n == 4096 and world == 1 else (None, None)
-    bytes_per_launch = bytes_per_round(eng, n, d, m)
+    bytes_per_launch = bytes_per_round(eng, n, d, m, kname)
     avg_s = (kr_ms / launches) * 1e-3 if launches else float("nan")
     achieved = bytes_per_launch / avg_s / 1e9 if launches else None
     value = n_global * args.steps / dt

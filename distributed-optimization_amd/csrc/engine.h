@@ -97,6 +97,55 @@ struct FoldArgs {
   double* out_q;
 };
 
+// Row-space rounds (rowspace.hip): complete graph (uniform W_ii), quadratic objective, full
+// shards of 1..kRsMaxRows rows, iterates that start equal.  x_i = Z + X_i^T beta_i.
+constexpr int kRsMaxRows = 64;  // rows per worker (one lane each in k_rs_rows; Gram pairs in k_rs_gram)
+struct RsArgs {
+  const void* X;           // [rows x ld] T shard rows
+  const void* y;           // [rows] T labels / targets
+  int32_t y_is_f32;
+  const int64_t* off;      // [n+1] first row of every worker
+  int64_t rows;            // all rows (upart stride)
+  int64_t ld;              // row stride in elements
+  int32_t nch;             // 16-byte chunks of a row
+  const int64_t* grow;     // [wg+1] row bounds of the pass's row groups
+  int32_t wg;              // row groups (cpart rows)
+  int32_t nblk;            // column blocks of the pass (64 * cb chunks each)
+  int32_t cb, nbuf;        // pass shape: 16-byte chunks per lane per block, rows in flight per wave
+  const void* xbar;        // [ld] T point of the pass's dots (xbar of the iterates)
+  double* coef_row;        // [rows] r_k / m_i of the current iterates (the pass's column-sum weights)
+  double* upart;           // [nblk x rows] partial dots X_k . xbar per column block
+  double* cpart;           // [wg x ld] partial column sums sum_k coef_k X_k per row group
+  int32_t bcap;            // row capacity per worker of z / v / beta / gram
+  double* z;               // [n x bcap] X_ik . x_i
+  double* v;               // [n x bcap] X_ik . Z
+  double* beta;            // [n x bcap]
+  const double* gram;      // [n x bcap x bcap] X_ik . X_il
+  double* gram_w;          // the same, written by the Gram fold
+  double* slab_cons;       // [n] ||x_i - xbar||^2 (k_rs_rows mode 1), or null
+  double* slab_loss;       // [n] sum_k (u_k - y_k)^2, or null
+  double* dpart;           // [nd] partials of ||Z - xbar||^2 (k_rs_cols / k_rs_init)
+  int32_t nd;
+  double* rZ;              // [ld] Z
+  double* rxbar;           // [ld] xbar (float64 master)
+  void* xbar_out;          // [ld] T copy of the updated xbar
+  const double* csum;      // [ld] all-reduced column sums C (multi-GPU), or null: sum cpart
+  double a1, q, eta, eta_n;  // w_off N, W_ii - w_off - eta mu, eta, eta / N
+};
+hipError_t launch_rs_pass(int dtype, bool cols, const RsArgs& a, hipStream_t s);
+// mode bits: 1 metric partials of the iterate the pass read, 2 next round's row state,
+// 4 initial state (z = v = u, beta = 0), 8 u = 0 without reading upart (zero start)
+hipError_t launch_rs_rows(const RsArgs& a, int n_workers, int mode, hipStream_t s);
+int rs_col_blocks(int64_t ld);  // blocks of k_rs_cols / k_rs_init (= RsArgs.nd)
+hipError_t launch_rs_cols(int dtype, const RsArgs& a, hipStream_t s);
+hipError_t launch_rs_csum(const RsArgs& a, double* out, hipStream_t s);
+hipError_t launch_rs_init(int dtype, const RsArgs& a, const void* x0, hipStream_t s);
+hipError_t launch_rs_check(int dtype, const void* x, int64_t n, int64_t ld, int32_t nch, int G, int32_t* flags,
+                           int32_t* zflag, hipStream_t s);
+hipError_t launch_rs_gram(int dtype, const RsArgs& a, int n_workers, int max_m, double* gpart, int G,
+                          hipStream_t s);
+hipError_t launch_rs_materialise(int dtype, const RsArgs& a, int n_workers, void* xout, hipStream_t s);
+
 // Kernel launchers (kernels.hip).  dtype: 0 = float, 1 = double.
 // k_round: dtype = iterates and arithmetic, xdtype = shard storage (equal, or float32 rows
 // under float64 arithmetic); cpl = 16-byte DATA chunks per lane (1, 2, 4, 8, 16); a.nchunks

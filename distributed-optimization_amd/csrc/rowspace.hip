@@ -1,0 +1,483 @@
+// rowspace.hip -- row-space D-SGD rounds for the complete graph with the quadratic objective
+// (config C5: N = 1024 workers, d = 2^20, m = b = 16).
+//
+// The reference round (trainer.py:173-175, obj_problems.py:46-53) with the complete-graph MH
+// matrix (w_off off the diagonal, W_ii on it, the same for every worker) is
+//   x_i' = w_off S + (W_ii - w_off) x_i - eta (X_i^T r_i / m_i + mu x_i),   r_ik = x_i . X_ik - y_ik
+//        = a1 xbar + q x_i - eta X_i^T (r_i / m_i),      a1 = w_off N, q = W_ii - w_off - eta mu.
+// Every term but q x_i lies in span{xbar} + rowspace(X_i), so iterates that start equal
+// (Worker.x = zeros, worker.py:13) stay of the form
+//   x_i = Z + X_i^T beta_i       (Z shared: Z' = a1 xbar + q Z;  beta_i' = q beta_i - eta r_i / m_i)
+// and the row dots follow without touching x_i:
+//   z_ik' = X_ik . x_i' = a1 u_ik + q z_ik - eta sum_l Gram_i[k][l] r_il / m_i,   u_ik = X_ik . xbar
+//   xbar' = (a1 + q) xbar - (eta / N) C,   C = sum_ik (r_ik / m_i) X_ik.
+// So a round is ONE read-only pass over the shard rows (k_rs_pass: u and C together), a
+// per-worker scalar update (k_rs_rows) and an O(d) update (k_rs_cols) -- the 4 GB iterate
+// read and the 4 GB iterate write of the direct column-blocked step (k_split_step) are gone.
+// The metrics of x_t come out of the same pass:
+//   objective at xbar_t: (u_ik - y_ik)^2 over every row  (obj_problems.py:39-44)
+//   ||x_i - xbar||^2 = ||D||^2 + sum_k beta_ik (2 X_ik . D + (Gram_i beta_i)_k),  D = Z - xbar,
+//   X_ik . D = v_ik - u_ik with v_ik = X_ik . Z carried by v' = a1 u + q v     (trainer.py:185)
+// x_i is formed only when asked for (k_rs_materialise: dopt_get_models, other run kinds).
+// All sums have a fixed order: runs are bitwise reproducible and chains equal one run.
+#include <algorithm>
+
+#include "kcommon.h"
+
+namespace dopt {
+
+template <typename T>
+__device__ __forceinline__ typename VT<T>::v rs_ld_nt(const T* p) {
+  return __builtin_nontemporal_load((const typename VT<T>::v*)p);
+}
+
+// k_rs_pass<T, COLS, CB, NBUF>: workgroup (blk, g) = column block blk (64 * CB 16-byte chunks
+// of every row) over the rows of row group g.  Wave w streams a contiguous quarter of the
+// group's rows through NBUF rotating row buffers: the loads of rows r+1 .. r+NBUF-1 are in
+// flight while row r is processed, and a buffer is refilled right after its row is done (no
+// register copies, so the compiler's wait before a row covers that row only; loads past the
+// wave's rows re-read its last row).  Per row: the partial dot with xbar over the block
+// (64-lane DPP butterfly, stashed one row per lane, stored 64 rows at a time into
+// upart[blk][row]) and, with COLS, coef_row * row accumulated in float64 registers; the four
+// waves' column sums meet in LDS (fixed order) -> cpart[g][columns of blk].
+template <typename T, bool COLS, int CB, int NBUF>
+__global__ __launch_bounds__(NT) void k_rs_pass(const RsArgs a) {
+  using V = typename VT<T>::v;
+  constexpr int VN = VT<T>::n;
+  __shared__ double red[COLS ? NW * 64 * CB * VN : 1];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int blk = blockIdx.x, g = blockIdx.y;
+  const int nch = a.nch;
+  const int64_t ld = a.ld;
+  const T* __restrict__ X = (const T*)a.X;
+  const int64_t r0 = a.grow[g], r1 = a.grow[g + 1];
+  const int64_t per = (r1 - r0 + NW - 1) / NW;
+  const int64_t wr0 = min(r1, r0 + wave * per), wr1 = min(r1, wr0 + per);
+  int cc[CB];
+  V xb[CB];
+#pragma unroll
+  for (int j = 0; j < CB; ++j) {
+    const int c = blk * 64 * CB + j * 64 + lane;
+    const bool in = c < nch;
+    cc[j] = in ? c : nch - 1;  // lanes past the row re-read its last chunk (xbar is 0 there)
+    xb[j] = in ? *(const V*)((const T*)a.xbar + (int64_t)c * VN) : V(0);
+  }
+  double acc[CB][VN];
+#pragma unroll
+  for (int j = 0; j < CB; ++j)
+#pragma unroll
+    for (int e = 0; e < VN; ++e) acc[j][e] = 0.0;
+  double* __restrict__ up = a.upart + (int64_t)blk * a.rows;
+  double stash = 0.0;
+  auto load = [&](int64_t row, V (&dst)[CB]) {
+    const T* p = X + row * ld;
+#pragma unroll
+    for (int j = 0; j < CB; ++j) dst[j] = rs_ld_nt<T>(p + (int64_t)cc[j] * VN);
+  };
+  auto process = [&](const V (&rv)[CB], int64_t r) {
+    double p = 0.0;
+#pragma unroll
+    for (int j = 0; j < CB; ++j) p += (double)hsum<T>(rv[j] * xb[j]);
+    const double dot = wave_sum_dpp(p);
+    if constexpr (COLS) {
+      const double cf = a.coef_row[r];  // wave-uniform
+#pragma unroll
+      for (int j = 0; j < CB; ++j)
+#pragma unroll
+        for (int e = 0; e < VN; ++e) acc[j][e] += cf * (double)rv[j][e];
+    }
+    const int k = (int)((r - wr0) & 63);
+    if (lane == k) stash = dot;
+    if (k == 63 || r + 1 == wr1) {
+      if (lane <= k) up[r - k + lane] = stash;
+    }
+  };
+  if (wr0 < wr1) {
+    const int64_t last = wr1 - 1;
+    V buf[NBUF][CB];
+#pragma unroll
+    for (int k = 0; k < NBUF; ++k) load(min(wr0 + k, last), buf[k]);
+    int64_t r = wr0;
+    for (; r + NBUF <= wr1; r += NBUF) {
+#pragma unroll
+      for (int k = 0; k < NBUF; ++k) {
+        process(buf[k], r + k);
+        load(min(r + k + NBUF, last), buf[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NBUF; ++k)
+      if (r + k < wr1) process(buf[k], r + k);
+  }
+  if constexpr (COLS) {
+#pragma unroll
+    for (int j = 0; j < CB; ++j)
+#pragma unroll
+      for (int e = 0; e < VN; ++e) red[wave * 64 * CB * VN + (j * 64 + lane) * VN + e] = acc[j][e];
+    __syncthreads();
+    const int64_t col0 = (int64_t)blk * 64 * CB * VN;
+    double* __restrict__ out = a.cpart + (int64_t)g * ld + col0;
+    constexpr int W = 64 * CB * VN;
+    for (int q = threadIdx.x; q < W; q += NT) {
+      if (col0 + q < ld) out[q] = ((red[q] + red[W + q]) + red[2 * W + q]) + red[3 * W + q];
+    }
+  }
+}
+
+// k_rs_rows: one workgroup per worker (m_i <= 64 rows, lane k = row k).  u_k = sum over the
+// pass's column blocks (4 waves x a quarter each, then in wave order); then the metric partials
+// of the iterate the pass read (mode & 1), the next round's row state (mode & 2), or the
+// initial state z = v = u, beta = 0 (mode & 4).
+__global__ __launch_bounds__(NT) void k_rs_rows(const RsArgs a, int mode) {
+  __shared__ double ured[NW][64];
+  __shared__ double sb[64], sr[64];
+  __shared__ double dred[NW];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int i = blockIdx.x;
+  const int64_t row0 = a.off[i];
+  const int m = (int)(a.off[i + 1] - row0);
+  const int nb = a.nblk;
+  {
+    const int b0 = (int)((int64_t)nb * wave / NW), b1 = (int)((int64_t)nb * (wave + 1) / NW);
+    double s = 0.0;
+    if (lane < m && !(mode & 8))
+      for (int b = b0; b < b1; ++b) s += a.upart[(int64_t)b * a.rows + row0 + lane];
+    ured[wave][lane] = s;
+  }
+  // ||D||^2 = ||Z - xbar||^2 of the iterate the pass read: the block partials of k_rs_cols /
+  // k_rs_init, in one fixed order (every workgroup forms the same value)
+  double dn = 0.0;
+  if (mode & 1) {
+    for (int q = threadIdx.x; q < a.nd; q += NT) dn += a.dpart[q];
+    dn = wave_sum(dn);
+    if (lane == 0) dred[wave] = dn;
+  }
+  const int64_t s0 = (int64_t)i * a.bcap;
+  if (wave == 0) {
+    sb[lane] = (lane < m && !(mode & 4)) ? a.beta[s0 + lane] : 0.0;
+    sr[lane] = lane < m ? a.coef_row[row0 + lane] : 0.0;
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  if (mode & 1) dn = ((dred[0] + dred[1]) + dred[2]) + dred[3];
+  const bool live = lane < m;
+  const double u = live ? ((ured[0][lane] + ured[1][lane]) + ured[2][lane]) + ured[3][lane] : 0.0;
+  const double yv = live ? (a.y_is_f32 ? (double)((const float*)a.y)[row0 + lane] : ((const double*)a.y)[row0 + lane])
+                         : 0.0;
+  if (mode & 4) {  // initial state of iterates that all equal xbar: z = v = X . xbar, beta = 0
+    if (live) {
+      a.z[s0 + lane] = u;
+      a.v[s0 + lane] = u;
+      a.beta[s0 + lane] = 0.0;
+      a.coef_row[row0 + lane] = (u - yv) / (double)m;
+    }
+    return;
+  }
+  const double zv = live ? a.z[s0 + lane] : 0.0;
+  const double vv = live ? a.v[s0 + lane] : 0.0;
+  const double bk = sb[lane];
+  double gb = 0.0, gr = 0.0;
+  const double* gi = a.gram + ((int64_t)i * a.bcap + lane) * a.bcap;
+  if (live) {
+    for (int l = 0; l < m; ++l) {
+      const double gkl = gi[l];
+      gb += gkl * sb[l];
+      gr += gkl * sr[l];
+    }
+  }
+  if (mode & 1) {
+    const double e = u - yv;
+    const double ls = wave_sum(live ? e * e : 0.0);
+    const double cs = wave_sum(live ? bk * (2.0 * (vv - u) + gb) : 0.0);
+    if (lane == 0) {
+      if (a.slab_loss) a.slab_loss[i] = ls;
+      if (a.slab_cons) a.slab_cons[i] = dn + cs;
+    }
+  }
+  if ((mode & 2) && live) {
+    const double zn = a.a1 * u + a.q * zv - a.eta * gr;
+    a.z[s0 + lane] = zn;
+    a.v[s0 + lane] = a.a1 * u + a.q * vv;
+    a.beta[s0 + lane] = a.q * bk - a.eta * sr[lane];
+    a.coef_row[row0 + lane] = (zn - yv) / (double)m;
+  }
+}
+
+// k_rs_cols: C = sum_g cpart[g] (fixed order; or the all-reduced sums a.csum), then
+// xbar' = (a1 + q) xbar - (eta / N) C, Z' = a1 xbar + q Z, the T copy of xbar' for the next
+// pass and the metrics, and per-block partials of ||Z' - xbar'||^2.
+template <typename T>
+__global__ __launch_bounds__(NT) void k_rs_cols(const RsArgs a) {
+  __shared__ double red[NW];
+  const int64_t e = (int64_t)blockIdx.x * NT + threadIdx.x;
+  double dd = 0.0;
+  if (e < a.ld) {
+    double C;
+    if (a.csum) {
+      C = a.csum[e];
+    } else {
+      C = 0.0;
+      for (int g = 0; g < a.wg; ++g) C += a.cpart[(int64_t)g * a.ld + e];
+    }
+    const double xo = a.rxbar[e], zo = a.rZ[e];
+    const double xn = (a.a1 + a.q) * xo - a.eta_n * C;
+    const double zn = a.a1 * xo + a.q * zo;
+    a.rxbar[e] = xn;
+    a.rZ[e] = zn;
+    ((T*)a.xbar_out)[e] = (T)xn;
+    dd = (zn - xn) * (zn - xn);
+  }
+  dd = wave_sum(dd);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = dd;
+  __syncthreads();
+  if (threadIdx.x == 0) a.dpart[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// Local column sums C_rank = sum_g cpart[g] into csum (multi-GPU: all-reduced before k_rs_cols).
+__global__ __launch_bounds__(NT) void k_rs_csum(const RsArgs a, double* out) {
+  const int64_t e = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (e >= a.ld) return;
+  double C = 0.0;
+  for (int g = 0; g < a.wg; ++g) C += a.cpart[(int64_t)g * a.ld + e];
+  out[e] = C;
+}
+
+// Z = xbar = row 0 of x (iterates that all equal it), the T copy of xbar, ||D||^2 partials 0.
+template <typename T>
+__global__ __launch_bounds__(NT) void k_rs_init(const RsArgs a, const T* x0) {
+  const int64_t e = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (e < a.ld) {
+    const T v = x0[e];
+    a.rxbar[e] = (double)v;
+    a.rZ[e] = (double)v;
+    ((T*)a.xbar_out)[e] = v;
+  }
+  if (threadIdx.x == 0) a.dpart[blockIdx.x] = 0.0;
+}
+
+// flags[i * G + g] = 1 when row i of x differs from row 0 on the chunks of group g; zflag[g] = 1
+// when row 0 is nonzero there.
+template <typename T>
+__global__ __launch_bounds__(NT) void k_rs_check(const T* x, int64_t ld, int32_t nch, int32_t* flags,
+                                                 int32_t* zflag) {
+  using V = typename VT<T>::v;
+  constexpr int VN = VT<T>::n;
+  const int i = blockIdx.x, g = blockIdx.y, G = gridDim.y;
+  int diff = 0, nz = 0;
+  for (int c = g * NT + threadIdx.x; c < nch; c += G * NT) {
+    const V r0 = *(const V*)(x + (int64_t)c * VN);
+    const V ri = *(const V*)(x + (int64_t)i * ld + (int64_t)c * VN);
+#pragma unroll
+    for (int e = 0; e < VN; ++e) {
+      diff |= __builtin_bit_cast(typename std::conditional<sizeof(T) == 4, uint32_t, uint64_t>::type, ri[e]) !=
+              __builtin_bit_cast(typename std::conditional<sizeof(T) == 4, uint32_t, uint64_t>::type, r0[e]);
+      nz |= r0[e] != T(0);
+    }
+  }
+  diff = __syncthreads_or(diff);
+  nz = __syncthreads_or(nz);
+  if (threadIdx.x == 0) {
+    flags[(int64_t)i * G + g] = diff;
+    if (i == 0) zflag[g] = nz;
+  }
+}
+
+// Gram matrices Gram_i[k][l] = X_ik . X_il (float64), partial over column range g: rows of the
+// worker staged through LDS in tiles of 1 KiB per row; thread t accumulates pairs t, t + 256, ...
+// (k <= l) over each tile in column order.  gpart[(i * G + g) * P + p], P = m (m + 1) / 2.
+template <typename T>
+__global__ __launch_bounds__(NT) void k_rs_gram(const RsArgs a, double* gpart, int P) {
+  constexpr int TC = 1024 / sizeof(T);  // tile columns (1 KiB of every row)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* tile = (T*)smem;
+  const int i = blockIdx.x, g = blockIdx.y, G = gridDim.y;
+  const int64_t row0 = a.off[i];
+  const int m = (int)(a.off[i + 1] - row0);
+  const int64_t ntile = (a.ld + TC - 1) / TC;
+  const int64_t t0 = ntile * g / G, t1 = ntile * (g + 1) / G;
+  constexpr int MAXP = (64 * 65 / 2 + NT - 1) / NT;
+  double acc[MAXP];
+  int pk[MAXP], pl[MAXP];
+#pragma unroll
+  for (int s = 0; s < MAXP; ++s) {
+    acc[s] = 0.0;
+    int p = threadIdx.x + s * NT, k = 0;
+    while (p >= m - k && k < m) {  // pair index -> (k, l), l >= k
+      p -= m - k;
+      ++k;
+    }
+    pk[s] = k;
+    pl[s] = k + p;
+  }
+  const int np = m * (m + 1) / 2;
+  for (int64_t t = t0; t < t1; ++t) {
+    const int64_t c0 = t * TC;
+    const int w = (int)min((int64_t)TC, a.ld - c0);
+    __syncthreads();
+    for (int q = threadIdx.x; q < m * TC; q += NT) {
+      const int k = q / TC, c = q % TC;
+      tile[q] = c < w ? ((const T*)a.X)[(row0 + k) * a.ld + c0 + c] : T(0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < MAXP; ++s) {
+      if (threadIdx.x + s * NT < np) {
+        const T* rk = tile + pk[s] * TC;
+        const T* rl = tile + pl[s] * TC;
+        double sacc = 0.0;
+        for (int c = 0; c < TC; ++c) sacc += (double)rk[c] * (double)rl[c];
+        acc[s] += sacc;
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < MAXP; ++s) {
+    const int p = threadIdx.x + s * NT;
+    if (p < np) gpart[((int64_t)i * G + g) * P + p] = acc[s];
+  }
+}
+
+// Fold the partial Gram matrices over the column ranges (fixed order), symmetric fill.
+__global__ __launch_bounds__(NT) void k_rs_gram_fold(const RsArgs a, const double* gpart, int G, int P) {
+  const int i = blockIdx.x;
+  const int m = (int)(a.off[i + 1] - a.off[i]);
+  for (int p = threadIdx.x; p < m * (m + 1) / 2; p += NT) {
+    int q = p, k = 0;
+    while (q >= m - k) {
+      q -= m - k;
+      ++k;
+    }
+    const int l = k + q;
+    double s = 0.0;
+    for (int g = 0; g < G; ++g) s += gpart[((int64_t)i * G + g) * P + p];
+    double* gi = a.gram_w + (int64_t)i * a.bcap * a.bcap;
+    gi[k * a.bcap + l] = s;
+    gi[l * a.bcap + k] = s;
+  }
+}
+
+// x_i = Z + X_i^T beta_i for every worker (T), chunk-strided over column groups.
+template <typename T>
+__global__ __launch_bounds__(NT) void k_rs_materialise(const RsArgs a, T* xout) {
+  using V = typename VT<T>::v;
+  constexpr int VN = VT<T>::n;
+  __shared__ double sb[64];
+  const int i = blockIdx.x, g = blockIdx.y, G = gridDim.y;
+  const int64_t row0 = a.off[i];
+  const int m = (int)(a.off[i + 1] - row0);
+  if (threadIdx.x < 64) sb[threadIdx.x] = threadIdx.x < m ? a.beta[(int64_t)i * a.bcap + threadIdx.x] : 0.0;
+  __syncthreads();
+  for (int c = g * NT + threadIdx.x; c < a.nch; c += G * NT) {
+    double s[VN];
+#pragma unroll
+    for (int e = 0; e < VN; ++e) s[e] = a.rZ[(int64_t)c * VN + e];
+    for (int k = 0; k < m; ++k) {
+      const V r = rs_ld_nt<T>((const T*)a.X + (row0 + k) * a.ld + (int64_t)c * VN);
+#pragma unroll
+      for (int e = 0; e < VN; ++e) s[e] += sb[k] * (double)r[e];
+    }
+    V o;
+#pragma unroll
+    for (int e = 0; e < VN; ++e) o[e] = (T)s[e];
+    *(V*)(xout + (int64_t)i * a.ld + (int64_t)c * VN) = o;
+  }
+}
+
+// ---------------------------------------------------------------------------- launchers
+static const char* rs_tn(int dtype) { return dtype == 0 ? "float" : "double"; }
+
+// Pass shapes (RsArgs.cb / nbuf, picked by the runtime; DOPT_RS_CB / DOPT_RS_NBUF for A/B runs)
+template <typename T, bool COLS>
+static hipError_t rs_pass_shape(const RsArgs& a, dim3 grid, hipStream_t s) {
+#define RS_SHAPE(C_, B_) \
+  if (a.cb == C_ && a.nbuf == B_) { hipLaunchKernelGGL((k_rs_pass<T, COLS, C_, B_>), grid, dim3(NT), 0, s, a); return hipGetLastError(); }
+  RS_SHAPE(4, 2)
+  RS_SHAPE(4, 3)
+  RS_SHAPE(2, 3)
+  RS_SHAPE(2, 4)
+  RS_SHAPE(2, 6)
+  RS_SHAPE(1, 8)
+#undef RS_SHAPE
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_rs_pass(int dtype, bool cols, const RsArgs& a, hipStream_t s) {
+  const dim3 grid(a.nblk, a.wg);
+  char buf[112];
+  snprintf(buf, sizeof(buf), "void dopt::k_rs_pass<%s, %s, %d, %d>(dopt::RsArgs)", rs_tn(dtype),
+           cols ? "true" : "false", a.cb, a.nbuf);
+  if (cols) note_round_kernel(buf);
+  if (dtype == 0) return cols ? rs_pass_shape<float, true>(a, grid, s) : rs_pass_shape<float, false>(a, grid, s);
+  return cols ? rs_pass_shape<double, true>(a, grid, s) : rs_pass_shape<double, false>(a, grid, s);
+}
+
+hipError_t launch_rs_rows(const RsArgs& a, int n_workers, int mode, hipStream_t s) {
+  if (n_workers <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rs_rows, dim3(n_workers), dim3(NT), 0, s, a, mode);
+  return hipGetLastError();
+}
+
+int rs_col_blocks(int64_t ld) { return (int)((ld + NT - 1) / NT); }
+
+hipError_t launch_rs_cols(int dtype, const RsArgs& a, hipStream_t s) {
+  const dim3 grid(rs_col_blocks(a.ld));
+  if (dtype == 0) hipLaunchKernelGGL((k_rs_cols<float>), grid, dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL((k_rs_cols<double>), grid, dim3(NT), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_rs_csum(const RsArgs& a, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_rs_csum, dim3(rs_col_blocks(a.ld)), dim3(NT), 0, s, a, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_rs_init(int dtype, const RsArgs& a, const void* x0, hipStream_t s) {
+  const dim3 grid(rs_col_blocks(a.ld));
+  if (dtype == 0) hipLaunchKernelGGL((k_rs_init<float>), grid, dim3(NT), 0, s, a, (const float*)x0);
+  else hipLaunchKernelGGL((k_rs_init<double>), grid, dim3(NT), 0, s, a, (const double*)x0);
+  return hipGetLastError();
+}
+
+hipError_t launch_rs_check(int dtype, const void* x, int64_t n, int64_t ld, int32_t nch, int G, int32_t* flags,
+                           int32_t* zflag, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const dim3 grid((unsigned)n, G);
+  if (dtype == 0) hipLaunchKernelGGL((k_rs_check<float>), grid, dim3(NT), 0, s, (const float*)x, ld, nch, flags, zflag);
+  else hipLaunchKernelGGL((k_rs_check<double>), grid, dim3(NT), 0, s, (const double*)x, ld, nch, flags, zflag);
+  return hipGetLastError();
+}
+
+hipError_t launch_rs_gram(int dtype, const RsArgs& a, int n_workers, int max_m, double* gpart, int G, hipStream_t s) {
+  if (n_workers <= 0) return hipSuccess;
+  const int P = max_m * (max_m + 1) / 2;
+  const size_t lds = (size_t)max_m * 1024;
+  const dim3 grid(n_workers, G);
+  if (dtype == 0) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_rs_gram<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       64 * 1024);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_rs_gram<float>), grid, dim3(NT), lds, s, a, gpart, P);
+  } else {
+    hipError_t e = hipFuncSetAttribute((const void*)k_rs_gram<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       64 * 1024);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_rs_gram<double>), grid, dim3(NT), lds, s, a, gpart, P);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_rs_gram_fold, dim3(n_workers), dim3(NT), 0, s, a, (const double*)gpart, G, P);
+  return hipGetLastError();
+}
+
+hipError_t launch_rs_materialise(int dtype, const RsArgs& a, int n_workers, void* xout, hipStream_t s) {
+  if (n_workers <= 0) return hipSuccess;
+  const int G = (int)std::max<int64_t>(1, std::min<int64_t>((a.nch + NT - 1) / NT, (8192 + n_workers - 1) / n_workers));
+  const dim3 grid(n_workers, G);
+  if (dtype == 0) hipLaunchKernelGGL((k_rs_materialise<float>), grid, dim3(NT), 0, s, a, (float*)xout);
+  else hipLaunchKernelGGL((k_rs_materialise<double>), grid, dim3(NT), 0, s, a, (double*)xout);
+  return hipGetLastError();
+}
+
+}  // namespace dopt

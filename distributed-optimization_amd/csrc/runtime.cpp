@@ -184,6 +184,26 @@ struct dopt_ctx {
   int64_t sample_wid0 = 0;
   int64_t ph_round = 0;  // round index of the next dopt_phase_grad (device sampler counter)
 
+  // row-space rounds (rowspace.hip; complete graph, quadratic, full shards): while rs_live the
+  // iterates are x_i = rs_Z + X_i^T beta_i and xs[cur] holds them only when rs_xs_valid
+  bool rs_live = false;
+  bool rs_xs_valid = false;
+  bool rs_gram_ok = false;
+  bool wdiag_uniform = false;  // complete-graph mixing with one W_ii for every worker
+  double wdiag_u = 0.0;
+  int64_t min_m = 0;           // smallest shard
+  int rs_wg = 0, rs_nblk = 0, rs_nd = 0, rs_cb = 4, rs_nbuf = 3;
+  int64_t rs_bcap = 0;
+  double* rs_coef = nullptr;   // [rows]
+  double* rs_up = nullptr;     // [nblk x rows]
+  double* rs_cp = nullptr;     // [wg x ld]
+  double* rs_z = nullptr;      // [n x bcap] (z, v, beta back to back)
+  double* rs_gram = nullptr;   // [n x bcap x bcap]
+  double* rs_dpart = nullptr;  // [nd]
+  double* rs_Z = nullptr;      // [ld] (Z, xbar back to back)
+  int64_t* rs_grow = nullptr;  // [wg + 1]
+  int32_t* rs_flags = nullptr;
+
   // profiling of k_round
   bool prof = false;
   int64_t prof_every = 1;      // bracket every k-th gradient-kernel launch (events cost ~30 us per pair)
@@ -328,6 +348,8 @@ int alloc_state(dopt_ctx* c) {
 
 int set_layout(dopt_ctx* c, int problem, int64_t n, int64_t d) {
   c->carry_pending = false;
+  c->rs_live = c->rs_gram_ok = false;  // new data: the row-space state and the Gram matrices are gone
+  c->rs_wg = 0;
   if (problem != DOPT_LOGISTIC && problem != DOPT_QUADRATIC)
     return fail(DOPT_ERR_UNSUPPORTED, "unknown problem %d", problem);
   CHECK_ARG(n >= 1 && d >= 1, "n_workers (%lld) and d (%lld) must be >= 1", (long long)n, (long long)d);
@@ -701,6 +723,213 @@ int run_centralized_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64
   return finish_run(c, T, T, lam_obj, f_opt, want_obj ? obj_out : nullptr, nullptr, time_out);
 }
 
+// ---------------------------------------------------------------------------- row-space rounds
+// (rowspace.hip).  Complete graph with one W_ii, quadratic objective, full-shard batches of
+// 1..kRsMaxRows rows, one context (no rank slices), iterates that start equal: then
+// x_i = Z + X_i^T beta_i for the whole run and a round is one read-only pass over the rows.
+// DOPT_ROWSPACE=0 keeps the direct column-blocked rounds (A/B runs, tests).
+bool rs_enabled() {
+  const char* v = getenv("DOPT_ROWSPACE");
+  return !(v && v[0] == '0');
+}
+
+bool rs_eligible(dopt_ctx* c, int64_t batch, const int32_t* idx) {
+  return rs_enabled() && c->split && c->mean_mix && c->wdiag_uniform && c->problem == DOPT_QUADRATIC &&
+         !idx && batch >= c->max_m && !c->obj_sep && c->min_m >= 1 && c->max_m <= kRsMaxRows &&
+         c->n_global == 0 && !c->S_ext && c->xdtype == c->dtype;
+}
+
+RsArgs rs_args(dopt_ctx* c) {
+  RsArgs a;
+  memset(&a, 0, sizeof(a));
+  a.X = c->X;
+  a.y = c->y;
+  a.y_is_f32 = c->xdtype == DOPT_F32;
+  a.off = c->off;
+  a.rows = c->rows;
+  a.ld = c->ld;
+  a.nch = (int32_t)c->nch;
+  a.grow = c->rs_grow;
+  a.wg = c->rs_wg;
+  a.nblk = c->rs_nblk;
+  a.cb = c->rs_cb;
+  a.nbuf = c->rs_nbuf;
+  a.coef_row = c->rs_coef;
+  a.upart = c->rs_up;
+  a.cpart = c->rs_cp;
+  a.bcap = (int32_t)c->rs_bcap;
+  a.z = c->rs_z;
+  a.v = c->rs_z ? c->rs_z + c->n * c->rs_bcap : nullptr;
+  a.beta = c->rs_z ? c->rs_z + 2 * c->n * c->rs_bcap : nullptr;
+  a.gram = c->rs_gram;
+  a.gram_w = c->rs_gram;
+  a.dpart = c->rs_dpart;
+  a.nd = c->rs_nd;
+  a.rZ = c->rs_Z;
+  a.rxbar = c->rs_Z ? c->rs_Z + c->ld : nullptr;
+  return a;
+}
+
+constexpr int kRsCheckGroups = 16;  // column groups of the equal-start check
+
+int ensure_rs(dopt_ctx* c) {
+  if (c->rs_wg > 0) return DOPT_OK;
+  // pass shape (A/B knobs DOPT_RS_CB / DOPT_RS_NBUF: the compiled pairs in rowspace.hip)
+  const char* cbv = getenv("DOPT_RS_CB");
+  const char* nbv = getenv("DOPT_RS_NBUF");
+  c->rs_cb = cbv ? atoi(cbv) : 4;
+  c->rs_nbuf = nbv ? atoi(nbv) : 3;
+  const int64_t nblk = (c->nch + 64 * c->rs_cb - 1) / (64 * c->rs_cb);
+  // ~16k workgroups of ~1k rows: 4 MiB per workgroup at C5 (a short tail), partial sums
+  // (nblk x rows dots + wg x ld column sums) ~0.4 % of the shard bytes
+  const char* ev = getenv("DOPT_RS_WG");
+  int64_t wg = ev ? atoll(ev) : (16384 + nblk - 1) / nblk;
+  wg = std::max<int64_t>(1, std::min<int64_t>(wg, (c->rows + 255) / 256));
+  int rc;
+  c->rs_nblk = (int)nblk;
+  c->rs_nd = rs_col_blocks(c->ld);
+  c->rs_bcap = std::max<int64_t>(1, c->max_m);
+  const size_t nb = (size_t)c->n * c->rs_bcap;
+  if ((rc = dalloc_t(&c->rs_coef, (size_t)c->rows * sizeof(double)))) return rc;
+  if ((rc = dalloc_t(&c->rs_up, (size_t)nblk * c->rows * sizeof(double)))) return rc;
+  if ((rc = dalloc_t(&c->rs_cp, (size_t)wg * c->ld * sizeof(double)))) return rc;
+  if ((rc = dalloc_t(&c->rs_z, 3 * nb * sizeof(double)))) return rc;
+  if ((rc = dalloc_t(&c->rs_gram, nb * c->rs_bcap * sizeof(double)))) return rc;
+  if ((rc = dalloc_t(&c->rs_dpart, (size_t)c->rs_nd * sizeof(double)))) return rc;
+  if ((rc = dalloc_t(&c->rs_Z, 2 * (size_t)c->ld * sizeof(double)))) return rc;
+  if ((rc = dalloc_t(&c->rs_flags, ((size_t)c->n + 1) * kRsCheckGroups * sizeof(int32_t)))) return rc;
+  std::vector<int64_t> gr((size_t)wg + 1);
+  for (int64_t g = 0; g <= wg; ++g) gr[(size_t)g] = c->rows * g / wg;
+  if ((rc = dalloc_t(&c->rs_grow, gr.size() * sizeof(int64_t)))) return rc;
+  HIPOK(hipMemcpy(c->rs_grow, gr.data(), gr.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  c->rs_wg = (int)wg;
+  c->rs_gram_ok = false;
+  return DOPT_OK;
+}
+
+// xs[cur] = the iterates the row-space state holds (the state stays live).
+int rs_sync(dopt_ctx* c) {
+  if (!c->rs_live || c->rs_xs_valid) return DOPT_OK;
+  HIPOK(launch_rs_materialise(c->dtype == DOPT_F32 ? 0 : 1, rs_args(c), (int)c->n, c->xs[c->cur], c->stream));
+  c->rs_xs_valid = true;
+  return DOPT_OK;
+}
+
+// Leave row-space mode: xs[cur] holds the iterates, xbar[xb] their average.
+int rs_end(dopt_ctx* c) {
+  int rc;
+  if ((rc = rs_sync(c))) return rc;
+  c->rs_live = false;
+  return DOPT_OK;
+}
+
+enum { RS_FALLBACK = 1 };
+
+// Start row-space mode from xs[cur]: RS_FALLBACK when the iterates are not all equal.
+int rs_begin(dopt_ctx* c) {
+  int rc;
+  if ((rc = ensure_rs(c))) return rc;
+  const int dt = c->dtype == DOPT_F32 ? 0 : 1;
+  const int G = kRsCheckGroups;
+  HIPOK(launch_rs_check(dt, c->xs[c->cur], c->n, c->ld, (int32_t)c->nch, G, c->rs_flags, c->rs_flags + c->n * G,
+                        c->stream));
+  std::vector<int32_t> fl((size_t)(c->n + 1) * G);
+  HIPOK(hipMemcpyAsync(fl.data(), c->rs_flags, fl.size() * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPOK(hipStreamSynchronize(c->stream));
+  for (int64_t k = 0; k < c->n * G; ++k)
+    if (fl[(size_t)k]) return RS_FALLBACK;
+  bool zero = true;
+  for (int g = 0; g < G; ++g)
+    if (fl[(size_t)(c->n * G + g)]) zero = false;
+  RsArgs a = rs_args(c);
+  if (!c->rs_gram_ok) {
+    const int64_t P = c->rs_bcap * (c->rs_bcap + 1) / 2;
+    const int Gg = (int)std::max<int64_t>(1, std::min<int64_t>((c->ld + 255) / 256, (2048 + c->n - 1) / c->n));
+    double* gpart = nullptr;
+    if ((rc = dalloc_t(&gpart, (size_t)c->n * Gg * P * sizeof(double)))) return rc;
+    hipError_t e = launch_rs_gram(dt, a, (int)c->n, (int)c->rs_bcap, gpart, Gg, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dfree_t(gpart);
+    if (e != hipSuccess) return fail(DOPT_ERR_HIP, "Gram matrices: %s", hipGetErrorString(e));
+    c->rs_gram_ok = true;
+  }
+  a.xbar_out = c->xbar[c->xb];
+  HIPOK(launch_rs_init(dt, a, c->xs[c->cur], c->stream));  // Z = xbar = x_0, ||D||^2 = 0
+  if (zero) {
+    HIPOK(launch_rs_rows(a, (int)c->n, 4 | 8, c->stream));  // z = v = 0
+  } else {
+    a.xbar = c->xbar[c->xb];
+    HIPOK(launch_rs_pass(dt, false, a, c->stream));  // z = v = X . x_0
+    HIPOK(launch_rs_rows(a, (int)c->n, 4, c->stream));
+  }
+  c->rs_live = true;
+  c->rs_xs_valid = true;  // xs[cur] is x_0 itself
+  return DOPT_OK;
+}
+
+// D-SGD rounds in row-space mode; the history / carry contract of run_dsgd_split.
+// RS_FALLBACK: not applicable here (unequal starting iterates, or a direct chain is open).
+int run_dsgd_rs(dopt_ctx* c, int64_t t0, int64_t T, double eta0, double lam_grad, double lam_obj, double f_opt,
+                uint32_t flags, double* obj_out, double* cons_out, double* time_out, bool carry_in, bool pipelined,
+                int64_t* nh_out) {
+  int rc;
+  const bool want_obj = flags & DOPT_RUN_OBJECTIVE, want_cons = flags & DOPT_RUN_CONSENSUS;
+  const bool metrics = want_obj || want_cons;
+  if (!c->rs_live) {
+    if (carry_in) return RS_FALLBACK;
+    if ((rc = rs_begin(c))) return rc;
+  }
+  const int dt = c->dtype == DOPT_F32 ? 0 : 1;
+  const int64_t lag = carry_in ? 1 : 0;
+  int& xb = c->xb;
+  const double N = (double)n_div(c);
+  HIPOK(launch_stamp(c->stamps, c->stream));
+  for (int64_t h = 0; h < T; ++h) {
+    const int64_t t = t0 + h;
+    const double eta = eta0 / sqrt((double)(t + 1));  // trainer.py:138-140
+    RsArgs a = rs_args(c);
+    a.xbar = c->xbar[xb];
+    a.a1 = c->w_off * N;
+    a.q = c->wdiag_u - c->w_off - eta * lam_grad;
+    a.eta = eta;
+    a.eta_n = eta / N;
+    const bool met = metrics && (h > 0 || lag);
+    a.slab_cons = want_cons ? c->slab_cons : nullptr;
+    a.slab_loss = want_obj ? c->slab_loss : nullptr;
+    if (c->prof && (rc = prof_event(c, false))) return rc;
+    HIPOK(launch_rs_pass(dt, true, a, c->stream));
+    if (c->prof && (rc = prof_event(c, true))) return rc;
+    HIPOK(launch_rs_rows(a, (int)c->n, 2 | (met ? 1 : 0), c->stream));
+    if (met) {
+      c->loss_groups = c->n;
+      if ((rc = history(c, h - 1 + lag, c->xbar[xb], want_cons, want_obj, c->n))) return rc;
+    }
+    a.xbar_out = c->xbar[xb ^ 1];
+    HIPOK(launch_rs_cols(dt, a, c->stream));
+    HIPOK(launch_stamp(c->stamps + h + 1, c->stream));
+    xb ^= 1;
+    c->rs_xs_valid = false;
+  }
+  int64_t nh = T + lag;
+  if (pipelined && metrics && T > 0) {
+    nh -= 1;  // the metrics of x_T: owed to the next pipelined run
+    c->carry_pending = true;
+    c->carry_flags = flags & (DOPT_RUN_OBJECTIVE | DOPT_RUN_CONSENSUS);
+  } else if (metrics && (T > 0 || lag)) {  // one dots pass at xbar_T
+    RsArgs a = rs_args(c);
+    a.xbar = c->xbar[xb];
+    a.slab_cons = want_cons ? c->slab_cons : nullptr;
+    a.slab_loss = want_obj ? c->slab_loss : nullptr;
+    HIPOK(launch_rs_pass(dt, false, a, c->stream));
+    HIPOK(launch_rs_rows(a, (int)c->n, 1, c->stream));
+    c->loss_groups = c->n;
+    if ((rc = history(c, nh - 1, c->xbar[xb], want_cons, want_obj, c->n))) return rc;
+  }
+  if (nh_out) *nh_out = nh;
+  return finish_run(c, nh, T, lam_obj, f_opt, want_obj ? obj_out : nullptr, want_cons ? cons_out : nullptr,
+                    time_out);
+}
+
 // Minibatch rounds whose metrics need a pass over every shard row anyway take the gradient
 // inside that pass (k_round F_BIP).  DOPT_BIP=0: a separate metrics pass (A/B runs).
 static_assert(kMaxBipRows == DOPT_MAX_BIP_ROWS, "dopt.h and engine.h disagree");
@@ -831,6 +1060,9 @@ int dopt_destroy(dopt_ctx* c) {
   dfree_t(c->cpart);
   dfree_t(c->send_ids);
   dfree_t(c->stamps);
+  for (double** p : {&c->rs_coef, &c->rs_up, &c->rs_cp, &c->rs_z, &c->rs_gram, &c->rs_dpart, &c->rs_Z}) dfree_t(*p);
+  dfree_t(c->rs_grow);
+  dfree_t(c->rs_flags);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
@@ -846,15 +1078,17 @@ int dopt_load_shards(dopt_ctx* c, int problem, int64_t n_workers, int64_t d, con
   c->have_data = false;
   if ((rc = set_layout(c, problem, n_workers, d))) return rc;
   CHECK_ARG(off[0] == 0, "shard_offsets[0] must be 0");
-  int64_t max_m = 0;
+  int64_t max_m = 0, min_m = n_workers > 0 ? off[1] - off[0] : 0;
   for (int64_t i = 0; i < n_workers; ++i) {
     CHECK_ARG(off[i + 1] >= off[i], "shard_offsets must be non-decreasing");
     max_m = std::max(max_m, off[i + 1] - off[i]);
+    min_m = std::min(min_m, off[i + 1] - off[i]);
   }
   const int64_t rows = off[n_workers];
   CHECK_ARG(rows == 0 || (X && y), "X / y are NULL");
   c->rows = rows;
   c->max_m = max_m;
+  c->min_m = min_m;
   c->off_h.assign(off, off + n_workers + 1);
   if ((rc = dalloc(&c->X, (size_t)rows * c->ld * c->xesz))) return rc;
   if ((rc = dalloc(&c->y, (size_t)rows * c->xesz))) return rc;
@@ -878,6 +1112,7 @@ int dopt_generate_shards(dopt_ctx* c, int problem, int64_t n_workers, int64_t d,
   const int64_t rows = n_workers * rpw;
   c->rows = rows;
   c->max_m = rpw;
+  c->min_m = rpw;
   c->off_h.resize((size_t)n_workers + 1);
   for (int64_t i = 0; i <= n_workers; ++i) c->off_h[(size_t)i] = i * rpw;
   if ((rc = dalloc(&c->X, (size_t)rows * c->ld * c->xesz))) return rc;
@@ -954,6 +1189,7 @@ int dopt_set_topology(dopt_ctx* c, int64_t n_workers, const int64_t* row_ptr, co
               col[e], (long long)n_workers, (long long)c->n_halo);
   int rc;
   if ((rc = set_device(c))) return rc;
+  if ((rc = rs_end(c))) return rc;
   if ((rc = dalloc_t(&c->rp, (size_t)(n_workers + 1) * sizeof(int64_t)))) return rc;
   if ((rc = dalloc_t(&c->ci, (size_t)nnz * sizeof(int32_t)))) return rc;
   if ((rc = dalloc(&c->cw, (size_t)nnz * c->esz))) return rc;
@@ -982,6 +1218,8 @@ int dopt_set_mixing_mean(dopt_ctx* c, int64_t n_workers, double w_off, const dou
   CHECK_ARG(n_workers == c->n, "mixing has %lld workers, data has %lld", (long long)n_workers, (long long)c->n);
   int rc;
   if ((rc = set_device(c))) return rc;
+  if ((rc = rs_end(c))) return rc;
+  c->rs_wg = 0;  // the row-space pass is planned again (shape knobs re-read, Gram recomputed)
   if ((rc = dalloc(&c->wdiag, (size_t)n_workers * c->esz))) return rc;
   if (c->dtype == DOPT_F64) {
     HIPOK(hipMemcpy(c->wdiag, w_diag, (size_t)n_workers * sizeof(double), hipMemcpyHostToDevice));
@@ -992,11 +1230,19 @@ int dopt_set_mixing_mean(dopt_ctx* c, int64_t n_workers, double w_off, const dou
   c->w_off = w_off;
   c->mean_mix = true;
   c->have_topo = true;
+  // the row-space rounds need one W_ii for every worker (as the kernels read it: in T)
+  const double w0 = c->dtype == DOPT_F64 ? w_diag[0] : (double)(float)w_diag[0];
+  c->wdiag_uniform = true;
+  for (int64_t i = 1; i < n_workers; ++i) {
+    const double wi = c->dtype == DOPT_F64 ? w_diag[i] : (double)(float)w_diag[i];
+    if (wi != w0) c->wdiag_uniform = false;
+  }
+  c->wdiag_u = w0;
   return DOPT_OK;
 }
 
 int dopt_set_models(dopt_ctx* c, const double* x) {
-  if (c) c->send_fresh = c->carry_pending = false;
+  if (c) c->send_fresh = c->carry_pending = c->rs_live = false;
   CHECK_ARG(c && x, "NULL argument");
   if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");
   int rc;
@@ -1009,6 +1255,7 @@ int dopt_get_models(dopt_ctx* c, double* x) {
   if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");
   int rc;
   if ((rc = set_device(c))) return rc;
+  if ((rc = rs_sync(c))) return rc;
   return download_rows(c, c->dtype, c->xs[c->cur], x, c->n, c->d, c->ld);
 }
 
@@ -1072,6 +1319,20 @@ static int run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t bat
   const int64_t CH = idx ? idx_chunk_rounds(c, T, batch) : 1;
   int& xb = c->xb;
   if (c->split) {  // the column-blocked rounds pipeline the same way (full-shard batches)
+    if (rs_eligible(c, batch, idx)) {  // complete graph, quadratic: row-space rounds
+      int64_t nh = 0;
+      rc = run_dsgd_rs(c, t0, T, eta0, lam_grad, lam_obj, f_opt, flags, obj_out, cons_out, time_out, carry_in,
+                       pipelined, &nh);
+      if (rc != RS_FALLBACK) {
+        if (rc) return rc;
+        if (n_out) *n_out = nh;
+        return DOPT_OK;
+      }
+    } else {
+      if (carry_in && c->rs_live)
+        return fail(DOPT_ERR_INVALID, "pipelined run: the pending metrics belong to a row-space chain");
+      if ((rc = rs_end(c))) return rc;
+    }
     const bool sfused = batch >= c->max_m && !c->obj_sep && metrics;
     if (carry_in && !sfused) return fail(DOPT_ERR_INVALID, "pipelined run: the pending metrics need a fused run");
     int64_t nh = 0;
@@ -1445,6 +1706,8 @@ int dopt_set_partition(dopt_ctx* c, int64_t n_global, int64_t rows_global) {
   CHECK_ARG(c, "ctx is NULL");
   if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");
   CHECK_ARG(n_global >= c->n && rows_global >= 0, "global sizes smaller than the local slice");
+  int rc;
+  if ((rc = rs_end(c))) return rc;  // rank slices run the phase API (xs[cur] is the state)
   c->n_global = n_global;
   c->rows_global = rows_global;
   return DOPT_OK;
@@ -1460,6 +1723,7 @@ int dopt_set_halo(dopt_ctx* c, int64_t n_halo, void* halo_dev, int64_t n_send, v
   for (int64_t k = 0; k < n_send; ++k) CHECK_ARG(send_ids[k] >= 0 && send_ids[k] < c->n, "send id out of range");
   int rc;
   if ((rc = set_device(c))) return rc;
+  if ((rc = rs_end(c))) return rc;
   if ((rc = dalloc_t(&c->send_ids, (size_t)std::max<int64_t>(1, n_send) * sizeof(int32_t)))) return rc;
   if (n_send) HIPOK(hipMemcpy(c->send_ids, send_ids, (size_t)n_send * sizeof(int32_t), hipMemcpyHostToDevice));
   c->n_halo = n_halo;
@@ -1486,6 +1750,8 @@ int dopt_phase_gather(dopt_ctx* c) {
   CHECK_ARG(c, "ctx is NULL");
   if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
   if (c->send_fresh) return DOPT_OK;  // the last mix wrote these rows already
+  int rc;
+  if ((rc = rs_end(c))) return rc;
   HIPOK(launch_gather_rows(c->dtype, c->xs[c->cur], c->send_ids, c->n_send, c->ld, (int32_t)c->nchs, c->send,
                            c->stream));
   return DOPT_OK;
@@ -1505,6 +1771,7 @@ int dopt_phase_begin(dopt_ctx* c, int64_t batch) {
   if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
   c->send_fresh = false;  // the iterates may have been set since the last mix
   int rc;
+  if ((rc = rs_end(c))) return rc;
   if (c->split) {
     if ((rc = ensure_split(c))) return rc;
     if (std::min(batch, c->max_m) > kSplitMaxRows)
@@ -1678,6 +1945,8 @@ int dopt_phase_metrics_shared(dopt_ctx* c, int include_xnorm, double* out_dev) {
 
 int dopt_phase_colsum(dopt_ctx* c, double* sum_dev) {
   CHECK_ARG(c && sum_dev, "NULL argument");
+  int rc;
+  if ((rc = rs_end(c))) return rc;
   HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur], c->n, c->ld, (int32_t)c->nchs, kRowsPerGroup, c->part,
                               nullptr, c->stream));
   HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nchs, nullptr, nullptr, 0.0, 0,
@@ -1714,6 +1983,8 @@ int dopt_phase_fold(dopt_ctx* c, double* cons_out, double* xnorm_out, double* lo
 int dopt_phase_colsum_fold(dopt_ctx* c, double* sum_dev, double* cons_out, double* xnorm_out, double* loss_out) {
   CHECK_ARG(c && sum_dev, "NULL argument");
   if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
+  int rc;
+  if ((rc = rs_end(c))) return rc;
   HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur], c->n, c->ld, (int32_t)c->nchs, kRowsPerGroup, c->part,
                               nullptr, c->stream));
   const FoldArgs fold = {c->slab_cons, c->cons_n, c->slab_loss, c->slab_n[0], c->xbar[c->xb], cons_out, loss_out,

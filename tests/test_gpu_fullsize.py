@@ -113,3 +113,42 @@ def test_c5_d2pow20_1024_workers_full_size():
         np.testing.assert_allclose(x, x_all, rtol=1e-5, atol=1e-7 * np.abs(x_all).max())
     finally:
         eng.close()
+
+
+def test_c5_rowspace_full_size_vs_direct(monkeypatch):
+    """C5 from the reference's start (Worker.x = zeros, worker.py:13) through the row-space rounds
+    (rowspace.hip, the bench's C5 path): round 1 recomputed on the host for several workers,
+    then rounds 2-3 continued from the live row-space state, against the direct column-blocked
+    rounds (DOPT_ROWSPACE=0) on the same 64 GiB of float32 shards."""
+    n, d, m, T, eta0, lam = 1024, 1 << 20, 16, 3, 1e-5, 1e-4
+    if _free_gb() < 80:
+        pytest.skip("needs ~75 GB of free HBM")
+    top = TP.fully_connected(n)
+    w_off, diag = top.uniform_offdiag()
+    eng = _dopt.Engine(0, "float32")
+    try:
+        eng.generate_shards("quadratic", n, d, m, seed=3, noise=10.0)
+        eng.set_mixing_mean(w_off, diag)
+        monkeypatch.setenv("DOPT_ROWSPACE", "1")
+        o1, c1, _ = eng.run_dsgd(1, eta0, m, lam, lam, 0.0)
+        assert "k_rs_pass<float, true>" in _dopt.last_round_kernel()
+        x1 = eng.get_models()
+        for i in (0, 1, 700, 1023):  # x_1 = mix(0) - eta (X^T (0 - y) / m + lam 0)
+            X, y = eng.get_shard(i)
+            ref = -eta0 * O.quadratic_gradient(np.zeros(d), X, y, lam)
+            np.testing.assert_allclose(x1[i], ref, rtol=2e-5, atol=1e-7 * np.abs(ref).max())
+        xb = x1.mean(axis=0)
+        np.testing.assert_allclose(c1[0], np.mean(np.sum((x1 - xb) ** 2, axis=1)), rtol=1e-4)
+        del x1
+        o23, c23, _ = eng.run_dsgd(T - 1, eta0, m, lam, lam, 0.0, t0=1)
+        x_rs = eng.get_models()
+        monkeypatch.setenv("DOPT_ROWSPACE", "0")
+        eng.set_models(np.zeros((n, d), dtype=np.float32))
+        od, cd, _ = eng.run_dsgd(T, eta0, m, lam, lam, 0.0)
+        assert "k_split_step" in _dopt.last_round_kernel()
+        np.testing.assert_allclose(np.concatenate([o1, o23]), od, rtol=1e-4)
+        np.testing.assert_allclose(np.concatenate([c1, c23]), cd, rtol=1e-4)
+        x_d = eng.get_models()
+        np.testing.assert_allclose(x_rs, x_d, rtol=1e-4, atol=1e-5 * np.abs(x_d).max())
+    finally:
+        eng.close()

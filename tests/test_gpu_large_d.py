@@ -28,14 +28,17 @@ def _engine(shards, problem, dtype="float64"):
     return eng
 
 
-@pytest.mark.parametrize("problem,topo,batch,mean,m", [
-    ("logistic", "ring", 12, False, 12),        # full shard: next-round dots fused into the step
-    ("logistic", "ring", 5, False, 12),         # minibatches: separate dots pass per round
-    ("quadratic", "fully_connected", 12, True, 12),   # complete graph through column sums
-    ("quadratic", "grid", 4, False, 12),
-    ("logistic", "ring", 24, False, 24),        # > 16 rows per worker: the row-split step kernel
+@pytest.mark.parametrize("problem,topo,batch,mean,m,rowspace", [
+    ("logistic", "ring", 12, False, 12, "1"),        # full shard: next-round dots fused into the step
+    ("logistic", "ring", 5, False, 12, "1"),         # minibatches: separate dots pass per round
+    ("quadratic", "fully_connected", 12, True, 12, "0"),  # complete graph through column sums
+    ("quadratic", "fully_connected", 12, True, 12, "1"),  # ... in row space (rowspace.hip)
+    ("quadratic", "fully_connected", 5, True, 12, "1"),   # minibatches: direct rounds
+    ("quadratic", "grid", 4, False, 12, "1"),
+    ("logistic", "ring", 24, False, 24, "1"),        # > 16 rows per worker: the row-split step kernel
 ])
-def test_split_rounds_vs_oracle(problem, topo, batch, mean, m):
+def test_split_rounds_vs_oracle(problem, topo, batch, mean, m, rowspace, monkeypatch):
+    monkeypatch.setenv("DOPT_ROWSPACE", rowspace)
     n, d, T = 9, 2100, 6  # d = 2100 fp64 -> 1050 chunks > 1024: column-blocked path
     shards = _data(n, d, m, 1, problem)
     cfg = {"problem_type": problem, "local_batch_size": batch, "learning_rate_eta0": 0.05,
@@ -71,6 +74,7 @@ def test_split_glds_kernel_bitwise_equals_prefetch_kernel(dtype, monkeypatch):
     n, m, T = 9, 12, 5
     d = 2100 if dtype == "float64" else 9000
     monkeypatch.setenv("DOPT_SPLIT_WGS", "18")  # read when the layout is set: 2 groups per worker
+    monkeypatch.setenv("DOPT_ROWSPACE", "0")  # the direct column-blocked step (not the row-space rounds)
     shards = _data(n, d, m, 5, "quadratic")
     eng = _engine(shards, "quadratic", dtype)
     eng.set_mixing_mean(*TP.fully_connected(n).uniform_offdiag())
@@ -155,11 +159,12 @@ def test_single_evaluations_wide_rows_vs_oracle(d):
                                    rtol=1e-12)
 
 
-@pytest.mark.parametrize("mean", [True, False])
-def test_split_pipelined_runs_equal_one_run(mean):
+@pytest.mark.parametrize("mean,rowspace", [(True, "0"), (True, "1"), (False, "1")])
+def test_split_pipelined_runs_equal_one_run(mean, rowspace, monkeypatch):
     """Column-blocked rounds pipelined across calls (bench.py's C5 timing): the last step's
     next-round coefficients, S and xbar carry over, the owed metrics ride the next call's
     first step -- concatenated, exactly one run's history and iterates."""
+    monkeypatch.setenv("DOPT_ROWSPACE", rowspace)
     n, d, m = 9, 2100, 12
     shards = _data(n, d, m, 7, "quadratic")
     eng = _engine(shards, "quadratic")

@@ -1,0 +1,151 @@
+"""Row-space rounds (csrc/rowspace.hip): complete graph, quadratic objective, full shards,
+iterates that start equal -- x_i = Z + X_i^T beta_i, one read-only pass over the rows per
+round.  Pinned to the oracle (trainer.py:161-193 restated, float64, rtol 1e-9) and to the
+direct column-blocked rounds (DOPT_ROWSPACE=0) on the same data; chains and materialisation
+mid-chain equal one run bitwise; unequal starting iterates fall back to the direct rounds."""
+import numpy as np
+import pytest
+
+import _dopt
+import dsgd_oracle as O
+import topology as TP
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(sizes, d, seed):
+    rng = np.random.default_rng(seed)
+    shards = []
+    for m in sizes:
+        X = np.hstack([rng.standard_normal((m, d - 1)), np.ones((m, 1))])
+        y = rng.standard_normal(m) * 3
+        shards.append((X, y))
+    return shards
+
+
+def _engine(shards, dtype="float64"):
+    eng = _dopt.Engine(0, dtype)
+    off = np.concatenate([[0], np.cumsum([len(s[1]) for s in shards])])
+    eng.load_shards("quadratic", np.vstack([s[0] for s in shards]), np.concatenate([s[1] for s in shards]), off)
+    n = len(shards)
+    eng.set_mixing_mean(*TP.fully_connected(n).uniform_offdiag())
+    return eng
+
+
+def _cfg(b):
+    return {"problem_type": "quadratic", "local_batch_size": b, "learning_rate_eta0": 0.05,
+            "l2_regularization_lambda": 1e-3, "strong_convexity_mu": 2e-3}
+
+
+@pytest.mark.parametrize("start", ["zero", "common"])
+@pytest.mark.parametrize("sizes", [[12] * 9, [16, 3, 9, 16, 1, 7, 12, 16, 5, 11, 2]])
+def test_rowspace_vs_oracle(start, sizes):
+    n, d, T = len(sizes), 2100, 8  # d = 2100 float64: column-blocked rows
+    shards = _data(sizes, d, 3)
+    eng = _engine(shards)
+    x0 = np.zeros((n, d))
+    if start == "common":
+        x0[:] = np.random.default_rng(9).standard_normal(d) * 0.05
+        eng.set_models(x0)
+    b = max(sizes)
+    obj, cons, _ = eng.run_dsgd(T, 0.05, b, 2e-3, 1e-3, 0.1)
+    assert _dopt.last_round_kernel().startswith("void dopt::k_rs_pass<double, true>")
+    x = eng.get_models()
+    Xf = np.vstack([s[0] for s in shards])
+    yf = np.concatenate([s[1] for s in shards])
+    h, _, xr, _ = O.run_decentralized(shards, TP.fully_connected(n).dense_W(), T, _cfg(b), Xf, yf, 0.1, x0=x0)
+    np.testing.assert_allclose(obj, h["objective"], rtol=1e-9)
+    np.testing.assert_allclose(cons, h["consensus_error"], rtol=1e-9)
+    np.testing.assert_allclose(x, xr, rtol=1e-9, atol=1e-12 * np.abs(xr).max())
+    eng.close()
+
+
+@pytest.mark.parametrize("dtype,d", [("float64", 2100), ("float32", 4500)])
+def test_rowspace_vs_direct_rounds(dtype, d, monkeypatch):
+    """Same data, same engine: row-space vs direct column-blocked rounds (DOPT_ROWSPACE=0).
+    float64 agree to rtol 1e-9; float32 to the float32 engine's rounding (rtol 2e-4)."""
+    n, m, T = 40, 16, 12
+    shards = _data([m] * n, d, 5)
+    eng = _engine(shards, dtype)
+    out = {}
+    for knob in ("1", "0"):
+        monkeypatch.setenv("DOPT_ROWSPACE", knob)
+        eng.set_models(np.zeros((n, d)))
+        obj, cons, _ = eng.run_dsgd(T, 0.05, m, 2e-3, 2e-3, 0.0)
+        out[knob] = (np.asarray(obj), np.asarray(cons), eng.get_models(), _dopt.last_round_kernel())
+    assert "k_rs_pass" in out["1"][3] and "k_split_step" in out["0"][3]
+    tol = 1e-9 if dtype == "float64" else 2e-4
+    np.testing.assert_allclose(out["1"][0], out["0"][0], rtol=tol)
+    np.testing.assert_allclose(out["1"][1], out["0"][1], rtol=tol)
+    np.testing.assert_allclose(out["1"][2], out["0"][2], rtol=tol, atol=tol * np.abs(out["0"][2]).max())
+    eng.close()
+
+
+def test_rowspace_unequal_start_falls_back(monkeypatch):
+    """Iterates that do not all start equal cannot be written Z + X_i^T beta_i: the direct
+    rounds run (bitwise the DOPT_ROWSPACE=0 result)."""
+    n, m, d, T = 9, 12, 2100, 4
+    shards = _data([m] * n, d, 6)
+    eng = _engine(shards)
+    x0 = np.random.default_rng(2).standard_normal((n, d)) * 0.01
+    res = []
+    for knob in ("1", "0"):
+        monkeypatch.setenv("DOPT_ROWSPACE", knob)
+        eng.set_models(x0)
+        obj, cons, _ = eng.run_dsgd(T, 0.05, m, 2e-3, 2e-3, 0.0)
+        res.append((np.asarray(obj), np.asarray(cons), eng.get_models()))
+        assert "k_split_step" in _dopt.last_round_kernel()
+    for a, b in zip(*res):
+        assert np.array_equal(a, b)
+    eng.close()
+
+
+def test_rowspace_chain_and_midchain_models_equal_one_run():
+    """Pipelined chains continue the row-space state; get_models mid-chain materialises the
+    iterates without ending the chain; plain runs continue from the live state: all bitwise
+    one uninterrupted run."""
+    n, m, d = 11, 16, 2100
+    shards = _data([m] * n, d, 8)
+    eng = _engine(shards)
+    eng.set_models(np.zeros((n, d)))
+    obj_ref, cons_ref, _ = eng.run_dsgd(10, 0.05, m, 2e-3, 2e-3, 0.1)
+    x_ref = eng.get_models()
+    eng.set_models(np.zeros((n, d)))
+    objs, conss, t0 = [], [], 0
+    for k in (3, 2, 4, 0):
+        o, c = eng.run_dsgd_pipelined(k, 0.05, m, 2e-3, 2e-3, 0.1, t0=t0)
+        objs.append(o)
+        conss.append(c)
+        t0 += k
+        if k == 2:
+            eng.get_models()  # materialise mid-chain
+    assert np.array_equal(np.concatenate(objs), obj_ref[:9])
+    assert np.array_equal(np.concatenate(conss), cons_ref[:9])
+    o, c, _ = eng.run_dsgd(1, 0.05, m, 2e-3, 2e-3, 0.1, t0=9)  # continues from the live state
+    assert np.array_equal(o, obj_ref[9:]) and np.array_equal(c, cons_ref[9:])
+    assert np.array_equal(eng.get_models(), x_ref)
+    eng.close()
+
+
+def test_rowspace_then_other_run_kinds():
+    """After row-space rounds, a minibatch (direct) run and a topology change start from the
+    materialised iterates: same values as a fresh engine started from those iterates."""
+    n, m, d, T = 9, 12, 2100, 3
+    shards = _data([m] * n, d, 4)
+    eng = _engine(shards)
+    eng.run_dsgd(T, 0.05, m, 2e-3, 2e-3, 0.0)
+    x_mid = eng.get_models()
+    eng.run_dsgd(T, 0.05, m, 2e-3, 2e-3, 0.0, t0=T)  # row-space again (live state)
+    np.random.seed(1)
+    idx = _dopt.mt_choice_rounds(2, [m] * n, 5)
+    o1, c1, _ = eng.run_dsgd(2, 0.05, 5, 2e-3, 2e-3, 0.0, idx=idx, t0=2 * T)  # minibatch: direct rounds
+    x1 = eng.get_models()
+    ref = _engine(shards)
+    ref.set_models(x_mid)
+    ref.run_dsgd(T, 0.05, m, 2e-3, 2e-3, 0.0, t0=T)
+    o2, c2, _ = ref.run_dsgd(2, 0.05, 5, 2e-3, 2e-3, 0.0, idx=idx, t0=2 * T)
+    np.testing.assert_allclose(o1, o2, rtol=1e-9)
+    np.testing.assert_allclose(c1, c2, rtol=1e-9)
+    np.testing.assert_allclose(x1, ref.get_models(), rtol=1e-9, atol=1e-13)
+    eng.close()
+    ref.close()
