@@ -89,6 +89,10 @@ _SIGS = {
     "dopt_phase_loss_pass": ([_P, ctypes.c_int], ctypes.c_int),
     "dopt_phase_colsum_fold": ([_P, _P, _P, _P, _P], ctypes.c_int),
     "dopt_phase_mix_lagged": ([_P, _I64, _D, _P, ctypes.c_int], ctypes.c_int),
+    "dopt_rs_phase_begin": ([_P, ctypes.c_int, _P, _P], ctypes.c_int),
+    "dopt_rs_phase_round": ([_P, _I64, _D, _D, ctypes.c_uint32, _P], ctypes.c_int),
+    "dopt_rs_phase_cols": ([_P, _I64, _D, _D, _P], ctypes.c_int),
+    "dopt_rs_phase_metrics": ([_P, ctypes.c_uint32], ctypes.c_int),
     "dopt_sync": ([_P], ctypes.c_int),
     "dopt_finalize_metrics": ([ctypes.c_int, _I64, _P, _I64, _I64, _D, _D, _P, _P], ctypes.c_int),
     "dopt_eval_full": ([_P, _P, _D, _P, _P], ctypes.c_int),
@@ -456,6 +460,24 @@ class Engine:
 
     def phase_loss_pass(self, two_points):
         check(lib().dopt_phase_loss_pass(self._h, 1 if two_points else 0))
+
+    def rs_phase_begin(self, commit):
+        """(ok, sig): this rank's iterates all equal (row-space rounds possible) and a checksum of
+        that common iterate; commit=True also enters row-space mode."""
+        ok = ctypes.c_int(0)
+        sig = ctypes.c_double(0.0)
+        check(lib().dopt_rs_phase_begin(self._h, 1 if commit else 0, ctypes.byref(ok), ctypes.byref(sig)))
+        return bool(ok.value), float(sig.value)
+
+    def rs_phase_round(self, t, eta0, lam_grad, metric_flags, sum_ptr):
+        check(lib().dopt_rs_phase_round(self._h, int(t), float(eta0), float(lam_grad), int(metric_flags),
+                                        ctypes.c_void_p(sum_ptr)))
+
+    def rs_phase_cols(self, t, eta0, lam_grad, sum_ptr):
+        check(lib().dopt_rs_phase_cols(self._h, int(t), float(eta0), float(lam_grad), ctypes.c_void_p(sum_ptr)))
+
+    def rs_phase_metrics(self, metric_flags):
+        check(lib().dopt_rs_phase_metrics(self._h, int(metric_flags)))
 
     def sync(self):
         check(lib().dopt_sync(self._h))

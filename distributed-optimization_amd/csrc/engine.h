@@ -114,7 +114,7 @@ struct RsArgs {
   int32_t cb, nbuf;        // pass shape: 16-byte chunks per lane per block, rows in flight per wave
   const void* xbar;        // [ld] T point of the pass's dots (xbar of the iterates)
   double* coef_row;        // [rows] r_k / m_i of the current iterates (the pass's column-sum weights)
-  double* upart;           // [nblk x rows] partial dots X_k . xbar per column block
+  double* upart;           // [nblk x rows] partial dots X_k . xbar per column block (stored as T)
   double* cpart;           // [wg x ld] partial column sums sum_k coef_k X_k per row group
   int32_t bcap;            // row capacity per worker of z / v / beta / gram
   double* z;               // [n x bcap] X_ik . x_i
@@ -135,7 +135,7 @@ struct RsArgs {
 hipError_t launch_rs_pass(int dtype, bool cols, const RsArgs& a, hipStream_t s);
 // mode bits: 1 metric partials of the iterate the pass read, 2 next round's row state,
 // 4 initial state (z = v = u, beta = 0), 8 u = 0 without reading upart (zero start)
-hipError_t launch_rs_rows(const RsArgs& a, int n_workers, int mode, hipStream_t s);
+hipError_t launch_rs_rows(int dtype, const RsArgs& a, int n_workers, int mode, hipStream_t s);
 int rs_col_blocks(int64_t ld);  // blocks of k_rs_cols / k_rs_init (= RsArgs.nd)
 hipError_t launch_rs_cols(int dtype, const RsArgs& a, hipStream_t s);
 hipError_t launch_rs_csum(const RsArgs& a, double* out, hipStream_t s);

@@ -68,8 +68,15 @@ __global__ __launch_bounds__(NT) void k_rs_pass(const RsArgs a) {
   for (int j = 0; j < CB; ++j)
 #pragma unroll
     for (int e = 0; e < VN; ++e) acc[j][e] = 0.0;
-  double* __restrict__ up = a.upart + (int64_t)blk * a.rows;
+  // partial dots: T (a float32 context's 256-1024-element partial dots keep float precision;
+  // half the bytes of this launch's only large writes)
+  T* __restrict__ up = (T*)a.upart + (int64_t)blk * a.rows;
   double stash = 0.0;
+  // the rows' column-sum weights, 64 rows per vector load (lane k: row base + k), one window
+  // ahead; row r reads its weight with v_readlane (no scalar load and wait per row)
+  const double* __restrict__ cw = a.coef_row;
+  auto cwin_load = [&](int64_t base) { return (COLS && base + lane < wr1) ? cw[base + lane] : 0.0; };
+  double cw_cur = cwin_load(wr0), cw_nxt = cwin_load(wr0 + 64);
   auto load = [&](int64_t row, V (&dst)[CB]) {
     const T* p = X + row * ld;
 #pragma unroll
@@ -80,17 +87,21 @@ __global__ __launch_bounds__(NT) void k_rs_pass(const RsArgs a) {
 #pragma unroll
     for (int j = 0; j < CB; ++j) p += (double)hsum<T>(rv[j] * xb[j]);
     const double dot = wave_sum_dpp(p);
+    const int k = (int)((r - wr0) & 63);
     if constexpr (COLS) {
-      const double cf = a.coef_row[r];  // wave-uniform
+      const double cf = readlane_t(cw_cur, k);  // wave-uniform
 #pragma unroll
       for (int j = 0; j < CB; ++j)
 #pragma unroll
         for (int e = 0; e < VN; ++e) acc[j][e] += cf * (double)rv[j][e];
+      if (k == 63) {  // next window
+        cw_cur = cw_nxt;
+        cw_nxt = cwin_load(r + 65);
+      }
     }
-    const int k = (int)((r - wr0) & 63);
     if (lane == k) stash = dot;
     if (k == 63 || r + 1 == wr1) {
-      if (lane <= k) up[r - k + lane] = stash;
+      if (lane <= k) up[r - k + lane] = (T)stash;
     }
   };
   if (wr0 < wr1) {
@@ -129,6 +140,7 @@ __global__ __launch_bounds__(NT) void k_rs_pass(const RsArgs a) {
 // pass's column blocks (4 waves x a quarter each, then in wave order); then the metric partials
 // of the iterate the pass read (mode & 1), the next round's row state (mode & 2), or the
 // initial state z = v = u, beta = 0 (mode & 4).
+template <typename T>
 __global__ __launch_bounds__(NT) void k_rs_rows(const RsArgs a, int mode) {
   __shared__ double ured[NW][64];
   __shared__ double sb[64], sr[64];
@@ -143,7 +155,7 @@ __global__ __launch_bounds__(NT) void k_rs_rows(const RsArgs a, int mode) {
     const int b0 = (int)((int64_t)nb * wave / NW), b1 = (int)((int64_t)nb * (wave + 1) / NW);
     double s = 0.0;
     if (lane < m && !(mode & 8))
-      for (int b = b0; b < b1; ++b) s += a.upart[(int64_t)b * a.rows + row0 + lane];
+      for (int b = b0; b < b1; ++b) s += (double)((const T*)a.upart)[(int64_t)b * a.rows + row0 + lane];
     ured[wave][lane] = s;
   }
   // ||D||^2 = ||Z - xbar||^2 of the iterate the pass read: the block partials of k_rs_cols /
@@ -413,9 +425,10 @@ hipError_t launch_rs_pass(int dtype, bool cols, const RsArgs& a, hipStream_t s) 
   return cols ? rs_pass_shape<double, true>(a, grid, s) : rs_pass_shape<double, false>(a, grid, s);
 }
 
-hipError_t launch_rs_rows(const RsArgs& a, int n_workers, int mode, hipStream_t s) {
+hipError_t launch_rs_rows(int dtype, const RsArgs& a, int n_workers, int mode, hipStream_t s) {
   if (n_workers <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_rs_rows, dim3(n_workers), dim3(NT), 0, s, a, mode);
+  if (dtype == 0) hipLaunchKernelGGL((k_rs_rows<float>), dim3(n_workers), dim3(NT), 0, s, a, mode);
+  else hipLaunchKernelGGL((k_rs_rows<double>), dim3(n_workers), dim3(NT), 0, s, a, mode);
   return hipGetLastError();
 }
 

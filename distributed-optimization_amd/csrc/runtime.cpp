@@ -777,13 +777,15 @@ int ensure_rs(dopt_ctx* c) {
   // pass shape (A/B knobs DOPT_RS_CB / DOPT_RS_NBUF: the compiled pairs in rowspace.hip)
   const char* cbv = getenv("DOPT_RS_CB");
   const char* nbv = getenv("DOPT_RS_NBUF");
-  c->rs_cb = cbv ? atoi(cbv) : 4;
-  c->rs_nbuf = nbv ? atoi(nbv) : 3;
+  // C5 float32 (tools/rs_ab.py, interleaved on one box, round ms): CB / NBUF / row groups
+  // 2 / 6 / 2 11.22, 2 / 4 / 2 11.50, 1 / 8 / 4 11.46-11.84, 2 / 6 / 4 11.33-11.57, 4 / 2 / 4 12.36,
+  // 1 / 8 / 16 12.36, 4 / 2 / 16 13.1-13.2: the partial sums' writes (dots nblk x rows, column
+  // sums groups x ld) and long row visits matter more than the tail of ~4k 16 MiB workgroups
+  c->rs_cb = cbv ? atoi(cbv) : 2;
+  c->rs_nbuf = nbv ? atoi(nbv) : 6;
   const int64_t nblk = (c->nch + 64 * c->rs_cb - 1) / (64 * c->rs_cb);
-  // ~16k workgroups of ~1k rows: 4 MiB per workgroup at C5 (a short tail), partial sums
-  // (nblk x rows dots + wg x ld column sums) ~0.4 % of the shard bytes
   const char* ev = getenv("DOPT_RS_WG");
-  int64_t wg = ev ? atoll(ev) : (16384 + nblk - 1) / nblk;
+  int64_t wg = ev ? atoll(ev) : (c->rows + 8191) / 8192;  // ~8k rows per row group
   wg = std::max<int64_t>(1, std::min<int64_t>(wg, (c->rows + 255) / 256));
   int rc;
   c->rs_nblk = (int)nblk;
@@ -856,11 +858,11 @@ int rs_begin(dopt_ctx* c) {
   a.xbar_out = c->xbar[c->xb];
   HIPOK(launch_rs_init(dt, a, c->xs[c->cur], c->stream));  // Z = xbar = x_0, ||D||^2 = 0
   if (zero) {
-    HIPOK(launch_rs_rows(a, (int)c->n, 4 | 8, c->stream));  // z = v = 0
+    HIPOK(launch_rs_rows(dt, a, (int)c->n, 4 | 8, c->stream));  // z = v = 0
   } else {
     a.xbar = c->xbar[c->xb];
     HIPOK(launch_rs_pass(dt, false, a, c->stream));  // z = v = X . x_0
-    HIPOK(launch_rs_rows(a, (int)c->n, 4, c->stream));
+    HIPOK(launch_rs_rows(dt, a, (int)c->n, 4, c->stream));
   }
   c->rs_live = true;
   c->rs_xs_valid = true;  // xs[cur] is x_0 itself
@@ -899,7 +901,7 @@ int run_dsgd_rs(dopt_ctx* c, int64_t t0, int64_t T, double eta0, double lam_grad
     if (c->prof && (rc = prof_event(c, false))) return rc;
     HIPOK(launch_rs_pass(dt, true, a, c->stream));
     if (c->prof && (rc = prof_event(c, true))) return rc;
-    HIPOK(launch_rs_rows(a, (int)c->n, 2 | (met ? 1 : 0), c->stream));
+    HIPOK(launch_rs_rows(dt, a, (int)c->n, 2 | (met ? 1 : 0), c->stream));
     if (met) {
       c->loss_groups = c->n;
       if ((rc = history(c, h - 1 + lag, c->xbar[xb], want_cons, want_obj, c->n))) return rc;
@@ -921,7 +923,7 @@ int run_dsgd_rs(dopt_ctx* c, int64_t t0, int64_t T, double eta0, double lam_grad
     a.slab_cons = want_cons ? c->slab_cons : nullptr;
     a.slab_loss = want_obj ? c->slab_loss : nullptr;
     HIPOK(launch_rs_pass(dt, false, a, c->stream));
-    HIPOK(launch_rs_rows(a, (int)c->n, 1, c->stream));
+    HIPOK(launch_rs_rows(dt, a, (int)c->n, 1, c->stream));
     c->loss_groups = c->n;
     if ((rc = history(c, nh - 1, c->xbar[xb], want_cons, want_obj, c->n))) return rc;
   }
@@ -2025,6 +2027,105 @@ int dopt_phase_mix_lagged(dopt_ctx* c, int64_t t, double eta0, const double* sum
   c->S_ext = nullptr;
   c->send_fresh = c->n_send > 0;
   c->cur ^= 1;
+  return DOPT_OK;
+}
+
+// ---- row-space rounds on a rank's slice (complete graph, quadratic, full shards; rowspace.hip).
+// The replicated d-vectors (xbar, Z) take the all-reduced column sums, so every rank holds
+// the same ones; the metric partials are this rank's workers' (folded by dopt_phase_fold).
+int dopt_rs_phase_begin(dopt_ctx* c, int commit, int* ok, double* sig) {
+  CHECK_ARG(c && ok && sig, "NULL argument");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
+  *ok = 0;
+  *sig = 0.0;
+  if (!(rs_enabled() && c->split && c->mean_mix && c->wdiag_uniform && c->problem == DOPT_QUADRATIC &&
+        !c->obj_sep && c->min_m >= 1 && c->max_m <= kRsMaxRows && c->xdtype == c->dtype))
+    return DOPT_OK;
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  c->carry_pending = false;
+  if (c->rs_live) {
+    *ok = 1;
+    return DOPT_OK;
+  }
+  if ((rc = ensure_rs(c))) return rc;
+  const int dt = c->dtype == DOPT_F32 ? 0 : 1;
+  const int G = kRsCheckGroups;
+  HIPOK(launch_rs_check(dt, c->xs[c->cur], c->n, c->ld, (int32_t)c->nch, G, c->rs_flags, c->rs_flags + c->n * G,
+                        c->stream));
+  std::vector<int32_t> fl((size_t)(c->n + 1) * G);
+  HIPOK(hipMemcpyAsync(fl.data(), c->rs_flags, fl.size() * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  const size_t esz = c->esz;
+  std::vector<char> raw((size_t)c->ld * esz);
+  HIPOK(hipMemcpyAsync(raw.data(), c->xs[c->cur], raw.size(), hipMemcpyDeviceToHost, c->stream));
+  HIPOK(hipStreamSynchronize(c->stream));
+  for (int64_t k = 0; k < c->n * G; ++k)
+    if (fl[(size_t)k]) return DOPT_OK;
+  double s = 0.0;  // signature of the common iterate (the caller compares it across ranks)
+  for (int64_t k = 0; k < c->d; ++k)
+    s += (double)(k % 1021 + 1) * (esz == 4 ? (double)((const float*)raw.data())[k] : ((const double*)raw.data())[k]);
+  *sig = s;
+  *ok = 1;
+  if (!commit) return DOPT_OK;
+  return rs_begin(c) == RS_FALLBACK ? fail(DOPT_ERR_STATE, "row-space begin: iterates changed") : DOPT_OK;
+}
+
+int dopt_rs_phase_round(dopt_ctx* c, int64_t t, double eta0, double lam_grad, uint32_t metric_flags,
+                        double* sum_dev) {
+  CHECK_ARG(c && sum_dev, "NULL argument");
+  if (!c->rs_live) return fail(DOPT_ERR_STATE, "dopt_rs_phase_begin first");
+  const int dt = c->dtype == DOPT_F32 ? 0 : 1;
+  const double N = (double)n_div(c), eta = eta0 / sqrt((double)(t + 1));  // trainer.py:138-140
+  RsArgs a = rs_args(c);
+  a.xbar = c->xbar[c->xb];
+  a.a1 = c->w_off * N;
+  a.q = c->wdiag_u - c->w_off - eta * lam_grad;
+  a.eta = eta;
+  a.eta_n = eta / N;
+  const bool met = (metric_flags & (DOPT_RUN_OBJECTIVE | DOPT_RUN_CONSENSUS)) != 0;
+  a.slab_cons = (metric_flags & DOPT_RUN_CONSENSUS) ? c->slab_cons : nullptr;
+  a.slab_loss = (metric_flags & DOPT_RUN_OBJECTIVE) ? c->slab_loss : nullptr;
+  int rc;
+  if (c->prof && (rc = prof_event(c, false))) return rc;
+  HIPOK(launch_rs_pass(dt, true, a, c->stream));
+  if (c->prof && (rc = prof_event(c, true))) return rc;
+  HIPOK(launch_rs_rows(dt, a, (int)c->n, 2 | (met ? 1 : 0), c->stream));
+  HIPOK(launch_rs_csum(a, sum_dev, c->stream));
+  c->cons_n = c->n;
+  c->slab_n[0] = c->n;
+  c->rs_xs_valid = false;
+  return DOPT_OK;
+}
+
+int dopt_rs_phase_cols(dopt_ctx* c, int64_t t, double eta0, double lam_grad, const double* sum_dev) {
+  CHECK_ARG(c && sum_dev, "NULL argument");
+  if (!c->rs_live) return fail(DOPT_ERR_STATE, "dopt_rs_phase_begin first");
+  const int dt = c->dtype == DOPT_F32 ? 0 : 1;
+  const double N = (double)n_div(c), eta = eta0 / sqrt((double)(t + 1));
+  RsArgs a = rs_args(c);
+  a.a1 = c->w_off * N;
+  a.q = c->wdiag_u - c->w_off - eta * lam_grad;
+  a.eta = eta;
+  a.eta_n = eta / N;
+  a.csum = sum_dev;
+  a.xbar_out = c->xbar[c->xb ^ 1];
+  HIPOK(launch_rs_cols(dt, a, c->stream));
+  c->xb ^= 1;
+  return DOPT_OK;
+}
+
+int dopt_rs_phase_metrics(dopt_ctx* c, uint32_t metric_flags) {
+  CHECK_ARG(c, "ctx is NULL");
+  if (!c->rs_live) return fail(DOPT_ERR_STATE, "dopt_rs_phase_begin first");
+  const int dt = c->dtype == DOPT_F32 ? 0 : 1;
+  RsArgs a = rs_args(c);
+  a.xbar = c->xbar[c->xb];
+  a.slab_cons = (metric_flags & DOPT_RUN_CONSENSUS) ? c->slab_cons : nullptr;
+  a.slab_loss = (metric_flags & DOPT_RUN_OBJECTIVE) ? c->slab_loss : nullptr;
+  HIPOK(launch_rs_pass(dt, false, a, c->stream));
+  HIPOK(launch_rs_rows(dt, a, (int)c->n, 1, c->stream));
+  c->cons_n = c->n;
+  c->slab_n[0] = c->n;
   return DOPT_OK;
 }
 

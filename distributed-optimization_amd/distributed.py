@@ -224,6 +224,7 @@ class DistributedDSGD:
             engine.set_halo(0, None, np.zeros(0, np.int32), None)
             engine.set_mixing_mean(mean[0], mean[1])
             self._peers = []
+        self.mean = mean
         engine.set_stream(self.stream.cuda_stream)
         # the lagged schedule: CSR mixing on row-resident contexts (DOPT_LAGGED=0: the serial one)
         nch = (ld * esz) // 16
@@ -313,6 +314,8 @@ class DistributedDSGD:
                batch < int(rows.max()) <= _dopt.MAX_BIP_ROWS and os.environ.get("DOPT_BIP", "1") != "0")
         if (fused or bip) and flags and self._lagged_ok:
             return self._run_lagged(T, eta0, batch, lam_grad, lam_obj, f_opt, t0, objective, consensus, idx)
+        if self.mean is not None and fused and T > 0 and self._rowspace_ready():
+            return self._run_rowspace(T, eta0, lam_grad, lam_obj, f_opt, t0, objective, consensus)
         xnorm = self.plan.rank == 0  # ||xbar||^2 is global already: count it once
         with torch.cuda.stream(self.stream):
             partials = torch.zeros((max(1, T), 3), dtype=torch.float64, device=self.dev)
@@ -343,6 +346,51 @@ class DistributedDSGD:
                 eng.phase_metrics(flags, xnorm, partials[T - 1].data_ptr())
             self._all_reduce(partials)
             raw = partials[:T].cpu().numpy()
+        self.stream.synchronize()
+        obj, cons = _dopt.finalize_metrics(self.eng.problem, raw, self.n_global, self.rows_global, lam_obj, f_opt)
+        return (obj if objective else None), (cons if consensus else None)
+
+    def _rowspace_ready(self):
+        """Complete graph + quadratic + full shards of <= 64 rows and iterates that are equal on
+        every rank (checked here, checksum compared across ranks): the row-space rounds."""
+        torch = self.torch
+        ok, sig = self.eng.rs_phase_begin(False)
+        v = torch.tensor([1.0 if ok else 0.0, sig, -sig], dtype=torch.float64,
+                         device=self.dev if self.device_comm else "cpu")
+        if not self._solo():
+            self.dist.all_reduce(v, op=self.dist.ReduceOp.MIN, group=self.group)
+        ok_all, lo, hi = float(v[0]), float(v[1]), -float(v[2])
+        return ok_all == 1.0 and lo == hi
+
+    def _run_rowspace(self, T, eta0, lam_grad, lam_obj, f_opt, t0, objective, consensus):
+        """Complete graph, quadratic: the iterates stay Z + X_i^T beta_i.  Per round
+        one read-only pass over this rank's rows (row state, metric partials of the current
+        iterates, local column sums), the all-reduce of the d column sums, the replicated
+        average / Z update; history[h] = metrics of x_{h+1} from the next pass (the last from a
+        dots pass).  The iterates are formed when asked for (gather_models)."""
+        torch, eng = self.torch, self.eng
+        xnorm = self.plan.rank == 0
+        mf = (_dopt.RUN_OBJECTIVE if objective else 0) | (_dopt.RUN_CONSENSUS if consensus else 0)
+        eng.rs_phase_begin(True)
+        with torch.cuda.stream(self.stream):
+            partials = torch.zeros((T, 3), dtype=torch.float64, device=self.dev)
+
+            def fold(h):
+                base = partials.data_ptr() + 3 * h * 8
+                eng.phase_fold(base if consensus else None, base + 16 if objective and xnorm else None,
+                               base + 8 if objective else None, 0)
+
+            for h in range(T):
+                eng.rs_phase_round(t0 + h, eta0, lam_grad, mf if h > 0 else 0, self.sum.data_ptr())
+                if h > 0 and mf:
+                    fold(h - 1)
+                self._all_reduce(self.sum)
+                eng.rs_phase_cols(t0 + h, eta0, lam_grad, self.sum.data_ptr())
+            if mf:
+                eng.rs_phase_metrics(mf)
+                fold(T - 1)
+            self._all_reduce(partials)
+            raw = partials.cpu().numpy()
         self.stream.synchronize()
         obj, cons = _dopt.finalize_metrics(self.eng.problem, raw, self.n_global, self.rows_global, lam_obj, f_opt)
         return (obj if objective else None), (cons if consensus else None)

@@ -280,6 +280,24 @@ int dopt_phase_metrics(dopt_ctx *ctx, uint32_t flags, int include_xnorm, double 
 int dopt_phase_cons(dopt_ctx *ctx);
 int dopt_phase_fold(dopt_ctx *ctx, double *cons_out, double *xnorm_out, double *loss_out, int slab);
 int dopt_phase_loss_pass(dopt_ctx *ctx, int two_points);
+/* Row-space rounds on a rank's slice (complete graph with one W_ii, quadratic, full shards of
+ * 1..64 rows) -- replace the serial phase order of DistributedDSGD for that case
+ * (trainer.py:161-193 with the mix of trainer.py:173 through the all-reduced column sums):
+ * dopt_rs_phase_begin: *ok = 1 when this rank's iterates are all equal (or the row-space state
+ *   is live already), *sig = a checksum of that common iterate (the caller compares it across
+ *   ranks); commit = 1 also enters row-space mode (Gram matrices, Z = xbar = the iterate).
+ * dopt_rs_phase_round: round t's pass at the current average: the next row state, the metric
+ *   partials of the current iterates (metric_flags, folded by dopt_phase_fold slab 0) and this
+ *   rank's column sums into sum_dev[ld] (to be all-reduced).
+ * dopt_rs_phase_cols: the average / Z update of round t from the all-reduced sums.
+ * dopt_rs_phase_metrics: the metric partials of the current iterates (a dots pass).
+ * dopt_get_models forms the iterates; dopt_phase_begin, dopt_phase_colsum / _fold / _gather,
+ * dopt_set_models, dopt_set_mixing_mean and dopt_set_topology leave row-space mode. */
+int dopt_rs_phase_begin(dopt_ctx *ctx, int commit, int *ok, double *sig);
+int dopt_rs_phase_round(dopt_ctx *ctx, int64_t t, double eta0, double lam_grad, uint32_t metric_flags,
+                        double *sum_dev);
+int dopt_rs_phase_cols(dopt_ctx *ctx, int64_t t, double eta0, double lam_grad, const double *sum_dev);
+int dopt_rs_phase_metrics(dopt_ctx *ctx, uint32_t metric_flags);
 /* dopt_phase_colsum_fold: dopt_phase_colsum, plus (same launch) the fold of the consensus slab
  *   of the last dopt_phase_mix_lagged / dopt_phase_cons, loss slab 0 and ||xbar||^2 of the
  *   current average into the non-NULL outputs.

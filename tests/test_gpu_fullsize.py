@@ -131,7 +131,7 @@ def test_c5_rowspace_full_size_vs_direct(monkeypatch):
         eng.set_mixing_mean(w_off, diag)
         monkeypatch.setenv("DOPT_ROWSPACE", "1")
         o1, c1, _ = eng.run_dsgd(1, eta0, m, lam, lam, 0.0)
-        assert "k_rs_pass<float, true>" in _dopt.last_round_kernel()
+        assert "k_rs_pass<float, true," in _dopt.last_round_kernel()
         x1 = eng.get_models()
         for i in (0, 1, 700, 1023):  # x_1 = mix(0) - eta (X^T (0 - y) / m + lam 0)
             X, y = eng.get_shard(i)

@@ -49,7 +49,7 @@ def test_rowspace_vs_oracle(start, sizes):
         eng.set_models(x0)
     b = max(sizes)
     obj, cons, _ = eng.run_dsgd(T, 0.05, b, 2e-3, 1e-3, 0.1)
-    assert _dopt.last_round_kernel().startswith("void dopt::k_rs_pass<double, true>")
+    assert _dopt.last_round_kernel().startswith("void dopt::k_rs_pass<double, true,")
     x = eng.get_models()
     Xf = np.vstack([s[0] for s in shards])
     yf = np.concatenate([s[1] for s in shards])
@@ -149,3 +149,67 @@ def test_rowspace_then_other_run_kinds():
     np.testing.assert_allclose(x1, ref.get_models(), rtol=1e-9, atol=1e-13)
     eng.close()
     ref.close()
+
+
+SIZES_D = [12, 7, 12, 3, 12, 12, 9, 12, 1, 12, 12, 5, 12]  # ragged shards over the ranks' slices
+
+
+def _rs_rank(rank, world, port, out, T):
+    import os
+
+    import torch  # noqa: F401  (one HIP runtime, loaded before libdopt)
+    import torch.distributed as dist
+
+    import distributed as Dm
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    shards = _data(SIZES_D, 2100, 12)
+    n = len(shards)
+    bounds = Dm.partition_bounds(n, world)
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    plan = Dm.HaloPlan(rank, world, bounds, lo, hi, np.zeros(0, np.int64), np.zeros(world + 1, np.int64),
+                       np.zeros(0, np.int32), np.zeros(world + 1, np.int64), None, None, None)
+    eng = _dopt.Engine(0, "float64")
+    mine = shards[lo:hi]
+    off = np.concatenate([[0], np.cumsum([len(s[1]) for s in mine])])
+    eng.load_shards("quadratic", np.vstack([s[0] for s in mine]), np.concatenate([s[1] for s in mine]), off)
+    w_off, diag = TP.fully_connected(n).uniform_offdiag()
+    run = Dm.DistributedDSGD(eng, plan, n, sum(SIZES_D), device=0, mean=(w_off, diag[lo:hi]))
+    o1, c1 = run.run(3, 0.05, max(SIZES_D), 2e-3, 1e-3, 0.1)
+    kern = _dopt.last_round_kernel()
+    o2, c2 = run.run(T - 3, 0.05, max(SIZES_D), 2e-3, 1e-3, 0.1, t0=3)  # continues the live state
+    x = run.gather_models()
+    if rank == 0:
+        np.savez(os.path.join(out, "rs.npz"), obj=np.concatenate([o1, o2]), cons=np.concatenate([c1, c2]), x=x,
+                 kern=np.array(kern))
+    dist.barrier()
+    eng.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rowspace_ranks_vs_oracle(tmp_path, world):
+    """Row-space rounds across ranks (gloo, contexts sharing the GPU): each rank's pass gives its
+    column sums, all-reduced into the replicated average; history and gathered iterates vs the
+    oracle at rtol 1e-9 (float64)."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    T = 7
+    mp.start_processes(_rs_rank, args=(world, port, str(tmp_path), T), nprocs=world, join=True, start_method="spawn")
+    got = np.load(tmp_path / "rs.npz")
+    assert "k_rs_pass<double, true" in str(got["kern"])
+    shards = _data(SIZES_D, 2100, 12)
+    n = len(shards)
+    Xf = np.vstack([s[0] for s in shards])
+    yf = np.concatenate([s[1] for s in shards])
+    h, _, xr, _ = O.run_decentralized(shards, TP.fully_connected(n).dense_W(), T, _cfg(max(SIZES_D)), Xf, yf, 0.1)
+    np.testing.assert_allclose(got["obj"], h["objective"], rtol=1e-9)
+    np.testing.assert_allclose(got["cons"], h["consensus_error"], rtol=1e-9)
+    np.testing.assert_allclose(got["x"], xr, rtol=1e-9, atol=1e-12 * np.abs(xr).max())

@@ -30,7 +30,7 @@ def main():
     zeros = np.zeros((n, d), dtype=np.float32)
     res = {}
     for rep in range(args.reps):
-        for sh in args.shapes.split():
+        for sh in args.shapes.replace("_", " ").split():
             cb, nb, wg = sh.split(",")
             os.environ["DOPT_RS_CB"], os.environ["DOPT_RS_NBUF"] = cb, nb
             os.environ["DOPT_RS_WG"] = wg
