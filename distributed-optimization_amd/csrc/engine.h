@@ -124,7 +124,7 @@ struct RsArgs {
   double* gram_w;          // the same, written by the Gram fold
   double* slab_cons;       // [n] ||x_i - xbar||^2 (k_rs_rows mode 1), or null
   double* slab_loss;       // [n] sum_k (u_k - y_k)^2, or null
-  double* dpart;           // [nd] partials of ||Z - xbar||^2 (k_rs_cols / k_rs_init)
+  double* dpart;           // [2 nd] partials of ||Z - xbar||^2, then of ||xbar||^2 (k_rs_cols / k_rs_init)
   int32_t nd;
   double* rZ;              // [ld] Z
   double* rxbar;           // [ld] xbar (float64 master)
@@ -139,6 +139,8 @@ hipError_t launch_rs_rows(int dtype, const RsArgs& a, int n_workers, int mode, h
 int rs_col_blocks(int64_t ld);  // blocks of k_rs_cols / k_rs_init (= RsArgs.nd)
 hipError_t launch_rs_cols(int dtype, const RsArgs& a, hipStream_t s);
 hipError_t launch_rs_csum(const RsArgs& a, double* out, hipStream_t s);
+// History row (cons, loss, ||xbar||^2) of the row-space rounds from the slabs and partials.
+hipError_t launch_rs_hist(const RsArgs& a, int n_workers, double* out, hipStream_t s);
 hipError_t launch_rs_init(int dtype, const RsArgs& a, const void* x0, hipStream_t s);
 hipError_t launch_rs_check(int dtype, const void* x, int64_t n, int64_t ld, int32_t nch, int G, int32_t* flags,
                            int32_t* zflag, hipStream_t s);

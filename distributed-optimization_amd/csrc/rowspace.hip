@@ -142,7 +142,7 @@ __global__ __launch_bounds__(NT) void k_rs_pass(const RsArgs a) {
 // initial state z = v = u, beta = 0 (mode & 4).
 template <typename T>
 __global__ __launch_bounds__(NT) void k_rs_rows(const RsArgs a, int mode) {
-  __shared__ double ured[NW][64];
+  __shared__ double ured[16][64];
   __shared__ double sb[64], sr[64];
   __shared__ double dred[NW];
   const int lane = threadIdx.x & 63;
@@ -151,12 +151,26 @@ __global__ __launch_bounds__(NT) void k_rs_rows(const RsArgs a, int mode) {
   const int64_t row0 = a.off[i];
   const int m = (int)(a.off[i + 1] - row0);
   const int nb = a.nblk;
+  // u_k: the partial dots over the pass's column blocks, in slices of blocks (lane = (slice, row):
+  // R lanes per row set, 64 / R slices per wave), four accumulators per lane, slices in order
+  const int R = m <= 16 ? 16 : m <= 32 ? 32 : 64;
+  const int S = 64 / R, slices = NW * S;
   {
-    const int b0 = (int)((int64_t)nb * wave / NW), b1 = (int)((int64_t)nb * (wave + 1) / NW);
-    double s = 0.0;
-    if (lane < m && !(mode & 8))
-      for (int b = b0; b < b1; ++b) s += (double)((const T*)a.upart)[(int64_t)b * a.rows + row0 + lane];
-    ured[wave][lane] = s;
+    const int sub = lane / R, k = lane % R, sl = wave * S + sub;
+    const int b0 = (int)((int64_t)nb * sl / slices), b1 = (int)((int64_t)nb * (sl + 1) / slices);
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    if (k < m && !(mode & 8)) {
+      const T* u = (const T*)a.upart + row0 + k;
+      int b = b0;
+      for (; b + 3 < b1; b += 4) {
+        s0 += (double)u[(int64_t)b * a.rows];
+        s1 += (double)u[(int64_t)(b + 1) * a.rows];
+        s2 += (double)u[(int64_t)(b + 2) * a.rows];
+        s3 += (double)u[(int64_t)(b + 3) * a.rows];
+      }
+      for (; b < b1; ++b) s0 += (double)u[(int64_t)b * a.rows];
+    }
+    ured[sl][k] = (s0 + s1) + (s2 + s3);
   }
   // ||D||^2 = ||Z - xbar||^2 of the iterate the pass read: the block partials of k_rs_cols /
   // k_rs_init, in one fixed order (every workgroup forms the same value)
@@ -175,7 +189,9 @@ __global__ __launch_bounds__(NT) void k_rs_rows(const RsArgs a, int mode) {
   if (wave != 0) return;
   if (mode & 1) dn = ((dred[0] + dred[1]) + dred[2]) + dred[3];
   const bool live = lane < m;
-  const double u = live ? ((ured[0][lane] + ured[1][lane]) + ured[2][lane]) + ured[3][lane] : 0.0;
+  double u = 0.0;
+  if (live)
+    for (int q = 0; q < slices; ++q) u += ured[q][lane];
   const double yv = live ? (a.y_is_f32 ? (double)((const float*)a.y)[row0 + lane] : ((const double*)a.y)[row0 + lane])
                          : 0.0;
   if (mode & 4) {  // initial state of iterates that all equal xbar: z = v = X . xbar, beta = 0
@@ -222,9 +238,9 @@ __global__ __launch_bounds__(NT) void k_rs_rows(const RsArgs a, int mode) {
 // pass and the metrics, and per-block partials of ||Z' - xbar'||^2.
 template <typename T>
 __global__ __launch_bounds__(NT) void k_rs_cols(const RsArgs a) {
-  __shared__ double red[NW];
+  __shared__ double red[2 * NW];
   const int64_t e = (int64_t)blockIdx.x * NT + threadIdx.x;
-  double dd = 0.0;
+  double dd = 0.0, xx = 0.0;
   if (e < a.ld) {
     double C;
     if (a.csum) {
@@ -238,13 +254,22 @@ __global__ __launch_bounds__(NT) void k_rs_cols(const RsArgs a) {
     const double zn = a.a1 * xo + a.q * zo;
     a.rxbar[e] = xn;
     a.rZ[e] = zn;
-    ((T*)a.xbar_out)[e] = (T)xn;
+    const T xt = (T)xn;
+    ((T*)a.xbar_out)[e] = xt;
     dd = (zn - xn) * (zn - xn);
+    xx = (double)xt * (double)xt;
   }
   dd = wave_sum(dd);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = dd;
+  xx = wave_sum(xx);
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = dd;
+    red[NW + (threadIdx.x >> 6)] = xx;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) a.dpart[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+  if (threadIdx.x == 0) {
+    a.dpart[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+    a.dpart[a.nd + blockIdx.x] = ((red[NW] + red[NW + 1]) + red[NW + 2]) + red[NW + 3];  // ||xbar'||^2 (as T)
+  }
 }
 
 // Local column sums C_rank = sum_g cpart[g] into csum (multi-GPU: all-reduced before k_rs_cols).
@@ -259,14 +284,53 @@ __global__ __launch_bounds__(NT) void k_rs_csum(const RsArgs a, double* out) {
 // Z = xbar = row 0 of x (iterates that all equal it), the T copy of xbar, ||D||^2 partials 0.
 template <typename T>
 __global__ __launch_bounds__(NT) void k_rs_init(const RsArgs a, const T* x0) {
+  __shared__ double red[NW];
   const int64_t e = (int64_t)blockIdx.x * NT + threadIdx.x;
+  double xx = 0.0;
   if (e < a.ld) {
     const T v = x0[e];
     a.rxbar[e] = (double)v;
     a.rZ[e] = (double)v;
     ((T*)a.xbar_out)[e] = v;
+    xx = (double)v * (double)v;
   }
-  if (threadIdx.x == 0) a.dpart[blockIdx.x] = 0.0;
+  xx = wave_sum(xx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = xx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    a.dpart[blockIdx.x] = 0.0;
+    a.dpart[a.nd + blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+  }
+}
+
+// History row of the row-space rounds (one workgroup, fixed order): out[0] = sum slab_cons[0:n],
+// out[1] = sum slab_loss[0:n], out[2] = ||xbar||^2 from k_rs_cols' / k_rs_init's partials.
+__global__ __launch_bounds__(NT) void k_rs_hist(const RsArgs a, int n, double* out) {
+  __shared__ double red[3][NW];
+  auto sum4 = [&](const double* v, int64_t cnt) {
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int64_t k = threadIdx.x;
+    for (; k + 3 * NT < cnt; k += 4 * NT) {
+      s0 += v[k];
+      s1 += v[k + NT];
+      s2 += v[k + 2 * NT];
+      s3 += v[k + 3 * NT];
+    }
+    for (; k < cnt; k += NT) s0 += v[k];
+    return wave_sum((s0 + s1) + (s2 + s3));
+  };
+  const double c = a.slab_cons ? sum4(a.slab_cons, n) : 0.0;
+  const double l = a.slab_loss ? sum4(a.slab_loss, n) : 0.0;
+  const double q = a.slab_loss ? sum4(a.dpart + a.nd, a.nd) : 0.0;
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = c;
+    red[1][w] = l;
+    red[2][w] = q;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int k = 0; k < 3; ++k) out[k] = ((red[k][0] + red[k][1]) + red[k][2]) + red[k][3];
 }
 
 // flags[i * G + g] = 1 when row i of x differs from row 0 on the chunks of group g; zflag[g] = 1
@@ -438,6 +502,11 @@ hipError_t launch_rs_cols(int dtype, const RsArgs& a, hipStream_t s) {
   const dim3 grid(rs_col_blocks(a.ld));
   if (dtype == 0) hipLaunchKernelGGL((k_rs_cols<float>), grid, dim3(NT), 0, s, a);
   else hipLaunchKernelGGL((k_rs_cols<double>), grid, dim3(NT), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_rs_hist(const RsArgs& a, int n_workers, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_rs_hist, dim3(1), dim3(NT), 0, s, a, n_workers, out);
   return hipGetLastError();
 }
 

@@ -797,7 +797,7 @@ int ensure_rs(dopt_ctx* c) {
   if ((rc = dalloc_t(&c->rs_cp, (size_t)wg * c->ld * sizeof(double)))) return rc;
   if ((rc = dalloc_t(&c->rs_z, 3 * nb * sizeof(double)))) return rc;
   if ((rc = dalloc_t(&c->rs_gram, nb * c->rs_bcap * sizeof(double)))) return rc;
-  if ((rc = dalloc_t(&c->rs_dpart, (size_t)c->rs_nd * sizeof(double)))) return rc;
+  if ((rc = dalloc_t(&c->rs_dpart, 2 * (size_t)c->rs_nd * sizeof(double)))) return rc;
   if ((rc = dalloc_t(&c->rs_Z, 2 * (size_t)c->ld * sizeof(double)))) return rc;
   if ((rc = dalloc_t(&c->rs_flags, ((size_t)c->n + 1) * kRsCheckGroups * sizeof(int32_t)))) return rc;
   std::vector<int64_t> gr((size_t)wg + 1);
@@ -902,10 +902,7 @@ int run_dsgd_rs(dopt_ctx* c, int64_t t0, int64_t T, double eta0, double lam_grad
     HIPOK(launch_rs_pass(dt, true, a, c->stream));
     if (c->prof && (rc = prof_event(c, true))) return rc;
     HIPOK(launch_rs_rows(dt, a, (int)c->n, 2 | (met ? 1 : 0), c->stream));
-    if (met) {
-      c->loss_groups = c->n;
-      if ((rc = history(c, h - 1 + lag, c->xbar[xb], want_cons, want_obj, c->n))) return rc;
-    }
+    if (met) HIPOK(launch_rs_hist(a, (int)c->n, c->hraw + 3 * (h - 1 + lag), c->stream));
     a.xbar_out = c->xbar[xb ^ 1];
     HIPOK(launch_rs_cols(dt, a, c->stream));
     HIPOK(launch_stamp(c->stamps + h + 1, c->stream));
@@ -924,8 +921,7 @@ int run_dsgd_rs(dopt_ctx* c, int64_t t0, int64_t T, double eta0, double lam_grad
     a.slab_loss = want_obj ? c->slab_loss : nullptr;
     HIPOK(launch_rs_pass(dt, false, a, c->stream));
     HIPOK(launch_rs_rows(dt, a, (int)c->n, 1, c->stream));
-    c->loss_groups = c->n;
-    if ((rc = history(c, nh - 1, c->xbar[xb], want_cons, want_obj, c->n))) return rc;
+    HIPOK(launch_rs_hist(a, (int)c->n, c->hraw + 3 * (nh - 1), c->stream));
   }
   if (nh_out) *nh_out = nh;
   return finish_run(c, nh, T, lam_obj, f_opt, want_obj ? obj_out : nullptr, want_cons ? cons_out : nullptr,
