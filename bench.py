@@ -494,7 +494,9 @@ def main():
                    "halo_rows_per_gpu": int(plan.n_halo),
                    "parallelism": (f"dp{world}: one graph of {n_global} workers, "
                                    f"{'graph-partitioned' if args.config == 'c3' and args.partition == 'spectral' else 'contiguous'} "
-                                   f"slices per GPU, halo send/recv + all-reduce ({args.backend})") if world > 1
+                                   f"slices per GPU, "
+                                   f"{'all-reduce of the column sums' if mean is not None else 'halo send/recv + all-reduce'}"
+                                   f" ({args.backend})") if world > 1
                                   else ("single GPU: the multi-GPU phase path (lagged schedule, "
                                         f"{args.backend} world 1)") if args.phase
                                   else "single GPU: fused round kernel, one launch per round"},

@@ -97,13 +97,14 @@ struct FoldArgs {
   double* out_q;
 };
 
-// Row-space rounds (rowspace.hip): complete graph (uniform W_ii), quadratic objective, full
+// Row-space rounds (rowspace.hip): complete graph (uniform W_ii), either objective, full
 // shards of 1..kRsMaxRows rows, iterates that start equal.  x_i = Z + X_i^T beta_i.
 constexpr int kRsMaxRows = 64;  // rows per worker (one lane each in k_rs_rows; Gram pairs in k_rs_gram)
 struct RsArgs {
   const void* X;           // [rows x ld] T shard rows
   const void* y;           // [rows] T labels / targets
   int32_t y_is_f32;
+  int32_t problem;         // 0 logistic, 1 quadratic
   const int64_t* off;      // [n+1] first row of every worker
   int64_t rows;            // all rows (upart stride)
   int64_t ld;              // row stride in elements

@@ -1,11 +1,12 @@
-// rowspace.hip -- row-space D-SGD rounds for the complete graph with the quadratic objective
-// (config C5: N = 1024 workers, d = 2^20, m = b = 16).
+// rowspace.hip -- row-space D-SGD rounds for the complete graph (config C5: quadratic, N = 1024
+// workers, d = 2^20, m = b = 16; the logistic objective works the same way).
 //
 // The reference round (trainer.py:173-175, obj_problems.py:46-53) with the complete-graph MH
 // matrix (w_off off the diagonal, W_ii on it, the same for every worker) is
 //   x_i' = w_off S + (W_ii - w_off) x_i - eta (X_i^T r_i / m_i + mu x_i),   r_ik = x_i . X_ik - y_ik
 //        = a1 xbar + q x_i - eta X_i^T (r_i / m_i),      a1 = w_off N, q = W_ii - w_off - eta mu.
-// Every term but q x_i lies in span{xbar} + rowspace(X_i), so iterates that start equal
+// (logistic, obj_problems.py:13-20: r_ik -> c(z_ik) = -y_ik expit(-y_ik z_ik), still one weight per
+// row.)  Every term but q x_i lies in span{xbar} + rowspace(X_i), so iterates that start equal
 // (Worker.x = zeros, worker.py:13) stay of the form
 //   x_i = Z + X_i^T beta_i       (Z shared: Z' = a1 xbar + q Z;  beta_i' = q beta_i - eta r_i / m_i)
 // and the row dots follow without touching x_i:
@@ -194,12 +195,14 @@ __global__ __launch_bounds__(NT) void k_rs_rows(const RsArgs a, int mode) {
     for (int q = 0; q < slices; ++q) u += ured[q][lane];
   const double yv = live ? (a.y_is_f32 ? (double)((const float*)a.y)[row0 + lane] : ((const double*)a.y)[row0 + lane])
                          : 0.0;
+  // the gradient's row weight c(z) (obj_problems.py:16-17 logistic / :49-50 quadratic), / m_i
+  auto weight = [&](double z) { return (a.problem == 0 ? -yv / (1.0 + exp(yv * z)) : z - yv) / (double)m; };
   if (mode & 4) {  // initial state of iterates that all equal xbar: z = v = X . xbar, beta = 0
     if (live) {
       a.z[s0 + lane] = u;
       a.v[s0 + lane] = u;
       a.beta[s0 + lane] = 0.0;
-      a.coef_row[row0 + lane] = (u - yv) / (double)m;
+      a.coef_row[row0 + lane] = weight(u);
     }
     return;
   }
@@ -216,8 +219,7 @@ __global__ __launch_bounds__(NT) void k_rs_rows(const RsArgs a, int mode) {
     }
   }
   if (mode & 1) {
-    const double e = u - yv;
-    const double ls = wave_sum(live ? e * e : 0.0);
+    const double ls = wave_sum(live ? (a.problem == 0 ? row_loss<double, 0>(yv, u) : row_loss<double, 1>(yv, u)) : 0.0);
     const double cs = wave_sum(live ? bk * (2.0 * (vv - u) + gb) : 0.0);
     if (lane == 0) {
       if (a.slab_loss) a.slab_loss[i] = ls;
@@ -229,7 +231,7 @@ __global__ __launch_bounds__(NT) void k_rs_rows(const RsArgs a, int mode) {
     a.z[s0 + lane] = zn;
     a.v[s0 + lane] = a.a1 * u + a.q * vv;
     a.beta[s0 + lane] = a.q * bk - a.eta * sr[lane];
-    a.coef_row[row0 + lane] = (zn - yv) / (double)m;
+    a.coef_row[row0 + lane] = weight(zn);
   }
 }
 

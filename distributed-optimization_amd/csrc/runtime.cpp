@@ -724,7 +724,7 @@ int run_centralized_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64
 }
 
 // ---------------------------------------------------------------------------- row-space rounds
-// (rowspace.hip).  Complete graph with one W_ii, quadratic objective, full-shard batches of
+// (rowspace.hip).  Complete graph with one W_ii, either objective, full-shard batches of
 // 1..kRsMaxRows rows, one context (no rank slices), iterates that start equal: then
 // x_i = Z + X_i^T beta_i for the whole run and a round is one read-only pass over the rows.
 // DOPT_ROWSPACE=0 keeps the direct column-blocked rounds (A/B runs, tests).
@@ -734,8 +734,7 @@ bool rs_enabled() {
 }
 
 bool rs_eligible(dopt_ctx* c, int64_t batch, const int32_t* idx) {
-  return rs_enabled() && c->split && c->mean_mix && c->wdiag_uniform && c->problem == DOPT_QUADRATIC &&
-         !idx && batch >= c->max_m && !c->obj_sep && c->min_m >= 1 && c->max_m <= kRsMaxRows &&
+  return rs_enabled() && c->split && c->mean_mix && c->wdiag_uniform && !idx && batch >= c->max_m && !c->obj_sep && c->min_m >= 1 && c->max_m <= kRsMaxRows &&
          c->n_global == 0 && !c->S_ext && c->xdtype == c->dtype;
 }
 
@@ -745,6 +744,7 @@ RsArgs rs_args(dopt_ctx* c) {
   a.X = c->X;
   a.y = c->y;
   a.y_is_f32 = c->xdtype == DOPT_F32;
+  a.problem = c->problem == DOPT_LOGISTIC ? 0 : 1;
   a.off = c->off;
   a.rows = c->rows;
   a.ld = c->ld;
@@ -2034,8 +2034,7 @@ int dopt_rs_phase_begin(dopt_ctx* c, int commit, int* ok, double* sig) {
   if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
   *ok = 0;
   *sig = 0.0;
-  if (!(rs_enabled() && c->split && c->mean_mix && c->wdiag_uniform && c->problem == DOPT_QUADRATIC &&
-        !c->obj_sep && c->min_m >= 1 && c->max_m <= kRsMaxRows && c->xdtype == c->dtype))
+  if (!(rs_enabled() && c->split && c->mean_mix && c->wdiag_uniform && !c->obj_sep && c->min_m >= 1 && c->max_m <= kRsMaxRows && c->xdtype == c->dtype))
     return DOPT_OK;
   int rc;
   if ((rc = set_device(c))) return rc;

@@ -34,6 +34,7 @@ def _engine(shards, problem, dtype="float64"):
     ("quadratic", "fully_connected", 12, True, 12, "0"),  # complete graph through column sums
     ("quadratic", "fully_connected", 12, True, 12, "1"),  # ... in row space (rowspace.hip)
     ("quadratic", "fully_connected", 5, True, 12, "1"),   # minibatches: direct rounds
+    ("logistic", "fully_connected", 12, True, 12, "1"),   # logistic in row space
     ("quadratic", "grid", 4, False, 12, "1"),
     ("logistic", "ring", 24, False, 24, "1"),        # > 16 rows per worker: the row-split step kernel
 ])

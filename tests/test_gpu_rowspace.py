@@ -13,47 +13,50 @@ import topology as TP
 pytestmark = pytest.mark.gpu
 
 
-def _data(sizes, d, seed):
+def _data(sizes, d, seed, problem="quadratic"):
     rng = np.random.default_rng(seed)
     shards = []
     for m in sizes:
         X = np.hstack([rng.standard_normal((m, d - 1)), np.ones((m, 1))])
-        y = rng.standard_normal(m) * 3
+        y = rng.standard_normal(m) * 3 if problem == "quadratic" else rng.choice([-1.0, 1.0], m)
         shards.append((X, y))
     return shards
 
 
-def _engine(shards, dtype="float64"):
+def _engine(shards, dtype="float64", problem="quadratic"):
     eng = _dopt.Engine(0, dtype)
     off = np.concatenate([[0], np.cumsum([len(s[1]) for s in shards])])
-    eng.load_shards("quadratic", np.vstack([s[0] for s in shards]), np.concatenate([s[1] for s in shards]), off)
+    eng.load_shards(problem, np.vstack([s[0] for s in shards]), np.concatenate([s[1] for s in shards]), off)
     n = len(shards)
     eng.set_mixing_mean(*TP.fully_connected(n).uniform_offdiag())
     return eng
 
 
-def _cfg(b):
-    return {"problem_type": "quadratic", "local_batch_size": b, "learning_rate_eta0": 0.05,
+def _cfg(b, problem="quadratic"):
+    return {"problem_type": problem, "local_batch_size": b, "learning_rate_eta0": 0.05,
             "l2_regularization_lambda": 1e-3, "strong_convexity_mu": 2e-3}
 
 
+@pytest.mark.parametrize("problem", ["quadratic", "logistic"])
 @pytest.mark.parametrize("start", ["zero", "common"])
 @pytest.mark.parametrize("sizes", [[12] * 9, [16, 3, 9, 16, 1, 7, 12, 16, 5, 11, 2]])
-def test_rowspace_vs_oracle(start, sizes):
+def test_rowspace_vs_oracle(start, sizes, problem):
     n, d, T = len(sizes), 2100, 8  # d = 2100 float64: column-blocked rows
-    shards = _data(sizes, d, 3)
-    eng = _engine(shards)
+    shards = _data(sizes, d, 3, problem)
+    eng = _engine(shards, problem=problem)
     x0 = np.zeros((n, d))
     if start == "common":
         x0[:] = np.random.default_rng(9).standard_normal(d) * 0.05
         eng.set_models(x0)
     b = max(sizes)
-    obj, cons, _ = eng.run_dsgd(T, 0.05, b, 2e-3, 1e-3, 0.1)
+    lam_g = 2e-3 if problem == "quadratic" else 1e-3  # worker.py:36-42
+    obj, cons, _ = eng.run_dsgd(T, 0.05, b, lam_g, 1e-3, 0.1)
     assert _dopt.last_round_kernel().startswith("void dopt::k_rs_pass<double, true,")
     x = eng.get_models()
     Xf = np.vstack([s[0] for s in shards])
     yf = np.concatenate([s[1] for s in shards])
-    h, _, xr, _ = O.run_decentralized(shards, TP.fully_connected(n).dense_W(), T, _cfg(b), Xf, yf, 0.1, x0=x0)
+    h, _, xr, _ = O.run_decentralized(shards, TP.fully_connected(n).dense_W(), T, _cfg(b, problem), Xf, yf, 0.1,
+                                      x0=x0)
     np.testing.assert_allclose(obj, h["objective"], rtol=1e-9)
     np.testing.assert_allclose(cons, h["consensus_error"], rtol=1e-9)
     np.testing.assert_allclose(x, xr, rtol=1e-9, atol=1e-12 * np.abs(xr).max())
