@@ -817,10 +817,12 @@ int rs_sync(dopt_ctx* c) {
   return DOPT_OK;
 }
 
-// Leave row-space mode: xs[cur] holds the iterates, xbar[xb] their average.
+// Leave row-space mode: xs[cur] holds the iterates, xbar[xb] their average.  An owed metrics
+// entry of a row-space chain is dropped (the direct rounds carry other state).
 int rs_end(dopt_ctx* c) {
   int rc;
   if ((rc = rs_sync(c))) return rc;
+  if (c->rs_live) c->carry_pending = false;
   c->rs_live = false;
   return DOPT_OK;
 }
