@@ -44,6 +44,8 @@ from obj_problems import logistic_objective, quadratic_objective
 
 DENSE_LIMIT = 4096          # dense adj / W attributes up to this many workers
 MEAN_MIX_MIN = 128          # complete graphs from this size mix through the column sums
+ROW_RESIDENT_MAX = 2048     # longer float64 rows take the column-blocked rounds (complete graphs: the
+                            # row-space rounds, DESIGN.md 6c, which mix through the column sums)
 IDX_CHUNK_ELEMS = 1 << 24   # host index buffer per device call (64 MiB of int32)
 IDX_CHUNK_ROUNDS = 512      # rounds per device call when indices are drawn (the next chunk's draw
                             # runs on a host thread while the device runs this one)
@@ -562,7 +564,7 @@ class DecentralizedTrainer:
         eng = _engine(self.workers, self.n_features, cfg, X_full=X_full, y_full=y_full)
         want_obj = _set_objective_data(eng, self.workers, self.n_features, X_full, y_full)
         t = self._topo
-        uni = t.uniform_offdiag() if self.n_workers >= cfg.get("mean_mixing_min", MEAN_MIX_MIN) else None
+        uni = t.uniform_offdiag() if self._mean_mixing() else None
         if uni is not None:  # complete graph: w_off (S - x_i) + W_ii x_i, no N^2 neighbour reads
             eng.set_mixing_mean(*uni)
         else:
@@ -604,13 +606,19 @@ class DecentralizedTrainer:
         final_avg_model = np.mean([worker.x for worker in self.workers], axis=0)
         return self.history, final_avg_model
 
+    def _mean_mixing(self):
+        """Complete graphs mix through the column sums from MEAN_MIX_MIN workers on, and at any
+        size when the rows are longer than the row-resident kernel holds."""
+        return (self.n_workers >= self.config.get("mean_mixing_min", MEAN_MIX_MIN) or
+                self.n_features > ROW_RESIDENT_MAX)
+
     def _run_distributed(self, info, T, X_full, y_full, f_opt, lam_grad, reg_param, start_time):
         import distributed
 
         rank, world, _ = info
         cfg = self.config
         t = self._topo
-        uni = t.uniform_offdiag() if self.n_workers >= cfg.get("mean_mixing_min", MEAN_MIX_MIN) else None
+        uni = t.uniform_offdiag() if self._mean_mixing() else None
         plan = distributed.build_plan(t, world, rank)
         eng = _engine(self.workers, self.n_features, cfg, plan.lo, plan.hi, X_full=X_full, y_full=y_full)
         want_obj, rows_global, sep = _dist_objective(eng, self.workers, self.n_features, X_full, y_full, rank, world)

@@ -216,3 +216,31 @@ def test_rowspace_ranks_vs_oracle(tmp_path, world):
     np.testing.assert_allclose(got["obj"], h["objective"], rtol=1e-9)
     np.testing.assert_allclose(got["cons"], h["consensus_error"], rtol=1e-9)
     np.testing.assert_allclose(got["x"], xr, rtol=1e-9, atol=1e-12 * np.abs(xr).max())
+
+
+@pytest.mark.parametrize("problem", ["quadratic", "logistic"])
+def test_trainer_complete_graph_long_rows_vs_oracle(problem):
+    """The drop-in DecentralizedTrainer('fully_connected') with rows beyond the row-resident
+    kernel: few workers mix through the column sums too, so the run takes the row-space rounds;
+    history, final average and the RNG stream position vs the oracle (float64, rtol 1e-9)."""
+    from trainer import DecentralizedTrainer
+    from worker import Worker
+
+    sizes, d, T = [12] * 7, 2100, 6
+    shards = _data(sizes, d, 21, problem)
+    cfg = _cfg(12, problem)
+    ws = [Worker(i, {"X": X, "y": y}, cfg["local_batch_size"], d, cfg) for i, (X, y) in enumerate(shards)]
+    tr = DecentralizedTrainer(ws, "fully_connected", d, cfg)
+    Xf = np.vstack([s[0] for s in shards])
+    yf = np.concatenate([s[1] for s in shards])
+    np.random.seed(11)
+    st = np.random.get_state()
+    hist, xavg = tr.run(T, Xf, yf, 0.2)
+    assert "k_rs_pass<double, true" in _dopt.last_round_kernel()
+    pos = np.random.get_state()
+    h, xr_avg, _, st_after = O.run_decentralized(shards, TP.fully_connected(len(sizes)).dense_W(), T, cfg, Xf, yf,
+                                                 0.2, rng_state=st)
+    np.testing.assert_allclose(hist["objective"], h["objective"], rtol=1e-9)
+    np.testing.assert_allclose(hist["consensus_error"], h["consensus_error"], rtol=1e-9)
+    np.testing.assert_allclose(xavg, xr_avg, rtol=1e-9, atol=1e-12 * np.abs(xr_avg).max())
+    assert pos[2] == st_after[2] and np.array_equal(pos[1], st_after[1])
