@@ -419,7 +419,8 @@ def main():
                 "allreduce_bytes_per_round": ld * 8}
         log(f"comm: {comm}")
 
-        if runner._lagged_ok:  # the lagged schedule continued across calls (as on one GPU: timed_leg)
+        if runner._lagged_ok or (mean is not None and runner._rowspace_ready()):
+            # the lagged schedule / the row-space rounds continued across calls (as on one GPU: timed_leg)
             def rounds(k):
                 return runner.run_pipelined(k, eta0, b, lam, lam, 0.0)
 

@@ -2040,11 +2040,11 @@ int dopt_rs_phase_begin(dopt_ctx* c, int commit, int* ok, double* sig) {
     return DOPT_OK;
   int rc;
   if ((rc = set_device(c))) return rc;
-  c->carry_pending = false;
-  if (c->rs_live) {
+  if (c->rs_live) {  // (an open chain -- dopt_phase_chain -- stays open)
     *ok = 1;
     return DOPT_OK;
   }
+  c->carry_pending = false;
   if ((rc = ensure_rs(c))) return rc;
   const int dt = c->dtype == DOPT_F32 ? 0 : 1;
   const int G = kRsCheckGroups;

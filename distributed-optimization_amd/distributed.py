@@ -362,36 +362,53 @@ class DistributedDSGD:
         ok_all, lo, hi = float(v[0]), float(v[1]), -float(v[2])
         return ok_all == 1.0 and lo == hi
 
-    def _run_rowspace(self, T, eta0, lam_grad, lam_obj, f_opt, t0, objective, consensus):
-        """Complete graph, quadratic: the iterates stay Z + X_i^T beta_i.  Per round
-        one read-only pass over this rank's rows (row state, metric partials of the current
-        iterates, local column sums), the all-reduce of the d column sums, the replicated
-        average / Z update; history[h] = metrics of x_{h+1} from the next pass (the last from a
-        dots pass).  The iterates are formed when asked for (gather_models)."""
+    def _run_rowspace(self, T, eta0, lam_grad, lam_obj, f_opt, t0, objective, consensus, pipelined=False):
+        """Complete graph: the iterates stay Z + X_i^T beta_i.  Per round one
+        read-only pass over this rank's rows (row state, metric partials of the current iterates,
+        local column sums), the all-reduce of the d column sums, the replicated average / Z
+        update; history[h] = metrics of x_{h+1} from the next pass (the last from a dots pass).
+        pipelined: the last metrics stay owed and the next pipelined call's first pass takes
+        them (T = 0: a dots pass for them), as Engine.run_dsgd_pipelined on one context.  The
+        iterates are formed when asked for (gather_models)."""
         torch, eng = self.torch, self.eng
         xnorm = self.plan.rank == 0
         mf = (_dopt.RUN_OBJECTIVE if objective else 0) | (_dopt.RUN_CONSENSUS if consensus else 0)
-        eng.rs_phase_begin(True)
+        was_open = eng.phase_chain(False)  # any call ends an open chain; a pipelined one continues it
+        owed = pipelined and was_open and getattr(self, "_rs_flags", None) == mf
+        leave = pipelined and T > 0 and mf != 0
+        n_out = (T + (1 if owed else 0) - (1 if leave else 0)) if mf else 0
+        if not owed:
+            if T == 0:
+                return (np.zeros(0) if objective else None), (np.zeros(0) if consensus else None)
+            eng.rs_phase_begin(True)
         with torch.cuda.stream(self.stream):
-            partials = torch.zeros((T, 3), dtype=torch.float64, device=self.dev)
+            partials = torch.zeros((max(1, n_out), 3), dtype=torch.float64, device=self.dev)
+            e = 0
 
-            def fold(h):
-                base = partials.data_ptr() + 3 * h * 8
+            def fold(k):
+                base = partials.data_ptr() + 3 * k * 8
                 eng.phase_fold(base if consensus else None, base + 16 if objective and xnorm else None,
                                base + 8 if objective else None, 0)
 
             for h in range(T):
-                eng.rs_phase_round(t0 + h, eta0, lam_grad, mf if h > 0 else 0, self.sum.data_ptr())
-                if h > 0 and mf:
-                    fold(h - 1)
+                met = mf and (h > 0 or owed)
+                eng.rs_phase_round(t0 + h, eta0, lam_grad, mf if met else 0, self.sum.data_ptr())
+                if met:
+                    fold(e)
+                    e += 1
                 self._all_reduce(self.sum)
                 eng.rs_phase_cols(t0 + h, eta0, lam_grad, self.sum.data_ptr())
-            if mf:
+            if mf and not leave:
                 eng.rs_phase_metrics(mf)
-                fold(T - 1)
-            self._all_reduce(partials)
-            raw = partials.cpu().numpy()
+                fold(e)
+                e += 1
+            assert e == n_out
+            self._all_reduce(partials[:n_out])
+            raw = partials[:n_out].cpu().numpy()
         self.stream.synchronize()
+        if leave:
+            eng.phase_chain(True)
+            self._rs_flags = mf
         obj, cons = _dopt.finalize_metrics(self.eng.problem, raw, self.n_global, self.rows_global, lam_obj, f_opt)
         return (obj if objective else None), (cons if consensus else None)
 
@@ -408,8 +425,12 @@ class DistributedDSGD:
         rows = self.eng.shard_rows
         bip = (idx is not None and not self.obj_sep and rows is not None and len(rows) > 0 and
                batch < int(rows.max()) <= _dopt.MAX_BIP_ROWS and os.environ.get("DOPT_BIP", "1") != "0")
+        if (self.mean is not None and idx is None and not self.obj_sep and (objective or consensus) and
+                self._rowspace_ready()):  # complete graph: row-space rounds continued across calls
+            return self._run_rowspace(T, eta0, lam_grad, lam_obj, f_opt, t0, objective, consensus, pipelined=True)
         if not ((idx is None and not self.obj_sep) or bip) or not (objective or consensus) or not self._lagged_ok:
-            raise NotImplementedError("pipelined runs: the lagged schedule only (CSR mixing, fused metrics)")
+            raise NotImplementedError("pipelined runs: the lagged schedule (CSR mixing, fused metrics) or the "
+                                      "row-space rounds (complete graph, equal iterates)")
         return self._run_lagged(T, eta0, batch, lam_grad, lam_obj, f_opt, t0, objective, consensus, idx,
                                 pipelined=True)
 

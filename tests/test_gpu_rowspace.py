@@ -157,7 +157,7 @@ def test_rowspace_then_other_run_kinds():
 SIZES_D = [12, 7, 12, 3, 12, 12, 9, 12, 1, 12, 12, 5, 12]  # ragged shards over the ranks' slices
 
 
-def _rs_rank(rank, world, port, out, T):
+def _rs_rank(rank, world, port, out, T, pipe=False):
     import os
 
     import torch  # noqa: F401  (one HIP runtime, loaded before libdopt)
@@ -179,9 +179,17 @@ def _rs_rank(rank, world, port, out, T):
     eng.load_shards("quadratic", np.vstack([s[0] for s in mine]), np.concatenate([s[1] for s in mine]), off)
     w_off, diag = TP.fully_connected(n).uniform_offdiag()
     run = Dm.DistributedDSGD(eng, plan, n, sum(SIZES_D), device=0, mean=(w_off, diag[lo:hi]))
-    o1, c1 = run.run(3, 0.05, max(SIZES_D), 2e-3, 1e-3, 0.1)
+    b = max(SIZES_D)
+    o1, c1 = run.run(3, 0.05, b, 2e-3, 1e-3, 0.1)
     kern = _dopt.last_round_kernel()
-    o2, c2 = run.run(T - 3, 0.05, max(SIZES_D), 2e-3, 1e-3, 0.1, t0=3)  # continues the live state
+    if pipe:  # a chain of pipelined calls from the live state (owed metrics ride the next pass)
+        parts, t = [], 3
+        for k in (2, 1, T - 6, 0):
+            parts.append(run.run_pipelined(k, 0.05, b, 2e-3, 1e-3, 0.1, t0=t))
+            t += k
+        o2, c2 = np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts])
+    else:
+        o2, c2 = run.run(T - 3, 0.05, b, 2e-3, 1e-3, 0.1, t0=3)  # continues the live state
     x = run.gather_models()
     if rank == 0:
         np.savez(os.path.join(out, "rs.npz"), obj=np.concatenate([o1, o2]), cons=np.concatenate([c1, c2]), x=x,
@@ -191,11 +199,11 @@ def _rs_rank(rank, world, port, out, T):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_rowspace_ranks_vs_oracle(tmp_path, world):
+@pytest.mark.parametrize("world,pipe", [(2, False), (3, False), (2, True)])
+def test_rowspace_ranks_vs_oracle(tmp_path, world, pipe):
     """Row-space rounds across ranks (gloo, contexts sharing the GPU): each rank's pass gives its
     column sums, all-reduced into the replicated average; history and gathered iterates vs the
-    oracle at rtol 1e-9 (float64)."""
+    oracle at rtol 1e-9 (float64); pipe: the later rounds as a chain of pipelined calls."""
     import socket
 
     import torch.multiprocessing as mp
@@ -205,7 +213,8 @@ def test_rowspace_ranks_vs_oracle(tmp_path, world):
     port = s.getsockname()[1]
     s.close()
     T = 7
-    mp.start_processes(_rs_rank, args=(world, port, str(tmp_path), T), nprocs=world, join=True, start_method="spawn")
+    mp.start_processes(_rs_rank, args=(world, port, str(tmp_path), T, pipe), nprocs=world, join=True,
+                       start_method="spawn")
     got = np.load(tmp_path / "rs.npz")
     assert "k_rs_pass<double, true" in str(got["kern"])
     shards = _data(SIZES_D, 2100, 12)
