@@ -47,6 +47,17 @@ def main():
                 eng.phase_grad(m, 1e-4, flags)
         return f
 
+    ld, _ = eng.layout()
+    sums = torch.zeros(ld, dtype=torch.float64, device="cuda")
+
+    def sched():  # the lagged phase schedule at world 1: colsum (+ fold) -> grad (+ loss) -> mix
+        eng.phase_begin(m)
+        eng.phase_gather()
+        for h in range(K):
+            eng.phase_colsum_fold(sums.data_ptr())
+            eng.phase_grad(m, 1e-4, _dopt.RUN_OBJECTIVE if h >= 2 else 0)
+            eng.phase_mix_lagged(h, 0.05, sums.data_ptr(), True)
+
     for rep in range(3):
         eng.set_models(np.zeros((n, d)))
         if own is None:
@@ -63,6 +74,8 @@ def main():
         eng.set_models(x_now)
         timed("grad/none", grad(0))
         timed("grad/both", grad(_dopt.RUN_OBJECTIVE | _dopt.RUN_CONSENSUS))
+        with torch.cuda.stream(ts):
+            timed("sched", sched)
         eng.set_stream(0)
     for k, v in res.items():
         print(k, "best %.4f median %.4f" % (min(v), sorted(v)[len(v) // 2]))
