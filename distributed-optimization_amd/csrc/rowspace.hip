@@ -64,11 +64,30 @@ __global__ __launch_bounds__(NT) void k_rs_pass(const RsArgs a) {
     cc[j] = in ? c : nch - 1;  // lanes past the row re-read its last chunk (xbar is 0 there)
     xb[j] = in ? *(const V*)((const T*)a.xbar + (int64_t)c * VN) : V(0);
   }
+  // column sums: T products accumulated over each 64-row window in T, flushed into float64 (a
+  // float32 context trades the per-element float64 convert + FMA for one float FMA; float64
+  // contexts accumulate in float64 directly)
+  constexpr bool TACC = std::is_same<T, float>::value;
   double acc[CB][VN];
+  T acct[TACC ? CB : 1][VN];
 #pragma unroll
   for (int j = 0; j < CB; ++j)
 #pragma unroll
-    for (int e = 0; e < VN; ++e) acc[j][e] = 0.0;
+    for (int e = 0; e < VN; ++e) {
+      acc[j][e] = 0.0;
+      if constexpr (TACC) acct[j][e] = T(0);
+    }
+  auto flush = [&]() {
+    if constexpr (TACC) {
+#pragma unroll
+      for (int j = 0; j < CB; ++j)
+#pragma unroll
+        for (int e = 0; e < VN; ++e) {
+          acc[j][e] += (double)acct[j][e];
+          acct[j][e] = T(0);
+        }
+    }
+  };
   // partial dots: T (a float32 context's 256-1024-element partial dots keep float precision;
   // half the bytes of this launch's only large writes)
   T* __restrict__ up = (T*)a.upart + (int64_t)blk * a.rows;
@@ -91,11 +110,20 @@ __global__ __launch_bounds__(NT) void k_rs_pass(const RsArgs a) {
     const int k = (int)((r - wr0) & 63);
     if constexpr (COLS) {
       const double cf = readlane_t(cw_cur, k);  // wave-uniform
+      if constexpr (TACC) {
+        const T cft = (T)cf;
 #pragma unroll
-      for (int j = 0; j < CB; ++j)
+        for (int j = 0; j < CB; ++j)
 #pragma unroll
-        for (int e = 0; e < VN; ++e) acc[j][e] += cf * (double)rv[j][e];
+          for (int e = 0; e < VN; ++e) acct[j][e] += cft * rv[j][e];
+      } else {
+#pragma unroll
+        for (int j = 0; j < CB; ++j)
+#pragma unroll
+          for (int e = 0; e < VN; ++e) acc[j][e] += cf * (double)rv[j][e];
+      }
       if (k == 63) {  // next window
+        flush();
         cw_cur = cw_nxt;
         cw_nxt = cwin_load(r + 65);
       }
@@ -123,6 +151,7 @@ __global__ __launch_bounds__(NT) void k_rs_pass(const RsArgs a) {
       if (r + k < wr1) process(buf[k], r + k);
   }
   if constexpr (COLS) {
+    flush();
 #pragma unroll
     for (int j = 0; j < CB; ++j)
 #pragma unroll
