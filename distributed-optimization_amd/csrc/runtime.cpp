@@ -829,8 +829,9 @@ int rs_end(dopt_ctx* c) {
 
 enum { RS_FALLBACK = 1 };
 
-// Start row-space mode from xs[cur]: RS_FALLBACK when the iterates are not all equal.
-int rs_begin(dopt_ctx* c) {
+// Are the iterates xs[cur] all equal (*equal), and is that iterate zero (*zero)?  With sig != null
+// also a checksum of the first iterate (multi-rank callers compare it across ranks).
+int rs_check(dopt_ctx* c, bool* equal, bool* zero, double* sig) {
   int rc;
   if ((rc = ensure_rs(c))) return rc;
   const int dt = c->dtype == DOPT_F32 ? 0 : 1;
@@ -839,12 +840,41 @@ int rs_begin(dopt_ctx* c) {
                         c->stream));
   std::vector<int32_t> fl((size_t)(c->n + 1) * G);
   HIPOK(hipMemcpyAsync(fl.data(), c->rs_flags, fl.size() * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  std::vector<char> row(sig ? (size_t)c->ld * c->esz : 0);
+  if (sig) HIPOK(hipMemcpyAsync(row.data(), c->xs[c->cur], row.size(), hipMemcpyDeviceToHost, c->stream));
   HIPOK(hipStreamSynchronize(c->stream));
+  *equal = true;
+  *zero = true;
   for (int64_t k = 0; k < c->n * G; ++k)
-    if (fl[(size_t)k]) return RS_FALLBACK;
-  bool zero = true;
+    if (fl[(size_t)k]) *equal = false;
   for (int g = 0; g < G; ++g)
-    if (fl[(size_t)(c->n * G + g)]) zero = false;
+    if (fl[(size_t)(c->n * G + g)]) *zero = false;
+  if (sig) {
+    double s = 0.0;
+    for (int64_t k = 0; k < c->d; ++k)
+      s += (double)(k % 1021 + 1) *
+           (c->esz == 4 ? (double)((const float*)row.data())[k] : ((const double*)row.data())[k]);
+    *sig = s;
+  }
+  return DOPT_OK;
+}
+
+// Round t's scalars: a1 = w_off N, q = W_ii - w_off - eta lam, eta, eta / N (N: all ranks' workers).
+void rs_round_args(dopt_ctx* c, RsArgs& a, int64_t t, double eta0, double lam_grad) {
+  const double N = (double)n_div(c), eta = eta0 / sqrt((double)(t + 1));  // trainer.py:138-140
+  a.a1 = c->w_off * N;
+  a.q = c->wdiag_u - c->w_off - eta * lam_grad;
+  a.eta = eta;
+  a.eta_n = eta / N;
+}
+
+// Start row-space mode from xs[cur]: RS_FALLBACK when the iterates are not all equal.
+int rs_begin(dopt_ctx* c) {
+  int rc;
+  bool equal = false, zero = false;
+  if ((rc = rs_check(c, &equal, &zero, nullptr))) return rc;
+  if (!equal) return RS_FALLBACK;
+  const int dt = c->dtype == DOPT_F32 ? 0 : 1;
   RsArgs a = rs_args(c);
   if (!c->rs_gram_ok) {
     const int64_t P = c->rs_bcap * (c->rs_bcap + 1) / 2;
@@ -886,17 +916,11 @@ int run_dsgd_rs(dopt_ctx* c, int64_t t0, int64_t T, double eta0, double lam_grad
   const int dt = c->dtype == DOPT_F32 ? 0 : 1;
   const int64_t lag = carry_in ? 1 : 0;
   int& xb = c->xb;
-  const double N = (double)n_div(c);
   HIPOK(launch_stamp(c->stamps, c->stream));
   for (int64_t h = 0; h < T; ++h) {
-    const int64_t t = t0 + h;
-    const double eta = eta0 / sqrt((double)(t + 1));  // trainer.py:138-140
     RsArgs a = rs_args(c);
+    rs_round_args(c, a, t0 + h, eta0, lam_grad);
     a.xbar = c->xbar[xb];
-    a.a1 = c->w_off * N;
-    a.q = c->wdiag_u - c->w_off - eta * lam_grad;
-    a.eta = eta;
-    a.eta_n = eta / N;
     const bool met = metrics && (h > 0 || lag);
     a.slab_cons = want_cons ? c->slab_cons : nullptr;
     a.slab_loss = want_obj ? c->slab_loss : nullptr;
@@ -2036,7 +2060,8 @@ int dopt_rs_phase_begin(dopt_ctx* c, int commit, int* ok, double* sig) {
   if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
   *ok = 0;
   *sig = 0.0;
-  if (!(rs_enabled() && c->split && c->mean_mix && c->wdiag_uniform && !c->obj_sep && c->min_m >= 1 && c->max_m <= kRsMaxRows && c->xdtype == c->dtype))
+  if (!(rs_enabled() && c->split && c->mean_mix && c->wdiag_uniform && !c->obj_sep && c->min_m >= 1 &&
+        c->max_m <= kRsMaxRows && c->xdtype == c->dtype))
     return DOPT_OK;
   int rc;
   if ((rc = set_device(c))) return rc;
@@ -2045,23 +2070,9 @@ int dopt_rs_phase_begin(dopt_ctx* c, int commit, int* ok, double* sig) {
     return DOPT_OK;
   }
   c->carry_pending = false;
-  if ((rc = ensure_rs(c))) return rc;
-  const int dt = c->dtype == DOPT_F32 ? 0 : 1;
-  const int G = kRsCheckGroups;
-  HIPOK(launch_rs_check(dt, c->xs[c->cur], c->n, c->ld, (int32_t)c->nch, G, c->rs_flags, c->rs_flags + c->n * G,
-                        c->stream));
-  std::vector<int32_t> fl((size_t)(c->n + 1) * G);
-  HIPOK(hipMemcpyAsync(fl.data(), c->rs_flags, fl.size() * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-  const size_t esz = c->esz;
-  std::vector<char> raw((size_t)c->ld * esz);
-  HIPOK(hipMemcpyAsync(raw.data(), c->xs[c->cur], raw.size(), hipMemcpyDeviceToHost, c->stream));
-  HIPOK(hipStreamSynchronize(c->stream));
-  for (int64_t k = 0; k < c->n * G; ++k)
-    if (fl[(size_t)k]) return DOPT_OK;
-  double s = 0.0;  // signature of the common iterate (the caller compares it across ranks)
-  for (int64_t k = 0; k < c->d; ++k)
-    s += (double)(k % 1021 + 1) * (esz == 4 ? (double)((const float*)raw.data())[k] : ((const double*)raw.data())[k]);
-  *sig = s;
+  bool equal = false, zero = false;
+  if ((rc = rs_check(c, &equal, &zero, sig))) return rc;
+  if (!equal) return DOPT_OK;
   *ok = 1;
   if (!commit) return DOPT_OK;
   return rs_begin(c) == RS_FALLBACK ? fail(DOPT_ERR_STATE, "row-space begin: iterates changed") : DOPT_OK;
@@ -2072,13 +2083,9 @@ int dopt_rs_phase_round(dopt_ctx* c, int64_t t, double eta0, double lam_grad, ui
   CHECK_ARG(c && sum_dev, "NULL argument");
   if (!c->rs_live) return fail(DOPT_ERR_STATE, "dopt_rs_phase_begin first");
   const int dt = c->dtype == DOPT_F32 ? 0 : 1;
-  const double N = (double)n_div(c), eta = eta0 / sqrt((double)(t + 1));  // trainer.py:138-140
   RsArgs a = rs_args(c);
+  rs_round_args(c, a, t, eta0, lam_grad);
   a.xbar = c->xbar[c->xb];
-  a.a1 = c->w_off * N;
-  a.q = c->wdiag_u - c->w_off - eta * lam_grad;
-  a.eta = eta;
-  a.eta_n = eta / N;
   const bool met = (metric_flags & (DOPT_RUN_OBJECTIVE | DOPT_RUN_CONSENSUS)) != 0;
   a.slab_cons = (metric_flags & DOPT_RUN_CONSENSUS) ? c->slab_cons : nullptr;
   a.slab_loss = (metric_flags & DOPT_RUN_OBJECTIVE) ? c->slab_loss : nullptr;
@@ -2098,12 +2105,8 @@ int dopt_rs_phase_cols(dopt_ctx* c, int64_t t, double eta0, double lam_grad, con
   CHECK_ARG(c && sum_dev, "NULL argument");
   if (!c->rs_live) return fail(DOPT_ERR_STATE, "dopt_rs_phase_begin first");
   const int dt = c->dtype == DOPT_F32 ? 0 : 1;
-  const double N = (double)n_div(c), eta = eta0 / sqrt((double)(t + 1));
   RsArgs a = rs_args(c);
-  a.a1 = c->w_off * N;
-  a.q = c->wdiag_u - c->w_off - eta * lam_grad;
-  a.eta = eta;
-  a.eta_n = eta / N;
+  rs_round_args(c, a, t, eta0, lam_grad);
   a.csum = sum_dev;
   a.xbar_out = c->xbar[c->xb ^ 1];
   HIPOK(launch_rs_cols(dt, a, c->stream));
