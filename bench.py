@@ -200,7 +200,7 @@ def timed_leg(eng, rounds, steps, warmup, n_models, d, barrier, event_every, flu
 
     if flush is None and warmup > 0:
         rounds(warmup)
-    eng.set_models(np.zeros((n_models, d)))
+    eng.zero_models()  # the reset iterate (Worker.x = zeros), on the device
     if flush is not None:
         rounds(max(3, warmup))  # the multi-GPU lagged schedule completes history[t] 3 rounds later
     eng.kernel_stats()  # reset the event window

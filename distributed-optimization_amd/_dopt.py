@@ -93,6 +93,7 @@ _SIGS = {
     "dopt_rs_phase_round": ([_P, _I64, _D, _D, ctypes.c_uint32, _P], ctypes.c_int),
     "dopt_rs_phase_cols": ([_P, _I64, _D, _D, _P], ctypes.c_int),
     "dopt_rs_phase_metrics": ([_P, ctypes.c_uint32], ctypes.c_int),
+    "dopt_zero_models": ([_P], ctypes.c_int),
     "dopt_sync": ([_P], ctypes.c_int),
     "dopt_finalize_metrics": ([ctypes.c_int, _I64, _P, _I64, _I64, _D, _D, _P, _P], ctypes.c_int),
     "dopt_eval_full": ([_P, _P, _D, _P, _P], ctypes.c_int),
@@ -290,6 +291,10 @@ class Engine:
     def set_models(self, x):
         x = np.ascontiguousarray(x, dtype=np.float64).reshape(self.n, self.d)
         check(lib().dopt_set_models(self._h, _ptr(x)))
+
+    def zero_models(self):
+        """Every iterate = 0 on the device (no host copy)."""
+        check(lib().dopt_zero_models(self._h))
 
     def get_models(self):
         x = np.empty((self.n, self.d), dtype=np.float64)

@@ -1274,6 +1274,16 @@ int dopt_set_models(dopt_ctx* c, const double* x) {
   return upload_rows(c, c->dtype, x, 0, c->xs[c->cur], c->n, c->d, c->ld);
 }
 
+int dopt_zero_models(dopt_ctx* c) {
+  if (c) c->send_fresh = c->carry_pending = c->rs_live = false;
+  CHECK_ARG(c, "ctx is NULL");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  HIPOK(hipMemsetAsync(c->xs[c->cur], 0, (size_t)c->n * c->ld * c->esz, c->stream));  // worker.py:13
+  return DOPT_OK;
+}
+
 int dopt_get_models(dopt_ctx* c, double* x) {
   CHECK_ARG(c && x, "NULL argument");
   if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");

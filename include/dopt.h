@@ -149,6 +149,8 @@ int dopt_set_mixing_mean(dopt_ctx *ctx, int64_t n_workers, double w_off, const d
 /* Worker iterates (Worker.x, worker.py:13; trainer.py:162-163, :178-179). */
 int dopt_set_models(dopt_ctx *ctx, const double *x);
 int dopt_get_models(dopt_ctx *ctx, double *x);
+/* Every iterate = 0 (Worker.x, worker.py:13), enqueued on the context's stream (no host copy). */
+int dopt_zero_models(dopt_ctx *ctx);
 /* The shared iterate of the centralized trainer (trainer.py:11). */
 int dopt_set_global(dopt_ctx *ctx, const double *x);
 int dopt_get_global(dopt_ctx *ctx, double *x);
