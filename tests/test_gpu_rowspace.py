@@ -253,3 +253,21 @@ def test_trainer_complete_graph_long_rows_vs_oracle(problem):
     np.testing.assert_allclose(hist["consensus_error"], h["consensus_error"], rtol=1e-9)
     np.testing.assert_allclose(xavg, xr_avg, rtol=1e-9, atol=1e-12 * np.abs(xr_avg).max())
     assert pos[2] == st_after[2] and np.array_equal(pos[1], st_after[1])
+
+
+def test_zero_models_equals_host_zeros():
+    """dopt_zero_models (the device-side reset bench.py uses) = set_models(zeros): both path kinds
+    (row-space rounds from the zero iterate; direct rounds after a nonzero run) bitwise."""
+    n, m, d, T = 9, 12, 2100, 4
+    shards = _data([m] * n, d, 14)
+    eng = _engine(shards)
+    eng.set_models(np.random.default_rng(3).standard_normal((n, d)) * 0.01)
+    eng.run_dsgd(2, 0.05, m, 2e-3, 2e-3, 0.0)
+    eng.zero_models()
+    assert not np.any(eng.get_models())
+    a = eng.run_dsgd(T, 0.05, m, 2e-3, 2e-3, 0.0)[:2] + (eng.get_models(),)
+    eng.set_models(np.zeros((n, d)))
+    b = eng.run_dsgd(T, 0.05, m, 2e-3, 2e-3, 0.0)[:2] + (eng.get_models(),)
+    for u, v in zip(a, b):
+        assert np.array_equal(np.asarray(u), np.asarray(v))
+    eng.close()
