@@ -43,13 +43,18 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(kernel_name):
+def pmc_traffic(kernel_name, config="c3"):
     """Per-dispatch HBM bytes of `kernel_name` from the newest committed rocprofv3 PMC
-    summary (profiles/<tag>_pmc.json, written by scripts/pmc_summary.py from separate
-    FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 correction)."""
+    summary of this configuration (profiles/r<round>[_c4|_c5|_c5rs]_pmc.json, written by
+    scripts/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled
+    per the gfx950 correction).  C3 and C4 launch the same kernel instance, so the file is
+    picked by configuration, not by kernel name alone."""
     import glob
+    import re
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    pat = {"c3": r"r\d+_pmc\.json", "c4": r"r\d+_c4_pmc\.json", "c5": r"r\d+_c5(rs)?_pmc\.json"}[config]
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json"))
+                   if re.fullmatch(pat, os.path.basename(f)))
     for f in reversed(files):
         try:
             rec = json.load(open(f)).get(kernel_name)
@@ -462,7 +467,8 @@ def main():
     esz = 4 if eng.dtype == _dopt.F32 else 8
     xesz = 4 if eng.data_dtype == _dopt.F32 else 8
     kname = kernel_name()
-    traffic, traffic_src = pmc_traffic(kname) if args.config == "c3" and n == 4096 and world == 1 else (None, None)
+    full = {"c3": n == 4096, "c4": n == 65536, "c5": n == 1024}[args.config]  # the profiled shapes
+    traffic, traffic_src = pmc_traffic(kname, args.config) if full and world == 1 else (None, None)
     bytes_per_launch = bytes_per_round(eng, n, d, m, kname)
     avg_s = (kr_ms / launches) * 1e-3 if launches else float("nan")
     achieved = bytes_per_launch / avg_s / 1e9 if launches else None
