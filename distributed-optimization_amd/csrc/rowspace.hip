@@ -39,8 +39,10 @@ __device__ __forceinline__ typename VT<T>::v rs_ld_nt(const T* p) {
 // register copies, so the compiler's wait before a row covers that row only; loads past the
 // wave's rows re-read its last row).  Per row: the partial dot with xbar over the block
 // (64-lane DPP butterfly, stashed one row per lane, stored 64 rows at a time into
-// upart[blk][row]) and, with COLS, coef_row * row accumulated in float64 registers; the four
-// waves' column sums meet in LDS (fixed order) -> cpart[g][columns of blk].
+// upart[blk][row], in T) and, with COLS, coef_row * row summed into float64 registers (float32
+// contexts: in float over each 64-row window, then flushed); the four waves' column sums meet in
+// LDS (fixed order) -> cpart[g][columns of blk].  Row weights come 64 rows per vector load, read
+// with v_readlane.
 template <typename T, bool COLS, int CB, int NBUF>
 __global__ __launch_bounds__(NT) void k_rs_pass(const RsArgs a) {
   using V = typename VT<T>::v;
