@@ -271,3 +271,25 @@ def test_zero_models_equals_host_zeros():
     for u, v in zip(a, b):
         assert np.array_equal(np.asarray(u), np.asarray(v))
     eng.close()
+
+
+@pytest.mark.parametrize("problem", ["quadratic", "logistic"])
+def test_rowspace_long_horizon_vs_oracle(problem):
+    """300 rounds: the carried row state (z, v = X_i . Z, beta) does not drift from the reference
+    trajectory (float64, every history value rtol 1e-8; iterates 1e-8)."""
+    sizes, d, T = [16, 9, 16, 4, 16, 12, 16], 2100, 300
+    shards = _data(sizes, d, 31, problem)
+    eng = _engine(shards, problem=problem)
+    b = max(sizes)
+    lam_g = 2e-3 if problem == "quadratic" else 1e-3
+    obj, cons, _ = eng.run_dsgd(T, 0.05, b, lam_g, 1e-3, 0.0)
+    assert "k_rs_pass" in _dopt.last_round_kernel()
+    x = eng.get_models()
+    Xf = np.vstack([s[0] for s in shards])
+    yf = np.concatenate([s[1] for s in shards])
+    h, _, xr, _ = O.run_decentralized(shards, TP.fully_connected(len(sizes)).dense_W(), T, _cfg(b, problem), Xf, yf,
+                                      0.0)
+    np.testing.assert_allclose(obj, h["objective"], rtol=1e-8)
+    np.testing.assert_allclose(cons, h["consensus_error"], rtol=1e-8)
+    np.testing.assert_allclose(x, xr, rtol=1e-8, atol=1e-11 * np.abs(xr).max())
+    eng.close()
