@@ -45,14 +45,14 @@ def log(*a):
 
 def pmc_traffic(kernel_name, config="c3"):
     """Per-dispatch HBM bytes of `kernel_name` from the newest committed rocprofv3 PMC
-    summary of this configuration (profiles/r<round>[_c4|_c5|_c5rs]_pmc.json, written by
+    summary of this configuration (profiles/r<round>[_c4|_c5|_c5rs|_c5x32]_pmc.json, written by
     scripts/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled
     per the gfx950 correction).  C3 and C4 launch the same kernel instance, so the file is
     picked by configuration, not by kernel name alone."""
     import glob
     import re
 
-    pat = {"c3": r"r\d+_pmc\.json", "c4": r"r\d+_c4_pmc\.json", "c5": r"r\d+_c5(rs)?_pmc\.json"}[config]
+    pat = {"c3": r"r\d+_pmc\.json", "c4": r"r\d+_c4_pmc\.json", "c5": r"r\d+_c5(rs|x32)?_pmc\.json"}[config]
     files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json"))
                    if re.fullmatch(pat, os.path.basename(f)))
     for f in reversed(files):
@@ -398,8 +398,11 @@ def main():
                                     np.zeros(world + 1, np.int64), None, None, None)
     n = plan.n_local
     data_dtype = args.data_dtype
-    if args.dtype in ("float32", "fp32", "f32") or _chunks_per_lane(d, 4) > 8:
-        data_dtype = None  # float32 engine, or rows beyond the mixed kernel (C5): storage = compute dtype
+    if args.dtype in ("float32", "fp32", "f32") or (_chunks_per_lane(d, 4) > 8 and mean is None):
+        # float32 engine, or rows beyond the mixed row-resident kernel off the complete graph: storage =
+        # compute dtype (the complete graph's row-space rounds read float32 rows under float64
+        # arithmetic: k_rs_pass_x32)
+        data_dtype = None
     log(f"rank {rank}/{world}: generating {plan.n_local} x {m} x {d} shards ({args.dtype} arithmetic, "
         f"{data_dtype or args.dtype} storage) on device {dev}")
     eng = _dopt.Engine(dev, args.dtype, data_dtype=data_dtype)
@@ -506,6 +509,8 @@ def main():
                                    f" ({args.backend})") if world > 1
                                   else ("single GPU: the multi-GPU phase path (lagged schedule, "
                                         f"{args.backend} world 1)") if args.phase
+                                  else ("single GPU: row-space rounds (the pass over the rows, then per-worker "
+                                        "and per-column updates; DESIGN.md 6c)") if "k_rs_pass" in kname
                                   else "single GPU: fused round kernel, one launch per round"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,

@@ -133,7 +133,8 @@ struct RsArgs {
   const double* csum;      // [ld] all-reduced column sums C (multi-GPU), or null: sum cpart
   double a1, q, eta, eta_n;  // w_off N, W_ii - w_off - eta mu, eta, eta / N
 };
-hipError_t launch_rs_pass(int dtype, bool cols, const RsArgs& a, hipStream_t s);
+// dtype: arithmetic; xdtype: row storage (float32 rows under float64 arithmetic: k_rs_pass_x32).
+hipError_t launch_rs_pass(int dtype, int xdtype, bool cols, const RsArgs& a, hipStream_t s);
 // mode bits: 1 metric partials of the iterate the pass read, 2 next round's row state,
 // 4 initial state (z = v = u, beta = 0), 8 u = 0 without reading upart (zero start)
 hipError_t launch_rs_rows(int dtype, const RsArgs& a, int n_workers, int mode, hipStream_t s);
@@ -145,9 +146,9 @@ hipError_t launch_rs_hist(const RsArgs& a, int n_workers, double* out, hipStream
 hipError_t launch_rs_init(int dtype, const RsArgs& a, const void* x0, hipStream_t s);
 hipError_t launch_rs_check(int dtype, const void* x, int64_t n, int64_t ld, int32_t nch, int G, int32_t* flags,
                            int32_t* zflag, hipStream_t s);
-hipError_t launch_rs_gram(int dtype, const RsArgs& a, int n_workers, int max_m, double* gpart, int G,
+hipError_t launch_rs_gram(int xdtype, const RsArgs& a, int n_workers, int max_m, double* gpart, int G,
                           hipStream_t s);
-hipError_t launch_rs_materialise(int dtype, const RsArgs& a, int n_workers, void* xout, hipStream_t s);
+hipError_t launch_rs_materialise(int dtype, int xdtype, const RsArgs& a, int n_workers, void* xout, hipStream_t s);
 
 // Kernel launchers (kernels.hip).  dtype: 0 = float, 1 = double.
 // k_round: dtype = iterates and arithmetic, xdtype = shard storage (equal, or float32 rows

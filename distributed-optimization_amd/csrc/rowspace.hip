@@ -43,28 +43,39 @@ __device__ __forceinline__ typename VT<T>::v rs_ld_nt(const T* p) {
 // contexts: in float over each 64-row window, then flushed); the four waves' column sums meet in
 // LDS (fixed order) -> cpart[g][columns of blk].  Row weights come 64 rows per vector load, read
 // with v_readlane.
-template <typename T, bool COLS, int CB, int NBUF>
-__global__ __launch_bounds__(NT) void k_rs_pass(const RsArgs a) {
-  using V = typename VT<T>::v;
-  constexpr int VN = VT<T>::n;
-  __shared__ double red[COLS ? NW * 64 * CB * VN : 1];
+//
+// rs_pass_body<T, XT, ...>: T = arithmetic and state, XT = storage of the rows.  k_rs_pass<T, ...>
+// (XT = T) and k_rs_pass_x32<...> (float64 arithmetic over float32-stored rows, the C3 headline's
+// layout: the 16-byte chunk is 4 floats, xbar's 4 doubles stay in registers, every product and
+// sum in float64).
+template <typename T, typename XT, bool COLS, int CB, int NBUF>
+__device__ __forceinline__ void rs_pass_body(const RsArgs& a, double* red) {
+  using V = typename VT<XT>::v;
+  constexpr int VN = VT<XT>::n;
+  constexpr bool SAME = std::is_same<T, XT>::value;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int blk = blockIdx.x, g = blockIdx.y;
   const int nch = a.nch;
   const int64_t ld = a.ld;
-  const T* __restrict__ X = (const T*)a.X;
+  const XT* __restrict__ X = (const XT*)a.X;
   const int64_t r0 = a.grow[g], r1 = a.grow[g + 1];
   const int64_t per = (r1 - r0 + NW - 1) / NW;
   const int64_t wr0 = min(r1, r0 + wave * per), wr1 = min(r1, wr0 + per);
   int cc[CB];
-  V xb[CB];
+  V xb[SAME ? CB : 1];              // xbar chunks in the row type (XT = T)
+  T xbs[SAME ? 1 : CB][SAME ? 1 : VN];  // xbar elements in T (float32 rows, float64 arithmetic)
 #pragma unroll
   for (int j = 0; j < CB; ++j) {
     const int c = blk * 64 * CB + j * 64 + lane;
     const bool in = c < nch;
     cc[j] = in ? c : nch - 1;  // lanes past the row re-read its last chunk (xbar is 0 there)
-    xb[j] = in ? *(const V*)((const T*)a.xbar + (int64_t)c * VN) : V(0);
+    if constexpr (SAME) {
+      xb[j] = in ? *(const V*)((const T*)a.xbar + (int64_t)c * VN) : V(0);
+    } else {
+#pragma unroll
+      for (int e = 0; e < VN; ++e) xbs[j][e] = in ? ((const T*)a.xbar)[(int64_t)c * VN + e] : T(0);
+    }
   }
   // column sums: T products accumulated over each 64-row window in T, flushed into float64 (a
   // float32 context trades the per-element float64 convert + FMA for one float FMA; float64
@@ -100,14 +111,21 @@ __global__ __launch_bounds__(NT) void k_rs_pass(const RsArgs a) {
   auto cwin_load = [&](int64_t base) { return (COLS && base + lane < wr1) ? cw[base + lane] : 0.0; };
   double cw_cur = cwin_load(wr0), cw_nxt = cwin_load(wr0 + 64);
   auto load = [&](int64_t row, V (&dst)[CB]) {
-    const T* p = X + row * ld;
+    const XT* p = X + row * ld;
 #pragma unroll
-    for (int j = 0; j < CB; ++j) dst[j] = rs_ld_nt<T>(p + (int64_t)cc[j] * VN);
+    for (int j = 0; j < CB; ++j) dst[j] = rs_ld_nt<XT>(p + (int64_t)cc[j] * VN);
   };
   auto process = [&](const V (&rv)[CB], int64_t r) {
     double p = 0.0;
 #pragma unroll
-    for (int j = 0; j < CB; ++j) p += (double)hsum<T>(rv[j] * xb[j]);
+    for (int j = 0; j < CB; ++j) {
+      if constexpr (SAME) {
+        p += (double)hsum<T>(rv[j] * xb[j]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < VN; ++e) p += (double)rv[j][e] * xbs[j][e];
+      }
+    }
     const double dot = wave_sum_dpp(p);
     const int k = (int)((r - wr0) & 63);
     if constexpr (COLS) {
@@ -166,6 +184,18 @@ __global__ __launch_bounds__(NT) void k_rs_pass(const RsArgs a) {
       if (col0 + q < ld) out[q] = ((red[q] + red[W + q]) + red[2 * W + q]) + red[3 * W + q];
     }
   }
+}
+
+template <typename T, bool COLS, int CB, int NBUF>
+__global__ __launch_bounds__(NT) void k_rs_pass(const RsArgs a) {
+  __shared__ double red[COLS ? NW * 64 * CB * VT<T>::n : 1];
+  rs_pass_body<T, T, COLS, CB, NBUF>(a, red);
+}
+
+template <bool COLS, int CB, int NBUF>
+__global__ __launch_bounds__(NT) void k_rs_pass_x32(const RsArgs a) {
+  __shared__ double red[COLS ? NW * 64 * CB * VT<float>::n : 1];
+  rs_pass_body<double, float, COLS, CB, NBUF>(a, red);
 }
 
 // k_rs_rows: one workgroup per worker (m_i <= 64 rows, lane k = row k).  u_k = sum over the
@@ -467,11 +497,11 @@ __global__ __launch_bounds__(NT) void k_rs_gram_fold(const RsArgs a, const doubl
   }
 }
 
-// x_i = Z + X_i^T beta_i for every worker (T), chunk-strided over column groups.
-template <typename T>
-__global__ __launch_bounds__(NT) void k_rs_materialise(const RsArgs a, T* xout) {
-  using V = typename VT<T>::v;
-  constexpr int VN = VT<T>::n;
+// x_i = Z + X_i^T beta_i for every worker (T; rows stored as XT), chunk-strided over column groups.
+template <typename T, typename XT>
+__device__ __forceinline__ void rs_materialise_body(const RsArgs& a, T* xout) {
+  using V = typename VT<XT>::v;
+  constexpr int VN = VT<XT>::n;
   __shared__ double sb[64];
   const int i = blockIdx.x, g = blockIdx.y, G = gridDim.y;
   const int64_t row0 = a.off[i];
@@ -483,25 +513,51 @@ __global__ __launch_bounds__(NT) void k_rs_materialise(const RsArgs a, T* xout) 
 #pragma unroll
     for (int e = 0; e < VN; ++e) s[e] = a.rZ[(int64_t)c * VN + e];
     for (int k = 0; k < m; ++k) {
-      const V r = rs_ld_nt<T>((const T*)a.X + (row0 + k) * a.ld + (int64_t)c * VN);
+      const V r = rs_ld_nt<XT>((const XT*)a.X + (row0 + k) * a.ld + (int64_t)c * VN);
 #pragma unroll
       for (int e = 0; e < VN; ++e) s[e] += sb[k] * (double)r[e];
     }
-    V o;
+    if constexpr (std::is_same<T, XT>::value) {
+      V o;
 #pragma unroll
-    for (int e = 0; e < VN; ++e) o[e] = (T)s[e];
-    *(V*)(xout + (int64_t)i * a.ld + (int64_t)c * VN) = o;
+      for (int e = 0; e < VN; ++e) o[e] = (T)s[e];
+      *(V*)(xout + (int64_t)i * a.ld + (int64_t)c * VN) = o;
+    } else {
+      using W2 = typename VT<T>::v;  // 16-byte stores of T
+      constexpr int WN = VT<T>::n;
+#pragma unroll
+      for (int h = 0; h < VN / WN; ++h) {
+        W2 o;
+#pragma unroll
+        for (int e = 0; e < WN; ++e) o[e] = (T)s[h * WN + e];
+        *(W2*)(xout + (int64_t)i * a.ld + (int64_t)c * VN + h * WN) = o;
+      }
+    }
   }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void k_rs_materialise(const RsArgs a, T* xout) {
+  rs_materialise_body<T, T>(a, xout);
+}
+
+__global__ __launch_bounds__(NT) void k_rs_materialise_x32(const RsArgs a, double* xout) {
+  rs_materialise_body<double, float>(a, xout);
 }
 
 // ---------------------------------------------------------------------------- launchers
 static const char* rs_tn(int dtype) { return dtype == 0 ? "float" : "double"; }
 
-// Pass shapes (RsArgs.cb / nbuf, picked by the runtime; DOPT_RS_CB / DOPT_RS_NBUF for A/B runs)
-template <typename T, bool COLS>
+// Pass shapes (RsArgs.cb / nbuf, picked by the runtime; DOPT_RS_CB / DOPT_RS_NBUF for A/B runs).
+// X32: float64 arithmetic over float32-stored rows (k_rs_pass_x32).
+template <typename T, bool X32, bool COLS>
 static hipError_t rs_pass_shape(const RsArgs& a, dim3 grid, hipStream_t s) {
-#define RS_SHAPE(C_, B_) \
-  if (a.cb == C_ && a.nbuf == B_) { hipLaunchKernelGGL((k_rs_pass<T, COLS, C_, B_>), grid, dim3(NT), 0, s, a); return hipGetLastError(); }
+#define RS_SHAPE(C_, B_)                                                                       \
+  if (a.cb == C_ && a.nbuf == B_) {                                                            \
+    if constexpr (X32) hipLaunchKernelGGL((k_rs_pass_x32<COLS, C_, B_>), grid, dim3(NT), 0, s, a); \
+    else hipLaunchKernelGGL((k_rs_pass<T, COLS, C_, B_>), grid, dim3(NT), 0, s, a);          \
+    return hipGetLastError();                                                                  \
+  }
   RS_SHAPE(4, 2)
   RS_SHAPE(4, 3)
   RS_SHAPE(2, 3)
@@ -512,14 +568,22 @@ static hipError_t rs_pass_shape(const RsArgs& a, dim3 grid, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_rs_pass(int dtype, bool cols, const RsArgs& a, hipStream_t s) {
+hipError_t launch_rs_pass(int dtype, int xdtype, bool cols, const RsArgs& a, hipStream_t s) {
   const dim3 grid(a.nblk, a.wg);
+  const bool x32 = dtype == 1 && xdtype == 0;
+  if (dtype != xdtype && !x32) return hipErrorInvalidValue;
   char buf[112];
-  snprintf(buf, sizeof(buf), "void dopt::k_rs_pass<%s, %s, %d, %d>(dopt::RsArgs)", rs_tn(dtype),
-           cols ? "true" : "false", a.cb, a.nbuf);
+  if (x32)
+    snprintf(buf, sizeof(buf), "void dopt::k_rs_pass_x32<%s, %d, %d>(dopt::RsArgs)", cols ? "true" : "false", a.cb,
+             a.nbuf);
+  else
+    snprintf(buf, sizeof(buf), "void dopt::k_rs_pass<%s, %s, %d, %d>(dopt::RsArgs)", rs_tn(dtype),
+             cols ? "true" : "false", a.cb, a.nbuf);
   if (cols) note_round_kernel(buf);
-  if (dtype == 0) return cols ? rs_pass_shape<float, true>(a, grid, s) : rs_pass_shape<float, false>(a, grid, s);
-  return cols ? rs_pass_shape<double, true>(a, grid, s) : rs_pass_shape<double, false>(a, grid, s);
+  if (x32) return cols ? rs_pass_shape<double, true, true>(a, grid, s) : rs_pass_shape<double, true, false>(a, grid, s);
+  if (dtype == 0)
+    return cols ? rs_pass_shape<float, false, true>(a, grid, s) : rs_pass_shape<float, false, false>(a, grid, s);
+  return cols ? rs_pass_shape<double, false, true>(a, grid, s) : rs_pass_shape<double, false, false>(a, grid, s);
 }
 
 hipError_t launch_rs_rows(int dtype, const RsArgs& a, int n_workers, int mode, hipStream_t s) {
@@ -564,12 +628,12 @@ hipError_t launch_rs_check(int dtype, const void* x, int64_t n, int64_t ld, int3
   return hipGetLastError();
 }
 
-hipError_t launch_rs_gram(int dtype, const RsArgs& a, int n_workers, int max_m, double* gpart, int G, hipStream_t s) {
+hipError_t launch_rs_gram(int xdtype, const RsArgs& a, int n_workers, int max_m, double* gpart, int G, hipStream_t s) {
   if (n_workers <= 0) return hipSuccess;
   const int P = max_m * (max_m + 1) / 2;
   const size_t lds = (size_t)max_m * 1024;
   const dim3 grid(n_workers, G);
-  if (dtype == 0) {
+  if (xdtype == 0) {  // the Gram matrices read the rows only: their storage type
     hipError_t e = hipFuncSetAttribute((const void*)k_rs_gram<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        64 * 1024);
     if (e != hipSuccess) return e;
@@ -586,11 +650,13 @@ hipError_t launch_rs_gram(int dtype, const RsArgs& a, int n_workers, int max_m, 
   return hipGetLastError();
 }
 
-hipError_t launch_rs_materialise(int dtype, const RsArgs& a, int n_workers, void* xout, hipStream_t s) {
+hipError_t launch_rs_materialise(int dtype, int xdtype, const RsArgs& a, int n_workers, void* xout, hipStream_t s) {
   if (n_workers <= 0) return hipSuccess;
   const int G = (int)std::max<int64_t>(1, std::min<int64_t>((a.nch + NT - 1) / NT, (8192 + n_workers - 1) / n_workers));
   const dim3 grid(n_workers, G);
-  if (dtype == 0) hipLaunchKernelGGL((k_rs_materialise<float>), grid, dim3(NT), 0, s, a, (float*)xout);
+  if (dtype == 1 && xdtype == 0) hipLaunchKernelGGL(k_rs_materialise_x32, grid, dim3(NT), 0, s, a, (double*)xout);
+  else if (dtype != xdtype) return hipErrorInvalidValue;
+  else if (dtype == 0) hipLaunchKernelGGL((k_rs_materialise<float>), grid, dim3(NT), 0, s, a, (float*)xout);
   else hipLaunchKernelGGL((k_rs_materialise<double>), grid, dim3(NT), 0, s, a, (double*)xout);
   return hipGetLastError();
 }

@@ -358,9 +358,8 @@ int set_layout(dopt_ctx* c, int problem, int64_t n, int64_t d) {
   const int64_t nch = ld / c->vn;
   const int cpl = cpl_for(nch);
   c->split = cpl > max_chunks_per_lane(c->dtype, c->xdtype);
-  if (c->split && c->xdtype != c->dtype)
-    return fail(DOPT_ERR_UNSUPPORTED, "float32 shard storage under float64 arithmetic: rows of at most %d "
-                "elements (d = %lld); store the rows as float64", 64 * 8 * c->vn, (long long)d);
+  // float32 rows under float64 arithmetic past the row-resident kernel: the row-space rounds
+  // only (rowspace.hip k_rs_pass_x32); the direct column-blocked kernels refuse them (split_x_ok)
   if (c->split) {  // enough workgroups to fill 256 CUs several times over
     const int64_t nblk = (nch + 63) / 64;
     const char* gw = getenv("DOPT_SPLIT_WGS");  // A/B knob: target workgroups per column-blocked launch
@@ -562,8 +561,29 @@ int colsum_current(dopt_ctx* c) {
   return refresh_sums_t(c);
 }
 
+// The direct column-blocked kernels read the rows in the compute dtype: float32 rows under
+// float64 arithmetic (dopt_set_data_dtype) past the row-resident kernel take the row-space rounds
+// only.  ensure_split gives the error; the launch wrappers below are the backstop.
+int split_x_ok(dopt_ctx* c) {
+  if (c->xdtype == c->dtype) return DOPT_OK;
+  return fail(DOPT_ERR_UNSUPPORTED, "float32 shard storage under float64 arithmetic with rows of %lld elements: "
+              "only the row-space rounds (complete graph, full-shard batches of <= %d rows, equal starting "
+              "iterates, one context) read such rows; store the rows as float64", (long long)c->d, kRsMaxRows);
+}
+
+hipError_t split_dots(dopt_ctx* c, int mode, const RoundArgs& a) {
+  if (c->xdtype != c->dtype) return hipErrorNotSupported;
+  return launch_split_dots(c->dtype, mode, a, (int)c->n, c->stream);
+}
+
+hipError_t split_step(dopt_ctx* c, bool znext, bool met, const RoundArgs& a) {
+  if (c->xdtype != c->dtype) return hipErrorNotSupported;
+  return launch_split_step(c->dtype, znext, met, a, (int)c->n, c->stream);
+}
+
 // Column-blocked buffers: coefficients [n x bcap] and fp64 partial slabs.
 int ensure_split(dopt_ctx* c) {
+  if (int rc = split_x_ok(c)) return rc;
   int64_t bcap = std::max<int64_t>(1, c->max_m);
   if (c->obj_sep) bcap = std::max<int64_t>(bcap, (c->rows_o + c->n - 1) / c->n);
   const size_t need = (size_t)(c->n * bcap * c->split_groups);
@@ -592,7 +612,7 @@ int split_metrics(dopt_ctx* c, const void* x_state, const void* point, bool shar
   a.xbar = point;
   a.flags = (cons ? F_CONS : 0) | (loss ? F_LOSS : 0) | (shared ? F_SHARED : 0);
   if (a.flags & F_LOSS) c->loss_groups = c->n;  // per-worker loss slabs
-  HIPOK(launch_split_dots(c->dtype, 1, a, (int)c->n, c->stream));
+  HIPOK(split_dots(c, 1, a));
   HIPOK(launch_split_coef(c->dtype, c->problem, 2, a, (int)c->n, c->stream));
   return DOPT_OK;
 }
@@ -620,7 +640,7 @@ int run_dsgd_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batc
   RoundArgs p = base_args(c);
   p.x_old = c->xs[c->cur];
   if (full && !lag) {  // prologue: coefficients of the starting iterates (carried: the last step made them)
-    HIPOK(launch_split_dots(c->dtype, 0, p, (int)c->n, c->stream));
+    HIPOK(split_dots(c, 0, p));
     HIPOK(launch_split_coef(c->dtype, c->problem, 1, p, (int)c->n, c->stream));
   }
   HIPOK(launch_stamp(c->stamps, c->stream));
@@ -639,14 +659,14 @@ int run_dsgd_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batc
     a.eta = eta0 / sqrt((double)(t + 1));  // trainer.py:138-140
     a.lam = lam_grad;
     if (!full) {  // this round's minibatch coefficients
-      HIPOK(launch_split_dots(c->dtype, 0, a, (int)c->n, c->stream));
+      HIPOK(split_dots(c, 0, a));
       HIPOK(launch_split_coef(c->dtype, c->problem, 1, a, (int)c->n, c->stream));
     }
     const bool met = fused_met && metrics && (h > 0 || lag);
     a.flags |= (met && want_cons ? F_CONS : 0) | (met && want_obj ? F_LOSS : 0);
     if (a.flags & F_LOSS) c->loss_groups = c->n;  // per-worker loss slabs
     if (c->prof && (rc = prof_event(c, false))) return rc;
-    HIPOK(launch_split_step(c->dtype, full, met, a, (int)c->n, c->stream));
+    HIPOK(split_step(c, full, met, a));
     if (c->prof && (rc = prof_event(c, true))) return rc;
     if (full || met) {  // next coefficients (rows of the full shard) and the metric slabs
       RoundArgs q = a;
@@ -705,10 +725,10 @@ int run_centralized_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64
     a.g_out = c->G;
     a.lam = lam_grad;
     a.flags = F_SHARED | F_GOUT;  // no mixing here
-    HIPOK(launch_split_dots(c->dtype, 0, a, (int)c->n, c->stream));
+    HIPOK(split_dots(c, 0, a));
     HIPOK(launch_split_coef(c->dtype, c->problem, 1, a, (int)c->n, c->stream));
     if (c->prof && (rc = prof_event(c, false))) return rc;
-    HIPOK(launch_split_step(c->dtype, false, false, a, (int)c->n, c->stream));
+    HIPOK(split_step(c, false, false, a));
     if (c->prof && (rc = prof_event(c, true))) return rc;
     HIPOK(launch_colsum_partial(c->dtype, c->G, c->n, c->ld, (int32_t)c->nchs, kRowsPerGroup, c->part,
                                 c->stamps + h + 1, c->stream));
@@ -735,8 +755,11 @@ bool rs_enabled() {
 
 bool rs_eligible(dopt_ctx* c, int64_t batch, const int32_t* idx) {
   return rs_enabled() && c->split && c->mean_mix && c->wdiag_uniform && !idx && batch >= c->max_m && !c->obj_sep && c->min_m >= 1 && c->max_m <= kRsMaxRows &&
-         c->n_global == 0 && !c->S_ext && c->xdtype == c->dtype;
+         c->n_global == 0 && !c->S_ext;
 }
+
+// Row storage for the row-space launchers (0 float32, 1 float64).
+int rs_xdt(dopt_ctx* c) { return c->xdtype == DOPT_F32 ? 0 : 1; }
 
 RsArgs rs_args(dopt_ctx* c) {
   RsArgs a;
@@ -812,7 +835,7 @@ int ensure_rs(dopt_ctx* c) {
 // xs[cur] = the iterates the row-space state holds (the state stays live).
 int rs_sync(dopt_ctx* c) {
   if (!c->rs_live || c->rs_xs_valid) return DOPT_OK;
-  HIPOK(launch_rs_materialise(c->dtype == DOPT_F32 ? 0 : 1, rs_args(c), (int)c->n, c->xs[c->cur], c->stream));
+  HIPOK(launch_rs_materialise(c->dtype == DOPT_F32 ? 0 : 1, rs_xdt(c), rs_args(c), (int)c->n, c->xs[c->cur], c->stream));
   c->rs_xs_valid = true;
   return DOPT_OK;
 }
@@ -836,7 +859,7 @@ int rs_check(dopt_ctx* c, bool* equal, bool* zero, double* sig) {
   if ((rc = ensure_rs(c))) return rc;
   const int dt = c->dtype == DOPT_F32 ? 0 : 1;
   const int G = kRsCheckGroups;
-  HIPOK(launch_rs_check(dt, c->xs[c->cur], c->n, c->ld, (int32_t)c->nch, G, c->rs_flags, c->rs_flags + c->n * G,
+  HIPOK(launch_rs_check(dt, c->xs[c->cur], c->n, c->ld, (int32_t)c->nchs, G, c->rs_flags, c->rs_flags + c->n * G,
                         c->stream));
   std::vector<int32_t> fl((size_t)(c->n + 1) * G);
   HIPOK(hipMemcpyAsync(fl.data(), c->rs_flags, fl.size() * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
@@ -881,7 +904,7 @@ int rs_begin(dopt_ctx* c) {
     const int Gg = (int)std::max<int64_t>(1, std::min<int64_t>((c->ld + 255) / 256, (2048 + c->n - 1) / c->n));
     double* gpart = nullptr;
     if ((rc = dalloc_t(&gpart, (size_t)c->n * Gg * P * sizeof(double)))) return rc;
-    hipError_t e = launch_rs_gram(dt, a, (int)c->n, (int)c->rs_bcap, gpart, Gg, c->stream);
+    hipError_t e = launch_rs_gram(rs_xdt(c), a, (int)c->n, (int)c->rs_bcap, gpart, Gg, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     dfree_t(gpart);
     if (e != hipSuccess) return fail(DOPT_ERR_HIP, "Gram matrices: %s", hipGetErrorString(e));
@@ -893,7 +916,7 @@ int rs_begin(dopt_ctx* c) {
     HIPOK(launch_rs_rows(dt, a, (int)c->n, 4 | 8, c->stream));  // z = v = 0
   } else {
     a.xbar = c->xbar[c->xb];
-    HIPOK(launch_rs_pass(dt, false, a, c->stream));  // z = v = X . x_0
+    HIPOK(launch_rs_pass(dt, rs_xdt(c), false, a, c->stream));  // z = v = X . x_0
     HIPOK(launch_rs_rows(dt, a, (int)c->n, 4, c->stream));
   }
   c->rs_live = true;
@@ -925,7 +948,7 @@ int run_dsgd_rs(dopt_ctx* c, int64_t t0, int64_t T, double eta0, double lam_grad
     a.slab_cons = want_cons ? c->slab_cons : nullptr;
     a.slab_loss = want_obj ? c->slab_loss : nullptr;
     if (c->prof && (rc = prof_event(c, false))) return rc;
-    HIPOK(launch_rs_pass(dt, true, a, c->stream));
+    HIPOK(launch_rs_pass(dt, rs_xdt(c), true, a, c->stream));
     if (c->prof && (rc = prof_event(c, true))) return rc;
     HIPOK(launch_rs_rows(dt, a, (int)c->n, 2 | (met ? 1 : 0), c->stream));
     if (met) HIPOK(launch_rs_hist(a, (int)c->n, c->hraw + 3 * (h - 1 + lag), c->stream));
@@ -945,7 +968,7 @@ int run_dsgd_rs(dopt_ctx* c, int64_t t0, int64_t T, double eta0, double lam_grad
     a.xbar = c->xbar[xb];
     a.slab_cons = want_cons ? c->slab_cons : nullptr;
     a.slab_loss = want_obj ? c->slab_loss : nullptr;
-    HIPOK(launch_rs_pass(dt, false, a, c->stream));
+    HIPOK(launch_rs_pass(dt, rs_xdt(c), false, a, c->stream));
     HIPOK(launch_rs_rows(dt, a, (int)c->n, 1, c->stream));
     HIPOK(launch_rs_hist(a, (int)c->n, c->hraw + 3 * (nh - 1), c->stream));
   }
@@ -1813,7 +1836,7 @@ int dopt_phase_begin(dopt_ctx* c, int64_t batch) {
     if (batch >= c->max_m) {  // coefficients of the starting iterates
       RoundArgs p = base_args(c);
       p.x_old = c->xs[c->cur];
-      HIPOK(launch_split_dots(c->dtype, 0, p, (int)c->n, c->stream));
+      HIPOK(split_dots(c, 0, p));
       HIPOK(launch_split_coef(c->dtype, c->problem, 1, p, (int)c->n, c->stream));
     }
   }
@@ -1843,7 +1866,7 @@ int dopt_phase_grad(dopt_ctx* c, int64_t batch, const int32_t* idx, double lam_g
       a.b = batch;
       a.b_rows = (int32_t)std::min<int64_t>(a.b_rows, batch);
       a.x_old = c->xs[c->cur];
-      HIPOK(launch_split_dots(c->dtype, 0, a, (int)c->n, c->stream));
+      HIPOK(split_dots(c, 0, a));
       HIPOK(launch_split_coef(c->dtype, c->problem, 1, a, (int)c->n, c->stream));
     }
     return DOPT_OK;
@@ -1885,7 +1908,7 @@ int dopt_phase_mix(dopt_ctx* c, int64_t t, double eta0) {
     if (a.flags & F_LOSS) c->loss_groups = c->n;  // per-worker loss slabs
     int rc;
     if (c->prof && (rc = prof_event(c, false))) return rc;
-    HIPOK(launch_split_step(c->dtype, full, cons || loss, a, (int)c->n, c->stream));
+    HIPOK(split_step(c, full, cons || loss, a));
     if (c->prof && (rc = prof_event(c, true))) return rc;
     if (full || cons || loss) {
       RoundArgs q = a;
@@ -1929,10 +1952,10 @@ int dopt_phase_grad_shared(dopt_ctx* c, int64_t batch, const int32_t* idx, doubl
   if (c->split) {
     if (fuse_loss) return fail(DOPT_ERR_UNSUPPORTED, "column-blocked rounds: use dopt_phase_metrics_pass_shared");
     if ((rc = ensure_split(c))) return rc;
-    HIPOK(launch_split_dots(c->dtype, 0, a, (int)c->n, c->stream));
+    HIPOK(split_dots(c, 0, a));
     HIPOK(launch_split_coef(c->dtype, c->problem, 1, a, (int)c->n, c->stream));
     if (c->prof && (rc = prof_event(c, false))) return rc;
-    HIPOK(launch_split_step(c->dtype, false, false, a, (int)c->n, c->stream));
+    HIPOK(split_step(c, false, false, a));
     if (c->prof && (rc = prof_event(c, true))) return rc;
     return DOPT_OK;
   }
@@ -2071,7 +2094,7 @@ int dopt_rs_phase_begin(dopt_ctx* c, int commit, int* ok, double* sig) {
   *ok = 0;
   *sig = 0.0;
   if (!(rs_enabled() && c->split && c->mean_mix && c->wdiag_uniform && !c->obj_sep && c->min_m >= 1 &&
-        c->max_m <= kRsMaxRows && c->xdtype == c->dtype))
+        c->max_m <= kRsMaxRows))
     return DOPT_OK;
   int rc;
   if ((rc = set_device(c))) return rc;
@@ -2101,7 +2124,7 @@ int dopt_rs_phase_round(dopt_ctx* c, int64_t t, double eta0, double lam_grad, ui
   a.slab_loss = (metric_flags & DOPT_RUN_OBJECTIVE) ? c->slab_loss : nullptr;
   int rc;
   if (c->prof && (rc = prof_event(c, false))) return rc;
-  HIPOK(launch_rs_pass(dt, true, a, c->stream));
+  HIPOK(launch_rs_pass(dt, rs_xdt(c), true, a, c->stream));
   if (c->prof && (rc = prof_event(c, true))) return rc;
   HIPOK(launch_rs_rows(dt, a, (int)c->n, 2 | (met ? 1 : 0), c->stream));
   HIPOK(launch_rs_csum(a, sum_dev, c->stream));
@@ -2132,7 +2155,7 @@ int dopt_rs_phase_metrics(dopt_ctx* c, uint32_t metric_flags) {
   a.xbar = c->xbar[c->xb];
   a.slab_cons = (metric_flags & DOPT_RUN_CONSENSUS) ? c->slab_cons : nullptr;
   a.slab_loss = (metric_flags & DOPT_RUN_OBJECTIVE) ? c->slab_loss : nullptr;
-  HIPOK(launch_rs_pass(dt, false, a, c->stream));
+  HIPOK(launch_rs_pass(dt, rs_xdt(c), false, a, c->stream));
   HIPOK(launch_rs_rows(dt, a, (int)c->n, 1, c->stream));
   c->cons_n = c->n;
   c->slab_n[0] = c->n;

@@ -23,8 +23,8 @@ def _data(sizes, d, seed, problem="quadratic", scale=1.0):
     return shards
 
 
-def _engine(shards, dtype="float64", problem="quadratic"):
-    eng = _dopt.Engine(0, dtype)
+def _engine(shards, dtype="float64", problem="quadratic", data_dtype=None):
+    eng = _dopt.Engine(0, dtype, data_dtype=data_dtype)
     off = np.concatenate([[0], np.cumsum([len(s[1]) for s in shards])])
     eng.load_shards(problem, np.vstack([s[0] for s in shards]), np.concatenate([s[1] for s in shards]), off)
     n = len(shards)
@@ -318,3 +318,50 @@ def test_rowspace_float32_accuracy_not_worse_than_direct(monkeypatch):
     print("float32 max relative error (objective, consensus): row-space", err["1"], "direct", err["0"])
     assert err["1"][0] < 1e-4 and err["1"][1] < 1e-3, err
     assert err["1"][0] <= 2 * err["0"][0] + 1e-6 and err["1"][1] <= 2 * err["0"][1] + 1e-6, err
+
+
+@pytest.mark.parametrize("problem", ["quadratic", "logistic"])
+def test_rowspace_x32_float32_rows_float64_arithmetic(problem):
+    """Float32-stored rows under float64 arithmetic (k_rs_pass_x32, the C3 headline's layout) past
+    the row-resident kernel: on float32-representable data the same rounds as float64-stored rows
+    (float64 sums in another order: rtol 1e-12) and the oracle's (rtol 1e-9); the iterates formed
+    by k_rs_materialise_x32."""
+    sizes, d, T = [16, 9, 16, 4, 16, 12, 16], 2100, 8
+    shards = [(X.astype(np.float32).astype(np.float64), y.astype(np.float32).astype(np.float64))
+              for X, y in _data(sizes, d, 37, problem, scale=d ** -0.5)]
+    b = max(sizes)
+    lam_g = 2e-3 if problem == "quadratic" else 1e-3
+    out = {}
+    for xdt in ("float32", None):
+        eng = _engine(shards, problem=problem, data_dtype=xdt)
+        obj, cons, _ = eng.run_dsgd(T, 0.05, b, lam_g, 1e-3, 0.1)
+        out[xdt] = (np.asarray(obj), np.asarray(cons), eng.get_models(), _dopt.last_round_kernel())
+        eng.close()
+    assert out["float32"][3].startswith("void dopt::k_rs_pass_x32<true,"), out["float32"][3]
+    assert out[None][3].startswith("void dopt::k_rs_pass<double, true,")
+    for u, v in zip(out["float32"][:3], out[None][:3]):
+        np.testing.assert_allclose(u, v, rtol=1e-12, atol=1e-15 * np.abs(v).max())
+    Xf = np.vstack([s_[0] for s_ in shards])
+    yf = np.concatenate([s_[1] for s_ in shards])
+    h, _, xr, _ = O.run_decentralized(shards, TP.fully_connected(len(sizes)).dense_W(), T, _cfg(b, problem), Xf, yf,
+                                      0.1)
+    np.testing.assert_allclose(out["float32"][0], h["objective"], rtol=1e-9)
+    np.testing.assert_allclose(out["float32"][1], h["consensus_error"], rtol=1e-9)
+    np.testing.assert_allclose(out["float32"][2], xr, rtol=1e-9, atol=1e-12 * np.abs(xr).max())
+
+
+def test_rowspace_x32_refuses_direct_rounds():
+    """Float32 rows under float64 arithmetic past the row-resident kernel: runs the row-space
+    rounds cannot take (unequal starts, minibatches) fail loudly instead of reading the rows as
+    float64."""
+    sizes, d = [8] * 5, 2100
+    shards = _data(sizes, d, 43, scale=d ** -0.5)
+    eng = _engine(shards, data_dtype="float32")
+    x0 = np.random.default_rng(0).standard_normal((len(sizes), d))
+    eng.set_models(x0)
+    with pytest.raises(Exception, match="row-space"):
+        eng.run_dsgd(2, 0.05, 8, 2e-3, 1e-3, 0.0)
+    eng.set_models(np.zeros((len(sizes), d)))
+    eng.run_dsgd(2, 0.05, 8, 2e-3, 1e-3, 0.0)
+    assert "k_rs_pass_x32" in _dopt.last_round_kernel()
+    eng.close()

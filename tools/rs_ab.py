@@ -22,9 +22,11 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--n", type=int, default=1024)
     ap.add_argument("--dtype", default="float32")
+    ap.add_argument("--data-dtype", default=None, help="float32: rows stored as float32 under float64 arithmetic")
     args = ap.parse_args()
     n, d, m = args.n, 1 << 20, 16
-    eng = _dopt.Engine(0, args.dtype)
+    eng = _dopt.Engine(0, args.dtype, data_dtype=args.data_dtype)
+    xesz = 4 if (args.data_dtype or args.dtype) == "float32" else 8
     eng.generate_shards("quadratic", n, d, m, seed=3, noise=10.0)
     top = TP.fully_connected(n)
     zeros = np.zeros((n, d), dtype=np.float32)
@@ -51,7 +53,7 @@ def main():
             eng.run_dsgd_pipelined(0, 1e-5, m, 1e-4, 1e-4, 0.0)
             res.setdefault(sh, []).append((ms / k, dt * 1e3))
             print(f"rep {rep} shape {sh}: kernel {ms / k:.3f} ms, round {dt * 1e3:.3f} ms "
-                  f"({n * m * d * (4 if args.dtype == 'float32' else 8) / (ms / k) / 1e9:.0f} GB/s), setup {tb:.2f} s "
+                  f"({n * m * d * xesz / (ms / k) / 1e9:.2f} TB/s), setup {tb:.2f} s "
                   f"[{_dopt.last_round_kernel()}]", flush=True)
     for sh, v in res.items():
         print(sh, "best kernel %.3f ms, best round %.3f ms" % (min(a for a, _ in v), min(b for _, b in v)))
