@@ -490,8 +490,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32" if esz == 4 else "f64",
-        "data": "synthetic (device-generated X~N(0,1) rounded to float32 + bias column, planted-w* labels, "
-                "5% flips)",
+        "data": (f"synthetic (device-generated X~N(0,1){' rounded to float32' if xesz == 4 else ''} + bias column, "
+                 "planted-w* labels, " + ("5% flips)" if problem == "logistic" else "noise 10)")),
         "config": {"workload": workload,
                    "timing": ("pipelined calls: the timed call holds exactly `steps` fused rounds and `steps` "
                               "metric evaluations (its first pass takes the warmup's last metrics, its last "

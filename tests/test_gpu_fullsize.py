@@ -152,3 +152,45 @@ def test_c5_rowspace_full_size_vs_direct(monkeypatch):
         np.testing.assert_allclose(x_rs, x_d, rtol=1e-4, atol=1e-5 * np.abs(x_d).max())
     finally:
         eng.close()
+
+
+def test_c5_x32_full_size_host_rounds():
+    """C5 at the reference's float64 arithmetic over float32-stored rows (k_rs_pass_x32, the bench's
+    C5 default) from Worker.x = zeros: every round recomputed on the host for several workers
+    (mixing sum over all iterates, float64 gradient; trainer.py:173-175) at rtol 1e-8, consensus
+    over all iterates, and the per-round calls equal to one 3-round call."""
+    n, d, m, T, eta0, lam = 1024, 1 << 20, 16, 3, 1e-5, 1e-4
+    if _free_gb() < 90:
+        pytest.skip("needs ~85 GB of free HBM")
+    top = TP.fully_connected(n)
+    w_off, diag = top.uniform_offdiag()
+    eng = _dopt.Engine(0, "float64", data_dtype="float32")
+    try:
+        eng.generate_shards("quadratic", n, d, m, seed=3, noise=10.0)
+        eng.set_mixing_mean(w_off, diag)
+        o_all, c_all, _ = eng.run_dsgd(T, eta0, m, lam, lam, 0.0)
+        assert _dopt.last_round_kernel().startswith("void dopt::k_rs_pass_x32<true,")
+        x_all = eng.get_models()
+        eng.set_models(np.zeros((n, d)))
+        picks = [0, 1, 511, 1023, 77, 640]
+        shards = {i: eng.get_shard(i) for i in picks}
+        x = None
+        for t in range(T):
+            o, c, _ = eng.run_dsgd(1, eta0, m, lam, lam, 0.0, t0=t)
+            xn = eng.get_models()
+            eta = eta0 / np.sqrt(t + 1)
+            S = x.sum(axis=0) if x is not None else None
+            for i in picks:
+                X, y = shards[i]
+                xi = x[i] if x is not None else np.zeros(d)
+                mix = w_off * (S - xi) + diag[i] * xi if x is not None else np.zeros(d)
+                ref = mix - eta * O.quadratic_gradient(xi, X, y, lam)
+                np.testing.assert_allclose(xn[i], ref, rtol=1e-8, atol=1e-10 * np.abs(ref).max())
+            xb = xn.mean(axis=0)
+            np.testing.assert_allclose(c[0], np.mean(np.sum((xn - xb) ** 2, axis=1)), rtol=1e-8)
+            np.testing.assert_allclose(c[0], c_all[t], rtol=1e-12)
+            np.testing.assert_allclose(o[0], o_all[t], rtol=1e-12)
+            x = xn
+        np.testing.assert_allclose(x, x_all, rtol=1e-12, atol=1e-14 * np.abs(x_all).max())
+    finally:
+        eng.close()
