@@ -157,7 +157,14 @@ def test_rowspace_then_other_run_kinds():
 SIZES_D = [12, 7, 12, 3, 12, 12, 9, 12, 1, 12, 12, 5, 12]  # ragged shards over the ranks' slices
 
 
-def _rs_rank(rank, world, port, out, T, pipe=False):
+def _rs_data(x32):
+    shards = _data(SIZES_D, 2100, 12)
+    if x32:  # float32-representable values: float32 storage under float64 arithmetic is exact
+        shards = [(X.astype(np.float32).astype(np.float64), y.astype(np.float32).astype(np.float64)) for X, y in shards]
+    return shards
+
+
+def _rs_rank(rank, world, port, out, T, pipe=False, x32=False):
     import os
 
     import torch  # noqa: F401  (one HIP runtime, loaded before libdopt)
@@ -167,13 +174,13 @@ def _rs_rank(rank, world, port, out, T, pipe=False):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    shards = _data(SIZES_D, 2100, 12)
+    shards = _rs_data(x32)
     n = len(shards)
     bounds = Dm.partition_bounds(n, world)
     lo, hi = int(bounds[rank]), int(bounds[rank + 1])
     plan = Dm.HaloPlan(rank, world, bounds, lo, hi, np.zeros(0, np.int64), np.zeros(world + 1, np.int64),
                        np.zeros(0, np.int32), np.zeros(world + 1, np.int64), None, None, None)
-    eng = _dopt.Engine(0, "float64")
+    eng = _dopt.Engine(0, "float64", data_dtype="float32" if x32 else None)
     mine = shards[lo:hi]
     off = np.concatenate([[0], np.cumsum([len(s[1]) for s in mine])])
     eng.load_shards("quadratic", np.vstack([s[0] for s in mine]), np.concatenate([s[1] for s in mine]), off)
@@ -199,11 +206,12 @@ def _rs_rank(rank, world, port, out, T, pipe=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,pipe", [(2, False), (3, False), (2, True)])
-def test_rowspace_ranks_vs_oracle(tmp_path, world, pipe):
+@pytest.mark.parametrize("world,pipe,x32", [(2, False, False), (3, False, False), (2, True, False), (2, True, True)])
+def test_rowspace_ranks_vs_oracle(tmp_path, world, pipe, x32):
     """Row-space rounds across ranks (gloo, contexts sharing the GPU): each rank's pass gives its
     column sums, all-reduced into the replicated average; history and gathered iterates vs the
-    oracle at rtol 1e-9 (float64); pipe: the later rounds as a chain of pipelined calls."""
+    oracle at rtol 1e-9 (float64); pipe: the later rounds as a chain of pipelined calls; x32:
+    float32-stored rows under float64 arithmetic (k_rs_pass_x32)."""
     import socket
 
     import torch.multiprocessing as mp
@@ -213,11 +221,11 @@ def test_rowspace_ranks_vs_oracle(tmp_path, world, pipe):
     port = s.getsockname()[1]
     s.close()
     T = 7
-    mp.start_processes(_rs_rank, args=(world, port, str(tmp_path), T, pipe), nprocs=world, join=True,
+    mp.start_processes(_rs_rank, args=(world, port, str(tmp_path), T, pipe, x32), nprocs=world, join=True,
                        start_method="spawn")
     got = np.load(tmp_path / "rs.npz")
-    assert "k_rs_pass<double, true" in str(got["kern"])
-    shards = _data(SIZES_D, 2100, 12)
+    assert ("k_rs_pass_x32<true" if x32 else "k_rs_pass<double, true") in str(got["kern"])
+    shards = _rs_data(x32)
     n = len(shards)
     Xf = np.vstack([s[0] for s in shards])
     yf = np.concatenate([s[1] for s in shards])
