@@ -507,7 +507,8 @@ def main():
                                    f"slices per GPU, "
                                    f"{'all-reduce of the column sums' if mean is not None else 'halo send/recv + all-reduce'}"
                                    f" ({args.backend})") if world > 1
-                                  else ("single GPU: the multi-GPU phase path (lagged schedule, "
+                                  else ("single GPU: the multi-GPU phase path ("
+                                        f"{'row-space rounds, all-reduce of the column sums' if mean is not None else 'lagged schedule'}, "
                                         f"{args.backend} world 1)") if args.phase
                                   else ("single GPU: row-space rounds (the pass over the rows, then per-worker "
                                         "and per-column updates; DESIGN.md 6c)") if "k_rs_pass" in kname
