@@ -16,10 +16,13 @@ the float32 engine ('f32'), the device f(x*) solver (final suboptimality, as
 trainer.py:189-191 reports objective - f_opt), and the drop-in DecentralizedTrainer at C3
 with the reference's legacy RNG stream ('dropin').
 
-Multi-GPU (`--gpus N` under torch.distributed.run): ONE random 4-regular graph over
-4096 x N workers (weak scaling), each rank owning a contiguous slice; halo rows of
-the iterates move by grouped send/recv (RCCL) while the gradient kernel runs, and
-the average model is all-reduced every round (distributed.py).
+Multi-GPU: `python3 bench.py --gpus N` starts N ranks itself (torch.distributed.run as a
+child process, before anything touches the GPU); under an external torch.distributed.run
+WORLD_SIZE must equal --gpus.  Weak scaling (`value`): ONE random 4-regular graph over
+4096 x N workers, graph-partitioned so each rank owns a contiguous slice; halo rows of the
+iterates move by grouped send/recv (RCCL) while the gradient kernel runs, and the average
+model is all-reduced every round (distributed.py).  Strong scaling (`strong`, N > 1): the
+metric's literal N = 4096 workers in total over the N ranks, same graph construction.
 
 Prints ONE JSON line on rank 0 (driver contract), with `roofline` for the fused
 round kernel (HIP-event timed, same timed region) and `cpu_baseline` (the oracle,
@@ -29,6 +32,7 @@ import argparse
 import json
 import math
 import os
+import subprocess
 import sys
 import time
 
@@ -65,23 +69,17 @@ def pmc_traffic(kernel_name, config="c3"):
     return None, None
 
 
-def cpu_baseline(seconds, n_workers=64, d=1024, m=512, seed=11):
-    """The oracle (numpy restatement of the reference round, float64) on a bounded
-    sample: n_workers workers of the C3 shape, same per-round work as the reference
-    (per-worker minibatch draw + gradient, dense W @ X, objective over all sample rows,
-    consensus)."""
+# ---------------------------------------------------------------------------- CPU baseline
+def _cpu_sample(n_workers, d, m, seed, seconds):
+    """One process's share of the CPU baseline: the oracle's round (numpy float64 restatement
+    of trainer.py:161-193) on n_workers workers of the C3 shape for about `seconds`.
+    Returns (worker-iters/s, rounds, wall seconds)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
 
     import dsgd_oracle as O
     import topology
 
-    try:
-        from threadpoolctl import threadpool_info
-
-        threads = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
-    except Exception:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
     rng = np.random.default_rng(seed)
     wstar = rng.standard_normal(d)
     shards = []
@@ -104,22 +102,64 @@ def cpu_baseline(seconds, n_workers=64, d=1024, m=512, seed=11):
     t0 = time.perf_counter()
     O.run_decentralized(shards, W, rounds, cfg, Xf, yf, 0.0)
     dt = time.perf_counter() - t0
+    return n_workers * rounds / dt, rounds, dt
+
+
+def cpu_worker_main(argv):
+    """`bench.py --cpu-worker SEED SECONDS`: one single-threaded sample process (BLAS threads
+    set to 1 in its environment by the parent); prints its result as one JSON line."""
+    seed, seconds = int(argv[0]), float(argv[1])
+    rate, rounds, dt = _cpu_sample(64, 1024, 512, seed, seconds)
+    print(json.dumps({"rate": rate, "rounds": rounds, "wall_s": dt}), flush=True)
+
+
+def _cpu_share():
+    """CPUs this process may use: the affinity mask, capped at the GPU box's CPU share per GPU
+    (16: the pool grants 16 host CPUs per GPU, although nproc shows the whole machine)."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        avail = os.cpu_count() or 1
+    return max(1, min(avail, int(os.environ.get("DOPT_CPU_SHARE", "16"))))
+
+
+def cpu_baseline(seconds, procs=None):
+    """The oracle on the host cores: `procs` single-threaded processes (one per core of the
+    box's CPU share), each running its own 64-worker sample of the C3 shape concurrently for
+    ~`seconds`; value = the sum of their worker-iters/s.  Per-worker work is independent of N
+    but for the dense W @ X (trainer.py:173), 0.08-0.14 s of a 9.25 s reference round at
+    N = 4096: under 2 % of it, so per-worker extrapolation to 4096 flatters the
+    CPU by at most that much."""
+    procs = procs or _cpu_share()
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    env.pop("DOPT_CPU_SHARE", None)
+    ps = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker", str(11 + k), str(seconds)],
+                           stdout=subprocess.PIPE, env=env) for k in range(procs)]
+    res = []
+    for p in ps:
+        out, _ = p.communicate(timeout=seconds * 6 + 120)
+        if p.returncode != 0:
+            raise RuntimeError(f"cpu baseline worker exited {p.returncode}")
+        res.append(json.loads(out.decode().strip().splitlines()[-1]))
     cpu_model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
             cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), cpu_model)
     except OSError:
         pass
-    return {"value": n_workers * rounds / dt, "unit": "worker-iters/s", "cores": int(threads), "kind": "port",
-            "cpu_model": cpu_model, "nproc": os.cpu_count(),
-            "blas_threads": int(threads),
-            "sample": f"oracle (numpy float64 restatement of trainer.py:161-193) on {n_workers} workers x "
-                      f"{m} rows x d={d}, {rounds} rounds, {dt:.1f} s, full-shard batches, metrics every round; "
-                      f"extrapolated per worker to C3's 4096 (its dense W @ X, 0.08-0.14 s of a 9.25 s reference "
-                      f"round at N=4096 (SURVEY.md 3.3), is under 2 % of the per-worker work, so the "
-                      f"extrapolation flatters the CPU by at most that much)"}
+    rates = [r["rate"] for r in res]
+    return {"value": float(sum(rates)), "unit": "worker-iters/s", "cores": procs, "kind": "port",
+            "cpu_model": cpu_model, "nproc": os.cpu_count(), "processes": procs, "blas_threads_per_process": 1,
+            "per_process_rate": [float(r) for r in rates],
+            "sample": f"oracle (numpy float64 restatement of trainer.py:161-193), {procs} concurrent single-threaded "
+                      f"processes, each 64 workers x 512 rows x d=1024 ({min(r['rounds'] for r in res)}-"
+                      f"{max(r['rounds'] for r in res)} rounds, ~{seconds:.0f} s), full-shard batches, metrics every "
+                      f"round; aggregate per-worker rate, i.e. extrapolated per worker to C3's 4096 (the dense "
+                      f"W @ X is under 2 % of a reference round at N = 4096, SURVEY.md 3.3); cores = the box's CPU "
+                      f"share per GPU (affinity {len(os.sched_getaffinity(0))} CPUs, capped at 16)"}
 
 
+# ---------------------------------------------------------------------------- legs
 def pcie_leg(eng, top, n, d, m, b, lam, eta0, steps, dt_resident):
     """Boundary cost when the caller hands over host buffers (Worker.local_data numpy arrays
     -> dopt_load_shards): the device-generated shards are copied to host memory once
@@ -308,13 +348,230 @@ def dropin_leg(eng, n, d, m, lam, eta0, rounds=128):
                     "chunk ahead of the device); per-round rate excludes the fixed per-run cost"}
 
 
+# ---------------------------------------------------------------------------- launch
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv, limit_s):
+    """`--gpus N > 1` without an external launcher: run torch.distributed.run with N ranks on
+    this node as a CHILD process (this process has not touched the GPU and never does), pass
+    its output through, and return its exit code -- the worst rank's, as the launcher reports
+    it.  The child gets its own process group, ended whole if it outlives `limit_s`."""
+    import signal
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+    log(f"launching {n} ranks: {' '.join(cmd[1:])}")
+    p = subprocess.Popen(cmd, start_new_session=True)
+    try:
+        return p.wait(timeout=limit_s)
+    except subprocess.TimeoutExpired:
+        log(f"ranks still running after {limit_s:.0f} s: ending the launcher's process group")
+        os.killpg(p.pid, signal.SIGTERM)
+        try:
+            p.wait(timeout=20)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+        return 124
+    except KeyboardInterrupt:
+        os.killpg(p.pid, signal.SIGTERM)
+        p.wait()
+        return 130
+
+
+def dry_launch(args, rank, world, local):
+    """--dry-launch: the rank layout without any device work -- every rank joins a gloo
+    process group (bounded by the job timeout) and rank 0 prints who came up."""
+    import socket
+
+    import torch.distributed as dist
+
+    import distributed
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if "MASTER_PORT" not in os.environ:
+        os.environ["MASTER_PORT"] = str(_free_port())
+    distributed.init_process_group("gloo", rank=rank, world_size=world)
+    me = {"rank": rank, "local_rank": local, "pid": os.getpid(), "host": socket.gethostname()}
+    every = [None] * world
+    dist.all_gather_object(every, me)
+    if rank == 0:
+        print(json.dumps({"dry_launch": True, "n_gpus": world, "requested_backend": args.backend,
+                          "comm": {"world_size": dist.get_world_size(), "backend": dist.get_backend()},
+                          "ranks": every}), flush=True)
+    dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------- a leg
+class Setup:
+    """One configuration's engine, plan and round callables on this rank."""
+
+
+def setup_leg(args, config, n_global, world, rank, dev):
+    import numpy as np
+    import torch.distributed as dist
+
+    import _dopt
+    import distributed
+    import topology
+
+    S = Setup()
+    S.problem, S.mean, S.eta0 = "logistic", None, 0.05
+    if config == "c3":
+        S.d, S.m = args.d, args.m
+        S.top = topology.random_regular(n_global, args.degree, seed=0)
+        if world > 1 and args.partition == "spectral":  # relabel so each GPU's part is an id range
+            order = [distributed.partition_order(distributed.graph_partition(S.top, world)) if rank == 0 else None]
+            dist.broadcast_object_list(order, src=0)
+            S.top = topology.relabel(S.top, order[0])
+        S.workload = (f"C3: logistic, {n_global // world if n_global % world == 0 else n_global / world} "
+                      f"workers/GPU ({n_global} in all), d={S.d}, m=b={S.m}, random {args.degree}-regular MH "
+                      "mixing, objective+consensus every round")
+    elif config == "c4":
+        S.d, S.m = 1024, 512
+        S.top = topology.grid(n_global)
+        S.workload = f"C4: logistic, {n_global} workers total on a 256x256 torus, d=1024, m=b=512"
+    else:
+        S.problem, S.d, S.m = "quadratic", 1 << 20, 16
+        S.eta0 = 1e-5  # L ~ d/b for N(0,1) rows of length 2^20: eta0 = 0.05 (set for d = 81) diverges
+        S.top = topology.fully_connected(n_global)
+        S.mean = S.top.uniform_offdiag()
+        S.workload = f"C5: quadratic, {n_global} workers total, d=2^20, m=b=16, complete graph (column-sum mixing)"
+    S.n_global = n_global
+    plan = distributed.build_plan(S.top, world, rank) if S.mean is None else None
+    if plan is None:  # complete graph: contiguous slices, no halo plan needed
+        bounds = distributed.partition_bounds(n_global, world)
+        plan = distributed.HaloPlan(rank, world, bounds, int(bounds[rank]), int(bounds[rank + 1]),
+                                    np.zeros(0, np.int64), np.zeros(world + 1, np.int64), np.zeros(0, np.int32),
+                                    np.zeros(world + 1, np.int64), None, None, None)
+    S.plan = plan
+    d, m = S.d, S.m
+    data_dtype = args.data_dtype
+    if args.dtype in ("float32", "fp32", "f32") or (_chunks_per_lane(d, 4) > 8 and S.mean is None):
+        # float32 engine, or rows beyond the mixed row-resident kernel off the complete graph: storage =
+        # compute dtype (the complete graph's row-space rounds read float32 rows under float64
+        # arithmetic: k_rs_pass_x32)
+        data_dtype = None
+    log(f"rank {rank}/{world}: generating {plan.n_local} x {m} x {d} shards ({args.dtype} arithmetic, "
+        f"{data_dtype or args.dtype} storage) on device {dev}")
+    eng = _dopt.Engine(dev, args.dtype, data_dtype=data_dtype)
+    S.eng = eng
+    eng.generate_shards(S.problem, plan.n_local, d, m, seed=1000, flip=0.05, first_worker=plan.lo)
+    S.lam = lam = 1e-4
+    S.b = b = args.batch if 0 < args.batch < m else m
+    if b < m:  # minibatches drawn on the device inside the pass over all rows (the metrics need them all)
+        if config != "c3":
+            raise SystemExit("--batch < m: C3 only (device sampling)")
+        eng.set_sampler("device", seed=7, first_worker=plan.lo)
+        S.workload = S.workload.replace(f"m=b={m}", f"m={m}, b={b} (device-drawn minibatches)")
+    S.comm = None
+    eta0 = S.eta0
+    if world > 1 or args.phase:
+        mean_local = None if S.mean is None else (S.mean[0], S.mean[1][plan.lo:plan.hi])
+        runner = distributed.DistributedDSGD(eng, plan, n_global, n_global * m, device=dev, mean=mean_local)
+        ld, esz_state = eng.layout()
+        S.comm = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                  "halo_rows_in": int(plan.n_halo), "send_rows_out": int(len(plan.send_ids)),
+                  "halo_bytes_in_per_round": int(plan.n_halo) * ld * esz_state,
+                  "send_bytes_out_per_round": int(len(plan.send_ids)) * ld * esz_state,
+                  "peers": [int(p) for p in runner._peers],
+                  "allreduce_bytes_per_round": ld * 8}
+        log(f"comm: {S.comm}")
+        if runner._lagged_ok or (S.mean is not None and runner._rowspace_ready()):
+            # the lagged schedule / the row-space rounds continued across calls (as on one GPU: timed_leg)
+            S.rounds = lambda k: runner.run_pipelined(k, eta0, b, lam, lam, 0.0)
+            S.flush = lambda: runner.run_pipelined(0, eta0, b, lam, lam, 0.0)
+        else:
+            S.rounds = lambda k: runner.run(k, eta0, b, lam, lam, 0.0)
+            S.flush = None
+    else:
+        if S.mean is not None:
+            eng.set_mixing_mean(*S.mean)
+        else:
+            eng.set_topology(S.top.row_ptr, S.top.col, S.top.w)
+        # metrics pipelined across calls (dopt_run_dsgd_pipelined; timed_leg)
+        S.rounds = lambda k: eng.run_dsgd_pipelined(k, eta0, b, lam, lam, 0.0)
+        S.flush = lambda: eng.run_dsgd_pipelined(0, eta0, b, lam, lam, 0.0)
+    return S
+
+
+def run_leg(S, args, world, barrier, dev):
+    """Time the leg; returns (wall seconds max over ranks, launches, kernel ms, every, obj, cons)."""
+    import torch
+    import torch.distributed as dist
+
+    log(f"warmup {args.warmup}, timing {args.steps} rounds ({S.workload})")
+    dt, launches, kr_ms, every, obj, cons = timed_leg(S.eng, S.rounds, args.steps, args.warmup, S.plan.n_local,
+                                                      S.d, barrier, args.event_every, S.flush)
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}" if args.backend == "nccl" else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    return dt, launches, kr_ms, every, obj, cons
+
+
+def per_rank(world, item):
+    """item of every rank (rank order), gathered on every rank (host objects)."""
+    import torch.distributed as dist
+
+    if world == 1:
+        return [item]
+    out = [None] * world
+    dist.all_gather_object(out, item)
+    return out
+
+
+def strong_leg(args, world, rank, dev, barrier):
+    """The metric's literal configuration: N = args.strong_workers (4096) workers in TOTAL over
+    the ranks (4096 / world each), the same random 4-regular graph construction and spectral
+    partition as the weak-scaling leg; every rank's kernel time and halo bytes are reported."""
+    import _dopt
+
+    S = setup_leg(args, "c3", args.strong_workers, world, rank, dev)
+    try:
+        dt, launches, kr_ms, every, obj, cons = run_leg(S, args, world, barrier, dev)
+        kname = kernel_name()
+        bpl = bytes_per_round(S.eng, S.plan.n_local, S.d, S.m, kname)
+        avg_ms = kr_ms / launches if launches else float("nan")
+        mine = {"rank": rank, "workers": int(S.plan.n_local), "kernel_avg_ms": avg_ms,
+                "roofline_frac": bpl / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if launches else None,
+                "halo_rows_in": int(S.plan.n_halo),
+                "halo_bytes_in_per_round": (S.comm or {}).get("halo_bytes_in_per_round", 0),
+                "send_bytes_out_per_round": (S.comm or {}).get("send_bytes_out_per_round", 0),
+                "peers": (S.comm or {}).get("peers", [])}
+        ranks = per_rank(world, mine)
+        return {"value": S.n_global * args.steps / dt, "unit": "worker-iters/s", "n_workers_total": S.n_global,
+                "workers_per_gpu": S.n_global / world, "ms_per_step": dt / args.steps * 1e3,
+                "scaling": "strong", "kernel": kname, "per_rank": ranks,
+                "final_objective": float(obj[-1]), "final_consensus": float(cons[-1]),
+                "dtype": "f32" if S.eng.dtype == _dopt.F32 else "f64", "workload": S.workload}
+    finally:
+        S.eng.close()
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--cpu-worker":
+        return cpu_worker_main(sys.argv[2:])
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of this node; N > 1 without an external torch.distributed.run starts "
+                         "the N ranks itself.  Default: WORLD_SIZE, or 1")
     ap.add_argument("--steps", type=int, default=300,
                     help="rounds timed (one run: the last round's metrics pass is amortised over them)")
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workers", type=int, default=4096, help="workers per GPU")
+    ap.add_argument("--workers", type=int, default=4096, help="workers per GPU (C3 weak scaling)")
+    ap.add_argument("--strong-workers", type=int, default=4096,
+                    help="C3 strong-scaling leg at N > 1: workers in total (the metric's N = 4096)")
+    ap.add_argument("--scaling", default="both", choices=["weak", "strong", "both"],
+                    help="C3 at N > 1: the weak leg (value), the strong leg (under 'strong'), or both")
     ap.add_argument("--d", type=int, default=1024)
     ap.add_argument("--m", type=int, default=512)
     ap.add_argument("--dtype", default="float64", help="iterates and arithmetic (the reference: float64)")
@@ -326,10 +583,17 @@ def main():
                          "draws the minibatches on the device (sampling='device', Philox + Floyd)")
     ap.add_argument("--degree", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-procs", type=int, default=0, help="CPU baseline processes (0: the box's CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="N=1: skip the f64-storage / f32 legs, the f(x*) solver and the drop-in trainer leg")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (gloo: 1-GPU rehearsal)")
+    ap.add_argument("--timeout", type=float, default=None,
+                    help="seconds any collective may take before the job fails (default DOPT_PG_TIMEOUT or 300)")
+    ap.add_argument("--launch-limit", type=float, default=1800.0,
+                    help="self-launched N > 1 runs: seconds before the whole rank group is ended")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="start the ranks and report them (gloo process group only, no GPU work)")
     ap.add_argument("--event-every", type=int, default=0,
                     help="bracket every k-th round kernel with a HIP event pair (0: steps // 10, i.e. 10 "
                          "sampled launches whatever --steps is). A pair costs ~4-30 us of round time")
@@ -346,110 +610,45 @@ def main():
                     help="c3 (default, the metric's config); c4: 256x256 torus, 65536 workers total; "
                          "c5: quadratic, d=2^20, m=b=16, 1024 workers total, complete graph")
     args = ap.parse_args()
+    if args.timeout is not None:
+        os.environ["DOPT_PG_TIMEOUT"] = str(args.timeout)
 
+    # ---- the rank layout, decided before anything touches the GPU
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus is not None and args.gpus > 1:
+            return launch_ranks(args.gpus, sys.argv[1:], args.launch_limit)
+        world = 1
+    else:
+        world = int(env_world)
+        if args.gpus is not None and args.gpus != world:
+            log(f"refusing: --gpus {args.gpus} but WORLD_SIZE={world} (the launcher started {world} ranks)")
+            return 2
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_launch:
+        return dry_launch(args, rank, world, local)
+
     import torch  # plumbing only: barrier + max-over-ranks (one HIP runtime, loaded first)
     import torch.distributed as dist
 
-    import numpy as np
-
     import _dopt
     import distributed
-    import topology
 
-    dev = local % max(1, torch.cuda.device_count())
+    ndev = torch.cuda.device_count()
+    if world > 1 and args.backend == "nccl" and ndev < world:
+        log(f"refusing: {world} ranks over RCCL need {world} GPUs, {ndev} visible (--backend gloo rehearses "
+            "several ranks on one GPU)")
+        return 2
+    dev = local % max(1, ndev)
     if world > 1 or args.phase:
         torch.cuda.set_device(dev)
         if world == 1:  # --phase on one GPU: the multi-GPU code path incl. RCCL (one rank)
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", "29533")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
             distributed.init_process_group(args.backend, rank=0, world_size=1)
         else:
             distributed.init_process_group(args.backend)
-
-    problem, mean, eta0 = "logistic", None, 0.05
-    if args.config == "c3":
-        n, d, m = args.workers, args.d, args.m
-        n_global = n * world
-        top = topology.random_regular(n_global, args.degree, seed=0)
-        if world > 1 and args.partition == "spectral":  # relabel so each GPU's part is an id range
-            order = [distributed.partition_order(distributed.graph_partition(top, world)) if rank == 0 else None]
-            dist.broadcast_object_list(order, src=0)
-            top = topology.relabel(top, order[0])
-        workload = (f"C3: logistic, {n} workers/GPU, d={d}, m=b={m}, random {args.degree}-regular MH mixing, "
-                    "objective+consensus every round")
-    elif args.config == "c4":
-        d, m, n_global = 1024, 512, 65536
-        top = topology.grid(n_global)
-        workload = "C4: logistic, 65536 workers total on a 256x256 torus, d=1024, m=b=512"
-    else:
-        problem, d, m, n_global = "quadratic", 1 << 20, 16, 1024
-        eta0 = 1e-5  # L ~ d/b for N(0,1) rows of length 2^20: eta0 = 0.05 (set for d = 81) diverges
-        top = topology.fully_connected(n_global)
-        mean = top.uniform_offdiag()
-        workload = "C5: quadratic, 1024 workers total, d=2^20, m=b=16, complete graph (column-sum mixing)"
-    plan = distributed.build_plan(top, world, rank) if mean is None else None
-    if plan is None:  # complete graph: contiguous slices, no halo plan needed
-        bounds = distributed.partition_bounds(n_global, world)
-        plan = distributed.HaloPlan(rank, world, bounds, int(bounds[rank]), int(bounds[rank + 1]),
-                                    np.zeros(0, np.int64), np.zeros(world + 1, np.int64), np.zeros(0, np.int32),
-                                    np.zeros(world + 1, np.int64), None, None, None)
-    n = plan.n_local
-    data_dtype = args.data_dtype
-    if args.dtype in ("float32", "fp32", "f32") or (_chunks_per_lane(d, 4) > 8 and mean is None):
-        # float32 engine, or rows beyond the mixed row-resident kernel off the complete graph: storage =
-        # compute dtype (the complete graph's row-space rounds read float32 rows under float64
-        # arithmetic: k_rs_pass_x32)
-        data_dtype = None
-    log(f"rank {rank}/{world}: generating {plan.n_local} x {m} x {d} shards ({args.dtype} arithmetic, "
-        f"{data_dtype or args.dtype} storage) on device {dev}")
-    eng = _dopt.Engine(dev, args.dtype, data_dtype=data_dtype)
-    eng.generate_shards(problem, plan.n_local, d, m, seed=1000, flip=0.05, first_worker=plan.lo)
-    lam = 1e-4
-    b = args.batch if 0 < args.batch < m else m
-    if b < m:  # minibatches drawn on the device inside the pass over all rows (the metrics need them all)
-        if args.config != "c3":
-            raise SystemExit("--batch < m: C3 only (device sampling)")
-        eng.set_sampler("device", seed=7, first_worker=plan.lo)
-        workload = workload.replace(f"m=b={m}", f"m={m}, b={b} (device-drawn minibatches)")
-    comm = None
-    if world > 1 or args.phase:
-        mean_local = None if mean is None else (mean[0], mean[1][plan.lo:plan.hi])
-        runner = distributed.DistributedDSGD(eng, plan, n_global, n_global * m, device=dev, mean=mean_local)
-        ld, esz_state = eng.layout()
-        comm = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
-                "halo_rows_in": int(plan.n_halo), "send_rows_out": int(len(plan.send_ids)),
-                "halo_bytes_in_per_round": int(plan.n_halo) * ld * esz_state,
-                "send_bytes_out_per_round": int(len(plan.send_ids)) * ld * esz_state,
-                "peers": [int(p) for p in runner._peers],
-                "allreduce_bytes_per_round": ld * 8}
-        log(f"comm: {comm}")
-
-        if runner._lagged_ok or (mean is not None and runner._rowspace_ready()):
-            # the lagged schedule / the row-space rounds continued across calls (as on one GPU: timed_leg)
-            def rounds(k):
-                return runner.run_pipelined(k, eta0, b, lam, lam, 0.0)
-
-            def flush():
-                return runner.run_pipelined(0, eta0, b, lam, lam, 0.0)
-        else:
-            def rounds(k):
-                return runner.run(k, eta0, b, lam, lam, 0.0)
-
-            flush = None
-    else:
-        if mean is not None:
-            eng.set_mixing_mean(*mean)
-        else:
-            eng.set_topology(top.row_ptr, top.col, top.w)
-
-        def rounds(k):  # metrics pipelined across calls (dopt_run_dsgd_pipelined; timed_leg)
-            return eng.run_dsgd_pipelined(k, eta0, b, lam, lam, 0.0)
-
-        def flush():
-            return eng.run_dsgd_pipelined(0, eta0, b, lam, lam, 0.0)
 
     def barrier():
         if world > 1:
@@ -459,13 +658,14 @@ def main():
                 dist.barrier()
         torch.cuda.synchronize(dev)
 
-    log(f"warmup {args.warmup}, timing {args.steps} rounds")
-    dt, launches, kr_ms, every, obj, cons = timed_leg(eng, rounds, args.steps, args.warmup, plan.n_local, d, barrier,
-                                                      args.event_every, flush)
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}" if args.backend == "nccl" else "cpu")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    weak = args.config != "c3" or world == 1 or args.scaling != "strong"
+    n_global = {"c3": args.workers * world, "c4": 65536, "c5": 1024}[args.config]
+    if not weak:  # --scaling strong: the strong leg is the headline
+        n_global = args.strong_workers
+    S = setup_leg(args, args.config, n_global, world, rank, dev)
+    eng, plan, d, m, b, lam, eta0, top = S.eng, S.plan, S.d, S.m, S.b, S.lam, S.eta0, S.top
+    n = plan.n_local
+    dt, launches, kr_ms, every, obj, cons = run_leg(S, args, world, barrier, dev)
 
     esz = 4 if eng.dtype == _dopt.F32 else 8
     xesz = 4 if eng.data_dtype == _dopt.F32 else 8
@@ -475,9 +675,10 @@ def main():
     bytes_per_launch = bytes_per_round(eng, n, d, m, kname)
     avg_s = (kr_ms / launches) * 1e-3 if launches else float("nan")
     achieved = bytes_per_launch / avg_s / 1e9 if launches else None
-    value = n_global * args.steps / dt
+    value = S.n_global * args.steps / dt
     storage = ("float32 (every value exactly float32-representable; rows widened exactly to float64 as they "
                "are loaded)" if xesz == 4 and esz == 8 else ("float32" if esz == 4 else "float64"))
+    mean = S.mean
     out = {
         "metric": METRIC,
         "value": value,
@@ -487,22 +688,22 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if args.config == "c3" and weak else "strong",
         "vs_baseline": None,
         "dtype": "f32" if esz == 4 else "f64",
         "data": (f"synthetic (device-generated X~N(0,1){' rounded to float32' if xesz == 4 else ''} + bias column, "
-                 "planted-w* labels, " + ("5% flips)" if problem == "logistic" else "noise 10)")),
-        "config": {"workload": workload,
+                 "planted-w* labels, " + ("5% flips)" if S.problem == "logistic" else "noise 10)")),
+        "config": {"workload": S.workload,
                    "timing": ("pipelined calls: the timed call holds exactly `steps` fused rounds and `steps` "
                               "metric evaluations (its first pass takes the warmup's last metrics, its last "
                               "metrics are taken after the timed region; DESIGN.md section 7)"
-                              if flush is not None else "one call of `steps` rounds incl. its final metrics pass"),
+                              if S.flush is not None else "one call of `steps` rounds incl. its final metrics pass"),
                    "arithmetic": "float64" if esz == 8 else "float32",
                    "iterates": "float64" if esz == 8 else "float32", "shard_storage": storage,
-                   "workers_per_gpu": n, "d": d, "rows_per_worker": m, "batch": b, "topology": top.name,
-                   "degree": args.degree if args.config == "c3" else None,
+                   "workers_per_gpu": n, "workers_total": S.n_global, "d": d, "rows_per_worker": m, "batch": b,
+                   "topology": top.name, "degree": args.degree if args.config == "c3" else None,
                    "halo_rows_per_gpu": int(plan.n_halo),
-                   "parallelism": (f"dp{world}: one graph of {n_global} workers, "
+                   "parallelism": (f"dp{world}: one graph of {S.n_global} workers, "
                                    f"{'graph-partitioned' if args.config == 'c3' and args.partition == 'spectral' else 'contiguous'} "
                                    f"slices per GPU, "
                                    f"{'all-reduce of the column sums' if mean is not None else 'halo send/recv + all-reduce'}"
@@ -522,11 +723,15 @@ def main():
         "final_objective": float(obj[-1]),
         "final_consensus": float(cons[-1]),
     }
-    if comm is not None:
-        out["comm"] = comm
+    if S.comm is not None:
+        out["comm"] = S.comm
+    if world > 1:  # every rank's own kernel time and transfer volume
+        out["per_rank"] = per_rank(world, {"rank": rank, "workers": int(n),
+                                           "kernel_avg_ms": avg_s * 1e3 if launches else None,
+                                           "halo_bytes_in_per_round": (S.comm or {}).get("halo_bytes_in_per_round"),
+                                           "send_bytes_out_per_round": (S.comm or {}).get("send_bytes_out_per_round")})
     if args.config != "c3":
         out["metric"] = f"worker-iters/sec ({args.config.upper()}, secondary config)"
-        out["scaling"] = "strong"
     secondary = rank == 0 and world == 1 and not args.phase and args.config == "c3" and not args.no_secondary
     if secondary and b == m:
         log("f(x*): device L-BFGS")
@@ -536,6 +741,9 @@ def main():
     if args.pcie and world == 1 and args.config == "c3":
         out["pcie"] = pcie_leg(eng, top, n, d, m, b, lam, eta0, args.steps, dt)
     eng.close()
+    if args.config == "c3" and world > 1 and weak and args.scaling == "both":
+        log(f"strong-scaling leg: {args.strong_workers} workers over {world} ranks")
+        out["strong"] = strong_leg(args, world, rank, dev, barrier)
     if secondary and b == m:
         legs = {}
         if not (esz == 8 and xesz == 8):
@@ -549,12 +757,13 @@ def main():
         out["legs"] = legs
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
         log("cpu baseline")
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.cpu_procs or None)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1 or args.phase:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

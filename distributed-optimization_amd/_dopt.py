@@ -103,6 +103,7 @@ _SIGS = {
     "dopt_phase_set_round": ([_P, _I64], ctypes.c_int),
 }
 EXPORTED = tuple(_SIGS)
+ABI_VERSION = 2  # DOPT_ABI_VERSION of include/dopt.h
 
 
 def lib():
@@ -127,8 +128,8 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
-        if L.dopt_abi_version() != 1:
-            raise RuntimeError("libdopt.so ABI mismatch")
+        if L.dopt_abi_version() != ABI_VERSION:
+            raise RuntimeError(f"libdopt.so ABI {L.dopt_abi_version()} != {ABI_VERSION} (include/dopt.h): rebuild it")
         _lib = L
     return _lib
 
@@ -467,12 +468,14 @@ class Engine:
         check(lib().dopt_phase_loss_pass(self._h, 1 if two_points else 0))
 
     def rs_phase_begin(self, commit):
-        """(ok, sig): this rank's iterates all equal (row-space rounds possible) and a checksum of
-        that common iterate; commit=True also enters row-space mode."""
+        """(ok, hash): this rank's iterates all equal (row-space rounds possible) and the 64-bit
+        content hash of that common iterate (of the replicated state when already live, as a
+        signed int64); commit=True also enters row-space mode."""
         ok = ctypes.c_int(0)
-        sig = ctypes.c_double(0.0)
-        check(lib().dopt_rs_phase_begin(self._h, 1 if commit else 0, ctypes.byref(ok), ctypes.byref(sig)))
-        return bool(ok.value), float(sig.value)
+        h = ctypes.c_uint64(0)
+        check(lib().dopt_rs_phase_begin(self._h, 1 if commit else 0, ctypes.byref(ok), ctypes.byref(h)))
+        v = int(h.value)
+        return bool(ok.value), v - (1 << 64) if v >= (1 << 63) else v
 
     def rs_phase_round(self, t, eta0, lam_grad, metric_flags, sum_ptr):
         check(lib().dopt_rs_phase_round(self._h, int(t), float(eta0), float(lam_grad), int(metric_flags),

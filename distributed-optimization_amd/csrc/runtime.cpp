@@ -852,9 +852,27 @@ int rs_end(dopt_ctx* c) {
 
 enum { RS_FALLBACK = 1 };
 
-// Are the iterates xs[cur] all equal (*equal), and is that iterate zero (*zero)?  With sig != null
-// also a checksum of the first iterate (multi-rank callers compare it across ranks).
-int rs_check(dopt_ctx* c, bool* equal, bool* zero, double* sig) {
+// 64-bit content hash of a byte range (8-byte words through a multiply-rotate mix, a
+// SplitMix64-style finaliser): multi-rank callers compare the iterates ranks start from.
+uint64_t content_hash(const void* p, size_t n) {
+  const uint8_t* b = (const uint8_t*)p;
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    memcpy(&w, b + i, 8);
+    h ^= w * 0xBF58476D1CE4E5B9ull;
+    h = ((h << 27) | (h >> 37)) * 0x94D049BB133111EBull;
+  }
+  for (; i < n; ++i) h = (h ^ b[i]) * 0x100000001B3ull;
+  h ^= h >> 31;
+  h *= 0x9E3779B97F4A7C15ull;
+  return h ^ (h >> 29);
+}
+
+// Are the iterates xs[cur] all equal (*equal), and is that iterate zero (*zero)?  With hash != null
+// also the content hash of the first iterate's bytes (multi-rank callers compare it across ranks).
+int rs_check(dopt_ctx* c, bool* equal, bool* zero, uint64_t* hash) {
   int rc;
   if ((rc = ensure_rs(c))) return rc;
   const int dt = c->dtype == DOPT_F32 ? 0 : 1;
@@ -863,8 +881,8 @@ int rs_check(dopt_ctx* c, bool* equal, bool* zero, double* sig) {
                         c->stream));
   std::vector<int32_t> fl((size_t)(c->n + 1) * G);
   HIPOK(hipMemcpyAsync(fl.data(), c->rs_flags, fl.size() * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-  std::vector<char> row(sig ? (size_t)c->ld * c->esz : 0);
-  if (sig) HIPOK(hipMemcpyAsync(row.data(), c->xs[c->cur], row.size(), hipMemcpyDeviceToHost, c->stream));
+  std::vector<char> row(hash ? (size_t)c->d * c->esz : 0);
+  if (hash) HIPOK(hipMemcpyAsync(row.data(), c->xs[c->cur], row.size(), hipMemcpyDeviceToHost, c->stream));
   HIPOK(hipStreamSynchronize(c->stream));
   *equal = true;
   *zero = true;
@@ -872,13 +890,7 @@ int rs_check(dopt_ctx* c, bool* equal, bool* zero, double* sig) {
     if (fl[(size_t)k]) *equal = false;
   for (int g = 0; g < G; ++g)
     if (fl[(size_t)(c->n * G + g)]) *zero = false;
-  if (sig) {
-    double s = 0.0;
-    for (int64_t k = 0; k < c->d; ++k)
-      s += (double)(k % 1021 + 1) *
-           (c->esz == 4 ? (double)((const float*)row.data())[k] : ((const double*)row.data())[k]);
-    *sig = s;
-  }
+  if (hash) *hash = content_hash(row.data(), row.size());
   return DOPT_OK;
 }
 
@@ -2088,23 +2100,29 @@ int dopt_phase_mix_lagged(dopt_ctx* c, int64_t t, double eta0, const double* sum
 // ---- row-space rounds on a rank's slice (complete graph, quadratic, full shards; rowspace.hip).
 // The replicated d-vectors (xbar, Z) take the all-reduced column sums, so every rank holds
 // the same ones; the metric partials are this rank's workers' (folded by dopt_phase_fold).
-int dopt_rs_phase_begin(dopt_ctx* c, int commit, int* ok, double* sig) {
-  CHECK_ARG(c && ok && sig, "NULL argument");
+int dopt_rs_phase_begin(dopt_ctx* c, int commit, int* ok, uint64_t* hash) {
+  CHECK_ARG(c && ok && hash, "NULL argument");
   if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
   *ok = 0;
-  *sig = 0.0;
+  *hash = 0;
   if (!(rs_enabled() && c->split && c->mean_mix && c->wdiag_uniform && !c->obj_sep && c->min_m >= 1 &&
         c->max_m <= kRsMaxRows))
     return DOPT_OK;
   int rc;
   if ((rc = set_device(c))) return rc;
   if (c->rs_live) {  // (an open chain -- dopt_phase_chain -- stays open)
+    // the replicated part of the state (Z, then the float64 average), bitwise equal on every
+    // rank that took the same all-reduced sums
+    std::vector<double> zx(2 * (size_t)c->ld);
+    HIPOK(hipMemcpyAsync(zx.data(), c->rs_Z, zx.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPOK(hipStreamSynchronize(c->stream));
+    *hash = content_hash(zx.data(), zx.size() * sizeof(double));
     *ok = 1;
     return DOPT_OK;
   }
   c->carry_pending = false;
   bool equal = false, zero = false;
-  if ((rc = rs_check(c, &equal, &zero, sig))) return rc;
+  if ((rc = rs_check(c, &equal, &zero, hash))) return rc;
   if (!equal) return DOPT_OK;
   *ok = 1;
   if (!commit) return DOPT_OK;

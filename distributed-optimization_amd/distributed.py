@@ -35,17 +35,53 @@ import numpy as np
 import _dopt
 
 
-def init_process_group(backend, **kw):
-    """torch.distributed.init_process_group; for "nccl" (RCCL) with high-priority internal
+DEFAULT_TIMEOUT_S = 300.0
+
+
+class CollectiveError(RuntimeError):
+    """A collective or halo transfer of the round failed or timed out on this rank (peer and
+    operation named), instead of a hang until the driver's limit."""
+
+
+def timeout_seconds():
+    """Bound on every collective of a job (DOPT_PG_TIMEOUT seconds, default 300): a peer that
+    never joins a send/recv or all-reduce ends the job with an error within this time."""
+    return float(os.environ.get("DOPT_PG_TIMEOUT", DEFAULT_TIMEOUT_S))
+
+
+def init_process_group(backend, timeout=None, **kw):
+    """torch.distributed.init_process_group with a bounded collective timeout (`timeout`
+    seconds, default timeout_seconds()); for "nccl" (RCCL) with high-priority internal
     streams, so the halo send/recv and the all-reduce of a round get CU slots ahead of the
-    4096-workgroup gradient kernel they overlap (DOPT_NCCL_HIPRI=0: default priority)."""
+    4096-workgroup gradient kernel they overlap (DOPT_NCCL_HIPRI=0: default priority).
+    With RCCL the watchdog aborts a rank whose collective exceeds the timeout (the work, its
+    sequence number and op type in the message) and the launcher ends the other ranks; with
+    gloo the waiting call raises, which the transport below turns into CollectiveError."""
+    import datetime
+
     import torch.distributed as dist
 
     if backend == "nccl" and os.environ.get("DOPT_NCCL_HIPRI", "1") != "0":
         opts = dist.ProcessGroupNCCL.Options()
         opts.is_high_priority_stream = True
         kw["pg_options"] = opts
+    kw.setdefault("timeout", datetime.timedelta(seconds=timeout if timeout is not None else timeout_seconds()))
     dist.init_process_group(backend, **kw)
+
+
+def _wait(work, what, rank, timeout_s=None):
+    """work.wait(), with a failure or timeout re-raised as CollectiveError naming the rank and
+    the operation (`what`: op and peer).  For RCCL works the wait only orders the current
+    stream after the transfer (no host block); the process group's watchdog bounds them."""
+    import datetime
+
+    try:
+        if timeout_s is None:
+            work.wait()
+        else:
+            work.wait(datetime.timedelta(seconds=timeout_s))
+    except Exception as e:  # gloo: timeout / peer gone; RCCL: aborted communicator
+        raise CollectiveError(f"rank {rank}: {what} failed: {e}") from e
 
 
 def partition_bounds(n, world):
@@ -191,6 +227,61 @@ def build_plan(topo, world, rank):
                     w=topo.w[e0:e1].copy())
 
 
+class HaloExchange:
+    """The per-round halo transfer of a HaloPlan: rows send[send_off[p]:send_off[p+1]] go to
+    peer p, rows halo[recv_off[p]:recv_off[p+1]] come from peer p.
+
+    RCCL (device_comm): one grouped batch_isend_irecv over the device buffers, enqueued behind
+    the current stream's work; finish() makes the current stream wait for it (the host does not
+    block; the process group's watchdog bounds it).  gloo: the rows go through host memory and
+    finish() waits on the host with the job's timeout, so a peer that never sends ends this rank
+    with a CollectiveError naming it."""
+
+    def __init__(self, plan, send, halo, group=None, device_comm=False):
+        import torch.distributed as dist
+
+        self.dist, self.plan, self.group, self.device_comm = dist, plan, group, device_comm
+        self.send, self.halo = send, halo
+        self.peers = plan.peers()
+        self.rank = plan.rank
+
+    def _ops(self, send, halo):
+        """(kind, peer, buffer, rows) for every transfer, sends first per peer, peers ascending."""
+        P = self.plan
+        for p in self.peers:
+            s0, s1 = P.send_off[p], P.send_off[p + 1]
+            r0, r1 = P.recv_off[p], P.recv_off[p + 1]
+            if s1 > s0:
+                yield "isend", p, send[s0:s1], int(s1 - s0)
+            if r1 > r0:
+                yield "irecv", p, halo[r0:r1], int(r1 - r0)
+
+    def start(self):
+        if not self.peers:
+            return None
+        dist = self.dist
+        if self.device_comm:
+            ops = [dist.P2POp(dist.isend if k == "isend" else dist.irecv, buf, p, self.group)
+                   for k, p, buf, _ in self._ops(self.send, self.halo)]
+            return [(w, "batch_isend_irecv with peers %s" % self.peers) for w in dist.batch_isend_irecv(ops)]
+        send = self.send.cpu()
+        halo = self.halo.cpu()
+        works = []
+        for k, p, buf, rows in self._ops(send, halo):
+            fn = dist.isend if k == "isend" else dist.irecv
+            what = f"{k} of {rows} halo rows {'to' if k == 'isend' else 'from'} rank {p}"
+            works.append((fn(buf, p, group=self.group), what))
+        for w, what in works:
+            _wait(w, what, self.rank, timeout_seconds())
+        if halo.data_ptr() != self.halo.data_ptr():
+            self.halo.copy_(halo)
+        return None
+
+    def finish(self, works):
+        for w, what in works or ():
+            _wait(w, what, self.rank)
+
+
 class DistributedDSGD:
     """Drives one rank's engine through the round phases with torch.distributed."""
 
@@ -215,6 +306,7 @@ class DistributedDSGD:
         self.halo = torch.zeros((max(1, plan.n_halo), ld), dtype=tdt, device=self.dev)
         self.send = torch.zeros((max(1, len(plan.send_ids)), ld), dtype=tdt, device=self.dev)
         self.sum = torch.zeros(ld, dtype=torch.float64, device=self.dev)
+        self.exchange = HaloExchange(plan, self.send, self.halo, group, self.device_comm)
         engine.set_partition(self.n_global, self.rows_global)
         if mean is None:
             engine.set_halo(plan.n_halo, self.halo.data_ptr(), plan.send_ids, self.send.data_ptr())
@@ -224,6 +316,7 @@ class DistributedDSGD:
             engine.set_halo(0, None, np.zeros(0, np.int32), None)
             engine.set_mixing_mean(mean[0], mean[1])
             self._peers = []
+            self.exchange.peers = []
         self.mean = mean
         engine.set_stream(self.stream.cuda_stream)
         # the lagged schedule: CSR mixing on row-resident contexts (DOPT_LAGGED=0: the serial one)
@@ -238,38 +331,10 @@ class DistributedDSGD:
 
     # -- transport
     def _start_exchange(self):
-        P = self.plan
-        if not self._peers:
-            return None
-        if self.device_comm:
-            ops = []
-            for p in self._peers:
-                s0, s1 = P.send_off[p], P.send_off[p + 1]
-                r0, r1 = P.recv_off[p], P.recv_off[p + 1]
-                if s1 > s0:
-                    ops.append(self.dist.P2POp(self.dist.isend, self.send[s0:s1], p, self.group))
-                if r1 > r0:
-                    ops.append(self.dist.P2POp(self.dist.irecv, self.halo[r0:r1], p, self.group))
-            return self.dist.batch_isend_irecv(ops)
-        # gloo: stage through host memory, synchronously
-        send = self.send.cpu()
-        halo = self.halo.cpu()
-        works = []
-        for p in self._peers:
-            s0, s1 = P.send_off[p], P.send_off[p + 1]
-            r0, r1 = P.recv_off[p], P.recv_off[p + 1]
-            if s1 > s0:
-                works.append(self.dist.isend(send[s0:s1], p, group=self.group))
-            if r1 > r0:
-                works.append(self.dist.irecv(halo[r0:r1], p, group=self.group))
-        for w in works:
-            w.wait()
-        self.halo.copy_(halo)
-        return None
+        return self.exchange.start()
 
     def _finish_exchange(self, works):
-        for w in works or ():
-            w.wait()
+        self.exchange.finish(works)
 
     def _solo(self):
         """One rank: the reductions are identities and are skipped, unless
@@ -277,24 +342,24 @@ class DistributedDSGD:
         return self.dist.get_world_size(self.group) == 1 and os.environ.get("DOPT_FORCE_COLLECTIVES") != "1"
 
     def _all_reduce(self, t):
-        if self._solo():
-            return
-        if self.device_comm:
-            self.dist.all_reduce(t, group=self.group)
-        else:
-            c = t.cpu()
-            self.dist.all_reduce(c, group=self.group)
-            t.copy_(c)
+        w = self._all_reduce_start(t)
+        if w is not None:
+            _wait(w, f"all_reduce of {t.numel()} float64", self.plan.rank)
 
     def _all_reduce_start(self, t):
         """Enqueue an all-reduce of t behind the current stream's work; returns the work to
         wait on (RCCL: the current stream waits at .wait(), the host does not), or None
-        when the reduction is already complete (world 1, gloo)."""
+        when the reduction is already complete (world 1, gloo: done here on the host, bounded
+        by the job's timeout)."""
         if self._solo():
             return None
+        what = f"all_reduce of {t.numel()} float64"
         if self.device_comm:
             return self.dist.all_reduce(t, group=self.group, async_op=True)
-        self._all_reduce(t)
+        c = t.cpu()
+        _wait(self.dist.all_reduce(c, group=self.group, async_op=True), what, self.plan.rank, timeout_seconds())
+        if c.data_ptr() != t.data_ptr():
+            t.copy_(c)
         return None
 
     # -- rounds
@@ -314,7 +379,7 @@ class DistributedDSGD:
                batch < int(rows.max()) <= _dopt.MAX_BIP_ROWS and os.environ.get("DOPT_BIP", "1") != "0")
         if (fused or bip) and flags and self._lagged_ok:
             return self._run_lagged(T, eta0, batch, lam_grad, lam_obj, f_opt, t0, objective, consensus, idx)
-        if self.mean is not None and fused and T > 0 and self._rowspace_ready():
+        if self.mean is not None and fused and T > 0 and self._full_batch(batch) and self._rowspace_ready():
             return self._run_rowspace(T, eta0, lam_grad, lam_obj, f_opt, t0, objective, consensus)
         xnorm = self.plan.rank == 0  # ||xbar||^2 is global already: count it once
         with torch.cuda.stream(self.stream):
@@ -350,17 +415,33 @@ class DistributedDSGD:
         obj, cons = _dopt.finalize_metrics(self.eng.problem, raw, self.n_global, self.rows_global, lam_obj, f_opt)
         return (obj if objective else None), (cons if consensus else None)
 
+    def _full_batch(self, batch):
+        """Every local worker's minibatch is its whole shard (the row-space rounds take full-shard
+        gradients only; a smaller batch goes to the phase path, which draws it or refuses)."""
+        rows = self.eng.shard_rows
+        return rows is None or len(rows) == 0 or int(batch) >= int(np.max(rows))
+
     def _rowspace_ready(self):
         """Complete graph + quadratic + full shards of <= 64 rows and iterates that are equal on
-        every rank (checked here, checksum compared across ranks): the row-space rounds."""
+        every rank (checked here: the 64-bit content hash of each rank's common iterate -- of the
+        replicated state once live -- must be the same on all ranks): the row-space rounds."""
         torch = self.torch
-        ok, sig = self.eng.rs_phase_begin(False)
-        v = torch.tensor([1.0 if ok else 0.0, sig, -sig], dtype=torch.float64,
+        ok, h = self.eng.rs_phase_begin(False)
+        hi, lo = (h >> 32), (h & 0xFFFFFFFF)  # 32-bit halves: their negations fit an int64
+        v = torch.tensor([1 if ok else 0, hi, -hi, lo, -lo], dtype=torch.int64,
                          device=self.dev if self.device_comm else "cpu")
         if not self._solo():
-            self.dist.all_reduce(v, op=self.dist.ReduceOp.MIN, group=self.group)
-        ok_all, lo, hi = float(v[0]), float(v[1]), -float(v[2])
-        return ok_all == 1.0 and lo == hi
+            self._all_reduce_op(v, self.dist.ReduceOp.MIN)
+        v = [int(a) for a in v.cpu()]
+        return v[0] == 1 and v[1] == -v[2] and v[3] == -v[4]
+
+    def _all_reduce_op(self, t, op):
+        what = f"all_reduce ({op}) of {t.numel()} values"
+        if self.device_comm:
+            _wait(self.dist.all_reduce(t, op=op, group=self.group, async_op=True), what, self.plan.rank)
+        else:
+            _wait(self.dist.all_reduce(t, op=op, group=self.group, async_op=True), what, self.plan.rank,
+                  timeout_seconds())
 
     def _run_rowspace(self, T, eta0, lam_grad, lam_obj, f_opt, t0, objective, consensus, pipelined=False):
         """Complete graph: the iterates stay Z + X_i^T beta_i.  Per round one
@@ -374,7 +455,13 @@ class DistributedDSGD:
         xnorm = self.plan.rank == 0
         mf = (_dopt.RUN_OBJECTIVE if objective else 0) | (_dopt.RUN_CONSENSUS if consensus else 0)
         was_open = eng.phase_chain(False)  # any call ends an open chain; a pipelined one continues it
-        owed = pipelined and was_open and getattr(self, "_rs_flags", None) == mf
+        if pipelined and was_open and getattr(self, "_rs_flags", None) != mf:
+            # the open chain owes an entry with the other flags: refuse (as dopt_run_dsgd_pipelined
+            # does on one context) rather than drop it; the chain stays open
+            eng.phase_chain(True)
+            raise ValueError("pipelined run: the open chain owes the metrics of its last iterate with other "
+                             "objective / consensus flags; continue or close it (T = 0) with the same flags")
+        owed = pipelined and was_open
         leave = pipelined and T > 0 and mf != 0
         n_out = (T + (1 if owed else 0) - (1 if leave else 0)) if mf else 0
         if not owed:
@@ -426,7 +513,7 @@ class DistributedDSGD:
         bip = (idx is not None and not self.obj_sep and rows is not None and len(rows) > 0 and
                batch < int(rows.max()) <= _dopt.MAX_BIP_ROWS and os.environ.get("DOPT_BIP", "1") != "0")
         if (self.mean is not None and idx is None and not self.obj_sep and (objective or consensus) and
-                self._rowspace_ready()):  # complete graph: row-space rounds continued across calls
+                self._full_batch(batch) and self._rowspace_ready()):  # complete graph: row-space rounds continued across calls
             return self._run_rowspace(T, eta0, lam_grad, lam_obj, f_opt, t0, objective, consensus, pipelined=True)
         if not ((idx is None and not self.obj_sep) or bip) or not (objective or consensus) or not self._lagged_ok:
             raise NotImplementedError("pipelined runs: the lagged schedule (CSR mixing, fused metrics) or the "

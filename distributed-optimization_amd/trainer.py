@@ -327,6 +327,22 @@ class _Checkpoint:
         self.kind, self.tr, self.rank = kind, trainer, rank
         self.meta = {"kind": kind, "n_workers": trainer.n_workers, "n_features": trainer.n_features,
                      "problem_type": cfg["problem_type"], "topology": getattr(trainer, "topology", "")}
+        if self.path or self.resume:
+            # everything else a resumed run must share with the saved one to continue bit for bit:
+            # the step size (trainer.py:138-140), the minibatch size, the arithmetic, both regulariser
+            # keys (worker.py:36-37) and the shard contents
+            ws = trainer.workers
+            self.meta.update(
+                learning_rate_eta0=float(cfg.get("learning_rate_eta0", 0.0)),
+                local_batch_size=int(_batch_size(ws)), dtype=str(cfg.get("dtype", "float64")),
+                l2_regularization_lambda=float(cfg.get("l2_regularization_lambda", 0.0)),
+                strong_convexity_mu=float(cfg.get("strong_convexity_mu", 0.0)),
+                data=_fingerprint([a for w in ws for a in (w.X_local, w.y_local)]))
+
+    @staticmethod
+    def _meta_value(v):
+        k = v.dtype.kind
+        return str(v) if k == "U" else float(v) if k == "f" else int(v)
 
     def max_chunk(self):
         return self.every if self.path and self.every > 0 else 0
@@ -340,7 +356,10 @@ class _Checkpoint:
         if not self.resume:
             return 0, None, 0.0
         with np.load(self.resume, allow_pickle=False) as z:
-            got = {k: (str(z[k]) if z[k].dtype.kind == "U" else int(z[k])) for k in self.meta}
+            missing = [k for k in self.meta if k not in z.files]
+            if missing:
+                raise ValueError(f"checkpoint {self.resume} lacks {missing}: written by another version")
+            got = {k: self._meta_value(z[k]) for k in self.meta}
             if got != self.meta:
                 raise ValueError(f"checkpoint {self.resume} does not match this trainer: {got} vs {self.meta}")
             t = int(z["t"])

@@ -29,7 +29,16 @@
 extern "C" {
 #endif
 
-#define DOPT_ABI_VERSION 1
+/* ABI history.
+ *   1  round 1: contexts, shards, topology / mean mixing, D-SGD and centralized runs, single
+ *      evaluations, the legacy-MT19937 sampler, the multi-GPU phase calls.
+ *   2  round 2-3 additions: dopt_set_data_dtype / dopt_get_data_dtype (float32 rows under float64
+ *      arithmetic), dopt_run_dsgd_pipelined, dopt_zero_models, dopt_set_sampler (device
+ *      minibatches), dopt_eval_full, dopt_phase_chain / _colsum_fold / _mix_lagged / _cons /
+ *      _fold / _loss_pass (lagged multi-GPU schedule), the dopt_rs_phase_* row-space calls; and
+ *      one signature change: dopt_rs_phase_begin reports a 64-bit content hash (was a double
+ *      checksum). */
+#define DOPT_ABI_VERSION 2
 
 typedef struct dopt_ctx dopt_ctx;
 
@@ -286,8 +295,9 @@ int dopt_phase_loss_pass(dopt_ctx *ctx, int two_points);
  * 1..64 rows) -- replace the serial phase order of DistributedDSGD for that case
  * (trainer.py:161-193 with the mix of trainer.py:173 through the all-reduced column sums):
  * dopt_rs_phase_begin: *ok = 1 when this rank's iterates are all equal (or the row-space state
- *   is live already), *sig = a checksum of that common iterate (the caller compares it across
- *   ranks); commit = 1 also enters row-space mode (Gram matrices, Z = xbar = the iterate).
+ *   is live already), *hash = a 64-bit content hash of that common iterate's bytes (of the
+ *   replicated Z and average when the state is live; the caller compares it across ranks);
+ *   commit = 1 also enters row-space mode (Gram matrices, Z = xbar = the iterate).
  * dopt_rs_phase_round: round t's pass at the current average: the next row state, the metric
  *   partials of the current iterates (metric_flags, folded by dopt_phase_fold slab 0) and this
  *   rank's column sums into sum_dev[ld] (to be all-reduced).
@@ -295,7 +305,7 @@ int dopt_phase_loss_pass(dopt_ctx *ctx, int two_points);
  * dopt_rs_phase_metrics: the metric partials of the current iterates (a dots pass).
  * dopt_get_models forms the iterates; dopt_phase_begin, dopt_phase_colsum / _fold / _gather,
  * dopt_set_models, dopt_set_mixing_mean and dopt_set_topology leave row-space mode. */
-int dopt_rs_phase_begin(dopt_ctx *ctx, int commit, int *ok, double *sig);
+int dopt_rs_phase_begin(dopt_ctx *ctx, int commit, int *ok, uint64_t *hash);
 int dopt_rs_phase_round(dopt_ctx *ctx, int64_t t, double eta0, double lam_grad, uint32_t metric_flags,
                         double *sum_dev);
 int dopt_rs_phase_cols(dopt_ctx *ctx, int64_t t, double eta0, double lam_grad, const double *sum_dev);

@@ -131,6 +131,64 @@ def test_graph_partition_balanced_and_better_than_ranges(n, parts):
     assert halo_new < halo_old
 
 
+def _rank_skip_send(rank, world, port, timeout_s, out):
+    """Rank 1 never sends its halo rows; then every rank joins an all-reduce.  Each rank writes
+    the error it ended with and exits non-zero."""
+    import sys
+    import time
+
+    import torch
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DOPT_PG_TIMEOUT=str(timeout_s))
+    D.init_process_group("gloo", rank=rank, world_size=world)
+    topo = TP.ring(8)
+    plan = D.build_plan(topo, world, rank)
+    send = torch.zeros((max(1, len(plan.send_ids)), 3), dtype=torch.float64)
+    halo = torch.zeros((max(1, plan.n_halo), 3), dtype=torch.float64)
+
+    class Lossy(D.HaloExchange):
+        def _ops(self, send, halo):
+            for op in super()._ops(send, halo):
+                if not (self.rank == 1 and op[0] == "isend"):
+                    yield op
+
+    ex = Lossy(plan, send, halo)
+    t0 = time.time()
+    try:
+        ex.finish(ex.start())
+        work = dist.all_reduce(torch.ones(1, dtype=torch.float64), async_op=True)
+        D._wait(work, "all_reduce of 1 float64", rank, D.timeout_seconds())
+        msg, code = "no error", 0
+    except D.CollectiveError as e:
+        msg, code = str(e), 3
+    with open(os.path.join(out, f"rank{rank}.txt"), "w") as f:
+        f.write(f"{time.time() - t0:.2f}\n{msg}\n")
+    sys.stdout.flush()
+    os._exit(code)
+
+
+def test_a_rank_that_skips_its_send_ends_both_ranks_within_the_timeout(tmp_path):
+    """a peer that never sends its halo rows must not hang the job -- the rank
+    waiting for them fails at the collective timeout with the peer and the operation named, and
+    its partner (which got its rows and went on to the next collective) fails right after."""
+    import time
+
+    timeout_s = 4
+    t0 = time.time()
+    ctx = mp.start_processes(_rank_skip_send, args=(2, _free_port(), timeout_s, str(tmp_path)), nprocs=2,
+                             join=False, start_method="fork")
+    for p in ctx.processes:
+        p.join(60)
+    wall = time.time() - t0
+    codes = [p.exitcode for p in ctx.processes]
+    assert codes == [3, 3], codes
+    assert wall < 6 * timeout_s + 20
+    r0 = (tmp_path / "rank0.txt").read_text()
+    assert "rank 0: irecv of 2 halo rows from rank 1 failed" in r0, r0
+    r1 = (tmp_path / "rank1.txt").read_text()
+    assert "rank 1: all_reduce" in r1, r1
+
+
 def test_relabelled_rounds_match_oracle(tmp_path):
     """Partitioned rounds on a relabelled graph are the oracle's rounds on that graph."""
     n, world, T = 24, 3, 4

@@ -85,3 +85,15 @@ def test_resume_rejects_a_mismatched_checkpoint(tmp_path):
         _trainer("D-SGD (Fully Connected)", shards, dict(cfg, resume_from=ck)).run(10, Xf, yf, meta["f_opt"])
     with pytest.raises(ValueError):
         _trainer("D-SGD (Ring)", shards, dict(cfg, resume_from=ck)).run(3, Xf, yf, meta["f_opt"])
+    # anything else the saved trajectory depends on: step size, minibatch size, arithmetic, the
+    # regulariser keys (worker.py:36-37), the shard contents
+    for change in ({"learning_rate_eta0": cfg["learning_rate_eta0"] * 2}, {"dtype": "float32"},
+                   {"l2_regularization_lambda": 3e-3}, {"strong_convexity_mu": 3e-3}):
+        with pytest.raises(ValueError):
+            _trainer("D-SGD (Ring)", shards, dict(cfg, resume_from=ck, **change)).run(10, Xf, yf, meta["f_opt"])
+    edited = [(X.copy(), y.copy()) for X, y in shards]
+    edited[0][0][0, 0] += 1.0
+    with pytest.raises(ValueError):
+        _trainer("D-SGD (Ring)", edited, dict(cfg, resume_from=ck)).run(10, Xf, yf, meta["f_opt"])
+    # the unchanged configuration still resumes
+    _trainer("D-SGD (Ring)", shards, dict(cfg, resume_from=ck)).run(10, Xf, yf, meta["f_opt"])

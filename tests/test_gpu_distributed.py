@@ -220,6 +220,24 @@ def test_partitioned_graph_ranks_match_single_context(tmp_path, monkeypatch, wor
     _compare_single(got, "float64", False, 5, parts=world)
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_strong_split_bench_shape_matches_single_context(tmp_path, monkeypatch, world):
+    """bench.py's strong-scaling leg in miniature: a FIXED total of workers (512, d = 1024, the
+    headline's float64 arithmetic over float32 rows) split over 2 and 4 ranks by the spectral
+    partition, timed as a chain of pipelined calls -- bitwise one context's iterates, history
+    rtol 1e-12."""
+    import torch.multiprocessing as mp
+
+    n, d, m, t = 512, 1024, 16, 9
+    monkeypatch.setenv("DOPT_TEST_PARTITION", "1")
+    monkeypatch.setenv("DOPT_TEST_PIPE", "1")
+    mp.start_processes(_rank_main, args=(world, _free_port(), "float64/x32", str(tmp_path), False, t, "1", n, d, m),
+                       nprocs=world, join=True, start_method="spawn")
+    got = np.load(tmp_path / "dist.npz")
+    assert len(got["obj"]) == len(got["cons"]) == t
+    _compare_single(got, "float64/x32", False, t, n, d, m, parts=world)
+
+
 @pytest.mark.parametrize("lagged", ["1", "0"])
 def test_device_sampler_ranks_match_single_context(tmp_path, monkeypatch, lagged):
     """sampling='device' across ranks: worker i's minibatch of round t depends only on

@@ -50,26 +50,34 @@ def test_c4_torus_65536_workers_full_size():
         eng.set_topology(top.row_ptr, top.col, top.w)
         rng = np.random.default_rng(2)
         x0 = rng.standard_normal((n, d)) * 1e-2
-        eng.set_models(x0)
-        obj, cons, _ = eng.run_dsgd(1, eta0, m, lam, lam, 0.0)
-        x1 = eng.get_models()
         # torus corners / wrap-around rows and columns (neighbours ids i +- 1 mod 256, i +- 256 mod 65536)
-        picks = [0, 255, 256, 511, 65280, 65535, 32767, 32768] + list(rng.choice(n, 8, replace=False))
-        for i in picks:
-            X, y = eng.get_shard(int(i))
-            g = O.logistic_gradient(x0[i], X, y, lam)
-            np.testing.assert_allclose(x1[i], _mix_row(top, x0, i) - eta0 * g, rtol=1e-10, atol=1e-13)
-        xbar = x1.mean(axis=0)
-        np.testing.assert_allclose(cons[0], np.mean(np.sum((x1 - xbar) ** 2, axis=1)), rtol=1e-10)
-        # two more rounds in one call: the fused path (metrics of round t in round t+1's pass)
-        obj2, cons2, _ = eng.run_dsgd(T - 1, eta0, m, lam, lam, 0.0, t0=1)
-        x3 = eng.get_models()
-        assert np.all(np.isfinite(obj2)) and np.all(np.isfinite(cons2))
-        xbar3 = x3.mean(axis=0)
-        np.testing.assert_allclose(cons2[-1], np.mean(np.sum((x3 - xbar3) ** 2, axis=1)), rtol=1e-10)
-        for i in (0, 65535):  # the objective at xbar over a worker's rows enters history: spot-check sums
-            X, y = eng.get_shard(i)
-            assert np.isfinite(O.logistic_objective(xbar3, X, y, lam))
+        picks = [0, 255, 256, 511, 65280, 65535, 32767, 32768] + [int(i) for i in rng.choice(n, 8, replace=False)]
+        shards = {i: eng.get_shard(i) for i in picks}
+        eng.set_models(x0)
+        x, per_obj, per_cons = x0, [], []
+        for t in range(T):  # one round per call: every round's updates, consensus and objective pinned
+            obj, cons, _ = eng.run_dsgd(1, eta0, m, lam, lam, 0.0, t0=t)
+            xn = eng.get_models()
+            eta = eta0 / np.sqrt(t + 1)  # trainer.py:138-140
+            for i in picks:
+                X, y = shards[i]
+                g = O.logistic_gradient(x[i], X, y, lam)
+                np.testing.assert_allclose(xn[i], _mix_row(top, x, i) - eta * g, rtol=1e-10, atol=1e-13)
+            xbar = xn.mean(axis=0)
+            np.testing.assert_allclose(cons[0], np.mean(np.sum((xn - xbar) ** 2, axis=1)), rtol=1e-10)
+            # the objective at xbar over all 33.5M rows (trainer.py:188-191): an independent device
+            # evaluation (dopt_eval_full, pinned to the oracle in test_full_evaluation_and_device_optimum)
+            f_ref, _ = eng.eval_full(xbar, lam)
+            np.testing.assert_allclose(obj[0], f_ref, rtol=1e-10)
+            per_obj.append(obj[0])
+            per_cons.append(cons[0])
+            x = xn
+        # the same T rounds in one call (the fused path: the metrics of round t in round t+1's pass)
+        eng.set_models(x0)
+        obj_all, cons_all, _ = eng.run_dsgd(T, eta0, m, lam, lam, 0.0)
+        np.testing.assert_allclose(obj_all, per_obj, rtol=1e-12)
+        np.testing.assert_allclose(cons_all, per_cons, rtol=1e-12)
+        np.testing.assert_allclose(eng.get_models(), x, rtol=1e-13, atol=1e-16)
     finally:
         eng.close()
 

@@ -235,6 +235,61 @@ def test_rowspace_ranks_vs_oracle(tmp_path, world, pipe, x32):
     np.testing.assert_allclose(got["x"], xr, rtol=1e-9, atol=1e-12 * np.abs(xr).max())
 
 
+def _rs_rank_minibatch(rank, world, port, out):
+    import os
+
+    import torch  # noqa: F401  (one HIP runtime, loaded before libdopt)
+    import torch.distributed as dist
+
+    import distributed as Dm
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    shards = _rs_data(False)
+    n = len(shards)
+    bounds = Dm.partition_bounds(n, world)
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    plan = Dm.HaloPlan(rank, world, bounds, lo, hi, np.zeros(0, np.int64), np.zeros(world + 1, np.int64),
+                       np.zeros(0, np.int32), np.zeros(world + 1, np.int64), None, None, None)
+    eng = _dopt.Engine(0, "float64")
+    mine = shards[lo:hi]
+    off = np.concatenate([[0], np.cumsum([len(s[1]) for s in mine])])
+    eng.load_shards("quadratic", np.vstack([s[0] for s in mine]), np.concatenate([s[1] for s in mine]), off)
+    w_off, diag = TP.fully_connected(n).uniform_offdiag()
+    run = Dm.DistributedDSGD(eng, plan, n, sum(SIZES_D), device=0, mean=(w_off, diag[lo:hi]))
+    got = []
+    for call in (run.run, run.run_pipelined):
+        try:
+            call(2, 0.05, 5, 2e-3, 1e-3, 0.1)  # b = 5 < the 12-row shards, no indices
+            got.append("ran")
+        except (ValueError, NotImplementedError) as e:
+            got.append(type(e).__name__)
+    kern = _dopt.last_round_kernel()
+    if rank == 0:
+        np.savez(os.path.join(out, "mb.npz"), got=np.array(got), kern=np.array(kern))
+    dist.barrier()
+    eng.close()
+    dist.destroy_process_group()
+
+
+def test_rowspace_ranks_refuse_minibatches(tmp_path):
+    """across ranks the row-space rounds take full-shard gradients only, so a run with
+    batch < m and no index draws must not silently run full-batch D-SGD there: it goes to the
+    phase path, which refuses it (the host sampler needs the reference's indices)."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.start_processes(_rs_rank_minibatch, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    got = np.load(tmp_path / "mb.npz")
+    assert "ran" not in list(got["got"]), got["got"]
+    assert "k_rs_pass" not in str(got["kern"])
+
+
 @pytest.mark.parametrize("problem", ["quadratic", "logistic"])
 def test_trainer_complete_graph_long_rows_vs_oracle(problem):
     """The drop-in DecentralizedTrainer('fully_connected') with rows beyond the row-resident
