@@ -490,10 +490,11 @@ class Engine:
     def sync(self):
         check(lib().dopt_sync(self._h))
 
-    def eval_full(self, w, reg):
-        """(objective, gradient) over all loaded rows at w, one device pass."""
+    def eval_full(self, w, reg, gradient=True):
+        """(objective, gradient) over all loaded rows at w, one device pass; gradient=False:
+        (objective, None) -- the only form for column-blocked (large d) contexts."""
         w = np.ascontiguousarray(w, dtype=np.float64)
-        g = np.empty(self.d, dtype=np.float64)
+        g = np.empty(self.d, dtype=np.float64) if gradient else None
         f = np.zeros(1)
         check(lib().dopt_eval_full(self._h, _ptr(w), float(reg), _ptr(f), _ptr(g)))
         return float(f[0]), g

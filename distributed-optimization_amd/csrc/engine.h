@@ -174,14 +174,15 @@ constexpr int kSplitMaxRows = 64;  // rows held in registers by a step workgroup
 // Step: g_i = (1/nb) sum_k coef_k x_k + lam x_i, x_i' = mix - eta g_i (block by block); with
 // znext also the partial dots x_k . x_i' for the next round's coefficients (rows still in
 // registers); with met the metric partials of x_i at xbar.  nb <= kSplitMaxRows.
-hipError_t launch_split_step(int dtype, bool znext, bool met, const RoundArgs& a, int n_workers,
+// dtype = arithmetic / state, xdtype = row storage (equal, or float32 rows under float64 arithmetic).
+hipError_t launch_split_step(int dtype, int xdtype, bool znext, bool met, const RoundArgs& a, int n_workers,
                              hipStream_t s);
 // Dots only: mode 0 -> zpart = x_k . x_i (minibatch rows via idx, or all rows);
 // mode 1 -> upart = x_k . xbar over all rows, cpart = ||x_i - xbar||^2 partials.
-hipError_t launch_split_dots(int dtype, int mode, const RoundArgs& a, int n_workers, hipStream_t s);
+hipError_t launch_split_dots(int dtype, int xdtype, int mode, const RoundArgs& a, int n_workers, hipStream_t s);
 // Per worker: z_k = sum_g zpart -> coef (mode bit 1), sum_k loss(u_k) -> slab_loss and
 // sum_g cpart -> slab_cons (mode bit 2).  Fixed reduction order.
-hipError_t launch_split_coef(int dtype, int problem, int mode, const RoundArgs& a, int n_workers,
+hipError_t launch_split_coef(int dtype, int xdtype, int problem, int mode, const RoundArgs& a, int n_workers,
                              hipStream_t s);
 
 // Column sums of rows x[0:rows] in one launch when rows <= rpg (k_colsum_one), else the two

@@ -153,6 +153,14 @@ __device__ __forceinline__ void wave_sum_pair(T a, T b, T& sa, T& sb) {
   sb = readlane_t(x, 1);
 }
 
+// A row chunk in the state type: the identity when rows are stored in the arithmetic type, the
+// exact float -> double widening for float32 rows under float64 arithmetic.
+template <typename V, typename VX>
+__device__ __forceinline__ V widen(VX x) {
+  if constexpr (std::is_same<V, VX>::value) return x;
+  else return __builtin_convertvector(x, V);
+}
+
 template <typename T, typename V>
 __device__ __forceinline__ T hsum(V v) {
   T s = v[0];

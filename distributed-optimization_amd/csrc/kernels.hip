@@ -108,10 +108,14 @@ struct BlockWalk {
   }
 };
 
-template <typename T, int RPW, bool ZNEXT, bool MET, bool PF, int CPB = 1>
+// T = iterates and arithmetic, XT = row storage (XT = T, or float32 rows under float64 arithmetic:
+// a 16-byte row chunk is 4 floats, the state chunk at the same columns 4 doubles; every product
+// and sum is then the float64 one).
+template <typename T, typename XT, int RPW, bool ZNEXT, bool MET, bool PF, int CPB = 1>
 __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
-  using V = typename VT<T>::v;
-  constexpr int VN = VT<T>::n;
+  using V = typename KV<T, XT>::V;    // state chunk
+  using VX = typename KV<T, XT>::VX;  // row chunk (one 16-byte load)
+  constexpr int VN = KV<T, XT>::VN;
   constexpr int BC = 64 * CPB;  // chunks per column block
   __shared__ V gred[2][NW][BC];
   const int lane = threadIdx.x & 63;
@@ -122,7 +126,7 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
   const int64_t ld = a.ld;
   const int64_t row0 = a.off[i], m = a.off[i + 1] - row0;
   const int64_t nb = a.idx ? (a.b < m ? a.b : m) : m;  // <= NW * RPW (host-checked)
-  const T* __restrict__ X = (const T*)a.X;
+  const XT* __restrict__ X = (const XT*)a.X;
   const bool shared = (a.flags & F_SHARED) != 0;  // centralized: every worker at w_shared
   const bool gout = (a.flags & F_GOUT) != 0;
   const T* own_p = shared ? (const T*)a.w_shared : (const T*)a.x_old + (int64_t)i * ld;
@@ -162,7 +166,8 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
   asm volatile("" : "+v"(wii));  // loaded here, once: a load sunk into the block loop would wait for the prefetch
   const bool early = (a.flags & F_EARLYMIX) != 0 && !gout;
   struct Set {
-    V rw[RPW][CPB], own[CPB], xb[CPB], sv[CPB];
+    VX rw[RPW][CPB];
+    V own[CPB], xb[CPB], sv[CPB];
   };
   auto stage = [&](Set& S, int cbn) {  // small loads first, then the rows
     if (PF) {
@@ -183,7 +188,7 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
         const int c0 = cbc * BC + j * 64 + lane;
         const int c = c0 < nch ? c0 : nch - 1;
 #pragma unroll
-        for (int r = 0; r < RPW; ++r) S.rw[r][j] = ld_nt<T>(X + (rowp[r] >= 0 ? rowp[r] : row0 * ld) + (int64_t)c * VN);
+        for (int r = 0; r < RPW; ++r) S.rw[r][j] = ld_nt<XT>(X + (rowp[r] >= 0 ? rowp[r] : row0 * ld) + (int64_t)c * VN);
       }
       return;
     }
@@ -200,7 +205,7 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
       const int c = cbn * BC + j * 64 + lane;
       const bool in = blk && c < nch;
 #pragma unroll
-      for (int r = 0; r < RPW; ++r) S.rw[r][j] = (in && rowp[r] >= 0) ? ld_nt<T>(X + rowp[r] + (int64_t)c * VN) : V(0);
+      for (int r = 0; r < RPW; ++r) S.rw[r][j] = (in && rowp[r] >= 0) ? ld_nt<XT>(X + rowp[r] + (int64_t)c * VN) : VX(0);
     }
   };
   auto process = [&](Set& S, int cb, int buf) {
@@ -218,11 +223,11 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
       } else {
         // the mix does not depend on the gradient: with F_EARLYMIX its loads (column sums or the
         // neighbour rows) are issued before the block's barrier instead of after it
-        mixv[j] = (early && in) ? mix_chunk<T, T>(a, i, c, S.own[j]) : V(0);
+        mixv[j] = (early && in) ? mix_chunk<T, XT>(a, i, c, S.own[j]) : V(0);
       }
       V gp = V(0);
 #pragma unroll
-      for (int r = 0; r < RPW; ++r) gp += coef[r] * S.rw[r][j];  // absent rows: coef 0
+      for (int r = 0; r < RPW; ++r) gp += coef[r] * widen<V>(S.rw[r][j]);  // absent rows: coef 0
       gred[buf][wave][j * 64 + lane] = gp;
     }
     if (PF)
@@ -244,19 +249,19 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
         if (wave == 0 && in) *(V*)((T*)a.g_out + (int64_t)i * ld + (int64_t)c * VN) = g;
       } else if (in) {
         if constexpr (PF) xn = mixv[j] - inv_eta * g;
-        else xn = (early ? mixv[j] : mix_chunk<T, T>(a, i, c, S.own[j])) - inv_eta * g;
+        else xn = (early ? mixv[j] : mix_chunk<T, XT>(a, i, c, S.own[j])) - inv_eta * g;
         if (wave == 0) *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = xn;
       }
       if (ZNEXT) {
 #pragma unroll
-        for (int r = 0; r < RPW; ++r) zacc[r] += (double)hsum<T>(S.rw[r][j] * xn);
+        for (int r = 0; r < RPW; ++r) zacc[r] += (double)hsumn<T, VN>(widen<V>(S.rw[r][j]) * xn);
       }
       if (MET && in) {  // (PF: lanes past the row hold re-read chunks)
 #pragma unroll
-        for (int r = 0; r < RPW; ++r) uacc[r] += (double)hsum<T>(S.rw[r][j] * S.xb[j]);
+        for (int r = 0; r < RPW; ++r) uacc[r] += (double)hsumn<T, VN>(widen<V>(S.rw[r][j]) * S.xb[j]);
         if (wave == 0) {
           const V dv = S.own[j] - S.xb[j];
-          cacc += (double)hsum<T>(dv * dv);
+          cacc += (double)hsumn<T, VN>(dv * dv);
         }
       }
     }
@@ -298,6 +303,7 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
   }
 }
 
+#ifdef DOPT_AB  // A/B-only kernels (make AB=1): measured slower than k_split_step, kept for the record
 // LDS-DMA form of the prefetching step (DOPT_SPLIT_GLDS = D, complete-graph D-SGD steps with
 // the column sums in T, <= 16 rows per worker).  Every load of the block walk is a
 // global_load_lds_dwordx4 (1 KiB per wave instruction, no VGPR destination), so D blocks ahead
@@ -604,10 +610,12 @@ __global__ __launch_bounds__(NT) void k_split_colwave(const RoundArgs a) {
   if (MET && threadIdx.x == 0) a.cpart[(int64_t)i * G + grp] = ((cred[0] + cred[1]) + cred[2]) + cred[3];
 }
 
-template <typename T, int MODE, int RPW>
+#endif  // DOPT_AB
+
+template <typename T, typename S, int MODE, int RPW>
 __global__ __launch_bounds__(NT) void k_split_dots(const RoundArgs a) {
-  using V = typename VT<T>::v;
-  constexpr int VN = VT<T>::n;
+  using V = typename KV<T, S>::V;
+  constexpr int VN = KV<T, S>::VN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int i = blockIdx.x, grp = blockIdx.y, G = gridDim.y;
@@ -616,7 +624,7 @@ __global__ __launch_bounds__(NT) void k_split_dots(const RoundArgs a) {
   const int64_t ld = a.ld;
   const int64_t row0 = a.off[i], m = a.off[i + 1] - row0;
   const int64_t nb = (MODE == 0 && a.idx) ? (a.b < m ? a.b : m) : m;
-  const T* __restrict__ X = (const T*)a.X;
+  const S* __restrict__ X = (const S*)a.X;
   const T* own_p = (a.flags & F_SHARED) ? (const T*)a.w_shared : (const T*)a.x_old + (int64_t)i * ld;
   const T* pt = MODE == 0 ? own_p : (const T*)a.xbar;
   double* out = MODE == 0 ? a.zpart : a.upart;
@@ -626,7 +634,7 @@ __global__ __launch_bounds__(NT) void k_split_dots(const RoundArgs a) {
       const int c = cb * 64 + lane;
       if (c < nch) {
         const V dv = *(const V*)(own_p + (int64_t)c * VN) - *(const V*)(pt + (int64_t)c * VN);
-        cacc += (double)hsum<T>(dv * dv);
+        cacc += (double)hsumn<T, VN>(dv * dv);
       }
     }
     cacc = wave_sum(cacc);
@@ -650,7 +658,7 @@ __global__ __launch_bounds__(NT) void k_split_dots(const RoundArgs a) {
       const V pv = *(const V*)(pt + (int64_t)c * VN);
 #pragma unroll
       for (int r = 0; r < RPW; ++r)
-        if (rowp[r] >= 0) acc[r] += (double)hsum<T>(ld_nt<T>(X + rowp[r] + (int64_t)c * VN) * pv);
+        if (rowp[r] >= 0) acc[r] += (double)hsumn<T, VN>(widen<V>(ld_nt<S>(X + rowp[r] + (int64_t)c * VN)) * pv);
     }
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
@@ -661,12 +669,12 @@ __global__ __launch_bounds__(NT) void k_split_dots(const RoundArgs a) {
   }
 }
 
-template <typename T, int PROB>
+template <typename T, typename S, int PROB>
 __global__ __launch_bounds__(NT) void k_split_coef(const RoundArgs a, int mode) {
   __shared__ double red[NW];
   const int i = blockIdx.x, G = a.groups;
   const int64_t row0 = a.off[i], m = a.off[i + 1] - row0;
-  const T* Y = (const T*)a.y;
+  const S* Y = (const S*)a.y;  // labels / targets in the rows' storage type
   if (mode & 1) {  // next coefficients from the partial dots (obj_problems.py:16-17 / :49-50)
     const int64_t nb = a.idx ? (a.b < m ? a.b : m) : m;
     for (int64_t k = threadIdx.x; k < nb; k += NT) {
@@ -698,66 +706,94 @@ __global__ __launch_bounds__(NT) void k_split_coef(const RoundArgs a, int mode) 
   }
 }
 
-// A/B knob DOPT_SPLIT_CONTIG: contiguous block ranges per column-block group, or every G-th
-// block (default: C5 13.91 vs 14.02 ms contiguous, won 4 of 4 interleaved reps)
-static int split_contig() {
-  const char* v = getenv("DOPT_SPLIT_CONTIG");
-  return v ? atoi(v) != 0 : 0;
+// Launch-shape knobs are read only by A/B builds (make AB=1, -DDOPT_AB): the default build uses
+// the measured defaults and ignores the environment.
+#ifdef DOPT_AB
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
 }
+#else
+static int env_int(const char*, int dflt) { return dflt; }
+#endif
 
-static void note_split(const char* kernel, int dtype, const char* params) {
+// contiguous block ranges per column-block group, or every G-th block (A/B DOPT_SPLIT_CONTIG;
+// default: C5 13.91 vs 14.02 ms contiguous, won 4 of 4 interleaved reps)
+static int split_contig() { return env_int("DOPT_SPLIT_CONTIG", 0) != 0; }
+
+static void note_split(const char* kernel, int dtype, int xdtype, const char* params) {
   char buf[160];
-  snprintf(buf, sizeof(buf), "void dopt::%s<%s, %s>(dopt::RoundArgs)", kernel, dtype == 0 ? "float" : "double", params);
+  if (dtype == 1 && xdtype == 0)
+    snprintf(buf, sizeof(buf), "void dopt::%s<double, float, %s>(dopt::RoundArgs)", kernel, params);
+  else
+    snprintf(buf, sizeof(buf), "void dopt::%s<%s, %s, %s>(dopt::RoundArgs)", kernel, dtype == 0 ? "float" : "double",
+             dtype == 0 ? "float" : "double", params);
   note_round_kernel(buf);
 }
 static const char* tf(bool b) { return b ? "true" : "false"; }
 
-hipError_t launch_split_step(int dtype, bool znext, bool met, const RoundArgs& a, int n_workers,
+// element types of a launch: (0, 0) float, (1, 1) double, (1, 0) float64 over float32 rows
+static bool split_types_ok(int dtype, int xdtype) { return dtype == xdtype || (dtype == 1 && xdtype == 0); }
+
+template <typename T, typename S>
+static void split_step_t(bool znext, bool met, bool small, bool pf, int cpb, dim3 grid, const RoundArgs& a2,
+                         hipStream_t s) {
+#define SPLIT_STEP2(R_, P_, C_)                                                                                    \
+  if (znext && met) hipLaunchKernelGGL((k_split_step<T, S, R_, true, true, P_, C_>), grid, dim3(NT), 0, s, a2);     \
+  else if (znext) hipLaunchKernelGGL((k_split_step<T, S, R_, true, false, P_, C_>), grid, dim3(NT), 0, s, a2);      \
+  else if (met) hipLaunchKernelGGL((k_split_step<T, S, R_, false, true, P_, C_>), grid, dim3(NT), 0, s, a2);        \
+  else hipLaunchKernelGGL((k_split_step<T, S, R_, false, false, P_, C_>), grid, dim3(NT), 0, s, a2);
+  if (small) {
+#ifdef DOPT_AB
+    if (cpb == 4) { SPLIT_STEP2(4, false, 4) return; }
+    if (cpb == 2 && pf) { SPLIT_STEP2(4, true, 2) return; }
+    if (cpb == 2) { SPLIT_STEP2(4, false, 2) return; }
+#endif
+    if (pf) { SPLIT_STEP2(4, true, 1) } else { SPLIT_STEP2(4, false, 1) }
+  } else {
+    if (pf) { SPLIT_STEP2(16, true, 1) } else { SPLIT_STEP2(16, false, 1) }
+  }
+#undef SPLIT_STEP2
+}
+
+hipError_t launch_split_step(int dtype, int xdtype, bool znext, bool met, const RoundArgs& a, int n_workers,
                              hipStream_t s) {
   if (n_workers <= 0) return hipSuccess;
+  if (!split_types_ok(dtype, xdtype)) return hipErrorInvalidValue;
   char params[96];
   const dim3 grid(n_workers, a.groups);
   const bool small = a.b_rows <= 4 * NW;  // rows per worker this step touches
   RoundArgs a2 = a;
   a2.contig = split_contig();
-  {  // A/B knob DOPT_SPLIT_EARLYMIX (tools/split_ab.py): the block's mix before its barrier
-    const char* em = getenv("DOPT_SPLIT_EARLYMIX");
-    if (!(em && em[0] == '0')) a2.flags |= F_EARLYMIX;
-  }
-  // A/B knob DOPT_SPLIT_PREFETCH (tools/split_ab.py): the next block's loads in flight through
-  // the block's barrier; complete-graph D-SGD steps with the column sums in T only
-  // (default on: C5 14.60 -> 14.24 ms, and 13.99 with the exact 1/16, interleaved A/B)
-  const char* ev = getenv("DOPT_SPLIT_PREFETCH");
-  const bool pf = !(ev && ev[0] == '0') && (a.flags & F_MEAN) && !(a.flags & F_GOUT) &&
+  // the block's mix before its barrier (A/B DOPT_SPLIT_EARLYMIX=0: after it)
+  if (env_int("DOPT_SPLIT_EARLYMIX", 1) != 0) a2.flags |= F_EARLYMIX;
+  // the next block's loads in flight through the block's barrier: complete-graph D-SGD steps with
+  // the column sums in T (default on: C5 14.60 -> 14.24 ms, and 13.99 with the exact 1/16,
+  // interleaved A/B; DOPT_SPLIT_PREFETCH=0 in A/B builds)
+  const bool pf = env_int("DOPT_SPLIT_PREFETCH", 1) != 0 && (a.flags & F_MEAN) && !(a.flags & F_GOUT) &&
                   (dtype == 1 ? a.colsum != nullptr : a.colsum_t != nullptr);
-  // 2 or 4 chunks per lane per block for <= 16 rows when every group still walks >= 2
-  // blocks (the slab layout [n][bcap][G] does not depend on the block size)
-  // A/B knob DOPT_SPLIT_GLDS = D (2 or 3): the LDS-DMA kernel with D blocks in flight per wave,
-  // where the prefetching kernel would run with <= 16 rows
-  const char* gv = getenv("DOPT_SPLIT_GLDS");
-  const int glds = gv ? atoi(gv) : 0;
-  if (pf && small && (glds == 2 || glds == 3)) {
+#ifdef DOPT_AB
+  // DOPT_SPLIT_GLDS = D (2 or 3): the LDS-DMA kernel with D blocks in flight per wave, where the
+  // prefetching kernel would run with <= 16 rows (same element types only)
+  const int glds = env_int("DOPT_SPLIT_GLDS", 0);
+  if (pf && small && (glds == 2 || glds == 3) && dtype == xdtype) {
 #define GLDS2(T_, D_)                                                                                 \
   if (znext && met) hipLaunchKernelGGL((k_split_glds<T_, true, true, D_>), grid, dim3(NT), 0, s, a2); \
   else if (znext) hipLaunchKernelGGL((k_split_glds<T_, true, false, D_>), grid, dim3(NT), 0, s, a2);  \
   else if (met) hipLaunchKernelGGL((k_split_glds<T_, false, true, D_>), grid, dim3(NT), 0, s, a2);    \
   else hipLaunchKernelGGL((k_split_glds<T_, false, false, D_>), grid, dim3(NT), 0, s, a2);
-    snprintf(params, sizeof(params), "%s, %s, %d", tf(znext), tf(met), glds);
-    note_split("k_split_glds", dtype, params);
+    char nm[160];
+    snprintf(nm, sizeof(nm), "void dopt::k_split_glds<%s, %s, %s, %d>(dopt::RoundArgs)", dtype == 0 ? "float" : "double",
+             tf(znext), tf(met), glds);
+    note_round_kernel(nm);
 #define GLDS(T_) if (glds == 2) { GLDS2(T_, 2) } else { GLDS2(T_, 3) }
     if (dtype == 0) { GLDS(float) } else { GLDS(double) }
 #undef GLDS
 #undef GLDS2
     return hipGetLastError();
   }
-  const char* cv = getenv("DOPT_SPLIT_CPB");
-  int cpb = cv ? atoi(cv) : 1;
-  if (!small || (pf && cpb > 2) || (a.nchunks + 64 * cpb - 1) / (64 * cpb) < 2 * a.groups) cpb = 1;
-  // A/B knob DOPT_SPLIT_COLWAVE (tools/split_ab.py): the column-per-wave kernel for <= 16 rows
-  const char* cw = getenv("DOPT_SPLIT_COLWAVE");
-  if (small && cw && cw[0] == '1') {
-    snprintf(params, sizeof(params), "%s, %s", tf(znext), tf(met));
-    note_split("k_split_colwave", dtype, params);
+  // DOPT_SPLIT_COLWAVE=1: the column-per-wave kernel for <= 16 rows (same element types only)
+  if (small && env_int("DOPT_SPLIT_COLWAVE", 0) == 1 && dtype == xdtype) {
 #define COLWAVE(T_)                                                                                       \
   if (znext && met) hipLaunchKernelGGL((k_split_colwave<T_, true, true>), grid, dim3(NT), 0, s, a2);       \
   else if (znext) hipLaunchKernelGGL((k_split_colwave<T_, true, false>), grid, dim3(NT), 0, s, a2);        \
@@ -767,60 +803,51 @@ hipError_t launch_split_step(int dtype, bool znext, bool met, const RoundArgs& a
 #undef COLWAVE
     return hipGetLastError();
   }
-#define SPLIT_STEP2(T_, R_, P_, C_)                                                                              \
-  if (znext && met) hipLaunchKernelGGL((k_split_step<T_, R_, true, true, P_, C_>), grid, dim3(NT), 0, s, a2);     \
-  else if (znext) hipLaunchKernelGGL((k_split_step<T_, R_, true, false, P_, C_>), grid, dim3(NT), 0, s, a2);      \
-  else if (met) hipLaunchKernelGGL((k_split_step<T_, R_, false, true, P_, C_>), grid, dim3(NT), 0, s, a2);        \
-  else hipLaunchKernelGGL((k_split_step<T_, R_, false, false, P_, C_>), grid, dim3(NT), 0, s, a2);
-#define SPLIT_STEP(T_, R_) if (pf) { SPLIT_STEP2(T_, R_, true, 1) } else { SPLIT_STEP2(T_, R_, false, 1) }
-#define SPLIT_SMALL(T_)                           \
-  if (cpb == 4) { SPLIT_STEP2(T_, 4, false, 4) }  \
-  else if (cpb == 2 && pf) { SPLIT_STEP2(T_, 4, true, 2) } \
-  else if (cpb == 2) { SPLIT_STEP2(T_, 4, false, 2) } \
-  else { SPLIT_STEP(T_, 4) }
+#endif
+  // CPB: 16-byte chunks per lane per block (A/B DOPT_SPLIT_CPB = 2 / 4; default 1)
+  int cpb = env_int("DOPT_SPLIT_CPB", 1);
+  if (!small || (pf && cpb > 2) || (a.nchunks + 64 * cpb - 1) / (64 * cpb) < 2 * a.groups) cpb = 1;
   snprintf(params, sizeof(params), "%d, %s, %s, %s, %d", small ? 4 : 16, tf(znext), tf(met),
            tf(small ? (cpb == 4 ? false : pf) : pf), small ? cpb : 1);
-  note_split("k_split_step", dtype, params);
-  if (dtype == 0) {
-    if (small) { SPLIT_SMALL(float) } else { SPLIT_STEP(float, 16) }
-  } else {
-    if (small) { SPLIT_SMALL(double) } else { SPLIT_STEP(double, 16) }
-  }
-#undef SPLIT_SMALL
-#undef SPLIT_STEP
-#undef SPLIT_STEP2
+  note_split("k_split_step", dtype, xdtype, params);
+  if (dtype == 0) split_step_t<float, float>(znext, met, small, pf, cpb, grid, a2, s);
+  else if (xdtype == 0) split_step_t<double, float>(znext, met, small, pf, cpb, grid, a2, s);
+  else split_step_t<double, double>(znext, met, small, pf, cpb, grid, a2, s);
   return hipGetLastError();
 }
 
-hipError_t launch_split_dots(int dtype, int mode, const RoundArgs& a, int n_workers, hipStream_t s) {
+template <typename T, typename S>
+static void split_dots_t(int mode, bool small, dim3 grid, const RoundArgs& a2, hipStream_t s) {
+#define SPLIT_DOTS(R_)                                                                        \
+  if (mode == 0) hipLaunchKernelGGL((k_split_dots<T, S, 0, R_>), grid, dim3(NT), 0, s, a2);   \
+  else hipLaunchKernelGGL((k_split_dots<T, S, 1, R_>), grid, dim3(NT), 0, s, a2);
+  if (small) { SPLIT_DOTS(4) } else { SPLIT_DOTS(16) }
+#undef SPLIT_DOTS
+}
+
+hipError_t launch_split_dots(int dtype, int xdtype, int mode, const RoundArgs& a, int n_workers, hipStream_t s) {
   if (n_workers <= 0) return hipSuccess;
+  if (!split_types_ok(dtype, xdtype)) return hipErrorInvalidValue;
   const dim3 grid(n_workers, a.groups);
   const bool small = a.b_rows <= 4 * NW;  // <= 16 rows: one 4-row chunk per wave, high occupancy
   RoundArgs a2 = a;
   a2.contig = split_contig();
-#define SPLIT_DOTS(T_, R_)                                                                       \
-  if (mode == 0) hipLaunchKernelGGL((k_split_dots<T_, 0, R_>), grid, dim3(NT), 0, s, a2);        \
-  else hipLaunchKernelGGL((k_split_dots<T_, 1, R_>), grid, dim3(NT), 0, s, a2);
-  if (dtype == 0) {
-    if (small) { SPLIT_DOTS(float, 4) } else { SPLIT_DOTS(float, 16) }
-  } else {
-    if (small) { SPLIT_DOTS(double, 4) } else { SPLIT_DOTS(double, 16) }
-  }
-#undef SPLIT_DOTS
+  if (dtype == 0) split_dots_t<float, float>(mode, small, grid, a2, s);
+  else if (xdtype == 0) split_dots_t<double, float>(mode, small, grid, a2, s);
+  else split_dots_t<double, double>(mode, small, grid, a2, s);
   return hipGetLastError();
 }
 
-hipError_t launch_split_coef(int dtype, int problem, int mode, const RoundArgs& a, int n_workers,
+hipError_t launch_split_coef(int dtype, int xdtype, int problem, int mode, const RoundArgs& a, int n_workers,
                              hipStream_t s) {
   if (n_workers <= 0) return hipSuccess;
+  if (!split_types_ok(dtype, xdtype)) return hipErrorInvalidValue;
   const dim3 grid(n_workers);
-  if (dtype == 0) {
-    if (problem == 0) hipLaunchKernelGGL((k_split_coef<float, 0>), grid, dim3(NT), 0, s, a, mode);
-    else hipLaunchKernelGGL((k_split_coef<float, 1>), grid, dim3(NT), 0, s, a, mode);
-  } else {
-    if (problem == 0) hipLaunchKernelGGL((k_split_coef<double, 0>), grid, dim3(NT), 0, s, a, mode);
-    else hipLaunchKernelGGL((k_split_coef<double, 1>), grid, dim3(NT), 0, s, a, mode);
-  }
+#define COEF(T_, S_)                                                                                  \
+  if (problem == 0) hipLaunchKernelGGL((k_split_coef<T_, S_, 0>), grid, dim3(NT), 0, s, a, mode);   \
+  else hipLaunchKernelGGL((k_split_coef<T_, S_, 1>), grid, dim3(NT), 0, s, a, mode);
+  if (dtype == 0) { COEF(float, float) } else if (xdtype == 0) { COEF(double, float) } else { COEF(double, double) }
+#undef COEF
   return hipGetLastError();
 }
 

@@ -359,7 +359,7 @@ int set_layout(dopt_ctx* c, int problem, int64_t n, int64_t d) {
   const int cpl = cpl_for(nch);
   c->split = cpl > max_chunks_per_lane(c->dtype, c->xdtype);
   // float32 rows under float64 arithmetic past the row-resident kernel: the row-space rounds
-  // only (rowspace.hip k_rs_pass_x32); the direct column-blocked kernels refuse them (split_x_ok)
+  // (k_rs_pass_x32) or the direct column-blocked kernels (k_split_*<double, float, ...>)
   if (c->split) {  // enough workgroups to fill 256 CUs several times over
     const int64_t nblk = (nch + 63) / 64;
     const char* gw = getenv("DOPT_SPLIT_WGS");  // A/B knob: target workgroups per column-blocked launch
@@ -561,29 +561,18 @@ int colsum_current(dopt_ctx* c) {
   return refresh_sums_t(c);
 }
 
-// The direct column-blocked kernels read the rows in the compute dtype: float32 rows under
-// float64 arithmetic (dopt_set_data_dtype) past the row-resident kernel take the row-space rounds
-// only.  ensure_split gives the error; the launch wrappers below are the backstop.
-int split_x_ok(dopt_ctx* c) {
-  if (c->xdtype == c->dtype) return DOPT_OK;
-  return fail(DOPT_ERR_UNSUPPORTED, "float32 shard storage under float64 arithmetic with rows of %lld elements: "
-              "only the row-space rounds (complete graph, full-shard batches of <= %d rows, equal starting "
-              "iterates, one context) read such rows; store the rows as float64", (long long)c->d, kRsMaxRows);
-}
-
+// The direct column-blocked kernels read the rows in their storage type (float32 rows under
+// float64 arithmetic: every product and sum the float64 one).
 hipError_t split_dots(dopt_ctx* c, int mode, const RoundArgs& a) {
-  if (c->xdtype != c->dtype) return hipErrorNotSupported;
-  return launch_split_dots(c->dtype, mode, a, (int)c->n, c->stream);
+  return launch_split_dots(c->dtype, c->xdtype, mode, a, (int)c->n, c->stream);
 }
 
 hipError_t split_step(dopt_ctx* c, bool znext, bool met, const RoundArgs& a) {
-  if (c->xdtype != c->dtype) return hipErrorNotSupported;
-  return launch_split_step(c->dtype, znext, met, a, (int)c->n, c->stream);
+  return launch_split_step(c->dtype, c->xdtype, znext, met, a, (int)c->n, c->stream);
 }
 
 // Column-blocked buffers: coefficients [n x bcap] and fp64 partial slabs.
 int ensure_split(dopt_ctx* c) {
-  if (int rc = split_x_ok(c)) return rc;
   int64_t bcap = std::max<int64_t>(1, c->max_m);
   if (c->obj_sep) bcap = std::max<int64_t>(bcap, (c->rows_o + c->n - 1) / c->n);
   const size_t need = (size_t)(c->n * bcap * c->split_groups);
@@ -613,7 +602,7 @@ int split_metrics(dopt_ctx* c, const void* x_state, const void* point, bool shar
   a.flags = (cons ? F_CONS : 0) | (loss ? F_LOSS : 0) | (shared ? F_SHARED : 0);
   if (a.flags & F_LOSS) c->loss_groups = c->n;  // per-worker loss slabs
   HIPOK(split_dots(c, 1, a));
-  HIPOK(launch_split_coef(c->dtype, c->problem, 2, a, (int)c->n, c->stream));
+  HIPOK(launch_split_coef(c->dtype, c->xdtype, c->problem, 2, a, (int)c->n, c->stream));
   return DOPT_OK;
 }
 
@@ -641,7 +630,7 @@ int run_dsgd_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batc
   p.x_old = c->xs[c->cur];
   if (full && !lag) {  // prologue: coefficients of the starting iterates (carried: the last step made them)
     HIPOK(split_dots(c, 0, p));
-    HIPOK(launch_split_coef(c->dtype, c->problem, 1, p, (int)c->n, c->stream));
+    HIPOK(launch_split_coef(c->dtype, c->xdtype, c->problem, 1, p, (int)c->n, c->stream));
   }
   HIPOK(launch_stamp(c->stamps, c->stream));
   for (int64_t h = 0; h < T; ++h) {
@@ -660,7 +649,7 @@ int run_dsgd_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batc
     a.lam = lam_grad;
     if (!full) {  // this round's minibatch coefficients
       HIPOK(split_dots(c, 0, a));
-      HIPOK(launch_split_coef(c->dtype, c->problem, 1, a, (int)c->n, c->stream));
+      HIPOK(launch_split_coef(c->dtype, c->xdtype, c->problem, 1, a, (int)c->n, c->stream));
     }
     const bool met = fused_met && metrics && (h > 0 || lag);
     a.flags |= (met && want_cons ? F_CONS : 0) | (met && want_obj ? F_LOSS : 0);
@@ -671,7 +660,7 @@ int run_dsgd_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batc
     if (full || met) {  // next coefficients (rows of the full shard) and the metric slabs
       RoundArgs q = a;
       q.idx = nullptr;
-      HIPOK(launch_split_coef(c->dtype, c->problem, (full ? 1 : 0) | (met ? 2 : 0), q, (int)c->n, c->stream));
+      HIPOK(launch_split_coef(c->dtype, c->xdtype, c->problem, (full ? 1 : 0) | (met ? 2 : 0), q, (int)c->n, c->stream));
     }
     HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur ^ 1], c->n, c->ld, (int32_t)c->nchs, kRowsPerGroup,
                                 c->part, c->stamps + h + 1, c->stream));
@@ -726,7 +715,7 @@ int run_centralized_split(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64
     a.lam = lam_grad;
     a.flags = F_SHARED | F_GOUT;  // no mixing here
     HIPOK(split_dots(c, 0, a));
-    HIPOK(launch_split_coef(c->dtype, c->problem, 1, a, (int)c->n, c->stream));
+    HIPOK(launch_split_coef(c->dtype, c->xdtype, c->problem, 1, a, (int)c->n, c->stream));
     if (c->prof && (rc = prof_event(c, false))) return rc;
     HIPOK(split_step(c, false, false, a));
     if (c->prof && (rc = prof_event(c, true))) return rc;
@@ -1672,11 +1661,26 @@ int dopt_eval_objective(dopt_ctx* c, int problem, int64_t n, int64_t d, const do
 }
 
 int dopt_eval_full(dopt_ctx* c, const double* w, double reg, double* f_out, double* g_out) {
-  CHECK_ARG(c && w && f_out && g_out, "NULL argument");
+  CHECK_ARG(c && w && f_out, "NULL argument");
   if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
-  if (c->split) return fail(DOPT_ERR_UNSUPPORTED, "full-data evaluation of column-blocked rows");
   int rc;
   if ((rc = set_device(c))) return rc;
+  if (c->split) {
+    // column-blocked rows (large d): the objective only, by the direct kernels' dots pass at the
+    // shared point (k_split_dots mode 1 -> k_split_coef mode 2), independent of the round kernels
+    if (g_out) return fail(DOPT_ERR_UNSUPPORTED, "full-data gradient of column-blocked rows (pass g_out = NULL)");
+    if ((rc = ensure_split(c))) return rc;
+    if ((rc = ensure_hist(c, 1))) return rc;
+    if ((rc = upload_rows(c, c->dtype, w, 0, c->xg[c->gcur ^ 1], 1, c->d, c->ld))) return rc;
+    if ((rc = split_metrics(c, nullptr, c->xg[c->gcur ^ 1], true, false, true))) return rc;
+    if ((rc = history(c, 0, c->xg[c->gcur ^ 1], false, true, c->n))) return rc;
+    double raw[3];
+    HIPOK(hipMemcpyAsync(raw, c->hraw, sizeof(raw), hipMemcpyDeviceToHost, c->stream));
+    HIPOK(hipStreamSynchronize(c->stream));
+    finalize_metrics(raw, 1, c->problem, 1, obj_rows(c), reg, 0.0, f_out, nullptr);
+    return DOPT_OK;
+  }
+  CHECK_ARG(g_out, "NULL argument");
   if (!c->G && (rc = dalloc(&c->G, (size_t)c->n * c->ld * c->esz))) return rc;
   if ((rc = ensure_hist(c, 1))) return rc;
   if ((rc = upload_rows(c, c->dtype, w, 0, c->xg[c->gcur ^ 1], 1, c->d, c->ld))) return rc;
@@ -1849,7 +1853,7 @@ int dopt_phase_begin(dopt_ctx* c, int64_t batch) {
       RoundArgs p = base_args(c);
       p.x_old = c->xs[c->cur];
       HIPOK(split_dots(c, 0, p));
-      HIPOK(launch_split_coef(c->dtype, c->problem, 1, p, (int)c->n, c->stream));
+      HIPOK(launch_split_coef(c->dtype, c->xdtype, c->problem, 1, p, (int)c->n, c->stream));
     }
   }
   return DOPT_OK;
@@ -1879,7 +1883,7 @@ int dopt_phase_grad(dopt_ctx* c, int64_t batch, const int32_t* idx, double lam_g
       a.b_rows = (int32_t)std::min<int64_t>(a.b_rows, batch);
       a.x_old = c->xs[c->cur];
       HIPOK(split_dots(c, 0, a));
-      HIPOK(launch_split_coef(c->dtype, c->problem, 1, a, (int)c->n, c->stream));
+      HIPOK(launch_split_coef(c->dtype, c->xdtype, c->problem, 1, a, (int)c->n, c->stream));
     }
     return DOPT_OK;
   }
@@ -1925,7 +1929,7 @@ int dopt_phase_mix(dopt_ctx* c, int64_t t, double eta0) {
     if (full || cons || loss) {
       RoundArgs q = a;
       q.idx = nullptr;
-      HIPOK(launch_split_coef(c->dtype, c->problem, (full ? 1 : 0) | ((cons || loss) ? 2 : 0), q, (int)c->n,
+      HIPOK(launch_split_coef(c->dtype, c->xdtype, c->problem, (full ? 1 : 0) | ((cons || loss) ? 2 : 0), q, (int)c->n,
                               c->stream));
     }
     c->send_fresh = false;
@@ -1965,7 +1969,7 @@ int dopt_phase_grad_shared(dopt_ctx* c, int64_t batch, const int32_t* idx, doubl
     if (fuse_loss) return fail(DOPT_ERR_UNSUPPORTED, "column-blocked rounds: use dopt_phase_metrics_pass_shared");
     if ((rc = ensure_split(c))) return rc;
     HIPOK(split_dots(c, 0, a));
-    HIPOK(launch_split_coef(c->dtype, c->problem, 1, a, (int)c->n, c->stream));
+    HIPOK(launch_split_coef(c->dtype, c->xdtype, c->problem, 1, a, (int)c->n, c->stream));
     if (c->prof && (rc = prof_event(c, false))) return rc;
     HIPOK(split_step(c, false, false, a));
     if (c->prof && (rc = prof_event(c, true))) return rc;

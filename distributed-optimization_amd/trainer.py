@@ -142,15 +142,15 @@ def _f32_exact(arrays):
 
 
 def _data_dtype(config, d, arrays):
-    """Shard storage: config 'data_dtype' = 'auto' (default: float32 when dtype is float64,
-    the rows fit the row-resident kernel and every value -- shards and a separate X_full --
-    is exactly float32; the arithmetic stays float64), 'float32' or 'float64'."""
+    """Shard storage: config 'data_dtype' = 'auto' (default: float32 when dtype is float64 and
+    every value -- shards and a separate X_full -- is exactly float32; the arithmetic stays
+    float64, on every path: fused, column-blocked and row-space rounds), 'float32' or 'float64'."""
     dtype = config.get("dtype", "float64")
     want = config.get("data_dtype", "auto")
     if _dopt.DTYPES[dtype] == _dopt.F32:
         return dtype
     if want == "auto":
-        return "float32" if 0 < d <= 2048 and _f32_exact(arrays) else "float64"
+        return "float32" if d > 0 and _f32_exact(arrays) else "float64"
     return want
 
 

@@ -107,7 +107,8 @@ int dopt_destroy(dopt_ctx *ctx);
  * to float64 as they are loaded, so on data that is exactly float32-representable the
  * round is the reference's float64 round at half the HBM bytes per row.  Other values
  * are rounded to float32 on upload (the drop-in trainers only choose DOPT_F32 storage
- * when that rounding is the identity).  Row-resident contexts only (d <= 2048 here).
+ * when that rounding is the identity).  Every path reads such rows: the fused round kernel,
+ * the column-blocked kernels and the row-space rounds (rows beyond 2048 elements).
  * Call before loading / generating the shards; it drops the loaded data. */
 int dopt_set_data_dtype(dopt_ctx *ctx, int data_dtype);
 int dopt_get_data_dtype(dopt_ctx *ctx, int *data_dtype);
@@ -344,7 +345,9 @@ int dopt_finalize_metrics(int problem, int64_t T, const double *raw, int64_t n_w
  * :39-44), g = mean_k c_k x_k + reg w (the full-gradient shape of
  * obj_problems.py:22-36 / :55-69).  One pass over the data; the building block
  * of the device f(x*) solver (solver.py) that replaces sklearn's saga at sizes
- * sklearn cannot handle (simulator.py:32-69). */
+ * sklearn cannot handle (simulator.py:32-69).  g_out may be NULL (objective only);
+ * column-blocked contexts (rows beyond the row-resident kernel) evaluate the objective only,
+ * with the direct kernels' dots pass (g_out must be NULL there). */
 int dopt_eval_full(dopt_ctx *ctx, const double *w, double reg, double *f_out, double *g_out);
 
 /* Device time of the dominant kernel (the fused round kernel) since the last call:

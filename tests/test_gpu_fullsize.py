@@ -115,6 +115,9 @@ def test_c5_d2pow20_1024_workers_full_size():
             np.testing.assert_allclose(cons[0], np.mean(np.sum((xn - xb) ** 2, axis=1)), rtol=1e-3)
             np.testing.assert_allclose(cons[0], cons_all[t], rtol=1e-5)
             np.testing.assert_allclose(obj[0], obj_all[t], rtol=1e-5)
+            # the objective at xbar over all 16384 rows (trainer.py:188-191) by an independent pass
+            # (dopt_eval_full: the dots-only kernel at the shared point), float32 engine
+            np.testing.assert_allclose(obj[0], eng.eval_full(xb, lam, gradient=False)[0], rtol=1e-5)
             x = xn
         # one call (next round's coefficients fused into the step) or T calls (a dots pass per call):
         # the same rounds up to the row-dot summation tree
@@ -147,6 +150,7 @@ def test_c5_rowspace_full_size_vs_direct(monkeypatch):
             np.testing.assert_allclose(x1[i], ref, rtol=2e-5, atol=1e-7 * np.abs(ref).max())
         xb = x1.mean(axis=0)
         np.testing.assert_allclose(c1[0], np.mean(np.sum((x1 - xb) ** 2, axis=1)), rtol=1e-4)
+        np.testing.assert_allclose(o1[0], eng.eval_full(xb, lam, gradient=False)[0], rtol=1e-5)
         del x1
         o23, c23, _ = eng.run_dsgd(T - 1, eta0, m, lam, lam, 0.0, t0=1)
         x_rs = eng.get_models()
@@ -162,7 +166,7 @@ def test_c5_rowspace_full_size_vs_direct(monkeypatch):
         eng.close()
 
 
-def test_c5_x32_full_size_host_rounds():
+def test_c5_x32_full_size_host_rounds(monkeypatch):
     """C5 at the reference's float64 arithmetic over float32-stored rows (k_rs_pass_x32, the bench's
     C5 default) from Worker.x = zeros: every round recomputed on the host for several workers
     (mixing sum over all iterates, float64 gradient; trainer.py:173-175) at rtol 1e-8, consensus
@@ -198,7 +202,19 @@ def test_c5_x32_full_size_host_rounds():
             np.testing.assert_allclose(c[0], np.mean(np.sum((xn - xb) ** 2, axis=1)), rtol=1e-8)
             np.testing.assert_allclose(c[0], c_all[t], rtol=1e-12)
             np.testing.assert_allclose(o[0], o_all[t], rtol=1e-12)
+            # the objective at xbar over all 16384 rows (trainer.py:188-191) by an independent pass:
+            # dopt_eval_full's dots-only kernel over the float32 rows, float64 arithmetic
+            np.testing.assert_allclose(o[0], eng.eval_full(xb, lam, gradient=False)[0], rtol=1e-10)
             x = xn
         np.testing.assert_allclose(x, x_all, rtol=1e-12, atol=1e-14 * np.abs(x_all).max())
+        # the same 3 rounds by the DIRECT column-blocked kernels over the float32 rows (k_split_step
+        # <double, float, ...>: the row-space rounds off), from the same zero start
+        monkeypatch.setenv("DOPT_ROWSPACE", "0")
+        eng.set_models(np.zeros((n, d)))
+        od, cd, _ = eng.run_dsgd(T, eta0, m, lam, lam, 0.0)
+        assert _dopt.last_round_kernel().startswith("void dopt::k_split_step<double, float,")
+        np.testing.assert_allclose(od, o_all, rtol=1e-10)
+        np.testing.assert_allclose(cd, c_all, rtol=1e-9)
+        np.testing.assert_allclose(eng.get_models(), x_all, rtol=1e-10, atol=1e-12 * np.abs(x_all).max())
     finally:
         eng.close()

@@ -1,6 +1,8 @@
 """Column-blocked rounds (d beyond the row-resident kernel: config C5, d = 2^20) and
 complete-graph mean mixing, against the oracle (float64, rtol 1e-9) and against
 host recomputation at full C5 row length."""
+import os
+
 import numpy as np
 import pytest
 
@@ -22,12 +24,21 @@ def _data(n, d, m, seed, problem):
 
 
 def _engine(shards, problem, dtype="float64"):
-    eng = _dopt.Engine(0, dtype)
+    """dtype 'float64/x32': float64 arithmetic over float32-stored rows."""
+    if dtype == "float64/x32":
+        eng = _dopt.Engine(0, "float64", data_dtype="float32")
+    else:
+        eng = _dopt.Engine(0, dtype)
     off = np.concatenate([[0], np.cumsum([len(s[1]) for s in shards])])
     eng.load_shards(problem, np.vstack([s[0] for s in shards]), np.concatenate([s[1] for s in shards]), off)
     return eng
 
 
+def _f32_exact(shards):
+    return [(X.astype(np.float32).astype(np.float64), y.astype(np.float32).astype(np.float64)) for X, y in shards]
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float64/x32"])
 @pytest.mark.parametrize("problem,topo,batch,mean,m,rowspace", [
     ("logistic", "ring", 12, False, 12, "1"),        # full shard: next-round dots fused into the step
     ("logistic", "ring", 5, False, 12, "1"),         # minibatches: separate dots pass per round
@@ -38,14 +49,18 @@ def _engine(shards, problem, dtype="float64"):
     ("quadratic", "grid", 4, False, 12, "1"),
     ("logistic", "ring", 24, False, 24, "1"),        # > 16 rows per worker: the row-split step kernel
 ])
-def test_split_rounds_vs_oracle(problem, topo, batch, mean, m, rowspace, monkeypatch):
+def test_split_rounds_vs_oracle(problem, topo, batch, mean, m, rowspace, dtype, monkeypatch):
+    """float64/x32: the same rounds over float32-stored rows under float64 arithmetic (data exactly
+    float32; k_split_* / k_rs_pass_x32 <double, float>), against the same float64 oracle."""
     monkeypatch.setenv("DOPT_ROWSPACE", rowspace)
     n, d, T = 9, 2100, 6  # d = 2100 fp64 -> 1050 chunks > 1024: column-blocked path
     shards = _data(n, d, m, 1, problem)
+    if dtype == "float64/x32":
+        shards = _f32_exact(shards)
     cfg = {"problem_type": problem, "local_batch_size": batch, "learning_rate_eta0": 0.05,
            "l2_regularization_lambda": 1e-3, "strong_convexity_mu": 2e-3}
     top = TP.build(topo, n)
-    eng = _engine(shards, problem)
+    eng = _engine(shards, problem, dtype)
     if mean:
         eng.set_mixing_mean(*top.uniform_offdiag())
     else:
@@ -66,6 +81,8 @@ def test_split_rounds_vs_oracle(problem, topo, batch, mean, m, rowspace, monkeyp
     eng.close()
 
 
+@pytest.mark.skipif(os.environ.get("DOPT_AB") != "1",
+                    reason="A/B build only (make AB=1): k_split_glds is not in the shipped library")
 @pytest.mark.parametrize("dtype", ["float64", "float32"])
 def test_split_glds_kernel_bitwise_equals_prefetch_kernel(dtype, monkeypatch):
     """k_split_glds (LDS-DMA ring, DOPT_SPLIT_GLDS = 2 / 3 blocks in flight) does the prefetching
