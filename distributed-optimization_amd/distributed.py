@@ -648,6 +648,7 @@ class DistributedCentralized:
 
     _solo = DistributedDSGD._solo
     _all_reduce = DistributedDSGD._all_reduce
+    _all_reduce_start = DistributedDSGD._all_reduce_start
 
     def run(self, T, eta0, batch, lam_grad, lam_obj, f_opt=0.0, t0=0, objective=True, idx=None):
         torch = self.torch
