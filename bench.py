@@ -476,14 +476,16 @@ def setup_leg(args, config, n_global, world, rank, dev):
     eta0 = S.eta0
     if world > 1 or args.phase:
         mean_local = None if S.mean is None else (S.mean[0], S.mean[1][plan.lo:plan.hi])
-        runner = distributed.DistributedDSGD(eng, plan, n_global, n_global * m, device=dev, mean=mean_local)
+        runner = distributed.DistributedDSGD(eng, plan, n_global, n_global * m, device=dev, mean=mean_local,
+                                             rs_chunks=args.rs_chunks or None)
         ld, esz_state = eng.layout()
         S.comm = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
                   "halo_rows_in": int(plan.n_halo), "send_rows_out": int(len(plan.send_ids)),
                   "halo_bytes_in_per_round": int(plan.n_halo) * ld * esz_state,
                   "send_bytes_out_per_round": int(len(plan.send_ids)) * ld * esz_state,
                   "peers": [int(p) for p in runner._peers],
-                  "allreduce_bytes_per_round": ld * 8}
+                  "allreduce_bytes_per_round": ld * 8,
+                  "allreduce_chunks": runner.rs_chunks if S.mean is not None else 1}
         log(f"comm: {S.comm}")
         if runner._lagged_ok or (S.mean is not None and runner._rowspace_ready()):
             # the lagged schedule / the row-space rounds continued across calls (as on one GPU: timed_leg)
@@ -602,6 +604,9 @@ def main():
     ap.add_argument("--partition", default="spectral", choices=["spectral", "ranges"],
                     help="C3 at N > 1: workers -> GPUs by graph partition (recursive spectral bisection, "
                          "computed on rank 0 and broadcast) or by contiguous id ranges")
+    ap.add_argument("--rs-chunks", type=int, default=0,
+                    help="C5 across ranks (or --phase): column chunks of the row-space pass, each chunk's sums "
+                         "all-reduced while the next streams (0: distributed.RS_CHUNKS, 1 at world size 1)")
     ap.add_argument("--pcie", action="store_true",
                     help="C3, 1 GPU: after the timed region, hand the same shards over as host buffers "
                          "(dopt_load_shards, the drop-in boundary) and report the PCIe-inclusive rate in a "

@@ -93,6 +93,8 @@ _SIGS = {
     "dopt_rs_phase_round": ([_P, _I64, _D, _D, ctypes.c_uint32, _P], ctypes.c_int),
     "dopt_rs_phase_cols": ([_P, _I64, _D, _D, _P], ctypes.c_int),
     "dopt_rs_phase_metrics": ([_P, ctypes.c_uint32], ctypes.c_int),
+    "dopt_rs_phase_pass": ([_P, ctypes.c_int32, ctypes.c_int32, _P, _P], ctypes.c_int),
+    "dopt_rs_phase_rows": ([_P, _I64, _D, _D, ctypes.c_uint32], ctypes.c_int),
     "dopt_zero_models": ([_P], ctypes.c_int),
     "dopt_sync": ([_P], ctypes.c_int),
     "dopt_finalize_metrics": ([ctypes.c_int, _I64, _P, _I64, _I64, _D, _D, _P, _P], ctypes.c_int),
@@ -483,6 +485,16 @@ class Engine:
 
     def rs_phase_cols(self, t, eta0, lam_grad, sum_ptr):
         check(lib().dopt_rs_phase_cols(self._h, int(t), float(eta0), float(lam_grad), ctypes.c_void_p(sum_ptr)))
+
+    def rs_phase_pass(self, chunk, n_chunks, sum_ptr):
+        """The row-space pass over column chunk `chunk` of `n_chunks`; returns the column range
+        (c0, c1) whose local sums it wrote to sum_ptr[c0:c1)."""
+        rng = np.zeros(2, dtype=np.int64)
+        check(lib().dopt_rs_phase_pass(self._h, int(chunk), int(n_chunks), ctypes.c_void_p(sum_ptr), _ptr(rng)))
+        return int(rng[0]), int(rng[1])
+
+    def rs_phase_rows(self, t, eta0, lam_grad, metric_flags):
+        check(lib().dopt_rs_phase_rows(self._h, int(t), float(eta0), float(lam_grad), int(metric_flags)))
 
     def rs_phase_metrics(self, metric_flags):
         check(lib().dopt_rs_phase_metrics(self._h, int(metric_flags)))

@@ -132,15 +132,20 @@ struct RsArgs {
   void* xbar_out;          // [ld] T copy of the updated xbar
   const double* csum;      // [ld] all-reduced column sums C (multi-GPU), or null: sum cpart
   double a1, q, eta, eta_n;  // w_off N, W_ii - w_off - eta mu, eta, eta / N
+  int32_t blk0;            // first column block of this pass launch (column-chunked passes)
 };
 // dtype: arithmetic; xdtype: row storage (float32 rows under float64 arithmetic: k_rs_pass_x32).
-hipError_t launch_rs_pass(int dtype, int xdtype, bool cols, const RsArgs& a, hipStream_t s);
+// Column blocks [a.blk0, a.blk0 + nblk) of the pass (nblk <= 0: all of a.nblk from a.blk0 = 0).
+hipError_t launch_rs_pass(int dtype, int xdtype, bool cols, const RsArgs& a, hipStream_t s, int nblk = 0);
+// Elements [c0, c1) of one pass's column blocks [b0, b1) (clipped to the row stride).
+void rs_block_cols(const RsArgs& a, int xdtype, int b0, int b1, int64_t* c0, int64_t* c1);
 // mode bits: 1 metric partials of the iterate the pass read, 2 next round's row state,
 // 4 initial state (z = v = u, beta = 0), 8 u = 0 without reading upart (zero start)
 hipError_t launch_rs_rows(int dtype, const RsArgs& a, int n_workers, int mode, hipStream_t s);
 int rs_col_blocks(int64_t ld);  // blocks of k_rs_cols / k_rs_init (= RsArgs.nd)
 hipError_t launch_rs_cols(int dtype, const RsArgs& a, hipStream_t s);
-hipError_t launch_rs_csum(const RsArgs& a, double* out, hipStream_t s);
+// out[c0:c1) = sum_g cpart[g][c0:c1) (this rank's column sums of those columns).
+hipError_t launch_rs_csum(const RsArgs& a, double* out, hipStream_t s, int64_t c0 = 0, int64_t c1 = -1);
 // History row (cons, loss, ||xbar||^2) of the row-space rounds from the slabs and partials.
 hipError_t launch_rs_hist(const RsArgs& a, int n_workers, double* out, hipStream_t s);
 hipError_t launch_rs_init(int dtype, const RsArgs& a, const void* x0, hipStream_t s);

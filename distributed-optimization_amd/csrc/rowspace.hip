@@ -55,7 +55,7 @@ __device__ __forceinline__ void rs_pass_body(const RsArgs& a, double* red) {
   constexpr bool SAME = std::is_same<T, XT>::value;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int blk = blockIdx.x, g = blockIdx.y;
+  const int blk = blockIdx.x + a.blk0, g = blockIdx.y;
   const int nch = a.nch;
   const int64_t ld = a.ld;
   const XT* __restrict__ X = (const XT*)a.X;
@@ -335,10 +335,11 @@ __global__ __launch_bounds__(NT) void k_rs_cols(const RsArgs a) {
   }
 }
 
-// Local column sums C_rank = sum_g cpart[g] into csum (multi-GPU: all-reduced before k_rs_cols).
-__global__ __launch_bounds__(NT) void k_rs_csum(const RsArgs a, double* out) {
-  const int64_t e = (int64_t)blockIdx.x * NT + threadIdx.x;
-  if (e >= a.ld) return;
+// Local column sums C_rank = sum_g cpart[g] into csum, columns [c0, c1) (multi-GPU: all-reduced
+// before k_rs_cols; a column-chunked pass reduces each chunk's columns as soon as they are done).
+__global__ __launch_bounds__(NT) void k_rs_csum(const RsArgs a, double* out, int64_t c0, int64_t c1) {
+  const int64_t e = c0 + (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (e >= c1) return;
   double C = 0.0;
   for (int g = 0; g < a.wg; ++g) C += a.cpart[(int64_t)g * a.ld + e];
   out[e] = C;
@@ -568,8 +569,19 @@ static hipError_t rs_pass_shape(const RsArgs& a, dim3 grid, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_rs_pass(int dtype, int xdtype, bool cols, const RsArgs& a, hipStream_t s) {
-  const dim3 grid(a.nblk, a.wg);
+void rs_block_cols(const RsArgs& a, int xdtype, int b0, int b1, int64_t* c0, int64_t* c1) {
+  const int64_t per = (int64_t)64 * a.cb * (xdtype == 0 ? 4 : 2);  // elements of one column block
+  *c0 = std::min<int64_t>(a.ld, b0 * per);
+  *c1 = std::min<int64_t>(a.ld, b1 * per);
+}
+
+hipError_t launch_rs_pass(int dtype, int xdtype, bool cols, const RsArgs& a, hipStream_t s, int nblk) {
+  if (nblk <= 0) {
+    if (a.blk0 != 0) return hipErrorInvalidValue;
+    nblk = a.nblk;
+  }
+  if (a.blk0 < 0 || a.blk0 + nblk > a.nblk) return hipErrorInvalidValue;
+  const dim3 grid(nblk, a.wg);
   const bool x32 = dtype == 1 && xdtype == 0;
   if (dtype != xdtype && !x32) return hipErrorInvalidValue;
   char buf[112];
@@ -607,8 +619,10 @@ hipError_t launch_rs_hist(const RsArgs& a, int n_workers, double* out, hipStream
   return hipGetLastError();
 }
 
-hipError_t launch_rs_csum(const RsArgs& a, double* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_rs_csum, dim3(rs_col_blocks(a.ld)), dim3(NT), 0, s, a, out);
+hipError_t launch_rs_csum(const RsArgs& a, double* out, hipStream_t s, int64_t c0, int64_t c1) {
+  if (c1 < 0) c1 = a.ld;
+  if (c1 <= c0) return hipSuccess;
+  hipLaunchKernelGGL(k_rs_csum, dim3(rs_col_blocks(c1 - c0)), dim3(NT), 0, s, a, out, c0, c1);
   return hipGetLastError();
 }
 

@@ -2156,6 +2156,44 @@ int dopt_rs_phase_round(dopt_ctx* c, int64_t t, double eta0, double lam_grad, ui
   return DOPT_OK;
 }
 
+int dopt_rs_phase_pass(dopt_ctx* c, int32_t chunk, int32_t n_chunks, double* sum_dev, int64_t* col_range) {
+  CHECK_ARG(c && sum_dev && col_range, "NULL argument");
+  if (!c->rs_live) return fail(DOPT_ERR_STATE, "dopt_rs_phase_begin first");
+  CHECK_ARG(n_chunks >= 1 && chunk >= 0 && chunk < n_chunks, "chunk %d of %d", chunk, n_chunks);
+  const int dt = c->dtype == DOPT_F32 ? 0 : 1;
+  RsArgs a = rs_args(c);
+  a.xbar = c->xbar[c->xb];
+  const int nb = std::min<int>(n_chunks, a.nblk);  // more chunks than blocks: the extra ones are empty
+  const int b0 = chunk < nb ? (int)((int64_t)a.nblk * chunk / nb) : a.nblk;
+  const int b1 = chunk < nb ? (int)((int64_t)a.nblk * (chunk + 1) / nb) : a.nblk;
+  rs_block_cols(a, rs_xdt(c), b0, b1, &col_range[0], &col_range[1]);
+  int rc;
+  if (c->prof && chunk == 0 && (rc = prof_event(c, false))) return rc;  // one bracket around the whole pass
+  if (b1 > b0) {
+    a.blk0 = b0;
+    HIPOK(launch_rs_pass(dt, rs_xdt(c), true, a, c->stream, b1 - b0));
+    HIPOK(launch_rs_csum(a, sum_dev, c->stream, col_range[0], col_range[1]));
+  }
+  if (c->prof && chunk == n_chunks - 1 && (rc = prof_event(c, true))) return rc;
+  c->rs_xs_valid = false;
+  return DOPT_OK;
+}
+
+int dopt_rs_phase_rows(dopt_ctx* c, int64_t t, double eta0, double lam_grad, uint32_t metric_flags) {
+  CHECK_ARG(c, "ctx is NULL");
+  if (!c->rs_live) return fail(DOPT_ERR_STATE, "dopt_rs_phase_begin first");
+  const int dt = c->dtype == DOPT_F32 ? 0 : 1;
+  RsArgs a = rs_args(c);
+  rs_round_args(c, a, t, eta0, lam_grad);
+  const bool met = (metric_flags & (DOPT_RUN_OBJECTIVE | DOPT_RUN_CONSENSUS)) != 0;
+  a.slab_cons = (metric_flags & DOPT_RUN_CONSENSUS) ? c->slab_cons : nullptr;
+  a.slab_loss = (metric_flags & DOPT_RUN_OBJECTIVE) ? c->slab_loss : nullptr;
+  HIPOK(launch_rs_rows(dt, a, (int)c->n, 2 | (met ? 1 : 0), c->stream));
+  c->cons_n = c->n;
+  c->slab_n[0] = c->n;
+  return DOPT_OK;
+}
+
 int dopt_rs_phase_cols(dopt_ctx* c, int64_t t, double eta0, double lam_grad, const double* sum_dev) {
   CHECK_ARG(c && sum_dev, "NULL argument");
   if (!c->rs_live) return fail(DOPT_ERR_STATE, "dopt_rs_phase_begin first");

@@ -36,6 +36,7 @@ import _dopt
 
 
 DEFAULT_TIMEOUT_S = 300.0
+RS_CHUNKS = 4  # column chunks of the complete graph's row-space pass across ranks
 
 
 class CollectiveError(RuntimeError):
@@ -285,11 +286,14 @@ class HaloExchange:
 class DistributedDSGD:
     """Drives one rank's engine through the round phases with torch.distributed."""
 
-    def __init__(self, engine, plan, n_global, rows_global, device=0, group=None, mean=None, obj_sep=False):
+    def __init__(self, engine, plan, n_global, rows_global, device=0, group=None, mean=None, obj_sep=False,
+                 rs_chunks=None):
         """`mean` = (w_off, W_ii of the local workers) for the complete graph: the mix then
         uses the all-reduced column sums and no halo rows move at all.  `rows_global` is
         the row count of the objective data (all shards, or the X_full slices loaded with
-        Engine.load_objective_data when obj_sep)."""
+        Engine.load_objective_data when obj_sep).  `rs_chunks`: column chunks of the row-space
+        pass (complete graph), each chunk's sums all-reduced while the next one streams
+        (default: 1 at world size 1, else RS_CHUNKS)."""
         self.obj_sep = obj_sep
         import torch
         import torch.distributed as dist
@@ -307,6 +311,7 @@ class DistributedDSGD:
         self.send = torch.zeros((max(1, len(plan.send_ids)), ld), dtype=tdt, device=self.dev)
         self.sum = torch.zeros(ld, dtype=torch.float64, device=self.dev)
         self.exchange = HaloExchange(plan, self.send, self.halo, group, self.device_comm)
+        self.rs_chunks = int(rs_chunks) if rs_chunks else (1 if self._solo() else RS_CHUNKS)
         engine.set_partition(self.n_global, self.rows_global)
         if mean is None:
             engine.set_halo(plan.n_halo, self.halo.data_ptr(), plan.send_ids, self.send.data_ptr())
@@ -477,13 +482,21 @@ class DistributedDSGD:
                 eng.phase_fold(base if consensus else None, base + 16 if objective and xnorm else None,
                                base + 8 if objective else None, 0)
 
+            K = self.rs_chunks
             for h in range(T):
                 met = mf and (h > 0 or owed)
-                eng.rs_phase_round(t0 + h, eta0, lam_grad, mf if met else 0, self.sum.data_ptr())
+                works = []
+                for k in range(K):  # the sums of column chunk k are all-reduced while chunk k + 1 streams
+                    c0, c1 = eng.rs_phase_pass(k, K, self.sum.data_ptr())
+                    if c1 > c0:
+                        works.append(self._all_reduce_start(self.sum[c0:c1]))
+                eng.rs_phase_rows(t0 + h, eta0, lam_grad, mf if met else 0)
                 if met:
                     fold(e)
                     e += 1
-                self._all_reduce(self.sum)
+                for w in works:
+                    if w is not None:
+                        _wait(w, f"all_reduce of a column chunk of the {self.ld} column sums", self.plan.rank)
                 eng.rs_phase_cols(t0 + h, eta0, lam_grad, self.sum.data_ptr())
             if mf and not leave:
                 eng.rs_phase_metrics(mf)

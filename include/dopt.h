@@ -310,6 +310,15 @@ int dopt_rs_phase_begin(dopt_ctx *ctx, int commit, int *ok, uint64_t *hash);
 int dopt_rs_phase_round(dopt_ctx *ctx, int64_t t, double eta0, double lam_grad, uint32_t metric_flags,
                         double *sum_dev);
 int dopt_rs_phase_cols(dopt_ctx *ctx, int64_t t, double eta0, double lam_grad, const double *sum_dev);
+/* The same round with the pass split into column chunks, so the caller can all-reduce chunk k's
+ * sums while chunk k + 1 streams (distributed.py, the complete-graph average across ranks):
+ * dopt_rs_phase_pass: the pass over column chunk `chunk` of `n_chunks` (contiguous column
+ *   blocks) at the current average; this rank's column sums of those columns -> sum_dev[c0:c1),
+ *   col_range[2] = {c0, c1} (empty when there are more chunks than column blocks).
+ * dopt_rs_phase_rows: after every chunk's pass, round t's next row state and (metric_flags) the
+ *   metric partials of the current iterates; then dopt_rs_phase_cols with the reduced sums. */
+int dopt_rs_phase_pass(dopt_ctx *ctx, int32_t chunk, int32_t n_chunks, double *sum_dev, int64_t *col_range);
+int dopt_rs_phase_rows(dopt_ctx *ctx, int64_t t, double eta0, double lam_grad, uint32_t metric_flags);
 int dopt_rs_phase_metrics(dopt_ctx *ctx, uint32_t metric_flags);
 /* dopt_phase_colsum_fold: dopt_phase_colsum, plus (same launch) the fold of the consensus slab
  *   of the last dopt_phase_mix_lagged / dopt_phase_cons, loss slab 0 and ||xbar||^2 of the

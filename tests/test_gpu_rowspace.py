@@ -164,7 +164,7 @@ def _rs_data(x32):
     return shards
 
 
-def _rs_rank(rank, world, port, out, T, pipe=False, x32=False):
+def _rs_rank(rank, world, port, out, T, pipe=False, x32=False, chunks=None):
     import os
 
     import torch  # noqa: F401  (one HIP runtime, loaded before libdopt)
@@ -185,7 +185,7 @@ def _rs_rank(rank, world, port, out, T, pipe=False, x32=False):
     off = np.concatenate([[0], np.cumsum([len(s[1]) for s in mine])])
     eng.load_shards("quadratic", np.vstack([s[0] for s in mine]), np.concatenate([s[1] for s in mine]), off)
     w_off, diag = TP.fully_connected(n).uniform_offdiag()
-    run = Dm.DistributedDSGD(eng, plan, n, sum(SIZES_D), device=0, mean=(w_off, diag[lo:hi]))
+    run = Dm.DistributedDSGD(eng, plan, n, sum(SIZES_D), device=0, mean=(w_off, diag[lo:hi]), rs_chunks=chunks)
     b = max(SIZES_D)
     o1, c1 = run.run(3, 0.05, b, 2e-3, 1e-3, 0.1)
     kern = _dopt.last_round_kernel()
@@ -206,12 +206,16 @@ def _rs_rank(rank, world, port, out, T, pipe=False, x32=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,pipe,x32", [(2, False, False), (3, False, False), (2, True, False), (2, True, True)])
-def test_rowspace_ranks_vs_oracle(tmp_path, world, pipe, x32):
+@pytest.mark.parametrize("world,pipe,x32,chunks", [(2, False, False, None), (3, False, False, None),
+                                                  (2, True, False, None), (2, True, True, None),
+                                                  (2, False, False, 1), (3, True, True, 16)])
+def test_rowspace_ranks_vs_oracle(tmp_path, world, pipe, x32, chunks):
     """Row-space rounds across ranks (gloo, contexts sharing the GPU): each rank's pass gives its
     column sums, all-reduced into the replicated average; history and gathered iterates vs the
     oracle at rtol 1e-9 (float64); pipe: the later rounds as a chain of pipelined calls; x32:
-    float32-stored rows under float64 arithmetic (k_rs_pass_x32)."""
+    float32-stored rows under float64 arithmetic (k_rs_pass_x32); chunks: the pass in that many
+    column chunks, each chunk's sums all-reduced on their own (default RS_CHUNKS = 4; 16 is more
+    chunks than the pass has column blocks: empty chunks)."""
     import socket
 
     import torch.multiprocessing as mp
@@ -221,7 +225,7 @@ def test_rowspace_ranks_vs_oracle(tmp_path, world, pipe, x32):
     port = s.getsockname()[1]
     s.close()
     T = 7
-    mp.start_processes(_rs_rank, args=(world, port, str(tmp_path), T, pipe, x32), nprocs=world, join=True,
+    mp.start_processes(_rs_rank, args=(world, port, str(tmp_path), T, pipe, x32, chunks), nprocs=world, join=True,
                        start_method="spawn")
     got = np.load(tmp_path / "rs.npz")
     assert ("k_rs_pass_x32<true" if x32 else "k_rs_pass<double, true") in str(got["kern"])
