@@ -1440,9 +1440,8 @@ __global__ __launch_bounds__(NT) void k_mix(const RoundArgs a, const T* __restri
 
 template <typename T>
 static hipError_t launch_mix_t(int cpl, const RoundArgs& a, const T* G, int n, hipStream_t s) {
-  // A/B knob DOPT_MIX_ONEWAVE=1: one wave per worker for rows of 8 / 16 chunks per lane
-  const char* ov = getenv("DOPT_MIX_ONEWAVE");
-  const bool one = ov && ov[0] == '1';
+  // A/B builds: DOPT_MIX_ONEWAVE=1, one wave per worker for rows of 8 / 16 chunks per lane
+  const bool one = env_int("DOPT_MIX_ONEWAVE", 0) == 1;
   const dim3 grid((n + NW - 1) / NW);
   if (!one && (cpl == 8 || cpl == 16)) {
     const int wpw = cpl / 4;

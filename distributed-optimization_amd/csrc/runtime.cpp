@@ -58,6 +58,18 @@ int fail(int code, const char* fmt, ...) {
     if (e_ != hipSuccess) return fail(DOPT_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
 
+// Launch-shape tuning knobs: read from the environment only in A/B builds (make AB=1); the
+// shipped library uses the measured defaults whatever the environment holds.
+int64_t ab_knob(const char* name, int64_t dflt) {
+#ifdef DOPT_AB
+  const char* v = getenv(name);
+  return v ? atoll(v) : dflt;
+#else
+  (void)name;
+  return dflt;
+#endif
+}
+
 #define CHECK_ARG(cond, ...)                          \
   do {                                                \
     if (!(cond)) return fail(DOPT_ERR_INVALID, __VA_ARGS__); \
@@ -362,8 +374,7 @@ int set_layout(dopt_ctx* c, int problem, int64_t n, int64_t d) {
   // (k_rs_pass_x32) or the direct column-blocked kernels (k_split_*<double, float, ...>)
   if (c->split) {  // enough workgroups to fill 256 CUs several times over
     const int64_t nblk = (nch + 63) / 64;
-    const char* gw = getenv("DOPT_SPLIT_WGS");  // A/B knob: target workgroups per column-blocked launch
-    const int64_t target = gw ? std::max<int64_t>(1, atoll(gw)) : 4096;
+    const int64_t target = std::max<int64_t>(1, ab_knob("DOPT_SPLIT_WGS", 4096));  // workgroups per launch
     c->split_groups = (int)std::max<int64_t>(1, std::min<int64_t>(nblk, (target + n - 1) / n));
   }
   c->problem = problem;
@@ -395,11 +406,10 @@ int ensure_hist(dopt_ctx* c, int64_t T) {
   return DOPT_OK;
 }
 
-// fp32 complete-graph mixing reads the column sums as T (DOPT_MEAN_SUMS_T=0: as float64)
+// fp32 complete-graph mixing reads the column sums as T (A/B builds: DOPT_MEAN_SUMS_T=0, as float64)
 bool sums_t_enabled(dopt_ctx* c) {
   if (c->dtype != DOPT_F32) return false;
-  const char* v = getenv("DOPT_MEAN_SUMS_T");
-  return !(v && v[0] == '0');
+  return ab_knob("DOPT_MEAN_SUMS_T", 1) != 0;
 }
 
 // The T copy of the sums the next mix reads (after every producer of S / S_ext).
@@ -786,18 +796,15 @@ constexpr int kRsCheckGroups = 16;  // column groups of the equal-start check
 
 int ensure_rs(dopt_ctx* c) {
   if (c->rs_wg > 0) return DOPT_OK;
-  // pass shape (A/B knobs DOPT_RS_CB / DOPT_RS_NBUF: the compiled pairs in rowspace.hip)
-  const char* cbv = getenv("DOPT_RS_CB");
-  const char* nbv = getenv("DOPT_RS_NBUF");
+  // pass shape (A/B builds: DOPT_RS_CB / DOPT_RS_NBUF pick the compiled pairs in rowspace.hip)
   // C5 float32 (tools/rs_ab.py, interleaved on one box, round ms): CB / NBUF / row groups
   // 2 / 6 / 2 11.22, 2 / 4 / 2 11.50, 1 / 8 / 4 11.46-11.84, 2 / 6 / 4 11.33-11.57, 4 / 2 / 4 12.36,
   // 1 / 8 / 16 12.36, 4 / 2 / 16 13.1-13.2: the partial sums' writes (dots nblk x rows, column
   // sums groups x ld) and long row visits matter more than the tail of ~4k 16 MiB workgroups
-  c->rs_cb = cbv ? atoi(cbv) : 2;
-  c->rs_nbuf = nbv ? atoi(nbv) : 6;
+  c->rs_cb = (int)ab_knob("DOPT_RS_CB", 2);
+  c->rs_nbuf = (int)ab_knob("DOPT_RS_NBUF", 6);
   const int64_t nblk = (c->nch + 64 * c->rs_cb - 1) / (64 * c->rs_cb);
-  const char* ev = getenv("DOPT_RS_WG");
-  int64_t wg = ev ? atoll(ev) : (c->rows + 8191) / 8192;  // ~8k rows per row group
+  int64_t wg = ab_knob("DOPT_RS_WG", (c->rows + 8191) / 8192);  // ~8k rows per row group
   wg = std::max<int64_t>(1, std::min<int64_t>(wg, (c->rows + 255) / 256));
   int rc;
   c->rs_nblk = (int)nblk;

@@ -591,7 +591,10 @@ class DistributedDSGD:
                 colsum_fold(g)
                 ar = self._all_reduce_start(self.sum)
                 eng.phase_set_round(t0 + h)  # the device sampler's counter (sampling='device')
-                eng.phase_grad(batch, lam_grad, obj_f if g >= 2 else 0,  # loss at xbar_{g-1}
+                # loss at xbar_{g-1} (history[g-2]); at g = 1 it is the loss of x_0, which no history row
+                # holds -- taken anyway so round 1's gradient dots reduce in the same (paired) butterfly
+                # as the fused single-context round 1, whose pass carries the metrics of x_1
+                eng.phase_grad(batch, lam_grad, obj_f if g >= 1 else 0,
                                idx=None if idx is None else idx[h])
                 if ar is not None:
                     ar.wait()

@@ -222,13 +222,16 @@ def test_partitioned_graph_ranks_match_single_context(tmp_path, monkeypatch, wor
 
 @pytest.mark.parametrize("world", [2, 4])
 def test_strong_split_bench_shape_matches_single_context(tmp_path, monkeypatch, world):
-    """bench.py's strong-scaling leg in miniature: a FIXED total of workers (512, d = 1024, the
+    """bench.py's strong-scaling leg in miniature: a FIXED total of workers (1024, d = 1024, the
     headline's float64 arithmetic over float32 rows) split over 2 and 4 ranks by the spectral
     partition, timed as a chain of pipelined calls -- bitwise one context's iterates, history
-    rtol 1e-12."""
+    rtol 1e-12.  Every rank keeps >= 256 workers, so it launches the same
+    round-kernel instance as the single context (the headline's: software-pipelined row loop,
+    paired row-dot butterfly); below 256 workers a context takes the few-worker kernel, whose
+    row dots reduce in another order."""
     import torch.multiprocessing as mp
 
-    n, d, m, t = 512, 1024, 16, 9
+    n, d, m, t = 1024, 1024, 16, 9
     monkeypatch.setenv("DOPT_TEST_PARTITION", "1")
     monkeypatch.setenv("DOPT_TEST_PIPE", "1")
     mp.start_processes(_rank_main, args=(world, _free_port(), "float64/x32", str(tmp_path), False, t, "1", n, d, m),
