@@ -617,6 +617,8 @@ def main():
     args = ap.parse_args()
     if args.timeout is not None:
         os.environ["DOPT_PG_TIMEOUT"] = str(args.timeout)
+    else:  # a bench collective never needs minutes: a stuck peer fails the run well inside the driver's limit
+        os.environ.setdefault("DOPT_PG_TIMEOUT", "180")
 
     # ---- the rank layout, decided before anything touches the GPU
     env_world = os.environ.get("WORLD_SIZE")
