@@ -574,7 +574,7 @@ def test_last_round_kernel_names_the_launched_instance():
     dispatcher picked: float64 fused round kernel, and the column-blocked step for long rows."""
     rng = np.random.default_rng(3)
     for d, want in ((50, "void dopt::k_round<double, double, 1, 1, true, true, "),
-                    (2100, "void dopt::k_split_step<double, 4, true, true, ")):
+                    (2100, "void dopt::k_split_step<double, double, 4, true, true, ")):
         n, m = 4, 8
         X = rng.standard_normal((n * m, d))
         eng = _dopt.Engine(0, "float64")
