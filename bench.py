@@ -56,7 +56,8 @@ def pmc_traffic(kernel_name, config="c3"):
     import glob
     import re
 
-    pat = {"c3": r"r\d+_pmc\.json", "c4": r"r\d+_c4_pmc\.json", "c5": r"r\d+_c5(rs|x32)?_pmc\.json"}[config]
+    pat = {"c3": r"r\d+_pmc\.json", "c4": r"r\d+_c4_pmc\.json",
+           "c5": r"r\d+_c5(rs|x32|x32direct)?_pmc\.json"}[config]
     files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json"))
                    if re.fullmatch(pat, os.path.basename(f)))
     for f in reversed(files):

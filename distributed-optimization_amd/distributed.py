@@ -36,7 +36,11 @@ import _dopt
 
 
 DEFAULT_TIMEOUT_S = 300.0
-RS_CHUNKS = 4  # column chunks of the complete graph's row-space pass across ranks
+# Column chunks of the complete graph's row-space pass across ranks: each chunk's
+# sums are all-reduced while the next chunk streams, but every chunk boundary costs a launch tail --
+# C5 at RCCL world 1 (round 3): 1 chunk 11.30 ms per round, 4 chunks 11.62 ms, i.e. ~0.1 ms per
+# boundary, more than an 8 MB all-reduce over xGMI is expected to expose.  So one chunk by default.
+RS_CHUNKS = 1
 
 
 class CollectiveError(RuntimeError):

@@ -57,12 +57,19 @@ __global__ __launch_bounds__(256) void k_probe(const float* __restrict__ X, int6
   }
   float fs = 0.f;
   double stash = 0.0;
+  // COMP 2 / 3: the same blocks in a column-block-tiled layout (tile blk = every row's block blk,
+  // rows contiguous: X[blk][row][64 * CB * 4 floats]), so a wave streams contiguous memory
+  constexpr bool TILED = COMP >= 2;
+  constexpr int64_t TW = 64 * CB * 4;  // floats per row of a tile
   auto load = [&](int64_t r, f4 (&dst)[CB]) {
 #pragma unroll
-    for (int j = 0; j < CB; ++j) dst[j] = __builtin_nontemporal_load((const f4*)(X + r * ld + cc[j]));
+    for (int j = 0; j < CB; ++j) {
+      const float* p = TILED ? X + ((int64_t)blk * rows + r) * TW + (j * 64 + lane) * 4 : X + r * ld + cc[j];
+      dst[j] = __builtin_nontemporal_load((const f4*)p);
+    }
   };
   auto process = [&](const f4 (&rv)[CB], int64_t r) {
-    if constexpr (COMP == 0) {
+    if constexpr (COMP == 0 || COMP == 2) {
 #pragma unroll
       for (int j = 0; j < CB; ++j) fs += (rv[j][0] + rv[j][1]) + (rv[j][2] + rv[j][3]);
     } else {
@@ -153,6 +160,16 @@ int main() {
   run<1, 8, 1>(X, ld, rows, 2, xbar, out, "x32 arithmetic");
   run<2, 6, 1>(X, ld, rows, 2, xbar, out, "x32 arithmetic (again)");
   run<2, 6, 0>(X, ld, rows, 2, xbar, out, "pattern only (again)");
+  run<2, 6, 2>(X, ld, rows, 2, xbar, out, "tiled, pattern only");
+  run<2, 6, 3>(X, ld, rows, 2, xbar, out, "tiled, x32 arithmetic");
+  run<2, 12, 2>(X, ld, rows, 2, xbar, out, "tiled, pattern only");
+  run<2, 3, 3>(X, ld, rows, 2, xbar, out, "tiled, x32 arithmetic");
+  run<2, 6, 3>(X, ld, rows, 4, xbar, out, "tiled, x32 arithmetic");
+  run<2, 6, 3>(X, ld, rows, 1, xbar, out, "tiled, x32 arithmetic");
+  run<4, 6, 3>(X, ld, rows, 2, xbar, out, "tiled, x32 arithmetic");
+  run<1, 8, 3>(X, ld, rows, 2, xbar, out, "tiled, x32 arithmetic");
+  run<2, 6, 3>(X, ld, rows, 2, xbar, out, "tiled, x32 arithmetic (again)");
+  run<2, 6, 1>(X, ld, rows, 2, xbar, out, "x32 arithmetic (again)");
   CK(hipFree(X));
   return 0;
 }
