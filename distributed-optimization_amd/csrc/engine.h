@@ -27,7 +27,8 @@ constexpr int64_t kMaxBipRows = 65536;  // shard rows the F_BIP byte map holds i
 // One workgroup per worker (or per objective-row chunk).  All pointers are
 // device pointers; T-typed arrays are float or double per the launch.
 struct RoundArgs {
-  const void* X;          // [rows x ld] shard rows, back to back
+  const void* X;          // [rows x ld] shard rows, back to back (column-blocked contexts: tiled, kcommon.h XAddr)
+  int64_t xrows;          // tiled layout of X: rows of the X array (the tile stride); 0 = row-major, stride ld
   const void* y;          // [rows]
   const int64_t* off;     // [n+1] first row of every worker's rows
   const int32_t* idx;     // [n x b] local row ids of this round's minibatch, or null (all rows)
@@ -104,6 +105,7 @@ struct RsArgs {
   const void* X;           // [rows x ld] T shard rows
   const void* y;           // [rows] T labels / targets
   int32_t y_is_f32;
+  int32_t tiled;           // X in the column-block-tiled layout (tile stride: rows)
   int32_t problem;         // 0 logistic, 1 quadratic
   const int64_t* off;      // [n+1] first row of every worker
   int64_t rows;            // all rows (upart stride)
@@ -227,10 +229,18 @@ hipError_t launch_mix(int dtype, int cpl, const RoundArgs& a, const void* G, int
 // dst[k] = x[ids[k]] rows (halo send buffer).
 hipError_t launch_gather_rows(int dtype, const void* x, const int32_t* ids, int64_t n, int64_t ld,
                               int32_t nchunks, void* dst, hipStream_t s);
-// Synthetic shards (rows_per_worker rows per worker), X ~ N(0,1) + bias column.
+// Synthetic shards (rows_per_worker rows per worker), X ~ N(0,1) + bias column; xrows > 0: X in
+// the tiled layout of column-blocked contexts (ld = the padded row length, whole tiles);
+// wstar = d doubles of scratch (the planted w*).
 hipError_t launch_generate(int dtype, int problem, void* X, void* y, int64_t rows, int64_t d,
-                           int64_t ld, uint64_t seed, double flip, double noise, int64_t row_base,
-                           hipStream_t s);
+                           int64_t ld, int64_t xrows, double* wstar, uint64_t seed, double flip, double noise,
+                           int64_t row_base, hipStream_t s);
+// Host rows -> rows [r0, r0 + nr) of a tiled array of xrows rows (row length ld); and back
+// (rows of a tiled array -> row-major [nr x ld]).
+hipError_t launch_convert_tiled(int dtype, const void* src, int src_f32, void* dst, int64_t r0, int64_t nr, int64_t d,
+                                int64_t ld, int64_t xrows, hipStream_t s);
+hipError_t launch_untile(int dtype, const void* X, int64_t xrows, int64_t r0, int64_t nr, int64_t ld, void* dst,
+                         hipStream_t s);
 // Single float64 evaluation for rows too long for the row-resident kernel (obj_problems.py
 // API): part[rows x G] partial dots, rowbuf[rows] coefficients (grad) or loss terms
 // (objective), g_out[d] the gradient (grad).  Fixed reduction orders.

@@ -26,6 +26,8 @@
 //
 // No atomics anywhere: every reduction has a fixed order, so runs are bitwise
 // reproducible.
+#include <algorithm>
+
 #include "kcommon.h"
 
 namespace dopt {
@@ -127,6 +129,7 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
   const int64_t row0 = a.off[i], m = a.off[i + 1] - row0;
   const int64_t nb = a.idx ? (a.b < m ? a.b : m) : m;  // <= NW * RPW (host-checked)
   const XT* __restrict__ X = (const XT*)a.X;
+  const XAddr<VN> xa(a.xrows, ld);  // row-major or column-block tiled rows
   const bool shared = (a.flags & F_SHARED) != 0;  // centralized: every worker at w_shared
   const bool gout = (a.flags & F_GOUT) != 0;
   const T* own_p = shared ? (const T*)a.w_shared : (const T*)a.x_old + (int64_t)i * ld;
@@ -138,7 +141,7 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
     const int k = wave + NW * r;
     const bool ok = k < nb;
     const int64_t lr = ok ? (a.idx ? (int64_t)a.idx[(int64_t)i * a.b + k] : (int64_t)k) : 0;
-    rowp[r] = ok ? (row0 + lr) * ld : -1;
+    rowp[r] = ok ? (row0 + lr) * xa.rs : -1;
     coef[r] = ok ? ((const T*)a.coef)[(int64_t)i * a.bcap + k] : T(0);
     zacc[r] = 0.0;
     uacc[r] = 0.0;
@@ -188,7 +191,7 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
         const int c0 = cbc * BC + j * 64 + lane;
         const int c = c0 < nch ? c0 : nch - 1;
 #pragma unroll
-        for (int r = 0; r < RPW; ++r) S.rw[r][j] = ld_nt<XT>(X + (rowp[r] >= 0 ? rowp[r] : row0 * ld) + (int64_t)c * VN);
+        for (int r = 0; r < RPW; ++r) S.rw[r][j] = ld_nt<XT>(X + (rowp[r] >= 0 ? rowp[r] : row0 * xa.rs) + xa.col(c));
       }
       return;
     }
@@ -205,7 +208,7 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
       const int c = cbn * BC + j * 64 + lane;
       const bool in = blk && c < nch;
 #pragma unroll
-      for (int r = 0; r < RPW; ++r) S.rw[r][j] = (in && rowp[r] >= 0) ? ld_nt<XT>(X + rowp[r] + (int64_t)c * VN) : VX(0);
+      for (int r = 0; r < RPW; ++r) S.rw[r][j] = (in && rowp[r] >= 0) ? ld_nt<XT>(X + rowp[r] + xa.col(c)) : VX(0);
     }
   };
   auto process = [&](Set& S, int cb, int buf) {
@@ -625,6 +628,7 @@ __global__ __launch_bounds__(NT) void k_split_dots(const RoundArgs a) {
   const int64_t row0 = a.off[i], m = a.off[i + 1] - row0;
   const int64_t nb = (MODE == 0 && a.idx) ? (a.b < m ? a.b : m) : m;
   const S* __restrict__ X = (const S*)a.X;
+  const XAddr<VN> xa(a.xrows, ld);  // row-major or column-block tiled rows
   const T* own_p = (a.flags & F_SHARED) ? (const T*)a.w_shared : (const T*)a.x_old + (int64_t)i * ld;
   const T* pt = MODE == 0 ? own_p : (const T*)a.xbar;
   double* out = MODE == 0 ? a.zpart : a.upart;
@@ -649,16 +653,17 @@ __global__ __launch_bounds__(NT) void k_split_dots(const RoundArgs a) {
       const int64_t k = rc + wave + NW * r;
       const bool ok = k < nb;
       const int64_t lr = ok ? ((MODE == 0 && a.idx) ? (int64_t)a.idx[(int64_t)i * a.b + k] : k) : 0;
-      rowp[r] = ok ? (row0 + lr) * ld : -1;
+      rowp[r] = ok ? (row0 + lr) * xa.rs : -1;
       acc[r] = 0.0;
     }
     for (int cb = bw.b0; cb < bw.b1; cb += bw.st) {
       const int c = cb * 64 + lane;
       if (c >= nch) continue;
       const V pv = *(const V*)(pt + (int64_t)c * VN);
+      const int64_t co = xa.col(c);
 #pragma unroll
       for (int r = 0; r < RPW; ++r)
-        if (rowp[r] >= 0) acc[r] += (double)hsumn<T, VN>(widen<V>(ld_nt<S>(X + rowp[r] + (int64_t)c * VN)) * pv);
+        if (rowp[r] >= 0) acc[r] += (double)hsumn<T, VN>(widen<V>(ld_nt<S>(X + rowp[r] + co)) * pv);
     }
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
@@ -776,7 +781,7 @@ hipError_t launch_split_step(int dtype, int xdtype, bool znext, bool met, const 
   // DOPT_SPLIT_GLDS = D (2 or 3): the LDS-DMA kernel with D blocks in flight per wave, where the
   // prefetching kernel would run with <= 16 rows (same element types only)
   const int glds = env_int("DOPT_SPLIT_GLDS", 0);
-  if (pf && small && (glds == 2 || glds == 3) && dtype == xdtype) {
+  if (pf && small && (glds == 2 || glds == 3) && dtype == xdtype && a.xrows == 0) {  // row-major rows only
 #define GLDS2(T_, D_)                                                                                 \
   if (znext && met) hipLaunchKernelGGL((k_split_glds<T_, true, true, D_>), grid, dim3(NT), 0, s, a2); \
   else if (znext) hipLaunchKernelGGL((k_split_glds<T_, true, false, D_>), grid, dim3(NT), 0, s, a2);  \
@@ -793,7 +798,7 @@ hipError_t launch_split_step(int dtype, int xdtype, bool znext, bool met, const 
     return hipGetLastError();
   }
   // DOPT_SPLIT_COLWAVE=1: the column-per-wave kernel for <= 16 rows (same element types only)
-  if (small && env_int("DOPT_SPLIT_COLWAVE", 0) == 1 && dtype == xdtype) {
+  if (small && env_int("DOPT_SPLIT_COLWAVE", 0) == 1 && dtype == xdtype && a.xrows == 0) {
 #define COLWAVE(T_)                                                                                       \
   if (znext && met) hipLaunchKernelGGL((k_split_colwave<T_, true, true>), grid, dim3(NT), 0, s, a2);       \
   else if (znext) hipLaunchKernelGGL((k_split_colwave<T_, true, false>), grid, dim3(NT), 0, s, a2);        \
@@ -1509,10 +1514,19 @@ __device__ __forceinline__ double normal_at(uint64_t seed, uint64_t a, uint64_t 
   return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
 }
 
+// The planted w* of the synthetic labels, once per data set (k_generate reads it per element).
+__global__ __launch_bounds__(NT) void k_wstar(double* w, int64_t d, uint64_t seed) {
+  for (int64_t c = (int64_t)blockIdx.x * NT + threadIdx.x; c < d; c += (int64_t)gridDim.x * NT)
+    w[c] = normal_at(seed ^ 0x5DEECE66Dull, 0, (uint64_t)c);
+}
+
+// xrows > 0: X in the column-block tiled layout of column-blocked contexts (kcommon.h XAddr;
+// ld = the padded row length, whole tiles), else row-major with stride ld.
 template <typename T>
-__global__ __launch_bounds__(NT) void k_generate(T* X, T* y, int64_t rows, int64_t d, int64_t ld,
-                                                 uint64_t seed, double flip, double noise,
-                                                 int problem, int64_t row_base) {
+__global__ __launch_bounds__(NT) void k_generate(T* X, T* y, int64_t rows, int64_t d, int64_t ld, int64_t xrows,
+                                                 const double* __restrict__ wstar, uint64_t seed, double flip,
+                                                 double noise, int problem, int64_t row_base) {
+  constexpr int64_t TE = kTileChunks * (16 / sizeof(T));  // elements of a row in one tile
   const int lane = threadIdx.x & 63;
   const int64_t rl = (int64_t)blockIdx.x * NW + (threadIdx.x >> 6);
   if (rl >= rows) return;
@@ -1525,9 +1539,9 @@ __global__ __launch_bounds__(NT) void k_generate(T* X, T* y, int64_t rows, int64
       v = normal_at(seed, (uint64_t)r + 1, (uint64_t)c);
     else if (c == d - 1)
       v = 1.0;  // bias column, utils.py:28
-    X[rl * ld + c] = (T)v;
+    X[xrows ? ((c / TE) * xrows + rl) * TE + c % TE : rl * ld + c] = (T)v;
     // labels from the float64 values, so float32 and float64 engines get the same labels
-    if (c < d) dot += v * normal_at(seed ^ 0x5DEECE66Dull, 0, (uint64_t)c);  // planted w*
+    if (c < d) dot += v * wstar[c];  // planted w*
   }
   dot = wave_sum(dot);
   if (lane == 0) {
@@ -1542,15 +1556,17 @@ __global__ __launch_bounds__(NT) void k_generate(T* X, T* y, int64_t rows, int64
 }
 
 hipError_t launch_generate(int dtype, int problem, void* X, void* y, int64_t rows, int64_t d,
-                           int64_t ld, uint64_t seed, double flip, double noise, int64_t row_base,
-                           hipStream_t s) {
+                           int64_t ld, int64_t xrows, double* wstar, uint64_t seed, double flip, double noise,
+                           int64_t row_base, hipStream_t s) {
+  hipLaunchKernelGGL(k_wstar, dim3((unsigned)std::min<int64_t>(1024, (d + NT - 1) / NT)), dim3(NT), 0, s, wstar, d,
+                     seed);
   const dim3 grid((unsigned)((rows + NW - 1) / NW));
   if (dtype == 0)
-    hipLaunchKernelGGL(k_generate<float>, grid, dim3(NT), 0, s, (float*)X, (float*)y, rows, d, ld,
-                       seed, flip, noise, problem, row_base);
+    hipLaunchKernelGGL(k_generate<float>, grid, dim3(NT), 0, s, (float*)X, (float*)y, rows, d, ld, xrows,
+                       (const double*)wstar, seed, flip, noise, problem, row_base);
   else
-    hipLaunchKernelGGL(k_generate<double>, grid, dim3(NT), 0, s, (double*)X, (double*)y, rows, d, ld,
-                       seed, flip, noise, problem, row_base);
+    hipLaunchKernelGGL(k_generate<double>, grid, dim3(NT), 0, s, (double*)X, (double*)y, rows, d, ld, xrows,
+                       (const double*)wstar, seed, flip, noise, problem, row_base);
   return hipGetLastError();
 }
 
@@ -1571,6 +1587,57 @@ __global__ __launch_bounds__(NT) void k_convert(const S* __restrict__ src, T* __
     const int64_t r = k / ld, c = k - r * ld;
     dst[k] = c < d ? (T)src[r * d + c] : T(0);
   }
+}
+
+// Host rows [nr x d] -> rows r0 .. r0 + nr of a column-block tiled array of xrows rows (row length
+// ld, whole tiles), zero padded.
+template <typename T, typename S>
+__global__ __launch_bounds__(NT) void k_convert_tiled(const S* __restrict__ src, T* __restrict__ dst, int64_t r0,
+                                                      int64_t nr, int64_t d, int64_t ld, int64_t xrows) {
+  constexpr int64_t TE = kTileChunks * (16 / sizeof(T));
+  const int64_t total = nr * ld;
+  for (int64_t k = (int64_t)blockIdx.x * NT + threadIdx.x; k < total; k += (int64_t)gridDim.x * NT) {
+    const int64_t r = k / ld, c = k - r * ld;
+    dst[((c / TE) * xrows + r0 + r) * TE + c % TE] = c < d ? (T)src[r * d + c] : T(0);
+  }
+}
+
+// Rows r0 .. r0 + nr of a tiled array -> row-major dst [nr x ld] (downloads, parity checks).
+template <typename T>
+__global__ __launch_bounds__(NT) void k_untile(const T* __restrict__ X, int64_t xrows, int64_t r0, int64_t nr,
+                                               int64_t ld, T* __restrict__ dst) {
+  constexpr int64_t TE = kTileChunks * (16 / sizeof(T));
+  const int64_t total = nr * ld;
+  for (int64_t k = (int64_t)blockIdx.x * NT + threadIdx.x; k < total; k += (int64_t)gridDim.x * NT) {
+    const int64_t r = k / ld, c = k - r * ld;
+    dst[k] = X[((c / TE) * xrows + r0 + r) * TE + c % TE];
+  }
+}
+
+static dim3 grid_for(int64_t total) {
+  int64_t blocks = (total + NT - 1) / NT;
+  return dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(blocks, 8192)));
+}
+
+hipError_t launch_convert_tiled(int dtype, const void* src, int src_f32, void* dst, int64_t r0, int64_t nr, int64_t d,
+                                int64_t ld, int64_t xrows, hipStream_t s) {
+  const dim3 grid = grid_for(nr * ld);
+  if (dtype == 0) {
+    if (src_f32) hipLaunchKernelGGL((k_convert_tiled<float, float>), grid, dim3(NT), 0, s, (const float*)src, (float*)dst, r0, nr, d, ld, xrows);
+    else hipLaunchKernelGGL((k_convert_tiled<float, double>), grid, dim3(NT), 0, s, (const double*)src, (float*)dst, r0, nr, d, ld, xrows);
+  } else {
+    if (src_f32) hipLaunchKernelGGL((k_convert_tiled<double, float>), grid, dim3(NT), 0, s, (const float*)src, (double*)dst, r0, nr, d, ld, xrows);
+    else hipLaunchKernelGGL((k_convert_tiled<double, double>), grid, dim3(NT), 0, s, (const double*)src, (double*)dst, r0, nr, d, ld, xrows);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_untile(int dtype, const void* X, int64_t xrows, int64_t r0, int64_t nr, int64_t ld, void* dst,
+                         hipStream_t s) {
+  const dim3 grid = grid_for(nr * ld);
+  if (dtype == 0) hipLaunchKernelGGL(k_untile<float>, grid, dim3(NT), 0, s, (const float*)X, xrows, r0, nr, ld, (float*)dst);
+  else hipLaunchKernelGGL(k_untile<double>, grid, dim3(NT), 0, s, (const double*)X, xrows, r0, nr, ld, (double*)dst);
+  return hipGetLastError();
 }
 
 hipError_t launch_convert(int dtype, const void* src, int src_f32, void* dst, int64_t rows, int64_t d,

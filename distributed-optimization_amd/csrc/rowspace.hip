@@ -59,10 +59,12 @@ __device__ __forceinline__ void rs_pass_body(const RsArgs& a, double* red) {
   const int nch = a.nch;
   const int64_t ld = a.ld;
   const XT* __restrict__ X = (const XT*)a.X;
+  const XAddr<VN> xa(a.tiled ? a.rows : 0, ld);  // column-block tiled rows: each block streams contiguously
   const int64_t r0 = a.grow[g], r1 = a.grow[g + 1];
   const int64_t per = (r1 - r0 + NW - 1) / NW;
   const int64_t wr0 = min(r1, r0 + wave * per), wr1 = min(r1, wr0 + per);
   int cc[CB];
+  int64_t co[CB];                   // element offset of chunk cc[j] in row 0
   V xb[SAME ? CB : 1];              // xbar chunks in the row type (XT = T)
   T xbs[SAME ? 1 : CB][SAME ? 1 : VN];  // xbar elements in T (float32 rows, float64 arithmetic)
 #pragma unroll
@@ -70,6 +72,7 @@ __device__ __forceinline__ void rs_pass_body(const RsArgs& a, double* red) {
     const int c = blk * 64 * CB + j * 64 + lane;
     const bool in = c < nch;
     cc[j] = in ? c : nch - 1;  // lanes past the row re-read its last chunk (xbar is 0 there)
+    co[j] = xa.col(cc[j]);
     if constexpr (SAME) {
       xb[j] = in ? *(const V*)((const T*)a.xbar + (int64_t)c * VN) : V(0);
     } else {
@@ -111,9 +114,9 @@ __device__ __forceinline__ void rs_pass_body(const RsArgs& a, double* red) {
   auto cwin_load = [&](int64_t base) { return (COLS && base + lane < wr1) ? cw[base + lane] : 0.0; };
   double cw_cur = cwin_load(wr0), cw_nxt = cwin_load(wr0 + 64);
   auto load = [&](int64_t row, V (&dst)[CB]) {
-    const XT* p = X + row * ld;
+    const XT* p = X + row * xa.rs;
 #pragma unroll
-    for (int j = 0; j < CB; ++j) dst[j] = rs_ld_nt<XT>(p + (int64_t)cc[j] * VN);
+    for (int j = 0; j < CB; ++j) dst[j] = rs_ld_nt<XT>(p + co[j]);
   };
   auto process = [&](const V (&rv)[CB], int64_t r) {
     double p = 0.0;
@@ -458,7 +461,9 @@ __global__ __launch_bounds__(NT) void k_rs_gram(const RsArgs a, double* gpart, i
     __syncthreads();
     for (int q = threadIdx.x; q < m * TC; q += NT) {
       const int k = q / TC, c = q % TC;
-      tile[q] = c < w ? ((const T*)a.X)[(row0 + k) * a.ld + c0 + c] : T(0);
+      // a 1 KiB row tile IS one tile of the tiled layout: (t * rows + row) * TC
+      tile[q] = c < w ? ((const T*)a.X)[a.tiled ? (t * a.rows + row0 + k) * TC + c : (row0 + k) * a.ld + c0 + c]
+                      : T(0);
     }
     __syncthreads();
 #pragma unroll
@@ -507,6 +512,7 @@ __device__ __forceinline__ void rs_materialise_body(const RsArgs& a, T* xout) {
   const int i = blockIdx.x, g = blockIdx.y, G = gridDim.y;
   const int64_t row0 = a.off[i];
   const int m = (int)(a.off[i + 1] - row0);
+  const XAddr<VN> xa(a.tiled ? a.rows : 0, a.ld);
   if (threadIdx.x < 64) sb[threadIdx.x] = threadIdx.x < m ? a.beta[(int64_t)i * a.bcap + threadIdx.x] : 0.0;
   __syncthreads();
   for (int c = g * NT + threadIdx.x; c < a.nch; c += G * NT) {
@@ -514,7 +520,7 @@ __device__ __forceinline__ void rs_materialise_body(const RsArgs& a, T* xout) {
 #pragma unroll
     for (int e = 0; e < VN; ++e) s[e] = a.rZ[(int64_t)c * VN + e];
     for (int k = 0; k < m; ++k) {
-      const V r = rs_ld_nt<XT>((const XT*)a.X + (row0 + k) * a.ld + (int64_t)c * VN);
+      const V r = rs_ld_nt<XT>((const XT*)a.X + xa.at(row0 + k, c));
 #pragma unroll
       for (int e = 0; e < VN; ++e) s[e] += sb[k] * (double)r[e];
     }

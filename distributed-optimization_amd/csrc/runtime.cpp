@@ -58,6 +58,8 @@ int fail(int code, const char* fmt, ...) {
     if (e_ != hipSuccess) return fail(DOPT_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
 
+constexpr int64_t kTileRowChunks = 64;  // 16-byte data chunks of a row per tile (kcommon.h kTileChunks)
+
 // Launch-shape tuning knobs: read from the environment only in A/B builds (make AB=1); the
 // shipped library uses the measured defaults whatever the environment holds.
 int64_t ab_knob(const char* name, int64_t dflt) {
@@ -102,6 +104,11 @@ struct dopt_ctx {
   int cpls = 1;      // ... and per lane (k_mix)
   bool split = false;  // d too long for the row-resident kernel: column-blocked rounds
   int split_groups = 1;
+  // column-blocked contexts store X (and Xo) column-block TILED (kcommon.h XAddr): tile t = data
+  // chunks [64 t, 64 t + 64) of every row, rows contiguous; ldx = the row length in elements padded
+  // to whole tiles (row-major contexts: ldx = ld)
+  bool tiled = false;
+  int64_t ldx = 0;
   // dopt_run_dsgd_pipelined: the metrics of the current iterate (at xbar[xb]) are still owed
   // by the last pipelined run and ride the next pipelined run's first pass
   bool carry_pending = false;
@@ -268,9 +275,10 @@ int set_device(dopt_ctx* c) {
 }
 
 // Upload rows x d host values (float64 or float32) into a T-typed [rows x ld]
-// device array through the staging buffer and the convert kernel.
+// device array through the staging buffer and the convert kernel.  tile_rows > 0: dst is a
+// column-block tiled array of that many rows (row length ld, whole tiles).
 int upload_rows(dopt_ctx* c, int dtype, const void* src, int src_f32, void* dst, int64_t rows,
-                int64_t d, int64_t ld) {
+                int64_t d, int64_t ld, int64_t tile_rows = 0) {
   if (rows == 0) return DOPT_OK;
   const size_t src_esz = src_f32 ? 4 : 8;
   const size_t dst_esz = dtype == DOPT_F32 ? 4 : 8;
@@ -285,8 +293,11 @@ int upload_rows(dopt_ctx* c, int dtype, const void* src, int src_f32, void* dst,
     const int64_t nr = std::min(chunk, rows - r0);
     HIPOK(hipMemcpyAsync(c->staging, (const char*)src + r0 * row_bytes, (size_t)(nr * row_bytes),
                          hipMemcpyHostToDevice, c->stream));
-    HIPOK(launch_convert(dtype, c->staging, src_f32, (char*)dst + r0 * ld * (int64_t)dst_esz, nr, d, ld,
-                         c->stream));
+    if (tile_rows > 0)
+      HIPOK(launch_convert_tiled(dtype, c->staging, src_f32, dst, r0, nr, d, ld, tile_rows, c->stream));
+    else
+      HIPOK(launch_convert(dtype, c->staging, src_f32, (char*)dst + r0 * ld * (int64_t)dst_esz, nr, d, ld,
+                           c->stream));
   }
   HIPOK(hipStreamSynchronize(c->stream));
   return DOPT_OK;
@@ -384,6 +395,8 @@ int set_layout(dopt_ctx* c, int problem, int64_t n, int64_t d) {
   c->d = d;
   c->ld = ld;
   c->nch = nch;
+  c->tiled = c->split;
+  c->ldx = c->tiled ? (nch + kTileRowChunks - 1) / kTileRowChunks * kTileRowChunks * c->vn : ld;
   c->cpl = cpl;
   c->nchs = ld * (int64_t)c->esz / 16;
   c->cpls = cpl_for(c->nchs);
@@ -426,6 +439,7 @@ RoundArgs base_args(dopt_ctx* c) {
   a.y = c->y;
   a.off = c->off;
   a.ld = c->ld;
+  a.xrows = c->tiled ? c->rows : 0;
   a.nchunks = (int32_t)c->nch;
   a.slab_cons = c->slab_cons;
   a.slab_loss = c->slab_loss;
@@ -603,6 +617,7 @@ int split_metrics(dopt_ctx* c, const void* x_state, const void* point, bool shar
   RoundArgs a = base_args(c);
   if (c->obj_sep) {
     a.X = c->Xo;
+    a.xrows = c->tiled ? c->rows_o : 0;
     a.y = c->yo;
     a.off = c->offo;
   }
@@ -766,6 +781,7 @@ RsArgs rs_args(dopt_ctx* c) {
   a.X = c->X;
   a.y = c->y;
   a.y_is_f32 = c->xdtype == DOPT_F32;
+  a.tiled = c->tiled ? 1 : 0;
   a.problem = c->problem == DOPT_LOGISTIC ? 0 : 1;
   a.off = c->off;
   a.rows = c->rows;
@@ -1145,11 +1161,11 @@ int dopt_load_shards(dopt_ctx* c, int problem, int64_t n_workers, int64_t d, con
   c->max_m = max_m;
   c->min_m = min_m;
   c->off_h.assign(off, off + n_workers + 1);
-  if ((rc = dalloc(&c->X, (size_t)rows * c->ld * c->xesz))) return rc;
+  if ((rc = dalloc(&c->X, (size_t)rows * c->ldx * c->xesz))) return rc;
   if ((rc = dalloc(&c->y, (size_t)rows * c->xesz))) return rc;
   if ((rc = dalloc_t(&c->off, (size_t)(n_workers + 1) * sizeof(int64_t)))) return rc;
   HIPOK(hipMemcpy(c->off, off, (size_t)(n_workers + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
-  if ((rc = upload_rows(c, c->xdtype, X, src_f32, c->X, rows, d, c->ld))) return rc;
+  if ((rc = upload_rows(c, c->xdtype, X, src_f32, c->X, rows, d, c->ldx, c->tiled ? rows : 0))) return rc;
   if ((rc = upload_rows(c, c->xdtype, y, src_f32, c->y, rows, 1, 1))) return rc;
   if ((rc = alloc_state(c))) return rc;
   c->have_data = true;
@@ -1170,15 +1186,19 @@ int dopt_generate_shards(dopt_ctx* c, int problem, int64_t n_workers, int64_t d,
   c->min_m = rpw;
   c->off_h.resize((size_t)n_workers + 1);
   for (int64_t i = 0; i <= n_workers; ++i) c->off_h[(size_t)i] = i * rpw;
-  if ((rc = dalloc(&c->X, (size_t)rows * c->ld * c->xesz))) return rc;
+  if ((rc = dalloc(&c->X, (size_t)rows * c->ldx * c->xesz))) return rc;
   if ((rc = dalloc(&c->y, (size_t)rows * c->xesz))) return rc;
   if ((rc = dalloc_t(&c->off, (size_t)(n_workers + 1) * sizeof(int64_t)))) return rc;
   HIPOK(hipMemcpy(c->off, c->off_h.data(), (size_t)(n_workers + 1) * sizeof(int64_t),
                   hipMemcpyHostToDevice));
   CHECK_ARG(first_worker >= 0, "first_worker must be >= 0");
-  HIPOK(launch_generate(c->xdtype, problem, c->X, c->y, rows, d, c->ld, seed, flip, noise, first_worker * rpw,
-                        c->stream));
-  HIPOK(hipStreamSynchronize(c->stream));
+  double* wstar = nullptr;
+  if ((rc = dalloc_t(&wstar, (size_t)d * sizeof(double)))) return rc;
+  hipError_t e = launch_generate(c->xdtype, problem, c->X, c->y, rows, d, c->ldx, c->tiled ? rows : 0, wstar, seed,
+                                 flip, noise, first_worker * rpw, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  dfree_t(wstar);
+  if (e != hipSuccess) return fail(DOPT_ERR_HIP, "dopt_generate_shards: %s", hipGetErrorString(e));
   if ((rc = alloc_state(c))) return rc;
   c->have_data = true;
   return DOPT_OK;
@@ -1191,9 +1211,9 @@ int dopt_load_objective_data(dopt_ctx* c, int64_t n_rows, const void* X, const v
   CHECK_ARG(n_rows == 0 || (X && y), "X / y are NULL");
   int rc;
   if ((rc = set_device(c))) return rc;
-  if ((rc = dalloc(&c->Xo, (size_t)n_rows * c->ld * c->xesz))) return rc;
+  if ((rc = dalloc(&c->Xo, (size_t)n_rows * c->ldx * c->xesz))) return rc;
   if ((rc = dalloc(&c->yo, (size_t)n_rows * c->xesz))) return rc;
-  if ((rc = upload_rows(c, c->xdtype, X, src_f32, c->Xo, n_rows, c->d, c->ld))) return rc;
+  if ((rc = upload_rows(c, c->xdtype, X, src_f32, c->Xo, n_rows, c->d, c->ldx, c->tiled ? n_rows : 0))) return rc;
   if ((rc = upload_rows(c, c->xdtype, y, src_f32, c->yo, n_rows, 1, 1))) return rc;
   // split the objective rows over the N metric workgroups (array_split sizes)
   std::vector<int64_t> o((size_t)c->n + 1);
@@ -1223,8 +1243,18 @@ int dopt_get_shard(dopt_ctx* c, int64_t worker, double* X_out, double* y_out) {
   int rc;
   if ((rc = set_device(c))) return rc;
   const int64_t r0 = c->off_h[(size_t)worker], nr = c->off_h[(size_t)worker + 1] - r0;
-  if (X_out && (rc = download_rows(c, c->xdtype, (const char*)c->X + r0 * c->ld * (int64_t)c->xesz, X_out, nr, c->d, c->ld)))
+  if (X_out && c->tiled && nr > 0) {  // the worker's rows out of the tiles, row-major, then down
+    void* tmp = nullptr;
+    if ((rc = dalloc_t(&tmp, (size_t)(nr * c->ldx) * c->xesz))) return rc;
+    hipError_t e = launch_untile(c->xdtype == DOPT_F32 ? 0 : 1, c->X, c->rows, r0, nr, c->ldx, tmp, c->stream);
+    rc = e == hipSuccess ? download_rows(c, c->xdtype, tmp, X_out, nr, c->d, c->ldx)
+                         : fail(DOPT_ERR_HIP, "dopt_get_shard: %s", hipGetErrorString(e));
+    dfree_t(tmp);
+    if (rc) return rc;
+  } else if (X_out && (rc = download_rows(c, c->xdtype, (const char*)c->X + r0 * c->ld * (int64_t)c->xesz, X_out, nr,
+                                          c->d, c->ld))) {
     return rc;
+  }
   if (y_out && (rc = download_rows(c, c->xdtype, (const char*)c->y + r0 * (int64_t)c->xesz, y_out, nr, 1, 1))) return rc;
   return DOPT_OK;
 }

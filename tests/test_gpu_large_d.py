@@ -205,3 +205,65 @@ def test_split_pipelined_runs_equal_one_run(mean, rowspace, monkeypatch):
     assert np.array_equal(np.concatenate(conss), cons_ref)
     assert np.array_equal(eng.get_models(), x_ref)
     eng.close()
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float64/x32", "float32"])
+def test_tiled_rows_round_trip(dtype):
+    """Column-blocked contexts store the shards column-block tiled (kcommon.h XAddr): uploads
+    (ragged shards, a partial last tile) come back unchanged through dopt_get_shard, and generated
+    shards hold exactly the values of the same rows generated into a row-major (row-resident)
+    float32 context -- the generator is a function of (global row, column) only."""
+    rng = np.random.default_rng(11)
+    d = 2100 if dtype != "float32" else 5000
+    sizes = [3, 1, 7, 0, 5]
+    shards = [(rng.standard_normal((m, d)), rng.standard_normal(m)) for m in sizes]
+    if dtype == "float64/x32":
+        shards = _f32_exact(shards)
+    eng = _engine(shards, "quadratic", dtype)
+    for (X, y), i in zip(shards, range(len(sizes))):
+        Xg, yg = eng.get_shard(i)
+        np.testing.assert_array_equal(Xg, X.astype(np.float32) if dtype == "float32" else X)
+        np.testing.assert_array_equal(yg, y.astype(np.float32) if dtype == "float32" else y)
+    eng.close()
+    # generated: the x32 context (tiled, d = 2100 past the mixed row-resident kernel) vs the float32
+    # engine (row-resident at d = 2100, row-major): the same float32 values
+    if dtype == "float64/x32":
+        a = _dopt.Engine(0, "float64", data_dtype="float32")
+        b = _dopt.Engine(0, "float32")
+        for e in (a, b):
+            e.generate_shards("logistic", 6, 2100, 5, seed=17, flip=0.1, first_worker=3)
+        for i in range(6):
+            for u, v in zip(a.get_shard(i), b.get_shard(i)):
+                np.testing.assert_array_equal(u, v)
+        a.close()
+        b.close()
+
+
+@pytest.mark.parametrize("dtype", ["float64", "float64/x32"])
+def test_split_rounds_separate_objective_data_vs_oracle(dtype, monkeypatch):
+    """A separate X_full (trainer.py:154, 188-189) on a column-blocked context: the objective rows
+    are uploaded tiled too (their own tile stride) and read by the dots-only pass; every round's
+    objective and consensus vs the oracle (rtol 1e-9)."""
+    monkeypatch.setenv("DOPT_ROWSPACE", "1")
+    n, d, m, T = 7, 2100, 6, 5
+    shards = _data(n, d, m, 21, "logistic")
+    rng = np.random.default_rng(22)
+    Xo = np.hstack([rng.standard_normal((37, d - 1)), np.ones((37, 1))])
+    yo = rng.choice([-1.0, 1.0], 37)
+    if dtype == "float64/x32":
+        shards = _f32_exact(shards)
+        Xo, yo = _f32_exact([(Xo, yo)])[0]
+    cfg = {"problem_type": "logistic", "local_batch_size": m, "learning_rate_eta0": 0.05,
+           "l2_regularization_lambda": 1e-3, "strong_convexity_mu": 1e-3}
+    top = TP.build("ring", n)
+    eng = _engine(shards, "logistic", dtype)
+    eng.set_topology(top.row_ptr, top.col, top.w)
+    eng.load_objective_data(Xo, yo)
+    obj, cons, _ = eng.run_dsgd(T, 0.05, m, 1e-3, 1e-3, 0.05)
+    x = eng.get_models()
+    h, _, xr, _ = O.run_decentralized(shards, top.dense_W(), T, cfg, Xo, yo, 0.05,
+                                      indices=[[np.arange(m)] * n] * T)
+    np.testing.assert_allclose(obj, h["objective"], rtol=1e-9)
+    np.testing.assert_allclose(cons, h["consensus_error"], rtol=1e-9)
+    np.testing.assert_allclose(x, xr, rtol=1e-9, atol=1e-13)
+    eng.close()
