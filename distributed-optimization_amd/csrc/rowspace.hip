@@ -156,7 +156,75 @@ __device__ __forceinline__ void rs_pass_body(const RsArgs& a, double* red) {
       if (lane <= k) up[r - k + lane] = (T)stash;
     }
   };
-  if (wr0 < wr1) {
+  if constexpr (64 % NBUF == 0) {
+    // Windows of 64 rows (NBUF divides 64): a window's weights come in one vector load, its partial
+    // dots leave in one store, and no branch sits inside the unrolled row groups of a full window
+    // (the buffers rotate in step with the windows).  Partial windows (the wave's last) take the
+    // same groups with every row predicated.
+    if (wr0 < wr1) {
+      const int64_t last = wr1 - 1;
+      V buf[NBUF][CB];
+#pragma unroll
+      for (int k = 0; k < NBUF; ++k) load(min(wr0 + k, last), buf[k]);
+      for (int64_t w0 = wr0; w0 < wr1; w0 += 64) {
+        const double cwv = cw_cur;
+        cw_cur = cw_nxt;
+        cw_nxt = cwin_load(w0 + 128);
+        const int nw = (int)min((int64_t)64, wr1 - w0);
+        double st = 0.0;
+        auto row = [&](const V (&rv)[CB], int kk) {
+          double p = 0.0;
+#pragma unroll
+          for (int j = 0; j < CB; ++j) {
+            if constexpr (SAME) {
+              p += (double)hsum<T>(rv[j] * xb[j]);
+            } else {
+#pragma unroll
+              for (int e = 0; e < VN; ++e) p += (double)rv[j][e] * xbs[j][e];
+            }
+          }
+          const double dot = wave_sum_dpp(p);
+          if constexpr (COLS) {
+            const double cf = readlane_t(cwv, kk);  // wave-uniform
+            if constexpr (TACC) {
+              const T cft = (T)cf;
+#pragma unroll
+              for (int j = 0; j < CB; ++j)
+#pragma unroll
+                for (int e = 0; e < VN; ++e) acct[j][e] += cft * rv[j][e];
+            } else {
+#pragma unroll
+              for (int j = 0; j < CB; ++j)
+#pragma unroll
+                for (int e = 0; e < VN; ++e) acc[j][e] += cf * (double)rv[j][e];
+            }
+          }
+          st = lane == kk ? dot : st;
+        };
+        if (nw == 64) {
+          for (int g0 = 0; g0 < 64; g0 += NBUF) {
+#pragma unroll
+            for (int k = 0; k < NBUF; ++k) {
+              row(buf[k], g0 + k);
+              load(min(w0 + g0 + k + NBUF, last), buf[k]);
+            }
+          }
+        } else {
+          for (int g0 = 0; g0 < nw; g0 += NBUF) {
+#pragma unroll
+            for (int k = 0; k < NBUF; ++k) {
+              if (g0 + k < nw) {
+                row(buf[k], g0 + k);
+                load(min(w0 + g0 + k + NBUF, last), buf[k]);
+              }
+            }
+          }
+        }
+        flush();
+        if (lane < nw) up[w0 + lane] = (T)st;
+      }
+    }
+  } else if (wr0 < wr1) {
     const int64_t last = wr1 - 1;
     V buf[NBUF][CB];
 #pragma unroll
@@ -565,12 +633,17 @@ static hipError_t rs_pass_shape(const RsArgs& a, dim3 grid, hipStream_t s) {
     else hipLaunchKernelGGL((k_rs_pass<T, COLS, C_, B_>), grid, dim3(NT), 0, s, a);          \
     return hipGetLastError();                                                                  \
   }
+  RS_SHAPE(2, 6)  // the default; the others: A/B builds (DOPT_RS_CB / DOPT_RS_NBUF)
+#ifdef DOPT_AB
   RS_SHAPE(4, 2)
   RS_SHAPE(4, 3)
   RS_SHAPE(2, 3)
   RS_SHAPE(2, 4)
-  RS_SHAPE(2, 6)
   RS_SHAPE(1, 8)
+  RS_SHAPE(1, 12)
+  RS_SHAPE(2, 8)
+  RS_SHAPE(1, 16)
+#endif
 #undef RS_SHAPE
   return hipErrorInvalidValue;
 }

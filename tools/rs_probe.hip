@@ -59,17 +59,22 @@ __global__ __launch_bounds__(256) void k_probe(const float* __restrict__ X, int6
   double stash = 0.0;
   // COMP 2 / 3: the same blocks in a column-block-tiled layout (tile blk = every row's block blk,
   // rows contiguous: X[blk][row][64 * CB * 4 floats]), so a wave streams contiguous memory
+  // COMP 4 / 5: 1 KiB tiles (the engine's layout, kcommon.h XAddr): a block of CB = 2 chunks per
+  // lane reads two tiles, i.e. two contiguous streams per wave
   constexpr bool TILED = COMP >= 2;
-  constexpr int64_t TW = 64 * CB * 4;  // floats per row of a tile
+  constexpr bool T1K = COMP >= 4;
+  constexpr int64_t TW = 64 * CB * 4;  // floats per row of a tile (COMP 2 / 3)
   auto load = [&](int64_t r, f4 (&dst)[CB]) {
 #pragma unroll
     for (int j = 0; j < CB; ++j) {
-      const float* p = TILED ? X + ((int64_t)blk * rows + r) * TW + (j * 64 + lane) * 4 : X + r * ld + cc[j];
+      const float* p = T1K     ? X + (((int64_t)blk * CB + j) * rows + r) * 256 + lane * 4
+                       : TILED ? X + ((int64_t)blk * rows + r) * TW + (j * 64 + lane) * 4
+                               : X + r * ld + cc[j];
       dst[j] = __builtin_nontemporal_load((const f4*)p);
     }
   };
   auto process = [&](const f4 (&rv)[CB], int64_t r) {
-    if constexpr (COMP == 0 || COMP == 2) {
+    if constexpr (COMP == 0 || COMP == 2 || COMP == 4) {
 #pragma unroll
       for (int j = 0; j < CB; ++j) fs += (rv[j][0] + rv[j][1]) + (rv[j][2] + rv[j][3]);
     } else {
@@ -147,6 +152,12 @@ int main() {
   CK(hipMalloc(&xbar, 1024 * sizeof(double)));
   CK(hipMemset(xbar, 0, 1024 * sizeof(double)));
   CK(hipMalloc(&out, 1 << 20));
+  run<2, 6, 4>(X, ld, rows, 2, xbar, out, "1K tiles, pattern only");
+  run<2, 6, 5>(X, ld, rows, 2, xbar, out, "1K tiles, x32 arithmetic");
+  run<2, 12, 5>(X, ld, rows, 2, xbar, out, "1K tiles, x32 arithmetic");
+  run<1, 8, 5>(X, ld, rows, 2, xbar, out, "1K tiles, x32 arithmetic");
+  run<1, 12, 5>(X, ld, rows, 2, xbar, out, "1K tiles, x32 arithmetic");
+  run<2, 6, 3>(X, ld, rows, 2, xbar, out, "2K tiles, x32 arithmetic");
   run<2, 6, 0>(X, ld, rows, 2, xbar, out, "pattern only");
   run<2, 6, 1>(X, ld, rows, 2, xbar, out, "x32 arithmetic");
   run<2, 6, 0>(X, ld, rows, 4, xbar, out, "pattern only");
