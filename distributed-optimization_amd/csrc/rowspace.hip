@@ -633,15 +633,15 @@ static hipError_t rs_pass_shape(const RsArgs& a, dim3 grid, hipStream_t s) {
     else hipLaunchKernelGGL((k_rs_pass<T, COLS, C_, B_>), grid, dim3(NT), 0, s, a);          \
     return hipGetLastError();                                                                  \
   }
-  RS_SHAPE(2, 6)  // the default; the others: A/B builds (DOPT_RS_CB / DOPT_RS_NBUF)
+  RS_SHAPE(2, 8)  // the default; the others: A/B builds (DOPT_RS_CB / DOPT_RS_NBUF)
 #ifdef DOPT_AB
+  RS_SHAPE(2, 6)
   RS_SHAPE(4, 2)
   RS_SHAPE(4, 3)
   RS_SHAPE(2, 3)
   RS_SHAPE(2, 4)
   RS_SHAPE(1, 8)
   RS_SHAPE(1, 12)
-  RS_SHAPE(2, 8)
   RS_SHAPE(1, 16)
 #endif
 #undef RS_SHAPE

@@ -816,9 +816,12 @@ int ensure_rs(dopt_ctx* c) {
   // C5 float32 (tools/rs_ab.py, interleaved on one box, round ms): CB / NBUF / row groups
   // 2 / 6 / 2 11.22, 2 / 4 / 2 11.50, 1 / 8 / 4 11.46-11.84, 2 / 6 / 4 11.33-11.57, 4 / 2 / 4 12.36,
   // 1 / 8 / 16 12.36, 4 / 2 / 16 13.1-13.2: the partial sums' writes (dots nblk x rows, column
-  // sums groups x ld) and long row visits matter more than the tail of ~4k 16 MiB workgroups
+  // sums groups x ld) and long row visits matter more than the tail of ~4k 16 MiB workgroups.
+  // Round 3 (tiled rows, C5 x32, alternated twice on one box, scripts/r3_rs_shape.sh): the windowed
+  // row loop (NBUF dividing 64) at 2 / 8 10.66-10.83 ms, 2 / 4 10.79-10.81, 1 / 16 10.76-10.77,
+  // 1 / 8 10.93-11.41, the 2 / 6 row loop 10.87-11.12
   c->rs_cb = (int)ab_knob("DOPT_RS_CB", 2);
-  c->rs_nbuf = (int)ab_knob("DOPT_RS_NBUF", 6);
+  c->rs_nbuf = (int)ab_knob("DOPT_RS_NBUF", 8);
   const int64_t nblk = (c->nch + 64 * c->rs_cb - 1) / (64 * c->rs_cb);
   int64_t wg = ab_knob("DOPT_RS_WG", (c->rows + 8191) / 8192);  // ~8k rows per row group
   wg = std::max<int64_t>(1, std::min<int64_t>(wg, (c->rows + 255) / 256));
