@@ -1520,37 +1520,90 @@ __global__ __launch_bounds__(NT) void k_wstar(double* w, int64_t d, uint64_t see
     w[c] = normal_at(seed ^ 0x5DEECE66Dull, 0, (uint64_t)c);
 }
 
+// Two standard normals from one 64-bit hash: Box-Muller on two 24-bit uniforms, in float with
+// the hardware log / sqrt / sin / cos (both outputs of the transform are used).  The values are
+// float32 numbers, so float32 and float64 contexts hold exactly the same data.
+__device__ __forceinline__ void normal_pair(uint64_t key, uint64_t j, float& a, float& b) {
+  const uint64_t h = mix64(key ^ (j * 0xD1B54A32D192ED03ull));
+  const float u1 = ((float)(uint32_t)(h >> 40) + 1.0f) * (1.0f / 16777216.0f);  // (0, 1]
+  const float u2 = (float)(uint32_t)(h & 0xFFFFFFu) * (1.0f / 16777216.0f);     // [0, 1)
+  const float r = __builtin_sqrtf(-2.0f * __logf(u1));
+  float s, c;
+  __sincosf(6.28318530717958647f * u2, &s, &c);
+  a = r * c;
+  b = r * s;
+}
+
+// Workgroup = GR consecutive rows; thread t writes element quads t, t + NT, ... of each of them
+// (16-byte float stores / two 16-byte double stores), so w* is read once per GR rows and the
+// labels' dots (float64, the row's values times w*) fold over the threads in a fixed order.
 // xrows > 0: X in the column-block tiled layout of column-blocked contexts (kcommon.h XAddr;
 // ld = the padded row length, whole tiles), else row-major with stride ld.
+constexpr int kGenRows = 8;
 template <typename T>
 __global__ __launch_bounds__(NT) void k_generate(T* X, T* y, int64_t rows, int64_t d, int64_t ld, int64_t xrows,
                                                  const double* __restrict__ wstar, uint64_t seed, double flip,
                                                  double noise, int problem, int64_t row_base) {
+  constexpr int GR = kGenRows;
   constexpr int64_t TE = kTileChunks * (16 / sizeof(T));  // elements of a row in one tile
-  const int lane = threadIdx.x & 63;
-  const int64_t rl = (int64_t)blockIdx.x * NW + (threadIdx.x >> 6);
-  if (rl >= rows) return;
-  const int64_t r = row_base + rl;  // values depend on the GLOBAL row: a rank's slice equals
-                                    // the same rows of the single-GPU data set
-  double dot = 0.0;
-  for (int64_t c = lane; c < ld; c += 64) {
-    double v = 0.0;
-    if (c < d - 1)
-      v = normal_at(seed, (uint64_t)r + 1, (uint64_t)c);
-    else if (c == d - 1)
-      v = 1.0;  // bias column, utils.py:28
-    X[xrows ? ((c / TE) * xrows + rl) * TE + c % TE : rl * ld + c] = (T)v;
-    // labels from the float64 values, so float32 and float64 engines get the same labels
-    if (c < d) dot += v * wstar[c];  // planted w*
+  __shared__ double sdot[NW][GR];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t rl0 = (int64_t)blockIdx.x * GR;
+  const int nr = (int)min((int64_t)GR, rows - rl0);
+  uint64_t key[GR];
+  double dot[GR];
+#pragma unroll
+  for (int k = 0; k < GR; ++k) {
+    // values depend on the GLOBAL row: a rank's slice equals the same rows of the single-GPU set
+    key[k] = mix64(seed ^ mix64((uint64_t)(row_base + rl0 + k) + 1));
+    dot[k] = 0.0;
   }
-  dot = wave_sum(dot);
-  if (lane == 0) {
+  for (int64_t q = threadIdx.x; 4 * q < ld; q += NT) {
+    const int64_t c0 = 4 * q;
+    double ws[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ws[e] = c0 + e < d ? wstar[c0 + e] : 0.0;
+#pragma unroll
+    for (int k = 0; k < GR; ++k) {
+      if (k < nr) {
+        float v[4];
+        normal_pair(key[k], 2 * q, v[0], v[1]);
+        normal_pair(key[k], 2 * q + 1, v[2], v[3]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t c = c0 + e;
+          if (c >= d - 1) v[e] = c == d - 1 ? 1.0f : 0.0f;  // bias column (utils.py:28), then padding
+          dot[k] += (double)v[e] * ws[e];                   // planted w*
+        }
+        const int64_t rl = rl0 + k;
+        T* dst = X + (xrows ? ((c0 / TE) * xrows + rl) * TE + c0 % TE : rl * ld + c0);
+        if constexpr (sizeof(T) == 4) {
+          *(typename VT<float>::v*)dst = typename VT<float>::v{v[0], v[1], v[2], v[3]};
+        } else {
+          *(typename VT<double>::v*)dst = typename VT<double>::v{(double)v[0], (double)v[1]};
+          if (c0 + 2 < ld) *(typename VT<double>::v*)(dst + 2) = typename VT<double>::v{(double)v[2], (double)v[3]};
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < GR; ++k) {
+    const double s = wave_sum(dot[k]);
+    if (lane == 0) sdot[wave][k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < nr) {
+    const int k = threadIdx.x;
+    const int64_t r = row_base + rl0 + k;
+    double dt = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) dt += sdot[w][k];
     if (problem == 0) {
-      T lab = dot >= 0.0 ? T(1) : T(-1);
+      T lab = dt >= 0.0 ? T(1) : T(-1);
       if (unif01(mix64(seed ^ mix64(~(uint64_t)r))) <= flip) lab = -lab;
-      y[rl] = lab;
+      y[rl0 + k] = lab;
     } else {
-      y[rl] = (T)(dot + noise * normal_at(seed ^ 0xA5A5A5A5ull, (uint64_t)r, 0xFFFFFFFFull));
+      y[rl0 + k] = (T)(dt + noise * normal_at(seed ^ 0xA5A5A5A5ull, (uint64_t)r, 0xFFFFFFFFull));
     }
   }
 }
@@ -1560,7 +1613,9 @@ hipError_t launch_generate(int dtype, int problem, void* X, void* y, int64_t row
                            int64_t row_base, hipStream_t s) {
   hipLaunchKernelGGL(k_wstar, dim3((unsigned)std::min<int64_t>(1024, (d + NT - 1) / NT)), dim3(NT), 0, s, wstar, d,
                      seed);
-  const dim3 grid((unsigned)((rows + NW - 1) / NW));
+  if (rows <= 0) return hipGetLastError();
+  if (ld % (dtype == 0 ? 4 : 2) != 0) return hipErrorInvalidValue;  // rows are whole 16-byte chunks
+  const dim3 grid((unsigned)((rows + kGenRows - 1) / kGenRows));
   if (dtype == 0)
     hipLaunchKernelGGL(k_generate<float>, grid, dim3(NT), 0, s, (float*)X, (float*)y, rows, d, ld, xrows,
                        (const double*)wstar, seed, flip, noise, problem, row_base);

@@ -495,60 +495,96 @@ __global__ __launch_bounds__(NT) void k_rs_check(const T* x, int64_t ld, int32_t
   }
 }
 
-// Gram matrices Gram_i[k][l] = X_ik . X_il (float64), partial over column range g: rows of the
-// worker staged through LDS in tiles of 1 KiB per row; thread t accumulates pairs t, t + 256, ...
-// (k <= l) over each tile in column order.  gpart[(i * G + g) * P + p], P = m (m + 1) / 2.
-template <typename T>
+// Gram matrices Gram_i[k][l] = X_ik . X_il (float64) on the float64 matrix cores, partial over
+// the column range of workgroup (i, g).  v_mfma_f64_16x16x4_f64 with A = a 16-row block of the
+// worker's rows over 4 columns and B = the same (or another 16-row block) transposed: lane l holds
+// X[16 b + (l & 15)][col (l >> 4)] for both operands (A[l & 15][l >> 4], B[l >> 4][l & 15]), so one
+// 16-byte row chunk per lane feeds VN of them and a Gram block is a single register per operand.
+// Lane (i, k) of a wave loads chunk 4 s + k of row i at step s: every load instruction reads 64
+// contiguous bytes of each of 16 rows (1 KiB rows of the tiled layout), U steps in flight; the
+// waves of a workgroup take groups of U steps round-robin, their accumulators (two per block,
+// alternating when there is one block, for two independent dependency chains) fold in LDS in a fixed order.  Products of
+// float32 rows are exact in float64; the sums are float64 (the order is the MFMA's).  C/D: lane l,
+// register r = Gram block [(l >> 4) + 4 r][l & 15].  gpart[(i * G + g) * P + p], p = the pair
+// (k <= l) packed over this worker's m rows.  MB = 16-row blocks (1..4: up to kRsMaxRows rows).
+typedef double rs_d4 __attribute__((ext_vector_type(4)));
+template <typename XT, int MB>
 __global__ __launch_bounds__(NT) void k_rs_gram(const RsArgs a, double* gpart, int P) {
-  constexpr int TC = 1024 / sizeof(T);  // tile columns (1 KiB of every row)
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* tile = (T*)smem;
+  using V = typename VT<XT>::v;
+  constexpr int VN = VT<XT>::n;
+  constexpr int NB = MB * (MB + 1) / 2;  // blocks bi <= bj
+  constexpr int U = MB >= 3 ? 2 : 4;      // 4-chunk steps in flight per wave
+  constexpr int H = NB == 1 ? 2 : 1;      // accumulator sets (one block: two chains)
+  __shared__ rs_d4 red[NW - 1][NB][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = blockIdx.x, g = blockIdx.y, G = gridDim.y;
   const int64_t row0 = a.off[i];
   const int m = (int)(a.off[i + 1] - row0);
-  const int64_t ntile = (a.ld + TC - 1) / TC;
-  const int64_t t0 = ntile * g / G, t1 = ntile * (g + 1) / G;
-  constexpr int MAXP = (64 * 65 / 2 + NT - 1) / NT;
-  double acc[MAXP];
-  int pk[MAXP], pl[MAXP];
+  const int ri = lane & 15, kq = lane >> 4;
+  const XAddr<VN> xa(a.tiled ? a.rows : 0, a.ld);
+  const int64_t nstep = ((int64_t)a.nch + 3) / 4;
+  const int64_t s0 = nstep * g / G, s1 = nstep * (g + 1) / G;
+  bool rok[MB];
+  int64_t rbase[MB];
 #pragma unroll
-  for (int s = 0; s < MAXP; ++s) {
-    acc[s] = 0.0;
-    int p = threadIdx.x + s * NT, k = 0;
-    while (p >= m - k && k < m) {  // pair index -> (k, l), l >= k
-      p -= m - k;
-      ++k;
-    }
-    pk[s] = k;
-    pl[s] = k + p;
+  for (int b = 0; b < MB; ++b) {
+    rok[b] = b * 16 + ri < m;
+    rbase[b] = (rok[b] ? row0 + b * 16 + ri : row0) * xa.rs;
   }
-  const int np = m * (m + 1) / 2;
-  for (int64_t t = t0; t < t1; ++t) {
-    const int64_t c0 = t * TC;
-    const int w = (int)min((int64_t)TC, a.ld - c0);
-    __syncthreads();
-    for (int q = threadIdx.x; q < m * TC; q += NT) {
-      const int k = q / TC, c = q % TC;
-      // a 1 KiB row tile IS one tile of the tiled layout: (t * rows + row) * TC
-      tile[q] = c < w ? ((const T*)a.X)[a.tiled ? (t * a.rows + row0 + k) * TC + c : (row0 + k) * a.ld + c0 + c]
-                      : T(0);
-    }
-    __syncthreads();
+  rs_d4 acc[H][NB];
 #pragma unroll
-    for (int s = 0; s < MAXP; ++s) {
-      if (threadIdx.x + s * NT < np) {
-        const T* rk = tile + pk[s] * TC;
-        const T* rl = tile + pl[s] * TC;
-        double sacc = 0.0;
-        for (int c = 0; c < TC; ++c) sacc += (double)rk[c] * (double)rl[c];
-        acc[s] += sacc;
+  for (int h = 0; h < H; ++h)
+#pragma unroll
+    for (int p = 0; p < NB; ++p) acc[h][p] = rs_d4(0.0);
+  for (int64_t s = s0 + (int64_t)wave * U; s < s1; s += NW * U) {
+    V x[U][MB];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t c = 4 * (s + u) + kq;
+      const bool ok = s + u < s1 && c < a.nch;
+#pragma unroll
+      for (int b = 0; b < MB; ++b) x[u][b] = (ok && rok[b]) ? rs_ld_nt<XT>((const XT*)a.X + rbase[b] + xa.col(c)) : V(0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int e = 0; e < VN; ++e) {
+        double xd[MB];
+#pragma unroll
+        for (int b = 0; b < MB; ++b) xd[b] = (double)x[u][b][e];
+        int p = 0;
+#pragma unroll
+        for (int bi = 0; bi < MB; ++bi)
+#pragma unroll
+          for (int bj = bi; bj < MB; ++bj, ++p)
+            acc[e % H][p] = __builtin_amdgcn_mfma_f64_16x16x4f64(xd[bi], xd[bj], acc[e % H][p], 0, 0, 0);
       }
-    }
   }
+  if constexpr (H == 2) {
 #pragma unroll
-  for (int s = 0; s < MAXP; ++s) {
-    const int p = threadIdx.x + s * NT;
-    if (p < np) gpart[((int64_t)i * G + g) * P + p] = acc[s];
+    for (int p = 0; p < NB; ++p) acc[0][p] += acc[1][p];
+  }
+  if (wave > 0) {
+#pragma unroll
+    for (int p = 0; p < NB; ++p) red[wave - 1][p][lane] = acc[0][p];
+  }
+  __syncthreads();
+  if (wave == 0) {
+    double* out = gpart + ((int64_t)i * G + g) * P;
+    int p = 0;
+#pragma unroll
+    for (int bi = 0; bi < MB; ++bi)
+#pragma unroll
+      for (int bj = bi; bj < MB; ++bj, ++p) {
+        rs_d4 t = acc[0][p];
+#pragma unroll
+        for (int w = 0; w < NW - 1; ++w) t += red[w][p][lane];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int k = bi * 16 + (lane >> 4) + 4 * r, l = bj * 16 + (lane & 15);
+          if (k <= l && l < m) out[k * m - k * (k - 1) / 2 + (l - k)] = t[r];
+        }
+      }
   }
 }
 
@@ -723,20 +759,23 @@ hipError_t launch_rs_check(int dtype, const void* x, int64_t n, int64_t ld, int3
 
 hipError_t launch_rs_gram(int xdtype, const RsArgs& a, int n_workers, int max_m, double* gpart, int G, hipStream_t s) {
   if (n_workers <= 0) return hipSuccess;
+  if (max_m < 1 || max_m > kRsMaxRows) return hipErrorInvalidValue;
   const int P = max_m * (max_m + 1) / 2;
-  const size_t lds = (size_t)max_m * 1024;
   const dim3 grid(n_workers, G);
-  if (xdtype == 0) {  // the Gram matrices read the rows only: their storage type
-    hipError_t e = hipFuncSetAttribute((const void*)k_rs_gram<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       64 * 1024);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_rs_gram<float>), grid, dim3(NT), lds, s, a, gpart, P);
-  } else {
-    hipError_t e = hipFuncSetAttribute((const void*)k_rs_gram<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       64 * 1024);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_rs_gram<double>), grid, dim3(NT), lds, s, a, gpart, P);
+  const int mb = (max_m + 15) / 16;
+#define RS_GRAM(XT_)                                                                        \
+  switch (mb) {                                                                             \
+    case 1: hipLaunchKernelGGL((k_rs_gram<XT_, 1>), grid, dim3(NT), 0, s, a, gpart, P); break; \
+    case 2: hipLaunchKernelGGL((k_rs_gram<XT_, 2>), grid, dim3(NT), 0, s, a, gpart, P); break; \
+    case 3: hipLaunchKernelGGL((k_rs_gram<XT_, 3>), grid, dim3(NT), 0, s, a, gpart, P); break; \
+    default: hipLaunchKernelGGL((k_rs_gram<XT_, 4>), grid, dim3(NT), 0, s, a, gpart, P); break; \
   }
+  if (xdtype == 0) {  // the Gram matrices read the rows only: their storage type
+    RS_GRAM(float)
+  } else {
+    RS_GRAM(double)
+  }
+#undef RS_GRAM
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_rs_gram_fold, dim3(n_workers), dim3(NT), 0, s, a, (const double*)gpart, G, P);

@@ -928,7 +928,9 @@ int rs_begin(dopt_ctx* c) {
   RsArgs a = rs_args(c);
   if (!c->rs_gram_ok) {
     const int64_t P = c->rs_bcap * (c->rs_bcap + 1) / 2;
-    const int Gg = (int)std::max<int64_t>(1, std::min<int64_t>((c->ld + 255) / 256, (2048 + c->n - 1) / c->n));
+    // column ranges per worker: ~16k workgroups in all, each at least 64 four-chunk steps
+    const int64_t nstep = ((int64_t)a.nch + 3) / 4;
+    const int Gg = (int)std::max<int64_t>(1, std::min<int64_t>((nstep + 63) / 64, (16384 + c->n - 1) / c->n));
     double* gpart = nullptr;
     if ((rc = dalloc_t(&gpart, (size_t)c->n * Gg * P * sizeof(double)))) return rc;
     hipError_t e = launch_rs_gram(rs_xdt(c), a, (int)c->n, (int)c->rs_bcap, gpart, Gg, c->stream);
