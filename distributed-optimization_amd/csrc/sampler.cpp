@@ -11,8 +11,12 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <sched.h>
+#include <stdlib.h>
+
 #include <algorithm>
 #include <atomic>
+#include <memory>
 #include <thread>
 #include <vector>
 
@@ -388,13 +392,302 @@ static int choice_rounds(uint32_t key[624], int32_t* pos, int64_t T, int64_t n_w
   return DOPT_OK;
 }
 
+// ---------------------------------------------------------------------------- parallel advance
+// The stream advance of full-shard rounds over UNIFORM shards (every drawing worker has the same
+// m >= 2 rows: C3), speculatively in parallel.  The filter is a finite-state machine over the
+// word stream: its state before a word is the k of the Fisher-Yates step in progress (m-1 .. 1),
+// and two runs that are in the same state before the same word stay together from there on
+// (the next word's verdict depends on k alone).  So the stream is cut into segments of kSeg
+// blocks, each filtered on a thread of its own from a GUESSED state (k = m - 1; segment 0 from
+// the true one), recording the permutation ends it sees, its k before each of its first kWin
+// blocks' words and its k at its end.  The stitch (this thread, in segment order) knows the
+// true k at a segment's start (the previous segment's end state, true once that segment's run
+// had met the true one) and runs the filter from there itself until its k equals the recorded
+// k before the same word: from that word on the segment's run IS the true one, so the true
+// permutation ends are the stitch's own before it and the segment's after it.  Two runs from
+// different states meet after ~1e5 words on average at m = 512 (p90 ~2.6e5, the largest of 60
+// samples 4.1e5 words; kWin = 1680 blocks = 1.05M words); a segment whose window holds no
+// meeting point is finished by the stitch itself (correct, just sequential).  The words are the
+// same whichever thread filters them: a producer thread twists the key from segment start to
+// segment start (snapshots), each segment's thread twists and tempers its own blocks.
+namespace {
+
+struct ParSeg {
+  std::vector<uint16_t> pre;  // k before each word of the segment's first kWin blocks
+  std::vector<int64_t> pe;    // word index of the word completing each permutation
+  uint32_t kend = 0;          // k after the segment's last word
+  std::atomic<int> done{0};
+};
+
+int affinity_cpus() {
+  cpu_set_t s;
+  if (sched_getaffinity(0, sizeof(s), &s) != 0) return (int)std::thread::hardware_concurrency();
+  return CPU_COUNT(&s);
+}
+
+int64_t env_i64(const char* name, int64_t dflt) {
+  const char* v = getenv(name);
+  return v ? atoll(v) : dflt;
+}
+
+// the twist and the tempering of a whole block vectorise (x86 function multiversioning: the
+// widest of AVX-512 / AVX2 / baseline the host has, picked at load time; sanitizer builds define
+// DOPT_NO_MULTIVERSION -- their runtimes are not up yet when the loader runs ifunc resolvers)
+#if defined(__x86_64__) && !defined(DOPT_NO_MULTIVERSION)
+#define DOPT_MV __attribute__((target_clones("avx512f", "avx2", "default")))
+#else
+#define DOPT_MV
+#endif
+DOPT_MV void twist_key(uint32_t* __restrict__ key) {
+  int i = 0;
+  for (; i < kN - kM; ++i) {
+    const uint32_t y = (key[i] & kUpper) | (key[i + 1] & kLower);
+    key[i] = key[i + kM] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
+  }
+  for (; i < kN - 1; ++i) {
+    const uint32_t y = (key[i] & kUpper) | (key[i + 1] & kLower);
+    key[i] = key[i + (kM - kN)] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
+  }
+  const uint32_t y = (key[kN - 1] & kUpper) | (key[0] & kLower);
+  key[kN - 1] = key[kM - 1] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
+}
+
+DOPT_MV void temper_block(const uint32_t* __restrict__ key, uint32_t* __restrict__ out) {
+  for (int k = 0; k < kN; ++k) {
+    uint32_t y = key[k];
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    out[k] = y;
+  }
+}
+
+// filter_block that also records k before every word it reads (rec[q] for word q of the block)
+inline void filter_block_rec(const uint32_t* out, int32_t& q, uint32_t& k, uint32_t& t, uint32_t* js, uint16_t* rec) {
+  while (q < kN && k >= 1) {
+    const uint32_t mask = 0xffffffffu >> __builtin_clz(k);
+    const uint32_t klo = mask >> 1;
+    while (q + 8 <= kN && k - klo >= 8) {
+#pragma GCC unroll 8
+      for (int u = 0; u < 8; ++u) {
+        rec[q + u] = (uint16_t)k;
+        const uint32_t v = out[q + u] & mask;
+        const uint32_t keep = v <= k;
+        js[t] = v;
+        t += keep;
+        k -= keep;
+      }
+      q += 8;
+    }
+    while (q < kN && k > klo) {
+      rec[q] = (uint16_t)k;
+      const uint32_t v = out[q++] & mask;
+      const uint32_t keep = v <= k;
+      js[t] = v;
+      t += keep;
+      k -= keep;
+    }
+  }
+}
+
+class ParAdvance {
+ public:
+  ParAdvance(const uint32_t* key0, int32_t pos0, int64_t m, int64_t perms, int threads)
+      : m_(m), D_((uint32_t)(m - 1)), P_(perms), pos0_(pos0), seg_(std::max<int64_t>(1, env_i64("DOPT_MT_SEG_BLOCKS", 2048))),
+        win_(std::max<int64_t>(1, std::min<int64_t>(env_i64("DOPT_MT_WIN_BLOCKS", 1680), seg_))) {
+    // expected words per permutation: a draw at k is kept with probability (k + 1) / (mask(k) + 1)
+    double wpp = 0.0;
+    for (uint32_t k = 1; k <= D_; ++k) wpp += (double)((0xffffffffu >> __builtin_clz(k)) + 1ull) / (double)(k + 1);
+    nseg_ = (int64_t)((double)perms * wpp * 1.02 / (double)(seg_ * kN)) + 2;
+    key0_.assign(key0, key0 + kN);
+    snaps_.resize((size_t)(nseg_ + 1) * kN);
+    memcpy(snaps_.data(), key0, sizeof(uint32_t) * kN);
+    segs_.reserve((size_t)nseg_);
+    for (int64_t j = 0; j < nseg_; ++j) segs_.emplace_back(new ParSeg());
+    snap_ready_.store(1, std::memory_order_release);
+    try {
+      prod_ = std::thread([this] { produce(); });
+      for (int h = 0; h < threads; ++h) th_.emplace_back([this] { work(); });
+    } catch (...) {
+      stop_.store(true, std::memory_order_release);
+      join();
+      throw;
+    }
+  }
+  ~ParAdvance() {
+    stop_.store(true, std::memory_order_release);
+    join();
+  }
+  // the stitch; writes numpy's state after the last permutation's last word
+  void finish(uint32_t key[kN], int32_t* pos) {
+    int64_t done = 0, last = -1;
+    uint32_t ktrue = D_;  // the true k before the current segment's first word
+    std::vector<uint32_t> kk(kN), out(kN), js((size_t)m_);
+    for (int64_t j = 0; last < 0; ++j) {
+      const int64_t b0 = j * seg_, b1 = b0 + seg_;
+      ParSeg* s = j < nseg_ ? segs_[(size_t)j].get() : nullptr;
+      if (s)
+        while (!s->done.load(std::memory_order_acquire)) std::this_thread::yield();
+      if (j == 0) {  // segment 0 ran from the true state
+        for (int64_t e : s->pe)
+          if (++done == P_) {
+            last = e;
+            break;
+          }
+        ktrue = s->kend;
+        continue;
+      }
+      // from the true state until it meets the segment's recorded run (or to the segment's end)
+      key_of_block(b0, kk.data());
+      uint32_t k = ktrue, t = 0;
+      bool met = false;
+      int64_t meet = 0;
+      for (int64_t b = b0; b < b1 && !met && last < 0; ++b) {
+        if (b != b0) twist_key(kk.data());
+        temper_block(kk.data(), out.data());
+        const uint16_t* rec = (s && b < b0 + win_) ? s->pre.data() + (b - b0) * kN : nullptr;
+        for (int32_t q = 0; q < kN; ++q) {
+          if (rec && k == rec[q]) {
+            met = true;
+            meet = b * kN + q;
+            break;
+          }
+          const uint32_t mask = 0xffffffffu >> __builtin_clz(k);
+          if ((out[q] & mask) <= k && --k == 0) {
+            k = D_;
+            if (++done == P_) {
+              last = b * kN + q;
+              break;
+            }
+          }
+        }
+      }
+      if (last >= 0) break;
+      if (!met) {  // no meeting point (or a segment past the planned ones): the stitch's run is the truth
+        ktrue = k;
+        continue;
+      }
+      for (int64_t e : s->pe)
+        if (e >= meet && ++done == P_) {
+          last = e;
+          break;
+        }
+      ktrue = s->kend;
+      (void)t;
+    }
+    stop_.store(true, std::memory_order_release);
+    // numpy's state: the key of the block holding the last word, pos just past it (1 .. 624)
+    const int64_t blk = last / kN;
+    *pos = (int32_t)(last - blk * kN + 1);
+    key_of_block(blk, key);
+  }
+
+ private:
+  int64_t snap_count() const { return snap_ready_.load(std::memory_order_acquire); }
+  void produce() {
+    std::vector<uint32_t> k(key0_);
+    for (int64_t j = 1; j <= nseg_; ++j) {
+      for (int64_t b = 0; b < seg_; ++b) {
+        if (stop_.load(std::memory_order_relaxed)) return;
+        twist_key(k.data());
+      }
+      memcpy(snaps_.data() + (size_t)j * kN, k.data(), sizeof(uint32_t) * kN);
+      snap_ready_.store(j + 1, std::memory_order_release);
+    }
+  }
+  // the key of block b: from the nearest snapshot (waiting for the producer), twisted on
+  void key_of_block(int64_t b, uint32_t* key) {
+    const int64_t j = std::min(b / seg_, nseg_);
+    while (snap_count() <= j) std::this_thread::yield();  // the producer runs until stop_
+    memcpy(key, snaps_.data() + (size_t)j * kN, sizeof(uint32_t) * kN);
+    for (int64_t x = j * seg_; x < b; ++x) twist_key(key);
+  }
+  void work() {
+    for (;;) {
+      const int64_t j = next_.fetch_add(1);
+      if (j >= nseg_) return;
+      while (snap_count() <= j) {
+        if (stop_.load(std::memory_order_acquire)) return;
+        std::this_thread::yield();
+      }
+      ParSeg& s = *segs_[(size_t)j];
+      if (!run_segment(j, s)) return;
+      s.done.store(1, std::memory_order_release);
+    }
+  }
+  // Filter segment j (blocks [j seg, (j + 1) seg)) from k = m - 1 (segment 0: the call's start
+  // state, word pos0 of block 0); records pe, kend and (j > 0) k before each word of the first
+  // win blocks.
+  bool run_segment(int64_t j, ParSeg& s) {
+    const int64_t b0 = j * seg_, b1 = b0 + seg_;
+    std::vector<uint32_t> key(snaps_.begin() + j * kN, snaps_.begin() + (j + 1) * kN), out(kN), js((size_t)m_);
+    s.pe.clear();
+    s.pre.assign(j > 0 ? (size_t)(win_ * kN) : 0, 0);
+    uint32_t k = D_, t = 0;
+    for (int64_t b = b0; b < b1; ++b) {
+      if (b != b0) twist_key(key.data());  // the snapshot is block b0's key
+      temper_block(key.data(), out.data());
+      int32_t q = (b == 0) ? pos0_ : 0;
+      uint16_t* rec = (j > 0 && b < b0 + win_) ? s.pre.data() + (b - b0) * kN : nullptr;
+      while (q < kN) {
+        if (rec) filter_block_rec(out.data(), q, k, t, js.data(), rec);
+        else filter_block(out.data(), q, k, t, js.data());
+        if (k == 0) {
+          s.pe.push_back(b * kN + q - 1);
+          k = D_;
+          t = 0;
+        }
+      }
+      if ((b & 255) == 0 && stop_.load(std::memory_order_relaxed)) return false;
+    }
+    s.kend = k;
+    return true;
+  }
+  void join() {
+    for (auto& t : th_)
+      if (t.joinable()) t.join();
+    if (prod_.joinable()) prod_.join();
+  }
+
+  const int64_t m_;
+  const uint32_t D_;
+  const int64_t P_;
+  const int32_t pos0_;
+  const int64_t seg_, win_;
+  int64_t nseg_;
+  std::vector<uint32_t> key0_, snaps_;
+  std::vector<std::unique_ptr<ParSeg>> segs_;
+  std::atomic<int64_t> snap_ready_{0}, next_{0};
+  std::atomic<bool> stop_{false};
+  std::thread prod_;
+  std::vector<std::thread> th_;
+};
+
+}  // namespace
+
 static int advance_rounds(uint32_t key[624], int32_t* pos, int64_t T, int64_t n_workers, const int64_t* shard_rows) {
   if (int rc = check_rounds(key, pos, T, n_workers, shard_rows)) return rc;
   if (T == 0 || n_workers == 0) return DOPT_OK;
-  BlockRing ring(key, *pos);
-  RingStream st(ring);
   int64_t max_m = 1;
   for (int64_t i = 0; i < n_workers; ++i) max_m = std::max(max_m, shard_rows[i]);
+  // uniform shards (every drawing worker has m rows, the rest 0 / 1) and a long enough stream:
+  // the speculative parallel filter (DOPT_MT_THREADS: filter threads, 0 / 1 = this thread only)
+  int64_t drawing = 0;
+  bool uniform = max_m >= 2 && max_m <= 4096;
+  for (int64_t i = 0; i < n_workers && uniform; ++i) {
+    uniform = shard_rows[i] <= 1 || shard_rows[i] == max_m;
+    drawing += shard_rows[i] == max_m;
+  }
+  const int threads = (int)env_i64("DOPT_MT_THREADS", std::min(8, std::max(0, affinity_cpus() - 4)));
+  const int64_t seg_words = env_i64("DOPT_MT_SEG_BLOCKS", 2048) * kN;
+  if (uniform && threads >= 2 && (double)T * drawing * (max_m - 1) * 1.38 >= 3.0 * (double)seg_words) {
+    ParAdvance par(key, *pos, max_m, T * drawing, threads);
+    par.finish(key, pos);
+    return DOPT_OK;
+  }
+  BlockRing ring(key, *pos);
+  RingStream st(ring);
   // the recording filter into a scratch row (an L1-resident store per word is cheaper than the
   // branchy code the compiler makes of the counting-only form: 2.7 vs 3.2 ns per draw)
   std::vector<uint32_t> js((size_t)max_m);

@@ -1,5 +1,5 @@
 /* Host sanitizer driver for the legacy-MT19937 sampler (csrc/sampler.cpp): exercises
- * every argument path of dopt_mt_choice / dopt_mt_choice_rounds under
+ * every argument path of dopt_mt_choice / dopt_mt_choice_rounds / dopt_mt_advance_rounds under
  * -fsanitize=address,undefined (tests/test_sanitizers.py builds and runs it). */
 #include <stdint.h>
 #include <stdio.h>
@@ -42,6 +42,25 @@ int main(void) {
         if (k < eb ? (v < 0 || v >= rows[i]) : v != -1) return 4;
       }
   free(idx);
+  /* the parallel stream advance (uniform shards), small segments so every stitch path runs;
+   * compared with the sequential advance of the same stream */
+  {
+    uint32_t k1[624], k2[624];
+    int32_t p1 = pos, p2 = pos;
+    memcpy(k1, key, sizeof(k1));
+    memcpy(k2, key, sizeof(k2));
+    const int64_t urows[] = {512, 0, 512, 1, 512, 512};
+    setenv("DOPT_MT_SEG_BLOCKS", "40", 1);
+    setenv("DOPT_MT_WIN_BLOCKS", "12", 1);
+    setenv("DOPT_MT_THREADS", "3", 1);
+    if (dopt_mt_advance_rounds(k1, &p1, 30, 6, urows) != DOPT_OK) return 9;
+    setenv("DOPT_MT_THREADS", "0", 1);
+    if (dopt_mt_advance_rounds(k2, &p2, 30, 6, urows) != DOPT_OK) return 10;
+    if (p1 != p2 || memcmp(k1, k2, sizeof(k1)) != 0) return 11;
+    unsetenv("DOPT_MT_SEG_BLOCKS");
+    unsetenv("DOPT_MT_WIN_BLOCKS");
+    unsetenv("DOPT_MT_THREADS");
+  }
   /* invalid arguments are rejected, not dereferenced */
   if (dopt_mt_choice(NULL, &pos, 5, 2, NULL) == DOPT_OK) return 5;
   int32_t bad = 625;

@@ -216,3 +216,32 @@ def test_index_chunks_boundaries_and_rng_states(batch, max_chunk, t_begin):
                     np.testing.assert_array_equal(idx[t, i, :eb], want)
         now = np.random.get_state()
         assert now[2] == st[2] and np.array_equal(now[1], st[1])
+
+
+@pytest.mark.parametrize("seg,win,start_draws", [("64", "8", 0), ("64", "64", 101), ("48", "20", 7), (None, None, 3)])
+def test_parallel_advance_matches_numpy(monkeypatch, seg, win, start_draws):
+    """The speculative parallel stream advance (uniform shards: segments filtered from a guessed
+    state on their own threads, stitched where each meets the true run) leaves numpy's state
+    exactly where T x N np.random.choice calls do.  Small segments / windows force many stitches
+    and windows without a meeting point (the stitch then runs the segment itself); the last
+    case runs the default shape.  Workers with 0 / 1 rows draw nothing and keep the shards
+    uniform."""
+    monkeypatch.setenv("DOPT_MT_THREADS", "3")
+    if seg:
+        monkeypatch.setenv("DOPT_MT_SEG_BLOCKS", seg)
+        monkeypatch.setenv("DOPT_MT_WIN_BLOCKS", win)
+    rows = [512, 0, 512, 1] * 16 if seg else [512] * 64
+    T = 12 if seg else 120  # the default shape needs >= 3 segments of 2048 blocks
+    np.random.seed(29)
+    np.random.randint(0, 10, size=start_draws)
+    st0 = np.random.get_state()
+    _dopt.mt_advance_rounds(T, rows)
+    st_ours = np.random.get_state()
+    np.random.set_state(st0)
+    for _ in range(T):
+        for m in rows:
+            if m:
+                np.random.choice(m, m, replace=False)
+    st = np.random.get_state()
+    assert st[2] == st_ours[2]
+    np.testing.assert_array_equal(st[1], st_ours[1])

@@ -27,3 +27,23 @@ def test_sampler_under_asan_ubsan(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "sampler asan ok" in r.stdout
     assert "ERROR" not in r.stderr and "runtime error" not in r.stderr
+
+
+@pytest.mark.skipif(shutil.which("g++") is None or shutil.which("gcc") is None, reason="no host compiler")
+def test_sampler_threads_under_tsan(tmp_path):
+    """The sampler's threads (block ring, shuffle pool, the speculative parallel stream advance)
+    under -fsanitize=thread: the same driver, no race reports.  Built without the x86 function
+    multiversioning (its ifunc resolvers run before the TSan runtime is up)."""
+    exe = tmp_path / "sampler_tsan"
+    flags = ["-O1", "-g", "-fsanitize=thread", "-DDOPT_NO_MULTIVERSION", f"-I{ROOT}/include"]
+    subprocess.run(["g++", *flags, "-std=c++17", "-c", f"{ROOT}/distributed-optimization_amd/csrc/sampler.cpp",
+                    "-o", str(tmp_path / "sampler.o")], check=True)
+    subprocess.run(["gcc", *flags, "-c", f"{ROOT}/tests/native/sampler_asan.c", "-o", str(tmp_path / "drv.o")],
+                   check=True)
+    subprocess.run(["g++", "-fsanitize=thread", str(tmp_path / "drv.o"), str(tmp_path / "sampler.o"), "-o", str(exe),
+                    "-pthread"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "sampler asan ok" in r.stdout
+    assert "WARNING: ThreadSanitizer" not in r.stderr
