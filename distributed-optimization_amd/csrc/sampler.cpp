@@ -416,6 +416,7 @@ struct ParSeg {
   std::vector<uint16_t> pre;  // k before each word of the segment's first kWin blocks
   std::vector<int64_t> pe;    // word index of the word completing each permutation
   uint32_t kend = 0;          // k after the segment's last word
+  std::atomic<int64_t> pre_blocks{0};  // blocks of `pre` written so far
   std::atomic<int> done{0};
 };
 
@@ -494,7 +495,7 @@ inline void filter_block_rec(const uint32_t* out, int32_t& q, uint32_t& k, uint3
 class ParAdvance {
  public:
   ParAdvance(const uint32_t* key0, int32_t pos0, int64_t m, int64_t perms, int threads)
-      : m_(m), D_((uint32_t)(m - 1)), P_(perms), pos0_(pos0), seg_(std::max<int64_t>(1, env_i64("DOPT_MT_SEG_BLOCKS", 2048))),
+      : m_(m), D_((uint32_t)(m - 1)), P_(perms), pos0_(pos0), seg_(std::max<int64_t>(1, env_i64("DOPT_MT_SEG_BLOCKS", 4096))),
         win_(std::max<int64_t>(1, std::min<int64_t>(env_i64("DOPT_MT_WIN_BLOCKS", 1680), seg_))) {
     // expected words per permutation: a draw at k is kept with probability (k + 1) / (mask(k) + 1)
     double wpp = 0.0;
@@ -524,12 +525,12 @@ class ParAdvance {
     int64_t done = 0, last = -1;
     uint32_t ktrue = D_;  // the true k before the current segment's first word
     std::vector<uint32_t> kk(kN), out(kN), js((size_t)m_);
+    std::vector<uint16_t> rec(kN);
     for (int64_t j = 0; last < 0; ++j) {
       const int64_t b0 = j * seg_, b1 = b0 + seg_;
       ParSeg* s = j < nseg_ ? segs_[(size_t)j].get() : nullptr;
-      if (s)
-        while (!s->done.load(std::memory_order_acquire)) std::this_thread::yield();
       if (j == 0) {  // segment 0 ran from the true state
+        while (!s->done.load(std::memory_order_acquire)) std::this_thread::yield();
         for (int64_t e : s->pe)
           if (++done == P_) {
             last = e;
@@ -538,31 +539,47 @@ class ParAdvance {
         ktrue = s->kend;
         continue;
       }
-      // from the true state until it meets the segment's recorded run (or to the segment's end)
+      // from the true state until it meets the segment's recorded run (or to the segment's end),
+      // a block at a time: the recording filter, then the first word where the two k agree
       key_of_block(b0, kk.data());
       uint32_t k = ktrue, t = 0;
       bool met = false;
       int64_t meet = 0;
+      std::vector<int64_t> ends;
       for (int64_t b = b0; b < b1 && !met && last < 0; ++b) {
         if (b != b0) twist_key(kk.data());
         temper_block(kk.data(), out.data());
-        const uint16_t* rec = (s && b < b0 + win_) ? s->pre.data() + (b - b0) * kN : nullptr;
-        for (int32_t q = 0; q < kN; ++q) {
-          if (rec && k == rec[q]) {
-            met = true;
-            meet = b * kN + q;
-            break;
-          }
-          const uint32_t mask = 0xffffffffu >> __builtin_clz(k);
-          if ((out[q] & mask) <= k && --k == 0) {
+        ends.clear();
+        for (int32_t q = 0; q < kN;) {
+          filter_block_rec(out.data(), q, k, t, js.data(), rec.data());
+          if (k == 0) {
+            ends.push_back(b * kN + q - 1);
             k = D_;
-            if (++done == P_) {
-              last = b * kN + q;
-              break;
-            }
+            t = 0;
           }
         }
+        int32_t qm = kN;
+        if (s && b < b0 + win_) {
+          while (s->pre_blocks.load(std::memory_order_acquire) <= b - b0) std::this_thread::yield();
+          const uint16_t* pre = s->pre.data() + (b - b0) * kN;
+          for (int32_t x = 0; x < kN; ++x)
+            if (rec[(size_t)x] == pre[x]) {
+              qm = x;
+              break;
+            }
+        }
+        for (int64_t e : ends)
+          if (e < b * kN + qm && ++done == P_) {
+            last = e;
+            break;
+          }
+        if (qm < kN) {
+          met = true;
+          meet = b * kN + qm;
+        }
       }
+      if (met)
+        while (!s->done.load(std::memory_order_acquire)) std::this_thread::yield();
       if (last >= 0) break;
       if (!met) {  // no meeting point (or a segment past the planned ones): the stitch's run is the truth
         ktrue = k;
@@ -574,7 +591,6 @@ class ParAdvance {
           break;
         }
       ktrue = s->kend;
-      (void)t;
     }
     stop_.store(true, std::memory_order_release);
     // numpy's state: the key of the block holding the last word, pos just past it (1 .. 624)
@@ -639,6 +655,7 @@ class ParAdvance {
           t = 0;
         }
       }
+      if (rec) s.pre_blocks.store(b - b0 + 1, std::memory_order_release);
       if ((b & 255) == 0 && stop_.load(std::memory_order_relaxed)) return false;
     }
     s.kend = k;
@@ -680,7 +697,7 @@ static int advance_rounds(uint32_t key[624], int32_t* pos, int64_t T, int64_t n_
     drawing += shard_rows[i] == max_m;
   }
   const int threads = (int)env_i64("DOPT_MT_THREADS", std::min(8, std::max(0, affinity_cpus() - 4)));
-  const int64_t seg_words = env_i64("DOPT_MT_SEG_BLOCKS", 2048) * kN;
+  const int64_t seg_words = env_i64("DOPT_MT_SEG_BLOCKS", 4096) * kN;
   if (uniform && threads >= 2 && (double)T * drawing * (max_m - 1) * 1.38 >= 3.0 * (double)seg_words) {
     ParAdvance par(key, *pos, max_m, T * drawing, threads);
     par.finish(key, pos);

@@ -231,7 +231,7 @@ def test_parallel_advance_matches_numpy(monkeypatch, seg, win, start_draws):
         monkeypatch.setenv("DOPT_MT_SEG_BLOCKS", seg)
         monkeypatch.setenv("DOPT_MT_WIN_BLOCKS", win)
     rows = [512, 0, 512, 1] * 16 if seg else [512] * 64
-    T = 12 if seg else 120  # the default shape needs >= 3 segments of 2048 blocks
+    T = 12 if seg else 200  # the default shape needs >= 3 segments of 4096 blocks
     np.random.seed(29)
     np.random.randint(0, 10, size=start_draws)
     st0 = np.random.get_state()
