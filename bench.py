@@ -311,7 +311,7 @@ def suboptimality(eng, lam, final_objective):
             "note": "device L-BFGS on the full-data objective (replaces sklearn saga at sizes it cannot run)"}
 
 
-def dropin_leg(eng, n, d, m, lam, eta0, rounds=128):
+def dropin_leg(eng, n, d, m, lam, eta0, rounds=128, batch=None):
     """The drop-in DecentralizedTrainer (trainer.py API) on the same C3 shards as host arrays,
     sampling='legacy': every round draws the reference's numpy legacy-MT19937 stream
     (4096 permutations of 512 per round, worker.py:27) on the host before the device runs
@@ -330,10 +330,11 @@ def dropin_leg(eng, n, d, m, lam, eta0, rounds=128):
         Xi, yi = eng.get_shard(i)
         X[i * m:(i + 1) * m] = Xi
         y[i * m:(i + 1) * m] = yi
-    cfg = {"problem_type": "logistic", "local_batch_size": m, "learning_rate_eta0": eta0,
+    b = batch or m
+    cfg = {"problem_type": "logistic", "local_batch_size": b, "learning_rate_eta0": eta0,
            "l2_regularization_lambda": lam, "strong_convexity_mu": lam, "dtype": "float64",
            "sampling": "legacy", "regular_degree": 4, "topology_seed": 0, "spectral_gap": False}
-    ws = [Worker(i, {"X": X[i * m:(i + 1) * m], "y": y[i * m:(i + 1) * m]}, m, d, cfg) for i in range(n)]
+    ws = [Worker(i, {"X": X[i * m:(i + 1) * m], "y": y[i * m:(i + 1) * m]}, b, d, cfg) for i in range(n)]
     tr = DecentralizedTrainer(ws, "random_regular", d, cfg)
     np.random.seed(203)
     tr.run(2, X, y)  # loads the engine
@@ -344,7 +345,7 @@ def dropin_leg(eng, n, d, m, lam, eta0, rounds=128):
         hist, _ = tr.run(T, X, y)
         walls.append(time.perf_counter() - t0)
     per_round = (walls[2] - walls[1]) / rounds
-    return {"value": n / per_round, "unit": "worker-iters/s", "rounds": [rounds, 2 * rounds],
+    return {"value": n / per_round, "unit": "worker-iters/s", "batch": b, "rounds": [rounds, 2 * rounds],
             "run_wall_s": walls[1:], "zero_round_run_s": walls[0], "ms_per_round": per_round * 1e3,
             "final_objective": float(hist["objective"][-1]),
             "note": "trainer.DecentralizedTrainer, sampling='legacy' (numpy's stream, drawn on the host one "
@@ -749,6 +750,8 @@ def main():
         out["suboptimality"] = suboptimality(eng, lam, float(obj[-1]))
         log("drop-in trainer leg (legacy RNG stream)")
         out["dropin"] = dropin_leg(eng, n, d, m, lam, eta0)
+        log("drop-in trainer leg, b = 16 (minibatch indices from the legacy stream)")
+        out["dropin"]["b16"] = dropin_leg(eng, n, d, m, lam, eta0, batch=16)
     if args.pcie and world == 1 and args.config == "c3":
         out["pcie"] = pcie_leg(eng, top, n, d, m, b, lam, eta0, args.steps, dt)
     eng.close()

@@ -345,6 +345,10 @@ class ShufflePool {
   std::thread th_[kThreads];
 };
 
+// The speculative parallel draw for uniform shards (defined below); 1 = not applicable.
+static int choice_rounds_parallel(uint32_t key[624], int32_t* pos, int64_t T, int64_t n_workers,
+                                  const int64_t* shard_rows, int64_t b, int32_t* out, int64_t max_m);
+
 // The numpy state (key, pos) is written only when a call completes: a call that fails leaves
 // it where it was.
 static int choice_rounds(uint32_t key[624], int32_t* pos, int64_t T, int64_t n_workers, const int64_t* shard_rows,
@@ -354,12 +358,10 @@ static int choice_rounds(uint32_t key[624], int32_t* pos, int64_t T, int64_t n_w
   if (T == 0 || n_workers == 0) return DOPT_OK;
   int64_t max_m = 1;
   for (int64_t i = 0; i < n_workers; ++i) max_m = std::max(max_m, shard_rows[i]);
+  if (b == 0) return DOPT_OK;  // eb = 0 for every worker: no draw at all (worker.py:21-23)
+  if (int rc = choice_rounds_parallel(key, pos, T, n_workers, shard_rows, b, out, max_m); rc != 1) return rc;
   BlockRing ring(key, *pos);
   RingStream st(ring);
-  if (b == 0) {  // eb = 0 for every worker: no draw at all (worker.py:21-23)
-    st.save(key, pos);
-    return DOPT_OK;
-  }
   if (max_m > (int64_t(1) << 22)) {  // shards beyond 4M rows: shuffle inline (no 128 MiB js ring)
     std::vector<int64_t> perm;
     std::vector<uint32_t> js((size_t)max_m);
@@ -415,6 +417,8 @@ namespace {
 struct ParSeg {
   std::vector<uint16_t> pre;  // k before each word of the segment's first kWin blocks
   std::vector<int64_t> pe;    // word index of the word completing each permutation
+  std::vector<uint32_t> vals; // (minibatch draws) every kept word's value, in order
+  std::vector<int64_t> cum;   // (minibatch draws) kept words before each block
   uint32_t kend = 0;          // k after the segment's last word
   std::atomic<int64_t> pre_blocks{0};  // blocks of `pre` written so far
   std::atomic<int> done{0};
@@ -494,8 +498,12 @@ inline void filter_block_rec(const uint32_t* out, int32_t& q, uint32_t& k, uint3
 
 class ParAdvance {
  public:
-  ParAdvance(const uint32_t* key0, int32_t pos0, int64_t m, int64_t perms, int threads)
-      : m_(m), D_((uint32_t)(m - 1)), P_(perms), pos0_(pos0), seg_(std::max<int64_t>(1, env_i64("DOPT_MT_SEG_BLOCKS", 4096))),
+  // keep: also record every kept word's value (the Fisher-Yates j's of minibatch draws; m >= 3,
+  // so that every kept word changes k and the recorded k's locate the meeting point in the
+  // kept-value stream as well)
+  ParAdvance(const uint32_t* key0, int32_t pos0, int64_t m, int64_t perms, int threads, bool keep = false)
+      : m_(m), D_((uint32_t)(m - 1)), P_(perms), pos0_(pos0), keep_(keep),
+        seg_(std::max<int64_t>(1, env_i64("DOPT_MT_SEG_BLOCKS", 4096))),
         win_(std::max<int64_t>(1, std::min<int64_t>(env_i64("DOPT_MT_WIN_BLOCKS", 1680), seg_))) {
     // expected words per permutation: a draw at k is kept with probability (k + 1) / (mask(k) + 1)
     double wpp = 0.0;
@@ -520,17 +528,26 @@ class ParAdvance {
     stop_.store(true, std::memory_order_release);
     join();
   }
+  // The true kept-value stream (keep mode) as pieces (pointer, count) in order: the stitch's own
+  // values before each meeting word, then the segment's from there.
+  typedef std::pair<const uint32_t*, int64_t> Piece;
   // the stitch; writes numpy's state after the last permutation's last word
-  void finish(uint32_t key[kN], int32_t* pos) {
+  void finish(uint32_t key[kN], int32_t* pos, std::vector<Piece>* pieces = nullptr) {
     int64_t done = 0, last = -1;
     uint32_t ktrue = D_;  // the true k before the current segment's first word
     std::vector<uint32_t> kk(kN), out(kN), js((size_t)m_);
     std::vector<uint16_t> rec(kN);
+    auto trans = [](const uint16_t* r, int32_t n) {  // kept words among the first n (k changes on each)
+      int64_t c = 0;
+      for (int32_t x = 0; x < n; ++x) c += r[x + 1] != r[x];
+      return c;
+    };
     for (int64_t j = 0; last < 0; ++j) {
       const int64_t b0 = j * seg_, b1 = b0 + seg_;
       ParSeg* s = j < nseg_ ? segs_[(size_t)j].get() : nullptr;
       if (j == 0) {  // segment 0 ran from the true state
         while (!s->done.load(std::memory_order_acquire)) std::this_thread::yield();
+        if (keep_) pieces->emplace_back(s->vals.data(), s->cum[(size_t)seg_]);
         for (int64_t e : s->pe)
           if (++done == P_) {
             last = e;
@@ -544,14 +561,23 @@ class ParAdvance {
       key_of_block(b0, kk.data());
       uint32_t k = ktrue, t = 0;
       bool met = false;
-      int64_t meet = 0;
+      int64_t meet = 0, seg_at = 0;  // keep: the segment's kept words before the meeting word
       std::vector<int64_t> ends;
+      std::vector<uint32_t>* own = nullptr;  // keep: the stitch's own kept values in this segment
+      if (keep_) {
+        owns_.emplace_back(new std::vector<uint32_t>());
+        own = owns_.back().get();
+      }
       for (int64_t b = b0; b < b1 && !met && last < 0; ++b) {
         if (b != b0) twist_key(kk.data());
         temper_block(kk.data(), out.data());
         ends.clear();
+        const int64_t tb = keep_ ? (int64_t)own->size() : 0;  // kept before this block
+        if (keep_) own->resize((size_t)(tb + kN + 1));
+        uint32_t* jsb = keep_ ? own->data() + tb : js.data();
+        uint32_t tk = 0;
         for (int32_t q = 0; q < kN;) {
-          filter_block_rec(out.data(), q, k, t, js.data(), rec.data());
+          filter_block_rec(out.data(), q, k, keep_ ? tk : t, jsb, rec.data());
           if (k == 0) {
             ends.push_back(b * kN + q - 1);
             k = D_;
@@ -559,14 +585,22 @@ class ParAdvance {
           }
         }
         int32_t qm = kN;
+        const uint16_t* pre = nullptr;
         if (s && b < b0 + win_) {
           while (s->pre_blocks.load(std::memory_order_acquire) <= b - b0) std::this_thread::yield();
-          const uint16_t* pre = s->pre.data() + (b - b0) * kN;
+          pre = s->pre.data() + (b - b0) * kN;
           for (int32_t x = 0; x < kN; ++x)
             if (rec[(size_t)x] == pre[x]) {
               qm = x;
               break;
             }
+        }
+        if (keep_) {  // keep the stitch's values up to the meeting word (all of the block without one)
+          own->resize((size_t)(tb + (qm < kN ? trans(rec.data(), qm) : (int64_t)tk)));
+          if (qm < kN) {
+            while (!s->done.load(std::memory_order_acquire)) std::this_thread::yield();  // s->cum
+            seg_at = s->cum[(size_t)(b - b0)] + trans(pre, qm);
+          }
         }
         for (int64_t e : ends)
           if (e < b * kN + qm && ++done == P_) {
@@ -580,6 +614,10 @@ class ParAdvance {
       }
       if (met)
         while (!s->done.load(std::memory_order_acquire)) std::this_thread::yield();
+      if (keep_) {
+        pieces->emplace_back(own->data(), (int64_t)own->size());
+        if (met) pieces->emplace_back(s->vals.data() + seg_at, s->cum[(size_t)seg_] - seg_at);
+      }
       if (last >= 0) break;
       if (!met) {  // no meeting point (or a segment past the planned ones): the stitch's run is the truth
         ktrue = k;
@@ -640,25 +678,32 @@ class ParAdvance {
     std::vector<uint32_t> key(snaps_.begin() + j * kN, snaps_.begin() + (j + 1) * kN), out(kN), js((size_t)m_);
     s.pe.clear();
     s.pre.assign(j > 0 ? (size_t)(win_ * kN) : 0, 0);
+    if (keep_) {  // one index t over the whole segment: js[t] is the next kept word's slot
+      s.vals.resize((size_t)(seg_ * kN + 1));
+      s.cum.assign((size_t)(seg_ + 1), 0);
+    }
+    uint32_t* jsp = keep_ ? s.vals.data() : js.data();
     uint32_t k = D_, t = 0;
     for (int64_t b = b0; b < b1; ++b) {
       if (b != b0) twist_key(key.data());  // the snapshot is block b0's key
       temper_block(key.data(), out.data());
+      if (keep_) s.cum[(size_t)(b - b0)] = t;
       int32_t q = (b == 0) ? pos0_ : 0;
       uint16_t* rec = (j > 0 && b < b0 + win_) ? s.pre.data() + (b - b0) * kN : nullptr;
       while (q < kN) {
-        if (rec) filter_block_rec(out.data(), q, k, t, js.data(), rec);
-        else filter_block(out.data(), q, k, t, js.data());
+        if (rec) filter_block_rec(out.data(), q, k, t, jsp, rec);
+        else filter_block(out.data(), q, k, t, jsp);
         if (k == 0) {
           s.pe.push_back(b * kN + q - 1);
           k = D_;
-          t = 0;
+          if (!keep_) t = 0;
         }
       }
       if (rec) s.pre_blocks.store(b - b0 + 1, std::memory_order_release);
       if ((b & 255) == 0 && stop_.load(std::memory_order_relaxed)) return false;
     }
     s.kend = k;
+    if (keep_) s.cum[(size_t)seg_] = t;
     return true;
   }
   void join() {
@@ -671,8 +716,10 @@ class ParAdvance {
   const uint32_t D_;
   const int64_t P_;
   const int32_t pos0_;
+  const bool keep_;
   const int64_t seg_, win_;
   int64_t nseg_;
+  std::vector<std::unique_ptr<std::vector<uint32_t>>> owns_;  // the stitch's kept values (pieces point in)
   std::vector<uint32_t> key0_, snaps_;
   std::vector<std::unique_ptr<ParSeg>> segs_;
   std::atomic<int64_t> snap_ready_{0}, next_{0};
@@ -683,6 +730,88 @@ class ParAdvance {
 
 }  // namespace
 
+namespace {
+// Uniform shards (every drawing worker has m rows, the rest 0 / 1 -- they draw nothing): the
+// number of drawing workers, or -1.  min_m: 2 for the advance, 3 for minibatch draws (keep mode).
+int64_t uniform_drawing(int64_t n_workers, const int64_t* rows, int64_t max_m, int64_t min_m) {
+  if (max_m < min_m || max_m > 4096) return -1;
+  int64_t drawing = 0;
+  for (int64_t i = 0; i < n_workers; ++i) {
+    if (rows[i] > 1 && rows[i] != max_m) return -1;
+    drawing += rows[i] == max_m;
+  }
+  return drawing;
+}
+
+int par_threads() { return (int)env_i64("DOPT_MT_THREADS", std::min(12, std::max(0, affinity_cpus() - 4))); }
+
+bool par_worth(int64_t T, int64_t drawing, int64_t m) {  // >= 3 segments of words
+  return (double)T * drawing * (m - 1) * 1.38 >= 3.0 * (double)(env_i64("DOPT_MT_SEG_BLOCKS", 4096) * kN);
+}
+}  // namespace
+
+static int choice_rounds_parallel(uint32_t key[624], int32_t* pos, int64_t T, int64_t n, const int64_t* rows,
+                                  int64_t b, int32_t* out, int64_t max_m) {
+  const int64_t drawing = uniform_drawing(n, rows, max_m, 3);
+  const int threads = par_threads();
+  if (drawing <= 0 || threads < 2 || !par_worth(T, drawing, max_m)) return 1;
+  uint32_t key1[kN];
+  int32_t pos1 = *pos;
+  memcpy(key1, key, sizeof(key1));
+  ParAdvance par(key1, pos1, max_m, T * drawing, threads, true);
+  std::vector<ParAdvance::Piece> pieces;
+  par.finish(key1, &pos1, &pieces);
+  std::vector<int64_t> ps(pieces.size() + 1, 0);  // stream offset of each piece
+  for (size_t x = 0; x < pieces.size(); ++x) ps[x + 1] = ps[x] + pieces[x].second;
+  const int64_t D = max_m - 1;
+  if (ps.back() < T * drawing * D) return DOPT_ERR_RUNTIME;  // (the stitch ran to the P-th end)
+  std::vector<int64_t> rank((size_t)n, -1);
+  for (int64_t i = 0, r = 0; i < n; ++i)
+    if (rows[i] == max_m) rank[(size_t)i] = r++;
+  // the Fisher-Yates shuffles: jobs (round, worker) in contiguous ranges over the threads
+  const int64_t nj = T * n;
+  std::atomic<bool> fail{false};
+  auto body = [&](int64_t q0, int64_t q1) {
+    std::vector<int64_t> perm;
+    std::vector<uint32_t> js((size_t)max_m);
+    for (int64_t q = q0; q < q1; ++q) {
+      const int64_t t = q / n, i = q % n, m = rows[i];
+      const int64_t eb = (m == 0) ? 0 : (b < m ? b : m);
+      int32_t* o = out + q * b;
+      if (m == max_m) {  // gather the permutation's D kept values from the pieces
+        int64_t off = (t * drawing + rank[(size_t)i]) * D, got = 0;
+        size_t x = (size_t)(std::upper_bound(ps.begin(), ps.end(), off) - ps.begin()) - 1;
+        while (got < D) {
+          const int64_t in = off - ps[x], take = std::min(D - got, pieces[x].second - in);
+          memcpy(js.data() + got, pieces[x].first + in, (size_t)take * sizeof(uint32_t));
+          got += take;
+          off += take;
+          ++x;
+        }
+      }
+      if (eb > 0) shuffle_prefix(m, eb, js.data(), perm, o);  // m = 1: [0] without a draw
+      for (int64_t c = eb; c < b; ++c) o[c] = -1;
+    }
+  };
+  {
+    std::vector<std::thread> th;
+    const int64_t per = (nj + threads - 1) / threads;
+    try {
+      for (int h = 1; h < threads && h * per < nj; ++h) th.emplace_back(body, h * per, std::min(nj, (h + 1) * per));
+    } catch (...) {
+      fail.store(true);
+    }
+    body(0, std::min(nj, per));
+    for (auto& x : th) x.join();
+    if (fail.load()) {  // a thread that would not start: its range here
+      for (int h = 1 + (int)th.size(); h < threads && h * per < nj; ++h) body(h * per, std::min(nj, (h + 1) * per));
+    }
+  }
+  memcpy(key, key1, sizeof(key1));
+  *pos = pos1;
+  return DOPT_OK;
+}
+
 static int advance_rounds(uint32_t key[624], int32_t* pos, int64_t T, int64_t n_workers, const int64_t* shard_rows) {
   if (int rc = check_rounds(key, pos, T, n_workers, shard_rows)) return rc;
   if (T == 0 || n_workers == 0) return DOPT_OK;
@@ -690,15 +819,9 @@ static int advance_rounds(uint32_t key[624], int32_t* pos, int64_t T, int64_t n_
   for (int64_t i = 0; i < n_workers; ++i) max_m = std::max(max_m, shard_rows[i]);
   // uniform shards (every drawing worker has m rows, the rest 0 / 1) and a long enough stream:
   // the speculative parallel filter (DOPT_MT_THREADS: filter threads, 0 / 1 = this thread only)
-  int64_t drawing = 0;
-  bool uniform = max_m >= 2 && max_m <= 4096;
-  for (int64_t i = 0; i < n_workers && uniform; ++i) {
-    uniform = shard_rows[i] <= 1 || shard_rows[i] == max_m;
-    drawing += shard_rows[i] == max_m;
-  }
-  const int threads = (int)env_i64("DOPT_MT_THREADS", std::min(8, std::max(0, affinity_cpus() - 4)));
-  const int64_t seg_words = env_i64("DOPT_MT_SEG_BLOCKS", 4096) * kN;
-  if (uniform && threads >= 2 && (double)T * drawing * (max_m - 1) * 1.38 >= 3.0 * (double)seg_words) {
+  const int64_t drawing = uniform_drawing(n_workers, shard_rows, max_m, 2);
+  const int threads = par_threads();
+  if (drawing > 0 && threads >= 2 && par_worth(T, drawing, max_m)) {
     ParAdvance par(key, *pos, max_m, T * drawing, threads);
     par.finish(key, pos);
     return DOPT_OK;

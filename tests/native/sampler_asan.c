@@ -57,6 +57,20 @@ int main(void) {
     setenv("DOPT_MT_THREADS", "0", 1);
     if (dopt_mt_advance_rounds(k2, &p2, 30, 6, urows) != DOPT_OK) return 10;
     if (p1 != p2 || memcmp(k1, k2, sizeof(k1)) != 0) return 11;
+    /* minibatch draws through the parallel path vs the sequential one */
+    {
+      int32_t* i1 = (int32_t*)malloc(30 * 6 * 4 * sizeof(int32_t));
+      int32_t* i2 = (int32_t*)malloc(30 * 6 * 4 * sizeof(int32_t));
+      memcpy(k2, k1, sizeof(k1));
+      p2 = p1;
+      setenv("DOPT_MT_THREADS", "3", 1);
+      if (dopt_mt_choice_rounds(k1, &p1, 30, 6, urows, 4, i1) != DOPT_OK) return 12;
+      setenv("DOPT_MT_THREADS", "0", 1);
+      if (dopt_mt_choice_rounds(k2, &p2, 30, 6, urows, 4, i2) != DOPT_OK) return 13;
+      if (p1 != p2 || memcmp(k1, k2, sizeof(k1)) != 0 || memcmp(i1, i2, 30 * 6 * 4 * sizeof(int32_t)) != 0) return 14;
+      free(i1);
+      free(i2);
+    }
     unsetenv("DOPT_MT_SEG_BLOCKS");
     unsetenv("DOPT_MT_WIN_BLOCKS");
     unsetenv("DOPT_MT_THREADS");

@@ -245,3 +245,34 @@ def test_parallel_advance_matches_numpy(monkeypatch, seg, win, start_draws):
     st = np.random.get_state()
     assert st[2] == st_ours[2]
     np.testing.assert_array_equal(st[1], st_ours[1])
+
+
+@pytest.mark.parametrize("seg,win,rows,T,b", [("64", "8", [512, 0, 512, 1] * 16, 12, 16),
+                                              ("40", "40", [300] * 64, 10, 300),
+                                              ("40", "12", [3, 1, 3] * 50, 1500, 2),
+                                              (None, None, [512] * 64, 200, 16)])
+def test_parallel_minibatch_draws_match_numpy(monkeypatch, seg, win, rows, T, b):
+    """Minibatch draws (b < m) over uniform shards through the speculative parallel filter: the
+    kept words of every segment after its meeting point, spliced after the stitch's own, give
+    every worker's np.random.choice(m, b, replace=False) bit for bit, and numpy's state after the
+    call is numpy's.  m = 3 is the smallest shard the kept-word splice handles (every kept word
+    changes k); tiny segments / windows force windows without a meeting point."""
+    monkeypatch.setenv("DOPT_MT_THREADS", "4")
+    if seg:
+        monkeypatch.setenv("DOPT_MT_SEG_BLOCKS", seg)
+        monkeypatch.setenv("DOPT_MT_WIN_BLOCKS", win)
+    np.random.seed(31)
+    np.random.randint(0, 10, size=3)
+    st0 = np.random.get_state()
+    out = _dopt.mt_choice_rounds(T, rows, b)
+    st_ours = np.random.get_state()
+    np.random.set_state(st0)
+    for t in range(T):
+        for i, m in enumerate(rows):
+            eb = 0 if m == 0 else min(b, m)
+            if eb:
+                np.testing.assert_array_equal(out[t, i, :eb], np.random.choice(m, eb, replace=False))
+            assert np.all(out[t, i, eb:] == -1)
+    st = np.random.get_state()
+    assert st[2] == st_ours[2]
+    np.testing.assert_array_equal(st[1], st_ours[1])

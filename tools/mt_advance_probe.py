@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Host legacy-stream advance at the C3 chunk shape (8 rounds x 4096 workers x permutations of 512):
+"""Host legacy-stream advance (or, --batch b, minibatch draws) at the C3 chunk shape (8 rounds x 4096 workers x permutations of 512):
 the sequential filter (DOPT_MT_THREADS=0) vs the speculative parallel advance, alternated, with
 the resulting numpy state checked equal.  python tools/mt_advance_probe.py [--threads 0,4,8]"""
 import argparse
@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--threads", default="0,4,8")
     ap.add_argument("--reps", type=int, default=4)
     ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=0, help="b < 512: minibatch draws (dopt_mt_choice_rounds)")
     a = ap.parse_args()
     rows = np.full(4096, 512, np.int64)
     res = {}
@@ -29,7 +30,10 @@ def main():
             os.environ["DOPT_MT_THREADS"] = th
             np.random.seed(100 + rep)
             t0 = time.perf_counter()
-            _dopt.mt_advance_rounds(a.rounds, rows)
+            if a.batch:
+                _dopt.mt_choice_rounds(a.rounds, rows, a.batch)
+            else:
+                _dopt.mt_advance_rounds(a.rounds, rows)
             dt = time.perf_counter() - t0
             st = np.random.get_state()
             res.setdefault(th, []).append((dt, st[2], st[1][:4].tolist()))
