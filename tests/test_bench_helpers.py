@@ -16,7 +16,7 @@ if ROOT not in sys.path:
 import bench  # noqa: E402
 
 F32, F64 = _dopt.F32, _dopt.F64
-C3 = "void dopt::k_round<double, float, 4, 0, true, true, 161827>(dopt::RoundArgs)"
+C3 = "void dopt::k_round<double, float, 4, 0, true, true, 161843>(dopt::RoundArgs)"
 C5RS = "void dopt::k_rs_pass<float, true, 2, 6>(dopt::RsArgs)"
 C5X32 = "void dopt::k_rs_pass_x32<true, 2, 6>(dopt::RsArgs)"
 C5D = "void dopt::k_split_step<float, 4, true, true, true, 1>(dopt::RoundArgs)"  # round-2 spelling
@@ -31,7 +31,7 @@ def _eng(dtype, xdtype):
 CASES = [
     ("c3", C3, F64, F32, 4096, 1024, 512, 8.665, "profiles/r3_pmc.json"),
     ("c5", C5DX, F64, F32, 1024, 1 << 20, 16, 85.90, "profiles/r3_c5x32direct_pmc.json"),
-    ("c4", C3, F64, F32, 65536, 1024, 512, 138.6, "profiles/r2_c4_pmc.json"),
+    ("c4", C3, F64, F32, 65536, 1024, 512, 138.6, "profiles/r3_c4_pmc.json"),
     ("c5", C5D, F32, F32, 1024, 1 << 20, 16, 77.3, "profiles/r2_c5_pmc.json"),
     ("c5", C5RS, F32, F32, 1024, 1 << 20, 16, 68.72, "profiles/r2_c5rs_pmc.json"),
     ("c5", C5X32, F64, F32, 1024, 1 << 20, 16, 68.72, "profiles/r2_c5x32_pmc.json"),
