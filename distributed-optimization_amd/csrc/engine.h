@@ -135,6 +135,12 @@ struct RsArgs {
   const double* csum;      // [ld] all-reduced column sums C (multi-GPU), or null: sum cpart
   double a1, q, eta, eta_n;  // w_off N, W_ii - w_off - eta mu, eta, eta / N
   int32_t blk0;            // first column block of this pass launch (column-chunked passes)
+  // iterates that did not start equal: x_i = c x_i(0) + Z + X_i^T beta_i (else c = 0, pointers null)
+  double c;                // the x_i(0) coefficient of the iterates the pass reads (prod of q so far)
+  const double* xbar0;     // [ld] mean of the starting iterates
+  const double* p0;        // [n x bcap] X_ik . x_i(0)
+  const double* d0;        // [n] ||x_i(0) - xbar0||^2
+  const void* x0;          // [n x ld] T the starting iterates (materialisation)
 };
 // dtype: arithmetic; xdtype: row storage (float32 rows under float64 arithmetic: k_rs_pass_x32).
 // Column blocks [a.blk0, a.blk0 + nblk) of the pass (nblk <= 0: all of a.nblk from a.blk0 = 0).
@@ -156,6 +162,11 @@ hipError_t launch_rs_check(int dtype, const void* x, int64_t n, int64_t ld, int3
 hipError_t launch_rs_gram(int xdtype, const RsArgs& a, int n_workers, int max_m, double* gpart, int G,
                           hipStream_t s);
 hipError_t launch_rs_materialise(int dtype, int xdtype, const RsArgs& a, int n_workers, void* xout, hipStream_t s);
+// Unequal starting iterates x (T, [n x ld]): xbar0 = their mean (float64; xbar_out its T copy),
+// d0[i] = ||x_i - xbar0||^2, p0[i][k] = X_ik . x_i (partials over G column ranges in gpart, folded in
+// order), then the row-space state of such a start: Z = 0, xbar = xbar0, ||D||^2 partials 0.
+hipError_t launch_rs_x0(int dtype, int xdtype, const RsArgs& a, int n_workers, const void* x, double* xbar0,
+                        double* d0, double* p0, double* gpart, int G, hipStream_t s);
 
 // Kernel launchers (kernels.hip).  dtype: 0 = float, 1 = double.
 // k_round: dtype = iterates and arithmetic, xdtype = shard storage (equal, or float32 rows

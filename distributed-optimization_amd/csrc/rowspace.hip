@@ -271,8 +271,11 @@ __global__ __launch_bounds__(NT) void k_rs_pass_x32(const RsArgs a) {
 
 // k_rs_rows: one workgroup per worker (m_i <= 64 rows, lane k = row k).  u_k = sum over the
 // pass's column blocks (4 waves x a quarter each, then in wave order); then the metric partials
-// of the iterate the pass read (mode & 1), the next round's row state (mode & 2), or the
-// initial state z = v = u, beta = 0 (mode & 4).
+// of the iterate the pass read (mode & 1), the next round's row state (mode & 2), the initial
+// state z = v = u, beta = 0 (mode & 4), or that of unequal starts, z = p0, v = 0, beta = 0 (mode 16).
+// With unequal starts (x_i = c x_i(0) + Z + X_i^T beta_i, a.p0 set) the consensus partial of a
+// worker is c^2 ||x_i(0) - xbar0||^2 + ||D||^2 + beta . (2 (c p0 + v - u) + G beta), D = c xbar0 +
+// Z - xbar: the cross terms 2 c (x_i(0) - xbar0) . D sum to zero over the workers.
 template <typename T>
 __global__ __launch_bounds__(NT) void k_rs_rows(const RsArgs a, int mode) {
   __shared__ double ured[16][64];
@@ -338,6 +341,16 @@ __global__ __launch_bounds__(NT) void k_rs_rows(const RsArgs a, int mode) {
     }
     return;
   }
+  if (mode & 16) {  // unequal starts: z = X_i . x_i(0), v = X . Z = 0, beta = 0
+    if (live) {
+      const double z0 = a.p0[s0 + lane];
+      a.z[s0 + lane] = z0;
+      a.v[s0 + lane] = 0.0;
+      a.beta[s0 + lane] = 0.0;
+      a.coef_row[row0 + lane] = weight(z0);
+    }
+    return;
+  }
   const double zv = live ? a.z[s0 + lane] : 0.0;
   const double vv = live ? a.v[s0 + lane] : 0.0;
   const double bk = sb[lane];
@@ -352,10 +365,11 @@ __global__ __launch_bounds__(NT) void k_rs_rows(const RsArgs a, int mode) {
   }
   if (mode & 1) {
     const double ls = wave_sum(live ? (a.problem == 0 ? row_loss<double, 0>(yv, u) : row_loss<double, 1>(yv, u)) : 0.0);
-    const double cs = wave_sum(live ? bk * (2.0 * (vv - u) + gb) : 0.0);
+    const double xd = a.p0 && live ? a.c * a.p0[s0 + lane] : 0.0;  // X_ik . c x_i(0)
+    const double cs = wave_sum(live ? bk * (2.0 * (xd + vv - u) + gb) : 0.0);
     if (lane == 0) {
       if (a.slab_loss) a.slab_loss[i] = ls;
-      if (a.slab_cons) a.slab_cons[i] = dn + cs;
+      if (a.slab_cons) a.slab_cons[i] = dn + cs + (a.d0 ? a.c * a.c * a.d0[i] : 0.0);
     }
   }
   if ((mode & 2) && live) {
@@ -369,7 +383,8 @@ __global__ __launch_bounds__(NT) void k_rs_rows(const RsArgs a, int mode) {
 
 // k_rs_cols: C = sum_g cpart[g] (fixed order; or the all-reduced sums a.csum), then
 // xbar' = (a1 + q) xbar - (eta / N) C, Z' = a1 xbar + q Z, the T copy of xbar' for the next
-// pass and the metrics, and per-block partials of ||Z' - xbar'||^2.
+// pass and the metrics, and per-block partials of ||D'||^2, D' = Z' - xbar' (+ q c xbar0 for
+// unequal starts).
 template <typename T>
 __global__ __launch_bounds__(NT) void k_rs_cols(const RsArgs a) {
   __shared__ double red[2 * NW];
@@ -390,7 +405,8 @@ __global__ __launch_bounds__(NT) void k_rs_cols(const RsArgs a) {
     a.rZ[e] = zn;
     const T xt = (T)xn;
     ((T*)a.xbar_out)[e] = xt;
-    dd = (zn - xn) * (zn - xn);
+    const double dn = a.xbar0 ? (a.q * a.c) * a.xbar0[e] + (zn - xn) : zn - xn;  // D' = c' xbar0 + Z' - xbar'
+    dd = dn * dn;
     xx = (double)xt * (double)xt;
   }
   dd = wave_sum(dd);
@@ -607,7 +623,8 @@ __global__ __launch_bounds__(NT) void k_rs_gram_fold(const RsArgs a, const doubl
   }
 }
 
-// x_i = Z + X_i^T beta_i for every worker (T; rows stored as XT), chunk-strided over column groups.
+// x_i = Z + X_i^T beta_i (+ c x_i(0): unequal starts) for every worker (T; rows stored as XT),
+// chunk-strided over column groups.
 template <typename T, typename XT>
 __device__ __forceinline__ void rs_materialise_body(const RsArgs& a, T* xout) {
   using V = typename VT<XT>::v;
@@ -623,6 +640,10 @@ __device__ __forceinline__ void rs_materialise_body(const RsArgs& a, T* xout) {
     double s[VN];
 #pragma unroll
     for (int e = 0; e < VN; ++e) s[e] = a.rZ[(int64_t)c * VN + e];
+    if (a.x0) {  // unequal starts: + c x_i(0)
+#pragma unroll
+      for (int e = 0; e < VN; ++e) s[e] += a.c * (double)((const T*)a.x0)[(int64_t)i * a.ld + (int64_t)c * VN + e];
+    }
     for (int k = 0; k < m; ++k) {
       const V r = rs_ld_nt<XT>((const XT*)a.X + xa.at(row0 + k, c));
 #pragma unroll
@@ -654,6 +675,90 @@ __global__ __launch_bounds__(NT) void k_rs_materialise(const RsArgs a, T* xout) 
 
 __global__ __launch_bounds__(NT) void k_rs_materialise_x32(const RsArgs a, double* xout) {
   rs_materialise_body<double, float>(a, xout);
+}
+
+// ---------------------------------------------------------------------------- unequal starts
+// xbar0 = mean_i x_i (float64, workers in order; its T copy), Z = 0, xbar = xbar0, ||D||^2
+// partials 0 and ||xbar||^2 partials (as T) -- the state of k_rs_init for starts that differ.
+template <typename T>
+__global__ __launch_bounds__(NT) void k_rs_x0_mean(const RsArgs a, const T* __restrict__ x, int n, double* xbar0) {
+  __shared__ double red[NW];
+  const int64_t e = (int64_t)blockIdx.x * NT + threadIdx.x;
+  double xx = 0.0;
+  if (e < a.ld) {
+    double s = 0.0;
+    for (int i = 0; i < n; ++i) s += (double)x[(int64_t)i * a.ld + e];
+    const double xb = s / (double)n;
+    xbar0[e] = xb;
+    a.rxbar[e] = xb;
+    a.rZ[e] = 0.0;
+    const T xt = (T)xb;
+    ((T*)a.xbar_out)[e] = xt;
+    xx = (double)xt * (double)xt;
+  }
+  xx = wave_sum(xx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = xx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    a.dpart[blockIdx.x] = 0.0;
+    a.dpart[a.nd + blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+  }
+}
+
+// d0[i] = ||x_i - xbar0||^2 (thread-strided, then waves in order)
+template <typename T>
+__global__ __launch_bounds__(NT) void k_rs_x0_dev(const RsArgs a, const T* __restrict__ x, const double* xbar0,
+                                                   double* d0) {
+  __shared__ double red[NW];
+  const int i = blockIdx.x;
+  double s = 0.0;
+  for (int64_t e = threadIdx.x; e < a.ld; e += NT) {
+    const double t = (double)x[(int64_t)i * a.ld + e] - xbar0[e];
+    s += t * t;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) d0[i] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// Partial row dots X_ik . x_i over column range g of G (16-byte data chunks strided over the
+// workgroup's threads, each row's partial reduced in wave then wave order): gpart[(i * bcap + k)
+// * G + g].  XT: row storage, T: iterate type.
+template <typename T, typename XT>
+__global__ __launch_bounds__(NT) void k_rs_x0_dots(const RsArgs a, const T* __restrict__ x, double* gpart, int G) {
+  using VX = typename VT<XT>::v;
+  constexpr int VN = VT<XT>::n;
+  __shared__ double red[NW];
+  const int i = blockIdx.x, g = blockIdx.y;
+  const int64_t row0 = a.off[i];
+  const int m = (int)(a.off[i + 1] - row0);
+  const XAddr<VN> xa(a.tiled ? a.rows : 0, a.ld);
+  const int64_t c0 = (int64_t)a.nch * g / G, c1 = (int64_t)a.nch * (g + 1) / G;
+  const T* xi = x + (int64_t)i * a.ld;
+  for (int k = 0; k < m; ++k) {
+    double s = 0.0;
+    for (int64_t c = c0 + threadIdx.x; c < c1; c += NT) {
+      const VX r = rs_ld_nt<XT>((const XT*)a.X + xa.at(row0 + k, c));
+#pragma unroll
+      for (int e = 0; e < VN; ++e) s += (double)r[e] * (double)xi[c * VN + e];
+    }
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) gpart[((int64_t)i * a.bcap + k) * G + g] = ((red[0] + red[1]) + red[2]) + red[3];
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(64) void k_rs_x0_fold(const RsArgs a, const double* gpart, int G, double* p0) {
+  const int i = blockIdx.x, k = threadIdx.x;
+  const int m = (int)(a.off[i + 1] - a.off[i]);
+  if (k >= a.bcap) return;
+  double s = 0.0;
+  if (k < m)
+    for (int g = 0; g < G; ++g) s += gpart[((int64_t)i * a.bcap + k) * G + g];
+  p0[(int64_t)i * a.bcap + k] = s;
 }
 
 // ---------------------------------------------------------------------------- launchers
@@ -779,6 +884,29 @@ hipError_t launch_rs_gram(int xdtype, const RsArgs& a, int n_workers, int max_m,
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_rs_gram_fold, dim3(n_workers), dim3(NT), 0, s, a, (const double*)gpart, G, P);
+  return hipGetLastError();
+}
+
+hipError_t launch_rs_x0(int dtype, int xdtype, const RsArgs& a, int n_workers, const void* x, double* xbar0,
+                        double* d0, double* p0, double* gpart, int G, hipStream_t s) {
+  if (n_workers <= 0 || a.bcap > 64) return hipErrorInvalidValue;
+  const dim3 gc(rs_col_blocks(a.ld)), gd(n_workers, G);
+  if (dtype == 0 && xdtype == 0) {
+    hipLaunchKernelGGL((k_rs_x0_mean<float>), gc, dim3(NT), 0, s, a, (const float*)x, n_workers, xbar0);
+    hipLaunchKernelGGL((k_rs_x0_dev<float>), dim3(n_workers), dim3(NT), 0, s, a, (const float*)x, (const double*)xbar0, d0);
+    hipLaunchKernelGGL((k_rs_x0_dots<float, float>), gd, dim3(NT), 0, s, a, (const float*)x, gpart, G);
+  } else if (dtype == 1 && xdtype == 0) {
+    hipLaunchKernelGGL((k_rs_x0_mean<double>), gc, dim3(NT), 0, s, a, (const double*)x, n_workers, xbar0);
+    hipLaunchKernelGGL((k_rs_x0_dev<double>), dim3(n_workers), dim3(NT), 0, s, a, (const double*)x, (const double*)xbar0, d0);
+    hipLaunchKernelGGL((k_rs_x0_dots<double, float>), gd, dim3(NT), 0, s, a, (const double*)x, gpart, G);
+  } else if (dtype == 1 && xdtype == 1) {
+    hipLaunchKernelGGL((k_rs_x0_mean<double>), gc, dim3(NT), 0, s, a, (const double*)x, n_workers, xbar0);
+    hipLaunchKernelGGL((k_rs_x0_dev<double>), dim3(n_workers), dim3(NT), 0, s, a, (const double*)x, (const double*)xbar0, d0);
+    hipLaunchKernelGGL((k_rs_x0_dots<double, double>), gd, dim3(NT), 0, s, a, (const double*)x, gpart, G);
+  } else {
+    return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(k_rs_x0_fold, dim3(n_workers), dim3(64), 0, s, a, (const double*)gpart, G, p0);
   return hipGetLastError();
 }
 

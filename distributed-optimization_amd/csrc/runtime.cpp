@@ -208,6 +208,13 @@ struct dopt_ctx {
   bool rs_live = false;
   bool rs_xs_valid = false;
   bool rs_gram_ok = false;
+  // unequal starting iterates: x_i = rs_c x_i(0) + Z + X_i^T beta_i, x(0) kept in rs_x0buf and
+  // its mean / deviations / row dots in rs_x0d (rs_x0 false: starts that were all equal, rs_c = 0)
+  bool rs_x0 = false;
+  double rs_c = 0.0;
+  void* rs_x0buf = nullptr;
+  size_t rs_x0buf_bytes = 0;
+  double* rs_x0d = nullptr;
   bool wdiag_uniform = false;  // complete-graph mixing with one W_ii for every worker
   double wdiag_u = 0.0;
   int64_t min_m = 0;           // smallest shard
@@ -805,6 +812,13 @@ RsArgs rs_args(dopt_ctx* c) {
   a.nd = c->rs_nd;
   a.rZ = c->rs_Z;
   a.rxbar = c->rs_Z ? c->rs_Z + c->ld : nullptr;
+  if (c->rs_x0) {
+    a.c = c->rs_c;
+    a.xbar0 = c->rs_x0d;
+    a.d0 = c->rs_x0d + c->ld;
+    a.p0 = c->rs_x0d + c->ld + c->n;
+    a.x0 = c->rs_x0buf;
+  }
   return a;
 }
 
@@ -862,6 +876,7 @@ int rs_end(dopt_ctx* c) {
   if ((rc = rs_sync(c))) return rc;
   if (c->rs_live) c->carry_pending = false;
   c->rs_live = false;
+  c->rs_x0 = false;
   return DOPT_OK;
 }
 
@@ -918,13 +933,17 @@ void rs_round_args(dopt_ctx* c, RsArgs& a, int64_t t, double eta0, double lam_gr
   a.eta_n = eta / N;
 }
 
-// Start row-space mode from xs[cur]: RS_FALLBACK when the iterates are not all equal.
-int rs_begin(dopt_ctx* c) {
+// Start row-space mode from xs[cur].  Iterates that are not all equal (allow_unequal: one
+// context) are kept as x(0) with x_i = c x_i(0) + Z + X_i^T beta_i, c = 1 now and q times itself
+// every round; RS_FALLBACK when they differ and that is not allowed.
+int rs_begin(dopt_ctx* c, bool allow_unequal) {
   int rc;
   bool equal = false, zero = false;
   if ((rc = rs_check(c, &equal, &zero, nullptr))) return rc;
-  if (!equal) return RS_FALLBACK;
+  if (!equal && !allow_unequal) return RS_FALLBACK;
   const int dt = c->dtype == DOPT_F32 ? 0 : 1;
+  c->rs_x0 = false;
+  c->rs_c = 0.0;
   RsArgs a = rs_args(c);
   if (!c->rs_gram_ok) {
     const int64_t P = c->rs_bcap * (c->rs_bcap + 1) / 2;
@@ -940,6 +959,31 @@ int rs_begin(dopt_ctx* c) {
     c->rs_gram_ok = true;
   }
   a.xbar_out = c->xbar[c->xb];
+  if (!equal) {  // keep x(0); its mean, deviations and row dots; Z = 0, xbar = xbar0
+    const size_t xb = (size_t)c->n * c->ld * c->esz;
+    if (c->rs_x0buf_bytes < xb) {  // (dalloc frees the previous buffer)
+      c->rs_x0buf_bytes = 0;
+      if ((rc = dalloc(&c->rs_x0buf, xb))) return rc;
+      c->rs_x0buf_bytes = xb;
+    }
+    if ((rc = dalloc_t(&c->rs_x0d, ((size_t)c->ld + c->n + (size_t)c->n * c->rs_bcap) * sizeof(double)))) return rc;
+    HIPOK(hipMemcpyAsync(c->rs_x0buf, c->xs[c->cur], xb, hipMemcpyDeviceToDevice, c->stream));
+    const int G = (int)std::max<int64_t>(1, std::min<int64_t>((c->nch + 1023) / 1024, (16384 + c->n - 1) / c->n));
+    double* gpart = nullptr;
+    if ((rc = dalloc_t(&gpart, (size_t)c->n * c->rs_bcap * G * sizeof(double)))) return rc;
+    hipError_t e = launch_rs_x0(dt, rs_xdt(c), a, (int)c->n, c->xs[c->cur], c->rs_x0d, c->rs_x0d + c->ld,
+                                c->rs_x0d + c->ld + c->n, gpart, G, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dfree_t(gpart);
+    if (e != hipSuccess) return fail(DOPT_ERR_HIP, "row-space start from unequal iterates: %s", hipGetErrorString(e));
+    c->rs_x0 = true;
+    c->rs_c = 1.0;
+    a = rs_args(c);
+    HIPOK(launch_rs_rows(dt, a, (int)c->n, 16 | 8, c->stream));  // z = X_i . x_i(0), v = beta = 0
+    c->rs_live = true;
+    c->rs_xs_valid = true;  // xs[cur] is x(0) itself
+    return DOPT_OK;
+  }
   HIPOK(launch_rs_init(dt, a, c->xs[c->cur], c->stream));  // Z = xbar = x_0, ||D||^2 = 0
   if (zero) {
     HIPOK(launch_rs_rows(dt, a, (int)c->n, 4 | 8, c->stream));  // z = v = 0
@@ -963,7 +1007,7 @@ int run_dsgd_rs(dopt_ctx* c, int64_t t0, int64_t T, double eta0, double lam_grad
   const bool metrics = want_obj || want_cons;
   if (!c->rs_live) {
     if (carry_in) return RS_FALLBACK;
-    if ((rc = rs_begin(c))) return rc;
+    if ((rc = rs_begin(c, true))) return rc;
   }
   const int dt = c->dtype == DOPT_F32 ? 0 : 1;
   const int64_t lag = carry_in ? 1 : 0;
@@ -985,6 +1029,7 @@ int run_dsgd_rs(dopt_ctx* c, int64_t t0, int64_t T, double eta0, double lam_grad
     HIPOK(launch_rs_cols(dt, a, c->stream));
     HIPOK(launch_stamp(c->stamps + h + 1, c->stream));
     xb ^= 1;
+    c->rs_c *= a.q;  // the x(0) coefficient of x_{t+1} (0 stays 0)
     c->rs_xs_valid = false;
   }
   int64_t nh = T + lag;
@@ -1136,7 +1181,9 @@ int dopt_destroy(dopt_ctx* c) {
   dfree_t(c->cpart);
   dfree_t(c->send_ids);
   dfree_t(c->stamps);
-  for (double** p : {&c->rs_coef, &c->rs_up, &c->rs_cp, &c->rs_z, &c->rs_gram, &c->rs_dpart, &c->rs_Z}) dfree_t(*p);
+  for (double** p : {&c->rs_coef, &c->rs_up, &c->rs_cp, &c->rs_z, &c->rs_gram, &c->rs_dpart, &c->rs_Z, &c->rs_x0d})
+    dfree_t(*p);
+  dfree(c->rs_x0buf);
   dfree_t(c->rs_grow);
   dfree_t(c->rs_flags);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
@@ -2172,7 +2219,7 @@ int dopt_rs_phase_begin(dopt_ctx* c, int commit, int* ok, uint64_t* hash) {
   if (!equal) return DOPT_OK;
   *ok = 1;
   if (!commit) return DOPT_OK;
-  return rs_begin(c) == RS_FALLBACK ? fail(DOPT_ERR_STATE, "row-space begin: iterates changed") : DOPT_OK;
+  return rs_begin(c, false) == RS_FALLBACK ? fail(DOPT_ERR_STATE, "row-space begin: iterates changed") : DOPT_OK;
 }
 
 int dopt_rs_phase_round(dopt_ctx* c, int64_t t, double eta0, double lam_grad, uint32_t metric_flags,

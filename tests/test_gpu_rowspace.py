@@ -2,7 +2,8 @@
 iterates that start equal -- x_i = Z + X_i^T beta_i, one read-only pass over the rows per
 round.  Pinned to the oracle (trainer.py:161-193 restated, float64, rtol 1e-9) and to the
 direct column-blocked rounds (DOPT_ROWSPACE=0) on the same data; chains and materialisation
-mid-chain equal one run bitwise; unequal starting iterates fall back to the direct rounds."""
+mid-chain equal one run bitwise; iterates that start unequal keep their start as a term of its own
+(x_i = c x_i(0) + Z + X_i^T beta_i)."""
 import numpy as np
 import pytest
 
@@ -84,23 +85,61 @@ def test_rowspace_vs_direct_rounds(dtype, d, monkeypatch):
     eng.close()
 
 
-def test_rowspace_unequal_start_falls_back(monkeypatch):
-    """Iterates that do not all start equal cannot be written Z + X_i^T beta_i: the direct
-    rounds run (bitwise the DOPT_ROWSPACE=0 result)."""
-    n, m, d, T = 9, 12, 2100, 4
-    shards = _data([m] * n, d, 6)
-    eng = _engine(shards)
-    x0 = np.random.default_rng(2).standard_normal((n, d)) * 0.01
-    res = []
+@pytest.mark.parametrize("problem", ["quadratic", "logistic"])
+@pytest.mark.parametrize("dtype", ["float64", "float64/x32"])
+def test_rowspace_unequal_starts(problem, dtype, monkeypatch):
+    """Iterates that do NOT start equal (a checkpoint, a user's x_0): the row-space rounds keep
+    x_i = c x_i(0) + Z + X_i^T beta_i (c = 1, then q times itself each round) --
+    history and iterates equal the oracle's (rtol 1e-9) and the direct column-blocked rounds'
+    (DOPT_ROWSPACE=0), a chain with a mid-chain materialisation equals one run bitwise, and
+    'float64/x32' (float32 rows, float64 arithmetic) the float64-row rounds (rtol 1e-12)."""
+    sizes, d, T = [12, 5, 12, 9, 12, 1, 12, 7, 12], 2100, 6
+    n = len(sizes)
+    shards = _data(sizes, d, 6, problem, scale=d ** -0.5)
+    if dtype == "float64/x32":
+        shards = [(X.astype(np.float32).astype(np.float64), y.astype(np.float32).astype(np.float64))
+                  for X, y in shards]
+    x0 = np.random.default_rng(2).standard_normal((n, d)) * 0.3
+    b = max(sizes)
+    lam_g = 2e-3 if problem == "quadratic" else 1e-3
+    eng = _engine(shards, problem=problem, data_dtype="float32" if dtype == "float64/x32" else None)
+    res = {}
     for knob in ("1", "0"):
         monkeypatch.setenv("DOPT_ROWSPACE", knob)
         eng.set_models(x0)
-        obj, cons, _ = eng.run_dsgd(T, 0.05, m, 2e-3, 2e-3, 0.0)
-        res.append((np.asarray(obj), np.asarray(cons), eng.get_models()))
-        assert "k_split_step" in _dopt.last_round_kernel()
-    for a, b in zip(*res):
-        assert np.array_equal(a, b)
+        obj, cons, _ = eng.run_dsgd(T, 0.05, b, lam_g, 1e-3, 0.1)
+        res[knob] = (np.asarray(obj), np.asarray(cons), eng.get_models(), _dopt.last_round_kernel())
+    assert "k_rs_pass" in res["1"][3] and "k_split_step" in res["0"][3]
+    Xf = np.vstack([s[0] for s in shards])
+    yf = np.concatenate([s[1] for s in shards])
+    h, _, xr, _ = O.run_decentralized(shards, TP.fully_connected(n).dense_W(), T, _cfg(b, problem), Xf, yf, 0.1,
+                                      x0=x0)
+    np.testing.assert_allclose(res["1"][0], h["objective"], rtol=1e-9)
+    np.testing.assert_allclose(res["1"][1], h["consensus_error"], rtol=1e-9)
+    np.testing.assert_allclose(res["1"][2], xr, rtol=1e-9, atol=1e-12 * np.abs(xr).max())
+    for u, v in zip(res["1"][:3], res["0"][:3]):
+        np.testing.assert_allclose(u, v, rtol=1e-9, atol=1e-12 * np.abs(v).max())
+    # a pipelined chain from the same start, materialised mid-chain: bitwise the one run
+    monkeypatch.setenv("DOPT_ROWSPACE", "1")
+    eng.set_models(x0)
+    objs, conss, t0 = [], [], 0
+    for k in (2, 3, 1, 0):
+        o, c = eng.run_dsgd_pipelined(k, 0.05, b, lam_g, 1e-3, 0.1, t0=t0)
+        objs.append(o)
+        conss.append(c)
+        t0 += k
+        if k == 3:
+            eng.get_models()
+    assert np.array_equal(np.concatenate(objs), res["1"][0]) and np.array_equal(np.concatenate(conss), res["1"][1])
+    assert np.array_equal(eng.get_models(), res["1"][2])
     eng.close()
+    if dtype == "float64/x32":  # the float64-row engine on the same (float32-exact) data
+        e64 = _engine(shards, problem=problem)
+        e64.set_models(x0)
+        o64, c64, _ = e64.run_dsgd(T, 0.05, b, lam_g, 1e-3, 0.1)
+        for u, v in zip(res["1"][:3], (o64, c64, e64.get_models())):
+            np.testing.assert_allclose(u, v, rtol=1e-12, atol=1e-15 * np.abs(v).max())
+        e64.close()
 
 
 def test_rowspace_chain_and_midchain_models_equal_one_run():
@@ -417,12 +456,13 @@ def test_rowspace_x32_float32_rows_float64_arithmetic(problem):
     np.testing.assert_allclose(out["float32"][2], xr, rtol=1e-9, atol=1e-12 * np.abs(xr).max())
 
 
-def test_rowspace_x32_direct_rounds_from_unequal_starts():
+def test_rowspace_x32_direct_rounds_from_unequal_starts(monkeypatch):
     """Float32 rows under float64 arithmetic past the row-resident kernel, from iterates that are
-    NOT all equal (the row-space rounds do not apply): the direct column-blocked kernels read the
-    float32 rows themselves (k_split_step<double, float, ...>) and give the float64-row rounds'
-    history and iterates (rtol 1e-12, sums in the same order) -- VERDICT r2 item 7.  From equal
-    starts the same context takes the row-space rounds again."""
+    NOT all equal, through the DIRECT column-blocked kernels (DOPT_ROWSPACE=0; the path of sparse
+    graphs at such d): they read the float32 rows themselves (k_split_step<double, float, ...>) and
+    give the float64-row rounds' history and iterates (rtol 1e-12, sums in the same order) --
+    VERDICT r2 item 7.  With the row-space rounds back on, the same context takes them."""
+    monkeypatch.setenv("DOPT_ROWSPACE", "0")
     sizes, d = [8] * 5, 2100
     shards = [(X.astype(np.float32).astype(np.float64), y.astype(np.float32).astype(np.float64))
               for X, y in _data(sizes, d, 43, scale=d ** -0.5)]
@@ -434,9 +474,11 @@ def test_rowspace_x32_direct_rounds_from_unequal_starts():
         obj, cons, _ = eng.run_dsgd(4, 0.05, 8, 2e-3, 1e-3, 0.0)
         out[xdt] = (np.asarray(obj), np.asarray(cons), eng.get_models(), _dopt.last_round_kernel())
         if xdt == "float32":
+            monkeypatch.setenv("DOPT_ROWSPACE", "1")
             eng.set_models(np.zeros((len(sizes), d)))
             eng.run_dsgd(2, 0.05, 8, 2e-3, 1e-3, 0.0)
             assert "k_rs_pass_x32" in _dopt.last_round_kernel()
+            monkeypatch.setenv("DOPT_ROWSPACE", "0")
         eng.close()
     assert out["float32"][3].startswith("void dopt::k_split_step<double, float,"), out["float32"][3]
     assert out[None][3].startswith("void dopt::k_split_step<double, double,"), out[None][3]
