@@ -162,6 +162,10 @@ hipError_t launch_rs_check(int dtype, const void* x, int64_t n, int64_t ld, int3
 hipError_t launch_rs_gram(int xdtype, const RsArgs& a, int n_workers, int max_m, double* gpart, int G,
                           hipStream_t s);
 hipError_t launch_rs_materialise(int dtype, int xdtype, const RsArgs& a, int n_workers, void* xout, hipStream_t s);
+// Minibatch row weights of a round: the host indices idx ([n x b] local rows) or, idx == null,
+// the device sampler's draw (seed, round, wid0 + i); coef = c(z) / min(b, m_i) on the batch rows.
+hipError_t launch_rs_coef(const RsArgs& a, int n_workers, const int32_t* idx, int64_t b, uint64_t seed, int64_t round,
+                          int64_t wid0, hipStream_t s);
 // Unequal starting iterates x (T, [n x ld]): xbar0 = their mean (float64; xbar_out its T copy),
 // d0[i] = ||x_i - xbar0||^2, p0[i][k] = X_ik . x_i (partials over G column ranges in gpart, folded in
 // order), then the row-space state of such a start: Z = 0, xbar = xbar0, ||D||^2 partials 0.

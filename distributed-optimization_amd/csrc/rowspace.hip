@@ -677,6 +677,37 @@ __global__ __launch_bounds__(NT) void k_rs_materialise_x32(const RsArgs a, doubl
   rs_materialise_body<double, float>(a, xout);
 }
 
+// ---------------------------------------------------------------------------- minibatches
+// The pass's row weights for a round whose gradients take a minibatch (b < m_i rows, or host
+// indices): coef_k = c(z_k) / nb_i on the batch rows, 0 elsewhere (obj_problems.py:16-17 / 49-50
+// over X_b; nb_i = min(b, m_i), worker.py:21).  The batch is the round's host indices (idx: local
+// row ids, [n x b]) or the device sampler's Floyd subset of (seed, round, wid0 + i) -- the same
+// draw the direct kernels take.  One 64-lane workgroup per worker (m_i <= 64).
+__global__ __launch_bounds__(64) void k_rs_coef(const RsArgs a, const int32_t* idx, int64_t b, uint64_t seed,
+                                                int64_t round, int64_t wid0) {
+  __shared__ unsigned char mk[64];
+  const int i = blockIdx.x, k = threadIdx.x;
+  const int64_t row0 = a.off[i];
+  const int m = (int)(a.off[i + 1] - row0);
+  const int64_t nb = b < m ? b : m;
+  mk[k] = 0;
+  __syncthreads();
+  if (idx) {
+    if (k < nb) mk[idx[(int64_t)i * b + k]] = 1;
+  } else if (k == 0 && nb > 0) {
+    floyd_sample(mk, m, nb, seed, round, wid0 + i);
+  }
+  __syncthreads();
+  if (k >= m) return;
+  double w = 0.0;
+  if (mk[k]) {
+    const double z = a.z[(int64_t)i * a.bcap + k];
+    const double yv = a.y_is_f32 ? (double)((const float*)a.y)[row0 + k] : ((const double*)a.y)[row0 + k];
+    w = (a.problem == 0 ? -yv / (1.0 + exp(yv * z)) : z - yv) / (double)nb;
+  }
+  a.coef_row[row0 + k] = w;
+}
+
 // ---------------------------------------------------------------------------- unequal starts
 // xbar0 = mean_i x_i (float64, workers in order; its T copy), Z = 0, xbar = xbar0, ||D||^2
 // partials 0 and ||xbar||^2 partials (as T) -- the state of k_rs_init for starts that differ.
@@ -884,6 +915,14 @@ hipError_t launch_rs_gram(int xdtype, const RsArgs& a, int n_workers, int max_m,
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_rs_gram_fold, dim3(n_workers), dim3(NT), 0, s, a, (const double*)gpart, G, P);
+  return hipGetLastError();
+}
+
+hipError_t launch_rs_coef(const RsArgs& a, int n_workers, const int32_t* idx, int64_t b, uint64_t seed, int64_t round,
+                          int64_t wid0, hipStream_t s) {
+  if (n_workers <= 0) return hipSuccess;
+  if (a.bcap > 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_rs_coef, dim3(n_workers), dim3(64), 0, s, a, idx, b, seed, round, wid0);
   return hipGetLastError();
 }
 

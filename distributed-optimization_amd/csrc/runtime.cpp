@@ -774,9 +774,12 @@ bool rs_enabled() {
   return !(v && v[0] == '0');
 }
 
+// Minibatches (round 3): host indices, or batch < m with the device sampler -- the pass's row
+// weights come from k_rs_coef each round (zero off the batch).
 bool rs_eligible(dopt_ctx* c, int64_t batch, const int32_t* idx) {
-  return rs_enabled() && c->split && c->mean_mix && c->wdiag_uniform && !idx && batch >= c->max_m && !c->obj_sep && c->min_m >= 1 && c->max_m <= kRsMaxRows &&
-         c->n_global == 0 && !c->S_ext;
+  const bool batch_ok = idx || batch >= c->max_m || c->sampler == DOPT_SAMPLE_DEVICE;
+  return rs_enabled() && c->split && c->mean_mix && c->wdiag_uniform && batch_ok && !c->obj_sep && c->min_m >= 1 &&
+         c->max_m <= kRsMaxRows && c->n_global == 0 && !c->S_ext;
 }
 
 // Row storage for the row-space launchers (0 float32, 1 float64).
@@ -999,9 +1002,9 @@ int rs_begin(dopt_ctx* c, bool allow_unequal) {
 
 // D-SGD rounds in row-space mode; the history / carry contract of run_dsgd_split.
 // RS_FALLBACK: not applicable here (unequal starting iterates, or a direct chain is open).
-int run_dsgd_rs(dopt_ctx* c, int64_t t0, int64_t T, double eta0, double lam_grad, double lam_obj, double f_opt,
-                uint32_t flags, double* obj_out, double* cons_out, double* time_out, bool carry_in, bool pipelined,
-                int64_t* nh_out) {
+int run_dsgd_rs(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch, const int32_t* idx, int64_t CH,
+                double lam_grad, double lam_obj, double f_opt, uint32_t flags, double* obj_out, double* cons_out,
+                double* time_out, bool carry_in, bool pipelined, int64_t* nh_out) {
   int rc;
   const bool want_obj = flags & DOPT_RUN_OBJECTIVE, want_cons = flags & DOPT_RUN_CONSENSUS;
   const bool metrics = want_obj || want_cons;
@@ -1011,6 +1014,7 @@ int run_dsgd_rs(dopt_ctx* c, int64_t t0, int64_t T, double eta0, double lam_grad
   }
   const int dt = c->dtype == DOPT_F32 ? 0 : 1;
   const int64_t lag = carry_in ? 1 : 0;
+  const bool minibatch = idx || batch < c->max_m;
   int& xb = c->xb;
   HIPOK(launch_stamp(c->stamps, c->stream));
   for (int64_t h = 0; h < T; ++h) {
@@ -1020,6 +1024,11 @@ int run_dsgd_rs(dopt_ctx* c, int64_t t0, int64_t T, double eta0, double lam_grad
     const bool met = metrics && (h > 0 || lag);
     a.slab_cons = want_cons ? c->slab_cons : nullptr;
     a.slab_loss = want_obj ? c->slab_loss : nullptr;
+    if (minibatch) {  // this round's row weights: c(z) / nb on its batch rows
+      if (idx && h % CH == 0 && (rc = upload_idx_chunk(c, idx, h, std::min(CH, T - h), batch))) return rc;
+      HIPOK(launch_rs_coef(a, (int)c->n, idx ? c->idx + (h % CH) * c->n * batch : nullptr, batch, c->sample_seed,
+                           t0 + h, c->sample_wid0, c->stream));
+    }
     if (c->prof && (rc = prof_event(c, false))) return rc;
     HIPOK(launch_rs_pass(dt, rs_xdt(c), true, a, c->stream));
     if (c->prof && (rc = prof_event(c, true))) return rc;
@@ -1077,9 +1086,9 @@ int check_run(dopt_ctx* c, int64_t T, int64_t batch, const int32_t* idx, bool ne
     if (c->sampler != DOPT_SAMPLE_DEVICE)
       return fail(DOPT_ERR_INVALID, "idx == NULL needs full-shard batches (batch %lld < shard %lld) or the "
                   "device sampler", (long long)batch, (long long)c->max_m);
-    if (c->split || c->max_m > kMaxBipRows)
-      return fail(DOPT_ERR_UNSUPPORTED, "device sampling: row-resident contexts with shards of at most %lld rows",
-                  (long long)kMaxBipRows);
+    if ((c->split || c->max_m > kMaxBipRows) && !(c->split && rs_eligible(c, batch, nullptr)))
+      return fail(DOPT_ERR_UNSUPPORTED, "device sampling: row-resident contexts with shards of at most %lld rows, "
+                  "or the complete graph's row-space rounds", (long long)kMaxBipRows);
   }
   return DOPT_OK;
 }
@@ -1468,8 +1477,8 @@ static int run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t bat
   if (c->split) {  // the column-blocked rounds pipeline the same way (full-shard batches)
     if (rs_eligible(c, batch, idx)) {  // complete graph, quadratic: row-space rounds
       int64_t nh = 0;
-      rc = run_dsgd_rs(c, t0, T, eta0, lam_grad, lam_obj, f_opt, flags, obj_out, cons_out, time_out, carry_in,
-                       pipelined, &nh);
+      rc = run_dsgd_rs(c, t0, T, eta0, batch, idx, CH, lam_grad, lam_obj, f_opt, flags, obj_out, cons_out, time_out,
+                       carry_in, pipelined, &nh);
       if (rc != RS_FALLBACK) {
         if (rc) return rc;
         if (n_out) *n_out = nh;
@@ -1480,6 +1489,8 @@ static int run_dsgd(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t bat
         return fail(DOPT_ERR_INVALID, "pipelined run: the pending metrics belong to a row-space chain");
       if ((rc = rs_end(c))) return rc;
     }
+    if (!idx && batch < c->max_m)  // (the device sampler reaches here only past the row-space rounds)
+      return fail(DOPT_ERR_UNSUPPORTED, "device sampling on long rows: the complete graph's row-space rounds only");
     const bool sfused = batch >= c->max_m && !c->obj_sep && metrics;
     if (carry_in && !sfused) return fail(DOPT_ERR_INVALID, "pipelined run: the pending metrics need a fused run");
     int64_t nh = 0;

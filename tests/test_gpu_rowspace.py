@@ -142,6 +142,68 @@ def test_rowspace_unequal_starts(problem, dtype, monkeypatch):
         e64.close()
 
 
+@pytest.mark.parametrize("problem", ["quadratic", "logistic"])
+@pytest.mark.parametrize("sampler,start", [("host", "zero"), ("device", "zero"), ("host", "unequal")])
+def test_rowspace_minibatches(problem, sampler, start, monkeypatch):
+    """Minibatches (b < m) in the row-space rounds: each round's row weights are c(z) / nb on the
+    batch rows and 0 elsewhere (k_rs_coef; obj_problems.py:16-17 / 49-50 over X_b), the batch
+    being the host indices (the reference's legacy stream: dopt_mt_choice_rounds) or the device
+    sampler's draw.  History and iterates equal the oracle's on the same batches (rtol 1e-9) and,
+    for host indices, the direct column-blocked rounds' (DOPT_ROWSPACE=0); a pipelined chain with a
+    mid-chain materialisation equals one run bitwise."""
+    import device_sampler as DS
+
+    sizes, d, T, b = [12, 5, 12, 9, 12, 3, 12], 2100, 7, 4
+    n = len(sizes)
+    shards = _data(sizes, d, 11, problem, scale=d ** -0.5)
+    lam_g = 2e-3 if problem == "quadratic" else 1e-3
+    x0 = np.random.default_rng(4).standard_normal((n, d)) * 0.2 if start == "unequal" else np.zeros((n, d))
+    eng = _engine(shards, problem=problem)
+    if sampler == "device":
+        eng.set_sampler("device", seed=77)
+        idx = None
+        ind = DS.rounds(77, 0, T, sizes, b)
+    else:
+        np.random.seed(5)
+        idx = _dopt.mt_choice_rounds(T, sizes, b)
+        ind = idx
+    eng.set_models(x0)
+    obj, cons, _ = eng.run_dsgd(T, 0.05, b, lam_g, 1e-3, 0.1, idx=idx)
+    assert "k_rs_pass" in _dopt.last_round_kernel(), _dopt.last_round_kernel()
+    x = eng.get_models()
+    indices = [[ind[t, i, :min(b, m)] for i, m in enumerate(sizes)] for t in range(T)]
+    Xf = np.vstack([s[0] for s in shards])
+    yf = np.concatenate([s[1] for s in shards])
+    h, _, xr, _ = O.run_decentralized(shards, TP.fully_connected(n).dense_W(), T, _cfg(b, problem), Xf, yf, 0.1,
+                                      x0=x0, indices=indices)
+    np.testing.assert_allclose(obj, h["objective"], rtol=1e-9)
+    np.testing.assert_allclose(cons, h["consensus_error"], rtol=1e-9)
+    np.testing.assert_allclose(x, xr, rtol=1e-9, atol=1e-12 * np.abs(xr).max())
+    if sampler == "host":
+        monkeypatch.setenv("DOPT_ROWSPACE", "0")
+        eng.set_models(x0)
+        od, cd, _ = eng.run_dsgd(T, 0.05, b, lam_g, 1e-3, 0.1, idx=idx)
+        assert "k_split_step" in _dopt.last_round_kernel()
+        np.testing.assert_allclose(obj, od, rtol=1e-9)
+        np.testing.assert_allclose(cons, cd, rtol=1e-9)
+        np.testing.assert_allclose(x, eng.get_models(), rtol=1e-9, atol=1e-12 * np.abs(xr).max())
+        monkeypatch.setenv("DOPT_ROWSPACE", "1")
+    eng.set_models(x0)
+    objs, conss, t0 = [], [], 0
+    for k in (3, 1, 3, 0):
+        sub = None if idx is None else idx[t0:t0 + k]
+        o, c = eng.run_dsgd_pipelined(k, 0.05, b, lam_g, 1e-3, 0.1, t0=t0, idx=sub) if k else \
+            eng.run_dsgd_pipelined(0, 0.05, b, lam_g, 1e-3, 0.1, t0=t0)
+        objs.append(o)
+        conss.append(c)
+        t0 += k
+        if k == 1:
+            eng.get_models()
+    assert np.array_equal(np.concatenate(objs), obj) and np.array_equal(np.concatenate(conss), cons)
+    assert np.array_equal(eng.get_models(), x)
+    eng.close()
+
+
 def test_rowspace_chain_and_midchain_models_equal_one_run():
     """Pipelined chains continue the row-space state; get_models mid-chain materialises the
     iterates without ending the chain; plain runs continue from the live state: all bitwise

@@ -47,6 +47,25 @@ def main():
         np.testing.assert_allclose(o_rs, o_d, rtol=1e-9)
         np.testing.assert_allclose(c_rs, c_d, rtol=1e-8)
     print("histories agree (objective rtol 1e-9, consensus 1e-8)")
+    # minibatches of 4 of the 16 rows (the reference's legacy stream, host indices), from zeros
+    b = 4
+    np.random.seed(7)
+    idx = _dopt.mt_choice_rounds(T + 2, [m] * n, b)
+    for rep in range(2):
+        res = {}
+        for knob in ("1", "0"):
+            os.environ["DOPT_ROWSPACE"] = knob
+            eng.zero_models()
+            eng.run_dsgd(2, eta0, b, lam, lam, 0.0, idx=idx[:2])
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            o, c, _ = eng.run_dsgd(T, eta0, b, lam, lam, 0.0, idx=idx[2:], t0=2)
+            res[knob] = ((time.perf_counter() - t0) / T, o, c, _dopt.last_round_kernel())
+        print(f"rep {rep}: b = {b} of {m}: row-space {res['1'][0] * 1e3:.2f} ms per round ({res['1'][3][:40]}), "
+              f"direct {res['0'][0] * 1e3:.2f} ms ({res['0'][3][:40]})", flush=True)
+        np.testing.assert_allclose(res["1"][1], res["0"][1], rtol=1e-9)
+        np.testing.assert_allclose(res["1"][2], res["0"][2], rtol=1e-8)
+    print("minibatch histories agree")
     eng.close()
 
 
