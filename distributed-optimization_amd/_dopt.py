@@ -103,6 +103,7 @@ _SIGS = {
     "dopt_set_profiling": ([_P, ctypes.c_int], ctypes.c_int),
     "dopt_set_sampler": ([_P, ctypes.c_int, ctypes.c_uint64, _I64], ctypes.c_int),
     "dopt_phase_set_round": ([_P, _I64], ctypes.c_int),
+    "dopt_phase_set_step": ([_P, _I64, ctypes.c_double], ctypes.c_int),
 }
 EXPORTED = tuple(_SIGS)
 ABI_VERSION = 2  # DOPT_ABI_VERSION of include/dopt.h
@@ -425,6 +426,9 @@ class Engine:
 
     def phase_set_round(self, t):
         check(lib().dopt_phase_set_round(self._h, int(t)))
+
+    def phase_set_step(self, t, eta0):
+        check(lib().dopt_phase_set_step(self._h, int(t), float(eta0)))
 
     def phase_gather(self):
         check(lib().dopt_phase_gather(self._h))

@@ -77,6 +77,9 @@ struct RoundArgs {
   // sslot[sptr[i] .. sptr[i+1]) (null sptr: no halo plan)
   const int64_t* sptr;
   const int32_t* sslot;
+  // multi-GPU phase path: workers whose CSR row is all local (and who send no row) are mixed and
+  // stepped by the gradient kernel itself (F_STEP per worker; k_mix then skips them), or null
+  const uint8_t* interior;
   void* send;
   // lagged multi-GPU mix: xbar of x_old from the all-reduced column sums xsum / xsum_n, written
   // to xbar_out, and the per-worker consensus ||x_old[i] - xbar||^2 into slab_cons (if non-null)

@@ -1352,6 +1352,9 @@ __global__ __launch_bounds__(NT) void k_mix(const RoundArgs a, const T* __restri
   const int nch = a.nchunks;
   const T eta = (T)a.eta;
   V dv = V(0);  // consensus term of x_old[i] (a.xsum): formed as k_round's F_CONS forms it
+  // a.interior[i]: the gradient kernel mixed and stepped this worker already (no halo row, no
+  // send row): only its consensus term (and xbar) here
+  const bool skip = live && a.interior && a.interior[i];
   if (live) {
   const T* xo = (const T*)a.x_old + (int64_t)i * ld;
   V own[CPL], gc[CPL], acc[CPL];
@@ -1360,10 +1363,11 @@ __global__ __launch_bounds__(NT) void k_mix(const RoundArgs a, const T* __restri
     const int c = c0 + lane + 64 * j;
     const bool in = c < nch;
     own[j] = in ? *(const V*)(xo + (int64_t)c * VN) : V(0);
-    gc[j] = in ? *(const V*)(G + (int64_t)i * ld + (int64_t)c * VN) : V(0);
+    gc[j] = (in && !skip) ? *(const V*)(G + (int64_t)i * ld + (int64_t)c * VN) : V(0);
     acc[j] = V(0);
   }
-  if (a.flags & F_MEAN) {
+  if (skip) {
+  } else if (a.flags & F_MEAN) {
 #pragma unroll
     for (int j = 0; j < CPL; ++j)
       if (c0 + lane + 64 * j < nch) acc[j] = mix_chunk<T, T>(a, i, c0 + lane + 64 * j, own[j]);
@@ -1420,6 +1424,7 @@ __global__ __launch_bounds__(NT) void k_mix(const RoundArgs a, const T* __restri
       const V t = own[j] - xb;
       dv += t * t;
     }
+    if (skip) continue;
     const V xn = acc[j] - eta * gc[j];
     *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = xn;
     for (int64_t q = s0; q < s1; ++q)  // rows peers read next round: the send buffer is refreshed here

@@ -183,6 +183,12 @@ struct dopt_ctx {
   int32_t* send_ids = nullptr;
   int64_t* sptr = nullptr;   // send rows by worker: worker i's row goes to send rows sslot[sptr[i]..sptr[i+1])
   int32_t* sslot = nullptr;
+  std::vector<uint8_t> is_send;  // host: local workers whose row some peer reads
+  uint8_t* interior = nullptr;   // [n] CSR row all local and no send row (phase path: stepped in the gradient kernel)
+  int64_t n_interior = 0;
+  double ph_eta = 0.0;           // dopt_phase_set_step: the step size of the next dopt_phase_grad
+  bool ph_eta_set = false;
+  bool ph_interior = false;      // the last dopt_phase_grad stepped the interior workers
   bool send_fresh = false;   // the last dopt_phase_mix already wrote the current iterates' send rows
 
   // per-run buffers
@@ -1179,6 +1185,7 @@ int dopt_destroy(dopt_ctx* c) {
   dfree_t(c->slab_loss_b);
   dfree_t(c->sptr);
   dfree_t(c->sslot);
+  dfree_t(c->interior);
   dfree_t(c->rp);
   dfree_t(c->ci);
   dfree_t(c->idx);
@@ -1353,6 +1360,19 @@ int dopt_set_topology(dopt_ctx* c, int64_t n_workers, const int64_t* row_ptr, co
   int64_t mx = 0;
   for (int64_t i = 0; i < n_workers; ++i) mx = std::max(mx, row_ptr[i + 1] - row_ptr[i]);
   c->max_row_nnz = (int32_t)std::min<int64_t>(mx, 1 << 30);
+  // rank slices (a halo plan is set): the workers the gradient kernel can mix and step itself
+  c->n_interior = 0;
+  if (c->n_halo > 0 || !c->is_send.empty()) {
+    std::vector<uint8_t> in((size_t)n_workers, 0);
+    for (int64_t i = 0; i < n_workers; ++i) {
+      bool local = (size_t)i >= c->is_send.size() || !c->is_send[(size_t)i];
+      for (int64_t e = row_ptr[i]; e < row_ptr[i + 1] && local; ++e) local = col[e] < n_workers;
+      in[(size_t)i] = local;
+      c->n_interior += local;
+    }
+    if ((rc = dalloc_t(&c->interior, in.size()))) return rc;
+    HIPOK(hipMemcpy(c->interior, in.data(), in.size(), hipMemcpyHostToDevice));
+  }
   c->have_topo = true;
   c->mean_mix = false;
   return DOPT_OK;
@@ -1834,6 +1854,15 @@ int dopt_phase_set_round(dopt_ctx* c, int64_t t) {
   return DOPT_OK;
 }
 
+int dopt_phase_set_step(dopt_ctx* c, int64_t t, double eta0) {
+  CHECK_ARG(c, "ctx is NULL");
+  CHECK_ARG(t >= 0, "round must be >= 0");
+  c->ph_round = t;
+  c->ph_eta = eta0 / sqrt((double)(t + 1));  // trainer.py:138-140
+  c->ph_eta_set = true;
+  return DOPT_OK;
+}
+
 int dopt_set_profiling(dopt_ctx* c, int enable) {
   CHECK_ARG(c, "ctx is NULL");
   CHECK_ARG(enable >= 0, "enable must be >= 0");
@@ -1911,6 +1940,8 @@ int dopt_set_halo(dopt_ctx* c, int64_t n_halo, void* halo_dev, int64_t n_send, v
   std::vector<int32_t> slot((size_t)std::max<int64_t>(1, n_send));
   std::vector<int64_t> fill(sp.begin(), sp.end() - 1);
   for (int64_t k = 0; k < n_send; ++k) slot[(size_t)fill[(size_t)send_ids[k]]++] = (int32_t)k;
+  c->is_send.assign((size_t)c->n, 0);
+  for (int64_t k = 0; k < n_send; ++k) c->is_send[(size_t)send_ids[k]] = 1;
   if ((rc = dalloc_t(&c->sptr, sp.size() * sizeof(int64_t)))) return rc;
   if ((rc = dalloc_t(&c->sslot, slot.size() * sizeof(int32_t)))) return rc;
   HIPOK(hipMemcpy(c->sptr, sp.data(), sp.size() * sizeof(int64_t), hipMemcpyHostToDevice));
@@ -1998,6 +2029,19 @@ int dopt_phase_grad(dopt_ctx* c, int64_t batch, const int32_t* idx, double lam_g
   a.seed = c->sample_seed;
   a.round = c->ph_round;
   a.wid0 = c->sample_wid0;
+  // interior workers: mixed and stepped here (bitwise the fused round's arithmetic; k_mix skips
+  // them), when the round's step size is known (dopt_phase_set_step)
+  static const bool interior_on = [] {  // DOPT_PHASE_INTERIOR=0: every worker through k_mix (A/B runs)
+    const char* v = getenv("DOPT_PHASE_INTERIOR");
+    return !(v && v[0] == '0');
+  }();
+  c->ph_interior = interior_on && c->ph_eta_set && c->have_topo && !c->mean_mix && c->n_interior > 0 && c->interior;
+  c->ph_eta_set = false;
+  if (c->ph_interior) {
+    a.interior = c->interior;
+    a.x_new = c->xs[c->cur ^ 1];
+    a.eta = c->ph_eta;
+  }
   if (a.flags & F_LOSS) c->loss_groups = c->slab_n[0] = c->n;  // per-worker loss slabs
   if (c->prof && (rc = prof_event(c, false))) return rc;
   HIPOK(launch_round(c->dtype, c->xdtype, c->problem, c->cpl, true, cons || loss || dev, a, (int)c->n, c->stream));
@@ -2039,10 +2083,12 @@ int dopt_phase_mix(dopt_ctx* c, int64_t t, double eta0) {
       a.sslot = c->sslot;
       a.send = c->send;
     }
+    if (c->ph_interior) a.interior = c->interior;  // stepped by the gradient kernel already
     a.nchunks = (int32_t)c->nchs;  // k_mix walks state chunks
     HIPOK(launch_mix(c->dtype, c->cpls, a, c->G, (int)c->n, c->stream));
     c->send_fresh = c->n_send > 0;
   }
+  c->ph_interior = false;
   c->cur ^= 1;
   return DOPT_OK;
 }
@@ -2186,6 +2232,8 @@ int dopt_phase_mix_lagged(dopt_ctx* c, int64_t t, double eta0, const double* sum
   a.xsum_n = (double)n_div(c);
   a.xbar_out = c->xbar[c->xb ^ 1];
   a.slab_cons = consensus ? c->slab_cons : nullptr;
+  if (c->ph_interior) a.interior = c->interior;  // stepped by the gradient kernel already
+  c->ph_interior = false;
   if (c->n > 0) {
     a.nchunks = (int32_t)c->nchs;  // k_mix walks state chunks
     HIPOK(launch_mix(c->dtype, c->cpls, a, c->G, (int)c->n, c->stream));

@@ -403,7 +403,7 @@ class DistributedDSGD:
                 if self._peers:
                     eng.phase_gather()
                 pending = self._start_exchange()
-                eng.phase_set_round(t0 + h)
+                eng.phase_set_step(t0 + h, eta0)  # (the gradient kernel steps the interior workers)
                 eng.phase_grad(batch, lam_grad, flags if met else 0, idx=None if idx is None else idx[h])
                 self._finish_exchange(pending)
                 eng.phase_mix(t0 + h, eta0)
@@ -594,7 +594,9 @@ class DistributedDSGD:
                 pending = self._start_exchange()
                 colsum_fold(g)
                 ar = self._all_reduce_start(self.sum)
-                eng.phase_set_round(t0 + h)  # the device sampler's counter (sampling='device')
+                # the device sampler's counter (sampling='device') and the step size: the gradient
+                # kernel mixes and steps the workers whose rows need no halo (the mix skips them)
+                eng.phase_set_step(t0 + h, eta0)
                 # loss at xbar_{g-1} (history[g-2]); at g = 1 it is the loss of x_0, which no history row
                 # holds -- taken anyway so round 1's gradient dots reduce in the same (paired) butterfly
                 # as the fused single-context round 1, whose pass carries the metrics of x_1

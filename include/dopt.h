@@ -256,6 +256,11 @@ int dopt_phase_begin(dopt_ctx *ctx, int64_t batch);
 /* Round index t (trainer.py:138) of the next dopt_phase_grad: the counter of the device
  * sampler (dopt_set_sampler), so every rank draws worker i's minibatch of round t alike. */
 int dopt_phase_set_round(dopt_ctx *ctx, int64_t t);
+/* dopt_phase_set_round plus the round's step size eta0 / sqrt(t + 1) (trainer.py:138-140): the
+ * next dopt_phase_grad then also mixes and steps the workers whose CSR row needs no halo row and
+ * who send no row (rank slices), and the next mix skips them -- the same arithmetic as the fused
+ * round, one pass less over their iterates (round 3; ABI version 2 addition). */
+int dopt_phase_set_step(dopt_ctx *ctx, int64_t t, double eta0);
 /* Rows send_ids of the current iterates -> send.  A no-op when the last dopt_phase_mix
  * already wrote them (the mix kernel refreshes the send rows as it writes the iterates). */
 int dopt_phase_gather(dopt_ctx *ctx);
