@@ -595,6 +595,7 @@ class DecentralizedTrainer:
                                                                  for w in self.workers]))
         iteration_transmission = np.sum(self.degrees) * self.n_features  # trainer.py:169
         eta0 = cfg["learning_rate_eta0"]
+        loop_start = time.perf_counter()
         # chunks run as one pipelined chain (dopt_run_dsgd_pipelined: each chunk's last metrics ride
         # the next chunk's first pass), closed where the history must be complete: at a
         # checkpoint and at the end -- the same values as one run_dsgd over all the rounds
@@ -617,6 +618,9 @@ class DecentralizedTrainer:
                     self.total_floats_transmitted += iteration_transmission
                 if ck.due(t0 + n, T):
                     ck.save(t0 + n, eng.get_models(), rng)
+        # wall time of the round loop alone (the draws, the device rounds, the history), without
+        # the per-run data checks before it; bench.py's drop-in leg reads it
+        self.loop_seconds = time.perf_counter() - loop_start
         models = eng.get_models()
         for i, worker in enumerate(self.workers):  # trainer.py:178-179: row views
             worker.x = models[i, :]
