@@ -1,5 +1,8 @@
-"""Configs C4 and C5 at full size on ONE MI355X (288 GB of HBM holds either).
+"""Configs C3, C4 and C5 at full size on ONE MI355X (288 GB of HBM holds any of them).
 
+C3: the headline benchmark's exact instance (bench.py): 4096 workers, d = 1024, m = b = 512, random
+    4-regular graph, float64 over float32-stored rows, pipelined as the bench times it; every round
+    and the objective over all 2M rows recomputed on the host.
 C4: logistic, N = 65536 workers on the 256 x 256 torus, d = 1024, m = b = 512 -- the
     configuration the reference cannot run (trainer.py:93,118 build dense N x N matrices:
     64 GiB at this N).  Float64 arithmetic over float32-stored exact rows (137 GB of shards).
@@ -37,6 +40,67 @@ def _mix_row(top, x, i):
     for k in range(s, e):  # CSR order, as the kernel sums
         acc = acc + top.w[k] * x[top.col[k]]
     return acc
+
+
+def test_c3_headline_instance_full_size():
+    """C3 exactly as bench.py times it (4096 workers, d = 1024, m = b = 512, the random 4-regular
+    graph of seed 0, the same device-generated shards, float64 arithmetic over float32-stored rows,
+    a pipelined chain from the reference's zero start, worker.py:13): the chain runs the headline
+    kernel instance, and its history equals three one-round calls, each checked on the host --
+    sampled workers' updates (trainer.py:166-175), the consensus over all 4096 iterates
+    (trainer.py:182-186), and the objective at xbar over all 2M rows (trainer.py:188-191) by the
+    oracle's numpy formula, shard by shard."""
+    n, d, m, T, eta0, lam = 4096, 1024, 512, 3, 0.05, 1e-4
+    if _free_gb() < 20:
+        pytest.skip("needs ~15 GB of free HBM")
+    top = TP.random_regular(n, 4, seed=0)
+    eng = _dopt.Engine(0, "float64", data_dtype="float32")
+    try:
+        eng.generate_shards("logistic", n, d, m, seed=1000, flip=0.05)
+        eng.set_topology(top.row_ptr, top.col, top.w)
+        # the bench's form: pipelined calls (the last iterate's metrics owed to the next call)
+        eng.zero_models()
+        o0, c0 = eng.run_dsgd_pipelined(1, eta0, m, lam, lam, 0.0, t0=0)
+        o1, c1 = eng.run_dsgd_pipelined(2, eta0, m, lam, lam, 0.0, t0=1)
+        assert _dopt.last_round_kernel().startswith("void dopt::k_round<double, float, 4, 0, true, true,")
+        o2, c2 = eng.run_dsgd_pipelined(0, eta0, m, lam, lam, 0.0, t0=3)
+        obj_p, cons_p = np.concatenate([o0, o1, o2]), np.concatenate([c0, c1, c2])
+        assert len(obj_p) == T and len(cons_p) == T
+        x_p = eng.get_models()
+
+        eng.zero_models()
+        x = np.zeros((n, d))
+        rng = np.random.default_rng(5)
+        picks = [0, 1, n - 1] + [int(i) for i in rng.choice(n, 9, replace=False)]
+        shards = {i: eng.get_shard(i) for i in picks}
+        xbars = []
+        for t in range(T):  # one round per call: every round's updates and metrics pinned on the host
+            obj, cons, _ = eng.run_dsgd(1, eta0, m, lam, lam, 0.0, t0=t)
+            xn = eng.get_models()
+            eta = eta0 / np.sqrt(t + 1)  # trainer.py:138-140
+            for i in picks:
+                X, y = shards[i]
+                ref = _mix_row(top, x, i) - eta * O.logistic_gradient(x[i], X, y, lam)
+                np.testing.assert_allclose(xn[i], ref, rtol=1e-10, atol=1e-13)
+            xbar = xn.mean(axis=0)
+            np.testing.assert_allclose(cons[0], np.mean(np.sum((xn - xbar) ** 2, axis=1)), rtol=1e-10)
+            np.testing.assert_allclose(cons_p[t], cons[0], rtol=1e-11)
+            np.testing.assert_allclose(obj_p[t], obj[0], rtol=1e-12)
+            xbars.append((xbar, obj[0]))
+            x = xn
+        np.testing.assert_allclose(x_p, x, rtol=1e-11, atol=1e-14)
+        # the objective at every round's xbar over all 4096 x 512 rows: the oracle's formula
+        # (obj_problems.py:3-11) per shard, summed over shards
+        W = np.stack([xb for xb, _ in xbars], axis=1)
+        loss = np.zeros(T)
+        for i in range(n):
+            X, y = eng.get_shard(i)
+            yz = y[:, None] * (X @ W)
+            loss += np.sum(np.maximum(0, -yz) + np.log(1 + np.exp(-np.abs(yz))), axis=0)
+        for t, (xb, f) in enumerate(xbars):
+            np.testing.assert_allclose(f, loss[t] / (n * m) + lam / 2.0 * np.dot(xb, xb), rtol=1e-10)
+    finally:
+        eng.close()
 
 
 def test_c4_torus_65536_workers_full_size():
