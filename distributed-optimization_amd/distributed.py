@@ -5,7 +5,7 @@ rank r of a torch.distributed job (backend "nccl" = RCCL over xGMI on MI355X;
 "gloo" in tests) owns workers [lo_r, hi_r) -- their shards, iterates and rows of
 W -- on its own GPU.  Per round:
 
-  gather x_t rows the peers need --> grouped isend/irecv ------------.
+  gather x_t rows the peers need --> all-to-all of the halo rows ---.
   gradient of every local worker at x_t (+ metrics of x_t) ---------+--> mix + step
   local column sums --> all_reduce(d doubles) --> xbar_{t+1}
 
@@ -236,11 +236,17 @@ class HaloExchange:
     """The per-round halo transfer of a HaloPlan: rows send[send_off[p]:send_off[p+1]] go to
     peer p, rows halo[recv_off[p]:recv_off[p+1]] come from peer p.
 
-    RCCL (device_comm): one grouped batch_isend_irecv over the device buffers, enqueued behind
-    the current stream's work; finish() makes the current stream wait for it (the host does not
-    block; the process group's watchdog bounds it).  gloo: the rows go through host memory and
-    finish() waits on the host with the job's timeout, so a peer that never sends ends this rank
-    with a CollectiveError naming it."""
+    RCCL (device_comm): the whole exchange is ONE all_to_all_single over the device buffers --
+    the send rows are grouped by peer and the halo rows come in per-peer blocks, exactly the
+    split layout of an all-to-all-v -- enqueued behind the current stream's work; finish() makes
+    the current stream wait for it (the host does not block; the process group's watchdog
+    bounds it).  One collective call per round instead of an isend and an irecv per peer (14
+    P2P ops per rank at 8 ranks on the spectral partition of C3's graph), so the host's issue
+    cost per round stays far below a round kernel even at the strong leg's 512 workers per rank
+    (~0.19 ms per round).  Every rank of the group joins it each round, with or without rows
+    to move (zero split sizes).  gloo: per-peer isend / irecv through host memory, and finish()
+    waits on the host with the job's timeout, so a peer that never sends ends this rank with a
+    CollectiveError naming it."""
 
     def __init__(self, plan, send, halo, group=None, device_comm=False):
         import torch.distributed as dist
@@ -249,6 +255,16 @@ class HaloExchange:
         self.send, self.halo = send, halo
         self.peers = plan.peers()
         self.rank = plan.rank
+        # the RCCL all-to-all: at world > 1, or at world 1 with the collectives forced (the one-GPU
+        # box runs the call then, with zero rows or rows to itself)
+        self.collective = device_comm and (plan.world > 1 or os.environ.get("DOPT_FORCE_COLLECTIVES") == "1")
+        self.send_sizes = [int(plan.send_off[p + 1] - plan.send_off[p]) for p in range(plan.world)]
+        self.recv_sizes = [int(plan.recv_off[p + 1] - plan.recv_off[p]) for p in range(plan.world)]
+
+    def disable(self):
+        """No exchange at all (complete-graph mixing on every rank: no rows move)."""
+        self.peers = []
+        self.collective = False
 
     def _ops(self, send, halo):
         """(kind, peer, buffer, rows) for every transfer, sends first per peer, peers ascending."""
@@ -262,13 +278,14 @@ class HaloExchange:
                 yield "irecv", p, halo[r0:r1], int(r1 - r0)
 
     def start(self):
-        if not self.peers:
-            return None
         dist = self.dist
-        if self.device_comm:
-            ops = [dist.P2POp(dist.isend if k == "isend" else dist.irecv, buf, p, self.group)
-                   for k, p, buf, _ in self._ops(self.send, self.halo)]
-            return [(w, "batch_isend_irecv with peers %s" % self.peers) for w in dist.batch_isend_irecv(ops)]
+        if self.collective:
+            ns, nr = sum(self.send_sizes), sum(self.recv_sizes)
+            w = dist.all_to_all_single(self.halo[:nr], self.send[:ns], output_split_sizes=self.recv_sizes,
+                                       input_split_sizes=self.send_sizes, group=self.group, async_op=True)
+            return [(w, f"all_to_all_single of {ns} rows out / {nr} halo rows in (peers {self.peers})")]
+        if not self.peers or self.device_comm:
+            return None
         send = self.send.cpu()
         halo = self.halo.cpu()
         works = []
@@ -325,16 +342,15 @@ class DistributedDSGD:
             engine.set_halo(0, None, np.zeros(0, np.int32), None)
             engine.set_mixing_mean(mean[0], mean[1])
             self._peers = []
-            self.exchange.peers = []
+            self.exchange.disable()
         self.mean = mean
         engine.set_stream(self.stream.cuda_stream)
         # the lagged schedule: CSR mixing on row-resident contexts (DOPT_LAGGED=0: the serial one)
         nch = (ld * esz) // 16
         self._lagged_ok = (mean is None and nch <= 16 * 64 and
                            os.environ.get("DOPT_LAGGED", "1") != "0")
-        # every rank joins one collective before the first batched send/recv, which may
-        # involve only some ranks (a torus strip talks to two peers): with NCCL the first
-        # call in a group must include all of its ranks
+        # the communicator is created by one small collective here, not inside the first round
+        # (the halo all-to-all and the all-reduces of the rounds then find it ready)
         if self.device_comm and dist.get_world_size(group) > 1:
             dist.all_reduce(torch.zeros(1, device=self.dev), group=group)
 
@@ -545,7 +561,7 @@ class DistributedDSGD:
         Round g (counted from the start of the chain; one call = one chain unless pipelined),
         all on the engine stream except the two transfers:
 
-          P2P(send rows of x_g) -----------------------------------------------.
+          exchange(send rows of x_g) ------------------------------------------.
           colsum(x_g) [+ fold of history[g-2] / loss of history[g-3]] -> all-reduce --.
           grad(x_g) + loss of every row at xbar_{g-1} ------------------------------+-+-> mix
                                                       mix: xbar_g, consensus of x_g, x_{g+1},

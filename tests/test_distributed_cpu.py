@@ -199,3 +199,43 @@ def test_relabelled_rounds_match_oracle(tmp_path):
     idx = [[np.arange(7)] * n] * T
     _, _, ref, _ = O.run_decentralized(_data(n), topo.dense_W(), T, CFG, mixing="sparse", indices=idx)
     np.testing.assert_array_equal(got, ref)
+
+
+def _rank_alltoall(rank, world, port, topo, out):
+    """HaloExchange's RCCL form (one all_to_all_single per round over the peer-grouped buffers),
+    driven over gloo on CPU tensors: every halo row must arrive holding its global id."""
+    import torch
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    plan = D.build_plan(topo, world, rank)
+    send = torch.full((max(1, len(plan.send_ids)), 3), -1.0, dtype=torch.float64)
+    send[:len(plan.send_ids)] = torch.from_numpy((plan.send_ids + plan.lo).astype(np.float64))[:, None]
+    halo = torch.full((max(1, plan.n_halo), 3), -1.0, dtype=torch.float64)
+    ex = D.HaloExchange(plan, send, halo)
+    ex.collective = True  # the device path's call, here on gloo
+    for _ in range(2):  # every round is the same collective; repeated calls reuse the buffers
+        ex.finish(ex.start())
+    np.save(os.path.join(out, f"rank{rank}.npy"), halo[:plan.n_halo].numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,n,world", [("random_regular", 40, 4), ("ring", 12, 3), ("two_rings", 12, 3)])
+def test_alltoall_halo_layout(tmp_path, name, n, world):
+    """The split sizes of the all-to-all are the plan's per-peer blocks (send rows grouped by
+    peer, halo rows in per-peer blocks); every rank joins, also one without peers (two_rings: two
+    disjoint rings, one of them wholly on rank 2)."""
+    if name == "two_rings":
+        nb = ([sorted([(i - 1) % 8, (i + 1) % 8]) for i in range(8)] +
+              [sorted([8 + (i - 1) % 4, 8 + (i + 1) % 4]) for i in range(4)])
+        topo = TP.Topology("two_rings", nb)
+    else:
+        topo = _topo(name, n)
+    mp.start_processes(_rank_alltoall, args=(world, _free_port(), topo, str(tmp_path)), nprocs=world, join=True,
+                       start_method="fork")
+    for r in range(world):
+        plan = D.build_plan(topo, world, r)
+        got = np.load(tmp_path / f"rank{r}.npy")
+        np.testing.assert_array_equal(got, np.repeat(plan.halo_ids.astype(np.float64)[:, None], 3, axis=1))
+    if name == "two_rings":
+        assert D.build_plan(topo, world, 2).peers() == []

@@ -363,3 +363,41 @@ def test_trainers_multiprocess_checkpoint_resume(tmp_path):
         np.testing.assert_allclose(got[f"L{j}_objective"], z[f"L{j}_objective"][:50], rtol=1e-9)
         if label != "Centralized":
             np.testing.assert_allclose(got[f"L{j}_consensus"], z[f"L{j}_consensus"][:50], rtol=1e-9)
+
+
+def _rccl_self_exchange(rank, world, port, out):
+    """HaloExchange's all_to_all_single on an RCCL communicator of one rank, with rows sent to
+    itself (a hand-made plan: rows 0..k-1 out, k halo rows in) on the engine-like side stream."""
+    import torch
+    import torch.distributed as dist
+
+    import distributed as Dm
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DOPT_FORCE_COLLECTIVES="1")
+    torch.cuda.set_device(0)
+    Dm.init_process_group("nccl", rank=0, world_size=1)
+    k, ld = 37, 130
+    plan = Dm.HaloPlan(0, 1, np.array([0, 64]), 0, 64, np.arange(k), np.array([0, k]), np.arange(k, dtype=np.int32),
+                       np.array([0, k]), None, None, None)
+    send = torch.arange((k + 3) * ld, dtype=torch.float64, device="cuda").reshape(k + 3, ld)
+    halo = torch.full((k + 3, ld), -1.0, dtype=torch.float64, device="cuda")
+    ex = Dm.HaloExchange(plan, send, halo, device_comm=True)
+    assert ex.collective and ex.send_sizes == [k] and ex.recv_sizes == [k]
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        ex.finish(ex.start())
+        ok = bool(torch.equal(halo[:k], send[:k])) and bool((halo[k:] == -1.0).all())
+    s.synchronize()
+    np.save(os.path.join(out, "ok.npy"), np.array([ok]))
+    dist.destroy_process_group()
+
+
+def test_rccl_alltoall_halo_exchange_one_rank(tmp_path):
+    """The device halo exchange is one RCCL all_to_all_single with the plan's split sizes; at world
+    1 it runs with rows sent to the rank itself, which copies them (the layout over several ranks:
+    tests/test_distributed_cpu.py::test_alltoall_halo_layout, same call over gloo)."""
+    import torch.multiprocessing as mp
+
+    mp.start_processes(_rccl_self_exchange, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True,
+                       start_method="spawn")
+    assert np.load(tmp_path / "ok.npy")[0]
