@@ -360,17 +360,23 @@ def dropin_leg(eng, n, d, m, lam, eta0, rounds=128, batch=None, reps=5):
 
     per_round, lo, hi = med([(l3 - l1) / (2 * rounds) for _, _, l1, l3 in runs])
     run_slope = med([(w3 - w1) / (2 * rounds) for w1, w3, _, _ in runs])
-    return {"value": n / per_round, "unit": "worker-iters/s", "batch": b, "rounds": [rounds, 3 * rounds],
+    # the fixed cost of one run() (trainer set-up, data checks, the first chunk's draw before the device
+    # starts, the final metrics pass): every run's wall time less its rounds at the slope
+    fixed, fixed_lo, fixed_hi = med([w - k * per_round for w1, w3, _, _ in runs for w, k in ((w1, rounds), (w3, 3 * rounds))])
+    T_run = 10_000  # the reference's runs (main.py: 10^4 iterations)
+    whole = n * T_run / (fixed + T_run * per_round)
+    return {"value": whole, "unit": "worker-iters/s", "basis": f"one run({T_run}) = fixed_per_run_s + "
+            f"{T_run} x ms_per_round", "value_slope": n / per_round, "fixed_per_run_s": fixed,
+            "fixed_per_run_s_range": [fixed_lo, fixed_hi], "batch": b, "rounds": [rounds, 3 * rounds],
             "reps": reps, "ms_per_round": per_round * 1e3, "ms_per_round_range": [lo * 1e3, hi * 1e3],
             "loop_s": [[r[2], r[3]] for r in runs], "run_wall_s": [[r[0], r[1]] for r in runs],
             "run_slope_ms_per_round": [x * 1e3 for x in run_slope], "zero_round_run_s": zero,
             "final_objective": float(hist["objective"][-1]),
             "note": "trainer.DecentralizedTrainer, sampling='legacy' (numpy's stream, drawn on the host one "
-                    "chunk ahead of the device); per-round rate = the median over interleaved pairs of runs "
-                    "of the slope of the trainer's round-loop wall time (loop_seconds: draws + device rounds + "
-                    "history; the per-run content hash of the 8.6 GB host shards before the loop, whose "
-                    "host-memory jitter swamps whole-run slopes, is outside it -- run_slope_ms_per_round gives "
-                    "the whole-run slope [median, min, max] for reference)"}
+                    "chunk ahead of the device).  value = the whole-run rate of one run(10000): the fixed cost "
+                    "of a run (median over the timed runs of wall time less rounds x slope) plus 10^4 rounds at "
+                    "the per-round slope; value_slope = the per-round rate alone (median over interleaved "
+                    "pairs of runs of the slope of the trainer's round-loop time, loop_seconds)"}
 
 
 # ---------------------------------------------------------------------------- launch
@@ -504,13 +510,19 @@ def setup_leg(args, config, n_global, world, rank, dev):
         runner = distributed.DistributedDSGD(eng, plan, n_global, n_global * m, device=dev, mean=mean_local,
                                              rs_chunks=args.rs_chunks or None)
         ld, esz_state = eng.layout()
+        lay = runner.layout
         S.comm = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
                   "halo_rows_in": int(plan.n_halo), "send_rows_out": int(len(plan.send_ids)),
                   "halo_bytes_in_per_round": int(plan.n_halo) * ld * esz_state,
                   "send_bytes_out_per_round": int(len(plan.send_ids)) * ld * esz_state,
-                  "peers": [int(p) for p in runner._peers],
-                  "allreduce_bytes_per_round": ld * 8,
-                  "allreduce_chunks": runner.rs_chunks if S.mean is not None else 1}
+                  "peers": [int(p) for p in runner._peers]}
+        if S.mean is None:  # the lagged schedule: the column sums ride the halo all-to-all
+            S.comm.update({"collectives_per_round": 1 if world > 1 else 0,
+                           "exchange": "one all_to_all_single per round: halo rows + every rank's column sums",
+                           "colsum_bytes_per_peer_per_round": lay.ks * ld * esz_state,
+                           "exchange_bytes_out_per_round": lay.n_send_rows * ld * esz_state})
+        else:
+            S.comm.update({"allreduce_bytes_per_round": ld * 8, "allreduce_chunks": runner.rs_chunks})
         log(f"comm: {S.comm}")
         if runner._lagged_ok or (S.mean is not None and runner._rowspace_ready()):
             # the lagged schedule / the row-space rounds continued across calls (as on one GPU: timed_leg)
@@ -738,7 +750,7 @@ def main():
                    "parallelism": (f"dp{world}: one graph of {S.n_global} workers, "
                                    f"{'graph-partitioned' if args.config == 'c3' and args.partition == 'spectral' else 'contiguous'} "
                                    f"slices per GPU, "
-                                   f"{'all-reduce of the column sums' if mean is not None else 'halo send/recv + all-reduce'}"
+                                   f"{'all-reduce of the column sums' if mean is not None else 'one all-to-all per round (halo rows + column sums)'}"
                                    f" ({args.backend})") if world > 1
                                   else ("single GPU: the multi-GPU phase path ("
                                         f"{'row-space rounds, all-reduce of the column sums' if mean is not None else 'lagged schedule'}, "

@@ -84,11 +84,12 @@ _SIGS = {
     "dopt_phase_xbar": ([_P, _P], ctypes.c_int),
     "dopt_phase_metrics_pass": ([_P, ctypes.c_uint32], ctypes.c_int),
     "dopt_phase_metrics": ([_P, ctypes.c_uint32, ctypes.c_int, _P], ctypes.c_int),
-    "dopt_phase_cons": ([_P], ctypes.c_int),
     "dopt_phase_fold": ([_P, _P, _P, _P, ctypes.c_int], ctypes.c_int),
-    "dopt_phase_loss_pass": ([_P, ctypes.c_int], ctypes.c_int),
-    "dopt_phase_colsum_fold": ([_P, _P, _P, _P, _P], ctypes.c_int),
-    "dopt_phase_mix_lagged": ([_P, _I64, _D, _P, ctypes.c_int], ctypes.c_int),
+    "dopt_lagged_exchange_layout": ([_P, _I32, _I32, _P, _P], ctypes.c_int),
+    "dopt_lagged_begin": ([_P, _I64], ctypes.c_int),
+    "dopt_lagged_grad": ([_P, _I64, _D, _I64, _P, _D, ctypes.c_uint32], ctypes.c_int),
+    "dopt_lagged_mix": ([_P, _I64, _D, ctypes.c_int, _P, _P, _P], ctypes.c_int),
+    "dopt_lagged_tail": ([_P, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "dopt_rs_phase_begin": ([_P, ctypes.c_int, _P, _P], ctypes.c_int),
     "dopt_rs_phase_round": ([_P, _I64, _D, _D, ctypes.c_uint32, _P], ctypes.c_int),
     "dopt_rs_phase_cols": ([_P, _I64, _D, _D, _P], ctypes.c_int),
@@ -106,7 +107,7 @@ _SIGS = {
     "dopt_phase_set_step": ([_P, _I64, ctypes.c_double], ctypes.c_int),
 }
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 2  # DOPT_ABI_VERSION of include/dopt.h
+ABI_VERSION = 3  # DOPT_ABI_VERSION of include/dopt.h
 
 
 def lib():
@@ -453,25 +454,36 @@ class Engine:
     def phase_metrics(self, flags, include_xnorm, out_ptr):
         check(lib().dopt_phase_metrics(self._h, int(flags), 1 if include_xnorm else 0, ctypes.c_void_p(out_ptr)))
 
-    def phase_cons(self):
-        check(lib().dopt_phase_cons(self._h))
-
     def phase_fold(self, cons_ptr=None, xnorm_ptr=None, loss_ptr=None, slab=0):
         """Device-side sums into the given device addresses (None: skip that output)."""
         vp = lambda p: ctypes.c_void_p(p) if p else None  # noqa: E731
         check(lib().dopt_phase_fold(self._h, vp(cons_ptr), vp(xnorm_ptr), vp(loss_ptr), int(slab)))
 
-    def phase_colsum_fold(self, sum_ptr, cons_ptr=None, xnorm_ptr=None, loss_ptr=None):
-        vp = lambda p: ctypes.c_void_p(p) if p else None  # noqa: E731
-        check(lib().dopt_phase_colsum_fold(self._h, ctypes.c_void_p(sum_ptr), vp(cons_ptr), vp(xnorm_ptr),
-                                           vp(loss_ptr)))
+    # -- the lagged schedule (dopt_lagged_*; distributed.py _run_lagged): two calls per round
+    def lagged_exchange_layout(self, world, rank, sum_send_row, sum_recv_row):
+        so = np.ascontiguousarray(sum_send_row, dtype=np.int64)
+        ri = np.ascontiguousarray(sum_recv_row, dtype=np.int64)
+        check(lib().dopt_lagged_exchange_layout(self._h, int(world), int(rank), _ptr(so), _ptr(ri)))
 
-    def phase_mix_lagged(self, t, eta0, sum_ptr, consensus=True):
-        check(lib().dopt_phase_mix_lagged(self._h, int(t), float(eta0), ctypes.c_void_p(sum_ptr),
-                                          1 if consensus else 0))
+    def lagged_begin(self, batch):
+        check(lib().dopt_lagged_begin(self._h, int(batch)))
 
-    def phase_loss_pass(self, two_points):
-        check(lib().dopt_phase_loss_pass(self._h, 1 if two_points else 0))
+    def lagged_grad(self, t, eta0, batch, lam_grad, metric_flags=0, idx=None):
+        if idx is not None:
+            idx = np.ascontiguousarray(idx, dtype=np.int32)
+        rc = lib().dopt_lagged_grad(self._h, t, eta0, batch, _ptr(idx), lam_grad, metric_flags)
+        if rc:
+            check(rc)
+
+    def lagged_mix(self, t, eta0, consensus, cons_ptr=None, xnorm_ptr=None, loss_ptr=None):
+        """Per round; device addresses of the history row g-2 (None: not folded)."""
+        rc = lib().dopt_lagged_mix(self._h, t, eta0, 1 if consensus else 0, cons_ptr, xnorm_ptr, loss_ptr)
+        if rc:
+            check(rc)
+
+    def lagged_tail(self, consensus, objective, row1, row2):
+        """row1 / row2: (cons, xnorm, loss) device addresses of the history rows G-1 / G-2 (None: skip)."""
+        check(lib().dopt_lagged_tail(self._h, 1 if consensus else 0, 1 if objective else 0, *row1, *row2))
 
     def rs_phase_begin(self, commit):
         """(ok, hash): this rank's iterates all equal (row-space rounds possible) and the 64-bit

@@ -79,7 +79,7 @@ struct RoundArgs {
   const int32_t* sslot;
   // multi-GPU phase path: workers whose CSR row is all local (and who send no row) are mixed and
   // stepped by the gradient kernel itself (F_STEP per worker; k_mix then skips them), or null
-  const uint8_t* interior;
+  const int32_t* interior;
   void* send;
   // lagged multi-GPU mix: xbar of x_old from the all-reduced column sums xsum / xsum_n, written
   // to xbar_out, and the per-worker consensus ||x_old[i] - xbar||^2 into slab_cons (if non-null)
@@ -99,6 +99,26 @@ struct FoldArgs {
   double* out_c;
   double* out_l;
   double* out_q;
+};
+
+// The lagged multi-GPU mix with the column sums fused in (k_mixcs, kernels.hip).  Workgroup
+// (group g of R workers, column block cb of 64 * CPB state chunks) mixes and steps its workers'
+// slices (interior workers: stepped by the gradient kernel, read back), takes their consensus
+// partials at xbar = (rank-ordered sum of every rank's column sums of x_old) / n, and writes the
+// column-block partial of the column sums of x_new to part[g]; the last workgroup of a column
+// block to arrive (agent-scope ticket) sums the NG partials in group order into own_out and into
+// the send buffer's sum rows of every peer.  Block 0 folds a history row (FoldArgs).
+struct McsArgs {
+  double* part;            // [ng x ld] group partials of the column sums of x_new
+  unsigned* cnt;           // [ncb] arrival tickets (zero between launches: the last arriver resets)
+  int32_t ng, ncb, r;      // worker groups, column blocks, workers per group
+  int32_t world, rank;     // the rank-ordered global sums: p == rank -> own_in, else peer p's rows
+  const double* own_in;    // [ld] this rank's column sums of x_old
+  double* own_out;         // [ld] this rank's column sums of x_new
+  const int64_t* sum_in;   // [world] halo-buffer row of peer p's column sums of x_old (-1: self)
+  const int64_t* sum_out;  // [world] send-buffer row of the sums of x_new for peer p (-1: self)
+  double* cons_part;       // [ncb x n] consensus partial of (column block, worker), or null
+  double n_div;            // the mean's divisor (workers on all ranks)
 };
 
 // Row-space rounds (rowspace.hip): complete graph (uniform W_ii), either objective, full
@@ -244,7 +264,17 @@ hipError_t launch_cons(int dtype, const void* x, const void* xbar, int64_t n, in
                        double* slab, hipStream_t s);
 // x_next[i] = sum_e cw[e] * src(ci[e]) - eta * G[i]  (trainer.py:173-175), src = x_old or halo.
 hipError_t launch_mix(int dtype, int cpl, const RoundArgs& a, const void* G, int n_workers, hipStream_t s);
-// dst[k] = x[ids[k]] rows (halo send buffer).
+// The lagged mix with fused column sums (McsArgs); fold: the history row folded by block 0
+// (null: none).  xsum / xsum_n of `a` are unused (the rank-ordered sums of m replace them).
+hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_workers, const McsArgs& m,
+                        const FoldArgs* fold, hipStream_t s);
+// Column-block count / workers per group / groups of k_mixcs for n workers and nch state chunks.
+void mixcs_shape(int dtype, int64_t n, int32_t nch, int32_t* ncb, int32_t* r, int32_t* ng);
+// xbar_out = (T)(rank-ordered sum of the column sums, as k_mixcs forms it / n_div); with send != null
+// also own -> the send buffer's sum rows (the chain's first exchange of x_0's sums).
+hipError_t launch_xbar_ranks(int dtype, const McsArgs& m, const void* halo, int64_t ld, int32_t nch,
+                             void* xbar_out, void* send, hipStream_t s);
+// dst[k] = x[ids[k]] rows (halo send buffer); ids[k] < 0: row k left alone.
 hipError_t launch_gather_rows(int dtype, const void* x, const int32_t* ids, int64_t n, int64_t ld,
                               int32_t nchunks, void* dst, hipStream_t s);
 // Synthetic shards (rows_per_worker rows per worker), X ~ N(0,1) + bias column; xrows > 0: X in

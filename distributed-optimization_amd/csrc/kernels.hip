@@ -1477,6 +1477,289 @@ hipError_t launch_mix(int dtype, int cpl, const RoundArgs& a, const void* G, int
                     : launch_mix_t<double>(cpl, a, (const double*)G, n_workers, s);
 }
 
+// ---------------------------------------------------------------------------- lagged mix + column sums
+// k_mixcs (round 4): the lagged schedule's mix (k_mix with a.xsum) with the column sums of the new
+// iterates fused in, so a multi-GPU round is two kernels -- the gradient pass and this -- and the
+// next round's exchange carries the column sums beside the halo rows (no all-reduce; every rank
+// sums the ranks' vectors in rank order, so all ranks hold the same bits).
+//   block 0: the history fold of McsArgs' caller (FoldArgs; nothing when no output is set);
+//   block 1 + g * ncb + cb: workers [g R, g R + R) x state chunks [64 CPB cb, 64 CPB (cb + 1)).
+// A wave takes workers g R + w, g R + w + 4, ..., two at a time (every load of both in flight at
+// once); per worker: xbar of x_old from the rank-ordered sums, the consensus partial of this column
+// block, the mix + step (CSR order and arithmetic of k_mix / k_round: bitwise the same iterates) or,
+// for an interior worker the gradient kernel stepped, its new row read back; the new rows' column
+// sums accumulate per lane in float64 in worker order, meet in LDS in wave order, and go to part[g]
+// as write-through (sc1) stores.  The last arriving workgroup of column block cb (agent-scope
+// ticket, MI355X_MICROARCH.md "Valid forms" row 1: sc1 stores drained by every storing wave before
+// one lane's ticket add, sc1 loads after it; the acquire fence is kept as well) sums part[0..ng) in
+// group order and writes the block's sums to own_out and to every peer's sum rows in the send
+// buffer, then resets the ticket for the next launch.
+template <int RW>
+__device__ void fold_block_rw(const FoldArgs& f, int nch, int vn, double (*red)[RW]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double a = 0.0, b = 0.0, q = 0.0;
+  auto sum4 = [&](const double* v, int64_t cnt) {  // the fold_block order
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int64_t k = threadIdx.x;
+    for (; k + 3 * NT < cnt; k += 4 * NT) {
+      s0 += v[k];
+      s1 += v[k + NT];
+      s2 += v[k + 2 * NT];
+      s3 += v[k + 3 * NT];
+    }
+    for (; k < cnt; k += NT) s0 += v[k];
+    return (s0 + s1) + (s2 + s3);
+  };
+  if (f.sc && f.out_c) a = sum4(f.sc, f.nc);
+  if (f.sl && f.out_l) b = sum4(f.sl, f.nl);
+  if (f.xbar && f.out_q) {
+    for (int c = threadIdx.x; c < nch; c += NT)
+      for (int e = 0; e < vn; ++e) {
+        const int64_t k = (int64_t)c * vn + e;
+        const double v = vn == 2 ? ((const double*)f.xbar)[k] : (double)((const float*)f.xbar)[k];
+        q += v * v;
+      }
+  }
+  a = wave_sum(a);
+  b = wave_sum(b);
+  q = wave_sum(q);
+  if (lane == 0) {
+    red[wave][0] = a;
+    red[wave][1] = b;
+    red[wave][2] = q;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double sa = 0.0, sb = 0.0, sq = 0.0;
+    for (int k = 0; k < NW; ++k) {
+      sa += red[k][0];
+      sb += red[k][1];
+      sq += red[k][2];
+    }
+    if (f.out_c) *f.out_c = sa;
+    if (f.out_l) *f.out_l = sb;
+    if (f.out_q) *f.out_q = sq;
+  }
+}
+
+// Column sum of global column `col` over every rank's vector, in rank order (k_mixcs, k_xbar_ranks).
+template <typename T>
+__device__ __forceinline__ double ranks_sum(const McsArgs& m, const T* halo, int64_t ld, int64_t col) {
+  double s = 0.0;
+  for (int p = 0; p < m.world; ++p) {
+    const double v = p == m.rank ? m.own_in[col] : ((const double*)(halo + m.sum_in[p] * ld))[col];
+    s += v;
+  }
+  return s;
+}
+
+template <typename T, int CPB>
+__global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __restrict__ G, int n, const McsArgs m,
+                                              const FoldArgs fold) {
+  using V = typename VT<T>::v;
+  constexpr int VN = VT<T>::n;
+  constexpr int MAXE = 6;          // CSR entries held in registers (runtime: max row nnz <= 6)
+  constexpr int BC = 64 * CPB * VN;  // columns of a column block
+  __shared__ double red[NW][BC];
+  __shared__ int last;
+  if (blockIdx.x == 0) {
+    fold_block_rw<BC>(fold, a.nchunks, VN, red);
+    return;
+  }
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = (int)blockIdx.x - 1;
+  const int cb = b % m.ncb, g = b / m.ncb;
+  const int64_t ld = a.ld;
+  const int nch = a.nchunks;
+  const int cbase = cb * 64 * CPB;
+  const T eta = (T)a.eta;
+  const T* halo = (const T*)a.halo;
+  // xbar of x_old at this lane's chunks (as k_colsum_final / k_mix round it: (T)(sum / n))
+  V xb[CPB];
+#pragma unroll
+  for (int j = 0; j < CPB; ++j) {
+    const int c = cbase + lane + 64 * j;
+    xb[j] = V(0);
+    if (c < nch) {
+#pragma unroll
+      for (int e = 0; e < VN; ++e) xb[j][e] = (T)(ranks_sum<T>(m, halo, ld, (int64_t)c * VN + e) / m.n_div);
+      if (g == 0 && wave == 0 && a.xbar_out) *(V*)((T*)a.xbar_out + (int64_t)c * VN) = xb[j];
+    }
+  }
+  double cs[CPB][VN];
+#pragma unroll
+  for (int j = 0; j < CPB; ++j)
+#pragma unroll
+    for (int e = 0; e < VN; ++e) cs[j][e] = 0.0;
+  const int i_end = (g + 1) * m.r < n ? (g + 1) * m.r : n;
+  for (int i0 = g * m.r + wave; i0 < i_end; i0 += 2 * NW) {
+    // two workers of this wave: i0 and i0 + NW; every load of both is issued before any use
+    V own[2][CPB], gv[2][CPB], r[2][MAXE][CPB];
+    int64_t e0[2], e1[2];
+    bool live[2], skip[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = i0 + u * NW;
+      live[u] = i < i_end;
+      skip[u] = live[u] && a.interior && a.interior[i];
+      e0[u] = live[u] ? a.rp[i] : 0;
+      e1[u] = live[u] ? a.rp[i + 1] : 0;
+      if (e1[u] - e0[u] > MAXE) e1[u] = e0[u] + MAXE;  // (runtime guarantee: never taken)
+#pragma unroll
+      for (int j = 0; j < CPB; ++j) {
+        const int c = cbase + lane + 64 * j;
+        const bool in = live[u] && c < nch;
+        own[u][j] = in ? *(const V*)((const T*)a.x_old + (int64_t)i * ld + (int64_t)c * VN) : V(0);
+        // an interior worker's new row (written by the gradient kernel) comes back in gv
+        gv[u][j] = !in ? V(0) : skip[u] ? *(const V*)((const T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN)
+                                        : *(const V*)(G + (int64_t)i * ld + (int64_t)c * VN);
+      }
+#pragma unroll
+      for (int k = 0; k < MAXE; ++k) {
+        if (!skip[u] && e0[u] + k < e1[u]) {
+          const int col = a.ci[e0[u] + k];
+          const T* src = col < a.n_local ? (const T*)a.x_old + (int64_t)col * ld : halo + (int64_t)(col - a.n_local) * ld;
+#pragma unroll
+          for (int j = 0; j < CPB; ++j) {
+            const int c = cbase + lane + 64 * j;
+            r[u][k][j] = c < nch ? *(const V*)(src + (int64_t)c * VN) : V(0);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (!live[u]) continue;
+      const int i = i0 + u * NW;
+      V dv = V(0);
+      V xn[CPB];
+#pragma unroll
+      for (int j = 0; j < CPB; ++j) {
+        const V t = own[u][j] - xb[j];  // consensus term of x_old[i] (zero past the row: both 0)
+        dv += t * t;
+        if (skip[u]) {
+          xn[j] = gv[u][j];
+        } else {
+          V acc = V(0);
+#pragma unroll
+          for (int k = 0; k < MAXE; ++k)
+            if (e0[u] + k < e1[u]) acc += ((const T*)a.cw)[e0[u] + k] * r[u][k][j];
+          xn[j] = acc - eta * gv[u][j];
+        }
+      }
+      if (m.cons_part) {
+        const double t = wave_sum((double)hsum<T>(dv));
+        if (lane == 0) m.cons_part[(int64_t)cb * n + i] = t;
+      }
+      const int64_t s0 = (!skip[u] && a.sptr) ? a.sptr[i] : 0, s1 = (!skip[u] && a.sptr) ? a.sptr[i + 1] : 0;
+#pragma unroll
+      for (int j = 0; j < CPB; ++j) {
+        const int c = cbase + lane + 64 * j;
+        if (c >= nch) continue;
+#pragma unroll
+        for (int e = 0; e < VN; ++e) cs[j][e] += (double)xn[j][e];
+        if (skip[u]) continue;
+        *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = xn[j];
+        for (int64_t q = s0; q < s1; ++q)  // rows peers read next round
+          *(V*)((T*)a.send + (int64_t)a.sslot[q] * ld + (int64_t)c * VN) = xn[j];
+      }
+    }
+  }
+  // this group's partial of the column block: waves in order, write-through stores
+#pragma unroll
+  for (int j = 0; j < CPB; ++j)
+#pragma unroll
+    for (int e = 0; e < VN; ++e) red[wave][(lane + 64 * j) * VN + e] = cs[j][e];
+  __syncthreads();
+  const int64_t colbase = (int64_t)cbase * VN;
+  for (int t = threadIdx.x; t < BC; t += NT) {
+    if (colbase + t >= (int64_t)nch * VN) break;
+    const double s = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+    __hip_atomic_store(m.part + (int64_t)g * ld + colbase + t, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned ticket = __hip_atomic_fetch_add(m.cnt + cb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = ticket == (unsigned)(m.ng - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  for (int t = threadIdx.x; t < BC; t += NT) {
+    const int64_t col = colbase + t;
+    if (col >= (int64_t)nch * VN) break;
+    double s = 0.0;
+    int q = 0;
+    for (; q + 8 <= m.ng; q += 8) {  // eight partials in flight, summed in group order
+      double v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        v[k] = __hip_atomic_load(m.part + (int64_t)(q + k) * ld + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += v[k];
+    }
+    for (; q < m.ng; ++q) s += __hip_atomic_load(m.part + (int64_t)q * ld + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    m.own_out[col] = s;
+    for (int p = 0; p < m.world; ++p)
+      if (m.sum_out[p] >= 0) ((double*)((T*)a.send + m.sum_out[p] * ld))[col] = s;
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(m.cnt + cb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+void mixcs_shape(int dtype, int64_t n, int32_t nch, int32_t* ncb, int32_t* r, int32_t* ng) {
+  constexpr int CPB = 2;
+  (void)dtype;
+  *ncb = (nch + 64 * CPB - 1) / (64 * CPB);
+  // groups of 8 workers, at most 64 groups (the last arriver reads ng partials of its block)
+  int64_t rr = 8;
+  while ((n + rr - 1) / rr > 64) rr += 8;
+  *r = (int32_t)rr;
+  *ng = (int32_t)std::max<int64_t>(1, (n + rr - 1) / rr);
+}
+
+hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_workers, const McsArgs& m,
+                        const FoldArgs* fold, hipStream_t s) {
+  FoldArgs f;
+  memset(&f, 0, sizeof(f));
+  if (fold) f = *fold;
+  const dim3 grid(1 + (unsigned)m.ng * (unsigned)m.ncb);
+  if (dtype == 0)
+    hipLaunchKernelGGL((k_mixcs<float, 2>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, m, f);
+  else
+    hipLaunchKernelGGL((k_mixcs<double, 2>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, m, f);
+  return hipGetLastError();
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void k_xbar_ranks(const McsArgs m, const T* __restrict__ halo, int64_t ld, int nch,
+                                                   T* xbar_out, T* send) {
+  constexpr int VN = VT<T>::n;
+  const int64_t col = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (col >= (int64_t)nch * VN) return;
+  if (xbar_out) xbar_out[col] = (T)(ranks_sum<T>(m, halo, ld, col) / m.n_div);
+  if (send)
+    for (int p = 0; p < m.world; ++p)
+      if (m.sum_out[p] >= 0) ((double*)(send + m.sum_out[p] * ld))[col] = m.own_in[col];
+}
+
+hipError_t launch_xbar_ranks(int dtype, const McsArgs& m, const void* halo, int64_t ld, int32_t nch, void* xbar_out,
+                             void* send, hipStream_t s) {
+  const int vn = dtype == 0 ? 4 : 2;
+  const dim3 grid((unsigned)(((int64_t)nch * vn + NT - 1) / NT));
+  if (dtype == 0)
+    hipLaunchKernelGGL(k_xbar_ranks<float>, grid, dim3(NT), 0, s, m, (const float*)halo, ld, nch, (float*)xbar_out,
+                       (float*)send);
+  else
+    hipLaunchKernelGGL(k_xbar_ranks<double>, grid, dim3(NT), 0, s, m, (const double*)halo, ld, nch,
+                       (double*)xbar_out, (double*)send);
+  return hipGetLastError();
+}
+
 template <typename T>
 __global__ __launch_bounds__(NT) void k_gather_rows(const T* __restrict__ x, const int32_t* ids, int64_t n,
                                                     int64_t ld, int nch, T* __restrict__ dst) {
@@ -1486,6 +1769,7 @@ __global__ __launch_bounds__(NT) void k_gather_rows(const T* __restrict__ x, con
   const int64_t k = (int64_t)blockIdx.x * NW + (threadIdx.x >> 6);
   if (k >= n) return;
   const int64_t r = ids[k];
+  if (r < 0) return;  // not a worker's row (a column-sum row of the lagged exchange)
   for (int c = lane; c < nch; c += 64)
     *(V*)(dst + k * ld + (int64_t)c * VN) = *(const V*)(x + r * ld + (int64_t)c * VN);
 }

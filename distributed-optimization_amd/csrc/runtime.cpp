@@ -184,12 +184,27 @@ struct dopt_ctx {
   int64_t* sptr = nullptr;   // send rows by worker: worker i's row goes to send rows sslot[sptr[i]..sptr[i+1])
   int32_t* sslot = nullptr;
   std::vector<uint8_t> is_send;  // host: local workers whose row some peer reads
-  uint8_t* interior = nullptr;   // [n] CSR row all local and no send row (phase path: stepped in the gradient kernel)
+  int32_t* interior = nullptr;   // [n] CSR row all local and no send row (phase path: stepped in the gradient kernel);
+                                 // int32 so the kernels read it with one scalar load
   int64_t n_interior = 0;
   double ph_eta = 0.0;           // dopt_phase_set_step: the step size of the next dopt_phase_grad
   bool ph_eta_set = false;
   bool ph_interior = false;      // the last dopt_phase_grad stepped the interior workers
   bool send_fresh = false;   // the last dopt_phase_mix already wrote the current iterates' send rows
+  // lagged schedule with the column sums in the exchange (dopt_lagged_*, k_mixcs): every rank's
+  // sums of x_g travel beside the halo rows; the send / halo buffers hold one block of sum rows per
+  // peer at the rows dopt_lagged_exchange_layout names
+  int32_t lg_world = 1, lg_rank = 0;
+  std::vector<int64_t> lg_in_h, lg_out_h;  // host copies of the sum rows (-1: self)
+  int64_t* lg_sum_in = nullptr;            // [world] halo row of peer p's sums
+  int64_t* lg_sum_out = nullptr;           // [world] send row of the sums for peer p
+  double* lg_own[2] = {nullptr, nullptr};  // [ld] this rank's column sums of x_g (g parity)
+  double* lg_cons[2] = {nullptr, nullptr}; // [ncb x n] consensus partials of x_g (g parity)
+  double* lg_part = nullptr;               // [ng x ld] group partials of k_mixcs
+  unsigned* lg_cnt = nullptr;              // [ncb] k_mixcs tickets
+  int32_t lg_ncb = 0, lg_r = 0, lg_ng = 0;
+  int64_t lg_alloc_n = -1, lg_alloc_ld = -1;
+  int64_t lg = 0;                          // rounds of the current lagged chain
 
   // per-run buffers
   int32_t* idx = nullptr;
@@ -419,6 +434,10 @@ int set_layout(dopt_ctx* c, int problem, int64_t n, int64_t d) {
   c->n_halo = c->n_send = 0;
   c->halo = c->send = nullptr;
   c->send_fresh = false;
+  c->lg_world = 1;
+  c->lg_rank = 0;
+  c->lg_in_h.clear();
+  c->lg_out_h.clear();
   return DOPT_OK;
 }
 
@@ -1202,6 +1221,10 @@ int dopt_destroy(dopt_ctx* c) {
   dfree(c->rs_x0buf);
   dfree_t(c->rs_grow);
   dfree_t(c->rs_flags);
+  for (double** p : {&c->lg_own[0], &c->lg_own[1], &c->lg_cons[0], &c->lg_cons[1], &c->lg_part}) dfree_t(*p);
+  dfree_t(c->lg_cnt);
+  dfree_t(c->lg_sum_in);
+  dfree_t(c->lg_sum_out);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
@@ -1363,15 +1386,15 @@ int dopt_set_topology(dopt_ctx* c, int64_t n_workers, const int64_t* row_ptr, co
   // rank slices (a halo plan is set): the workers the gradient kernel can mix and step itself
   c->n_interior = 0;
   if (c->n_halo > 0 || !c->is_send.empty()) {
-    std::vector<uint8_t> in((size_t)n_workers, 0);
+    std::vector<int32_t> in((size_t)n_workers, 0);
     for (int64_t i = 0; i < n_workers; ++i) {
       bool local = (size_t)i >= c->is_send.size() || !c->is_send[(size_t)i];
       for (int64_t e = row_ptr[i]; e < row_ptr[i + 1] && local; ++e) local = col[e] < n_workers;
       in[(size_t)i] = local;
       c->n_interior += local;
     }
-    if ((rc = dalloc_t(&c->interior, in.size()))) return rc;
-    HIPOK(hipMemcpy(c->interior, in.data(), in.size(), hipMemcpyHostToDevice));
+    if ((rc = dalloc_t(&c->interior, in.size() * sizeof(int32_t)))) return rc;
+    HIPOK(hipMemcpy(c->interior, in.data(), in.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   }
   c->have_topo = true;
   c->mean_mix = false;
@@ -1922,7 +1945,8 @@ int dopt_set_halo(dopt_ctx* c, int64_t n_halo, void* halo_dev, int64_t n_send, v
   CHECK_ARG(n_halo >= 0 && n_send >= 0, "negative sizes");
   CHECK_ARG(n_halo == 0 || halo_dev, "halo buffer is NULL");
   CHECK_ARG(n_send == 0 || (send_dev && send_ids), "send buffer / ids are NULL");
-  for (int64_t k = 0; k < n_send; ++k) CHECK_ARG(send_ids[k] >= 0 && send_ids[k] < c->n, "send id out of range");
+  for (int64_t k = 0; k < n_send; ++k)  // -1: a row that carries no worker (column sums, dopt_lagged_*)
+    CHECK_ARG(send_ids[k] >= -1 && send_ids[k] < c->n, "send id out of range");
   int rc;
   if ((rc = set_device(c))) return rc;
   if ((rc = rs_end(c))) return rc;
@@ -1935,13 +1959,16 @@ int dopt_set_halo(dopt_ctx* c, int64_t n_halo, void* halo_dev, int64_t n_send, v
   c->send_fresh = false;
   // inverse map for dopt_phase_mix: worker -> the send rows that carry it (one row per peer)
   std::vector<int64_t> sp((size_t)c->n + 1, 0);
-  for (int64_t k = 0; k < n_send; ++k) sp[(size_t)send_ids[k] + 1]++;
+  for (int64_t k = 0; k < n_send; ++k)
+    if (send_ids[k] >= 0) sp[(size_t)send_ids[k] + 1]++;
   for (int64_t i = 0; i < c->n; ++i) sp[(size_t)i + 1] += sp[(size_t)i];
   std::vector<int32_t> slot((size_t)std::max<int64_t>(1, n_send));
   std::vector<int64_t> fill(sp.begin(), sp.end() - 1);
-  for (int64_t k = 0; k < n_send; ++k) slot[(size_t)fill[(size_t)send_ids[k]]++] = (int32_t)k;
+  for (int64_t k = 0; k < n_send; ++k)
+    if (send_ids[k] >= 0) slot[(size_t)fill[(size_t)send_ids[k]]++] = (int32_t)k;
   c->is_send.assign((size_t)c->n, 0);
-  for (int64_t k = 0; k < n_send; ++k) c->is_send[(size_t)send_ids[k]] = 1;
+  for (int64_t k = 0; k < n_send; ++k)
+    if (send_ids[k] >= 0) c->is_send[(size_t)send_ids[k]] = 1;
   if ((rc = dalloc_t(&c->sptr, sp.size() * sizeof(int64_t)))) return rc;
   if ((rc = dalloc_t(&c->sslot, slot.size() * sizeof(int32_t)))) return rc;
   HIPOK(hipMemcpy(c->sptr, sp.data(), sp.size() * sizeof(int64_t), hipMemcpyHostToDevice));
@@ -2182,70 +2209,11 @@ int dopt_phase_xbar(dopt_ctx* c, const double* sum_dev) {
   return refresh_sums_t(c);
 }
 
-int dopt_phase_cons(dopt_ctx* c) {
-  CHECK_ARG(c, "ctx is NULL");
-  if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
-  HIPOK(launch_cons(c->dtype, c->xs[c->cur], c->xbar[c->xb], c->n, c->ld, (int32_t)c->nchs, c->slab_cons,
-                    c->stream));
-  c->cons_n = (c->n + 63) / 64;
-  return DOPT_OK;
-}
-
 int dopt_phase_fold(dopt_ctx* c, double* cons_out, double* xnorm_out, double* loss_out, int slab) {
   CHECK_ARG(c, "ctx is NULL");
   CHECK_ARG(slab == 0 || slab == 1, "slab must be 0 or 1");
   HIPOK(launch_fold(c->dtype, c->slab_cons, c->cons_n, slab ? c->slab_loss_b : c->slab_loss, c->slab_n[slab],
                     c->xbar[c->xb], c->ld, (int32_t)c->nchs, cons_out, loss_out, xnorm_out, c->stream));
-  return DOPT_OK;
-}
-
-int dopt_phase_colsum_fold(dopt_ctx* c, double* sum_dev, double* cons_out, double* xnorm_out, double* loss_out) {
-  CHECK_ARG(c && sum_dev, "NULL argument");
-  if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
-  int rc;
-  if ((rc = rs_end(c))) return rc;
-  HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur], c->n, c->ld, (int32_t)c->nchs, kRowsPerGroup, c->part,
-                              nullptr, c->stream));
-  const FoldArgs fold = {c->slab_cons, c->cons_n, c->slab_loss, c->slab_n[0], c->xbar[c->xb], cons_out, loss_out,
-                         xnorm_out};
-  const bool any = cons_out || xnorm_out || loss_out;
-  HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nchs, nullptr, nullptr, 0.0, 0,
-                            c->stream, sum_dev, any ? &fold : nullptr));
-  return DOPT_OK;
-}
-
-int dopt_phase_mix_lagged(dopt_ctx* c, int64_t t, double eta0, const double* sum_dev, int consensus) {
-  CHECK_ARG(c && sum_dev, "NULL argument");
-  if (!c->have_topo || !c->G) return fail(DOPT_ERR_STATE, "topology / gradient phase missing");
-  if (c->split || c->mean_mix)
-    return fail(DOPT_ERR_UNSUPPORTED, "lagged mix: row-resident contexts with CSR mixing only");
-  RoundArgs a = base_args(c);
-  a.x_old = c->xs[c->cur];
-  a.x_new = c->xs[c->cur ^ 1];
-  a.eta = eta0 / sqrt((double)(t + 1));  // trainer.py:138-140
-  if (c->n_send > 0) {
-    a.sptr = c->sptr;
-    a.sslot = c->sslot;
-    a.send = c->send;
-  }
-  a.xsum = sum_dev;
-  a.xsum_n = (double)n_div(c);
-  a.xbar_out = c->xbar[c->xb ^ 1];
-  a.slab_cons = consensus ? c->slab_cons : nullptr;
-  if (c->ph_interior) a.interior = c->interior;  // stepped by the gradient kernel already
-  c->ph_interior = false;
-  if (c->n > 0) {
-    a.nchunks = (int32_t)c->nchs;  // k_mix walks state chunks
-    HIPOK(launch_mix(c->dtype, c->cpls, a, c->G, (int)c->n, c->stream));
-  } else {  // no worker here: the average still has to be written
-    HIPOK(launch_colsum_final(c->dtype, sum_dev, 1, n_div(c), c->ld, (int32_t)c->nchs, c->xbar[c->xb ^ 1], nullptr,
-                              0.0, 0, c->stream));
-  }
-  if (consensus) c->cons_n = c->n;
-  c->xb ^= 1;
-  c->S_ext = nullptr;
-  c->send_fresh = c->n_send > 0;
-  c->cur ^= 1;
   return DOPT_OK;
 }
 
@@ -2370,8 +2338,95 @@ int dopt_rs_phase_metrics(dopt_ctx* c, uint32_t metric_flags) {
   return DOPT_OK;
 }
 
-int dopt_phase_loss_pass(dopt_ctx* c, int two_points) {
+int dopt_phase_metrics_pass(dopt_ctx* c, uint32_t flags) {
   CHECK_ARG(c, "ctx is NULL");
+  if (c->split) {
+    int rc;
+    if ((rc = ensure_split(c))) return rc;
+    return split_metrics(c, c->xs[c->cur], c->xbar[c->xb], false, flags & DOPT_RUN_CONSENSUS,
+                         flags & DOPT_RUN_OBJECTIVE);
+  }
+  return metrics_pass(c, c->xs[c->cur], c->xbar[c->xb], false, flags & DOPT_RUN_CONSENSUS,
+                      flags & DOPT_RUN_OBJECTIVE);
+}
+
+int dopt_phase_metrics(dopt_ctx* c, uint32_t flags, int include_xnorm, double* out_dev) {
+  CHECK_ARG(c && out_dev, "NULL argument");
+  const bool cons = flags & DOPT_RUN_CONSENSUS, loss = flags & DOPT_RUN_OBJECTIVE;
+  HIPOK(launch_history(c->dtype, cons ? c->slab_cons : nullptr, loss ? c->slab_loss : nullptr, c->n,
+                       c->loss_groups, c->xbar[c->xb], c->ld, (int32_t)c->nchs, loss && include_xnorm, out_dev,
+                       c->stream));
+  return DOPT_OK;
+}
+
+// ---- the lagged schedule with the column sums in the exchange (round 4; distributed.py _run_lagged).
+// Round g of a chain: dopt_lagged_grad (gradient pass of x_g; interior workers stepped; loss of
+// every row at xbar_{g-1}) beside the exchange of x_g's send rows AND every rank's column sums of
+// x_g, then dopt_lagged_mix (k_mixcs: xbar_g from the rank-ordered sums, consensus of x_g, x_{g+1}
+// of the other workers and their send rows, the column sums of x_{g+1} into the send buffer, and
+// the fold of history[g-2]).  Two kernels and one collective per round.
+int dopt_lagged_exchange_layout(dopt_ctx* c, int32_t world, int32_t rank, const int64_t* sum_send_row,
+                                const int64_t* sum_recv_row) {
+  CHECK_ARG(c && sum_send_row && sum_recv_row, "NULL argument");
+  CHECK_ARG(world >= 1 && rank >= 0 && rank < world, "bad world / rank");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
+  const int64_t rows = (int64_t)(c->esz == 4 ? 2 : 1);  // rows of T holding ld doubles
+  for (int32_t p = 0; p < world; ++p) {
+    if (p == rank) {
+      CHECK_ARG(sum_send_row[p] < 0 && sum_recv_row[p] < 0, "rank %d: no sum rows to itself", rank);
+      continue;
+    }
+    CHECK_ARG(sum_send_row[p] >= 0 && sum_recv_row[p] >= 0, "peer %d: sum rows missing", p);
+    CHECK_ARG(sum_send_row[p] + rows <= std::max<int64_t>(c->n_send, 0) && sum_recv_row[p] + rows <= c->n_halo,
+              "peer %d: sum rows past the send (%lld) / halo (%lld) buffers (dopt_set_halo first)", p,
+              (long long)c->n_send, (long long)c->n_halo);
+  }
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  if ((rc = dalloc_t(&c->lg_sum_in, (size_t)world * sizeof(int64_t)))) return rc;
+  if ((rc = dalloc_t(&c->lg_sum_out, (size_t)world * sizeof(int64_t)))) return rc;
+  HIPOK(hipMemcpy(c->lg_sum_in, sum_recv_row, (size_t)world * sizeof(int64_t), hipMemcpyHostToDevice));
+  HIPOK(hipMemcpy(c->lg_sum_out, sum_send_row, (size_t)world * sizeof(int64_t), hipMemcpyHostToDevice));
+  c->lg_in_h.assign(sum_recv_row, sum_recv_row + world);
+  c->lg_out_h.assign(sum_send_row, sum_send_row + world);
+  c->lg_world = world;
+  c->lg_rank = rank;
+  return DOPT_OK;
+}
+
+namespace {
+int lagged_ready(dopt_ctx* c) {
+  if (c->split || c->mean_mix || !c->have_topo)
+    return fail(DOPT_ERR_UNSUPPORTED, "lagged rounds: row-resident contexts with CSR mixing only");
+  if (c->lg_world > 1 && (int64_t)c->lg_in_h.size() != c->lg_world)
+    return fail(DOPT_ERR_STATE, "lagged rounds: dopt_lagged_exchange_layout first");
+  if (!c->lg_sum_in) {  // world 1 without a layout call: one rank, no peer rows
+    const int64_t self = -1;
+    int rc;
+    if ((rc = dalloc_t(&c->lg_sum_in, sizeof(int64_t)))) return rc;
+    if ((rc = dalloc_t(&c->lg_sum_out, sizeof(int64_t)))) return rc;
+    HIPOK(hipMemcpy(c->lg_sum_in, &self, sizeof(int64_t), hipMemcpyHostToDevice));
+    HIPOK(hipMemcpy(c->lg_sum_out, &self, sizeof(int64_t), hipMemcpyHostToDevice));
+  }
+  if (c->lg_alloc_n == c->n && c->lg_alloc_ld == c->ld) return DOPT_OK;
+  mixcs_shape(c->dtype, c->n, (int32_t)c->nchs, &c->lg_ncb, &c->lg_r, &c->lg_ng);
+  int rc;
+  for (int k = 0; k < 2; ++k) {
+    if ((rc = dalloc_t(&c->lg_own[k], (size_t)c->ld * sizeof(double)))) return rc;
+    HIPOK(hipMemsetAsync(c->lg_own[k], 0, (size_t)c->ld * sizeof(double), c->stream));
+    if ((rc = dalloc_t(&c->lg_cons[k], (size_t)std::max<int64_t>(1, c->lg_ncb * c->n) * sizeof(double)))) return rc;
+  }
+  if ((rc = dalloc_t(&c->lg_part, (size_t)c->lg_ng * c->ld * sizeof(double)))) return rc;
+  if ((rc = dalloc_t(&c->lg_cnt, (size_t)std::max(16, c->lg_ncb) * sizeof(unsigned)))) return rc;
+  HIPOK(hipMemsetAsync(c->lg_cnt, 0, (size_t)std::max(16, c->lg_ncb) * sizeof(unsigned), c->stream));
+  c->lg_alloc_n = c->n;
+  c->lg_alloc_ld = c->ld;
+  return DOPT_OK;
+}
+
+// The lagged tail's loss pass: loss of every local objective row at the current average -> slab B,
+// and with two_points also at the previous average -> slab A (one pass over the rows).
+int lagged_loss_pass(dopt_ctx* c, int two_points) {
   if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
   if (c->split) return fail(DOPT_ERR_UNSUPPORTED, "lagged metrics: row-resident contexts only");
   RoundArgs a = base_args(c);
@@ -2396,24 +2451,115 @@ int dopt_phase_loss_pass(dopt_ctx* c, int two_points) {
   return DOPT_OK;
 }
 
-int dopt_phase_metrics_pass(dopt_ctx* c, uint32_t flags) {
+McsArgs lagged_args(dopt_ctx* c, const double* own_in, double* own_out, double* cons_part) {
+  McsArgs m;
+  memset(&m, 0, sizeof(m));
+  m.part = c->lg_part;
+  m.cnt = c->lg_cnt;
+  m.ng = c->lg_ng;
+  m.ncb = c->lg_ncb;
+  m.r = c->lg_r;
+  m.world = c->lg_world;
+  m.rank = c->lg_rank;
+  m.own_in = own_in;
+  m.own_out = own_out;
+  m.sum_in = c->lg_sum_in;
+  m.sum_out = c->lg_sum_out;
+  m.cons_part = cons_part;
+  m.n_div = (double)n_div(c);
+  return m;
+}
+}  // namespace
+
+int dopt_lagged_begin(dopt_ctx* c, int64_t batch) {
   CHECK_ARG(c, "ctx is NULL");
-  if (c->split) {
-    int rc;
-    if ((rc = ensure_split(c))) return rc;
-    return split_metrics(c, c->xs[c->cur], c->xbar[c->xb], false, flags & DOPT_RUN_CONSENSUS,
-                         flags & DOPT_RUN_OBJECTIVE);
-  }
-  return metrics_pass(c, c->xs[c->cur], c->xbar[c->xb], false, flags & DOPT_RUN_CONSENSUS,
-                      flags & DOPT_RUN_OBJECTIVE);
+  int rc;
+  if ((rc = dopt_phase_begin(c, batch))) return rc;
+  if ((rc = lagged_ready(c))) return rc;
+  if ((rc = dopt_phase_gather(c))) return rc;  // send rows of x_0 (later rounds: k_mixcs writes them)
+  // this rank's column sums of x_0 -> lg_own[0] and the send buffer's sum rows
+  HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur], c->n, c->ld, (int32_t)c->nchs, kRowsPerGroup, c->part, nullptr,
+                              c->stream));
+  HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nchs, nullptr, nullptr, 0.0, 0,
+                            c->stream, c->lg_own[0]));
+  const McsArgs m = lagged_args(c, c->lg_own[0], nullptr, nullptr);
+  if (c->lg_world > 1) HIPOK(launch_xbar_ranks(c->dtype, m, c->halo, c->ld, (int32_t)c->nchs, nullptr, c->send, c->stream));
+  c->lg = 0;
+  return DOPT_OK;
 }
 
-int dopt_phase_metrics(dopt_ctx* c, uint32_t flags, int include_xnorm, double* out_dev) {
-  CHECK_ARG(c && out_dev, "NULL argument");
-  const bool cons = flags & DOPT_RUN_CONSENSUS, loss = flags & DOPT_RUN_OBJECTIVE;
-  HIPOK(launch_history(c->dtype, cons ? c->slab_cons : nullptr, loss ? c->slab_loss : nullptr, c->n,
-                       c->loss_groups, c->xbar[c->xb], c->ld, (int32_t)c->nchs, loss && include_xnorm, out_dev,
-                       c->stream));
+int dopt_lagged_grad(dopt_ctx* c, int64_t t, double eta0, int64_t batch, const int32_t* idx, double lam_grad,
+                     uint32_t metric_flags) {
+  int rc;
+  if ((rc = dopt_phase_set_step(c, t, eta0))) return rc;
+  return dopt_phase_grad(c, batch, idx, lam_grad, metric_flags);
+}
+
+int dopt_lagged_mix(dopt_ctx* c, int64_t t, double eta0, int consensus, double* cons_out, double* xnorm_out,
+                    double* loss_out) {
+  CHECK_ARG(c, "ctx is NULL");
+  int rc;
+  if ((rc = lagged_ready(c))) return rc;
+  if (!c->G) return fail(DOPT_ERR_STATE, "gradient phase missing");
+  RoundArgs a = base_args(c);
+  a.x_old = c->xs[c->cur];
+  a.x_new = c->xs[c->cur ^ 1];
+  a.eta = eta0 / sqrt((double)(t + 1));  // trainer.py:138-140
+  a.sptr = c->n_send > 0 ? c->sptr : nullptr;
+  a.sslot = c->n_send > 0 ? c->sslot : nullptr;
+  a.send = c->send;
+  a.xbar_out = c->xbar[c->xb ^ 1];
+  if (c->ph_interior) a.interior = c->interior;  // stepped by the gradient kernel already
+  c->ph_interior = false;
+  a.nchunks = (int32_t)c->nchs;  // k_mixcs walks state chunks
+  const int par = (int)(c->lg & 1);
+  const McsArgs m = lagged_args(c, c->lg_own[par], c->lg_own[par ^ 1], consensus ? c->lg_cons[par] : nullptr);
+  // history[g-2]: the consensus partials of x_{g-1} (the previous mix), the losses at xbar_{g-1} (this
+  // round's gradient pass), ||xbar_{g-1}||^2
+  const bool any = cons_out || xnorm_out || loss_out;
+  FoldArgs f;
+  memset(&f, 0, sizeof(f));
+  f.sc = c->lg_cons[par ^ 1];
+  f.nc = (int64_t)c->lg_ncb * c->n;
+  f.sl = c->slab_loss;
+  f.nl = c->slab_n[0];
+  f.xbar = c->xbar[c->xb];
+  f.out_c = cons_out;
+  f.out_l = loss_out;
+  f.out_q = xnorm_out;
+  HIPOK(launch_mixcs(c->dtype, a, c->G, (int)c->n, m, any ? &f : nullptr, c->stream));
+  c->xb ^= 1;
+  c->cur ^= 1;
+  c->lg += 1;
+  c->S_ext = nullptr;
+  c->send_fresh = c->n_send > 0;
+  return DOPT_OK;
+}
+
+int dopt_lagged_tail(dopt_ctx* c, int consensus, int objective, double* cons1, double* xnorm1, double* loss1,
+                     double* cons2, double* xnorm2, double* loss2) {
+  CHECK_ARG(c, "ctx is NULL");
+  int rc;
+  if ((rc = lagged_ready(c))) return rc;
+  const int par = (int)(c->lg & 1);
+  // xbar_G from every rank's sums of x_G (the exchange that preceded this call)
+  const McsArgs m = lagged_args(c, c->lg_own[par], nullptr, nullptr);
+  HIPOK(launch_xbar_ranks(c->dtype, m, c->halo, c->ld, (int32_t)c->nchs, c->xbar[c->xb ^ 1], nullptr, c->stream));
+  c->xb ^= 1;
+  if (consensus) {
+    HIPOK(launch_cons(c->dtype, c->xs[c->cur], c->xbar[c->xb], c->n, c->ld, (int32_t)c->nchs, c->slab_cons,
+                      c->stream));
+    c->cons_n = (c->n + 63) / 64;
+  }
+  const bool two = c->lg >= 2;
+  if (objective && (rc = lagged_loss_pass(c, two ? 1 : 0))) return rc;
+  // history[G-1]: consensus of x_G, loss at xbar_G (slab B), ||xbar_G||^2
+  HIPOK(launch_fold(c->dtype, consensus ? c->slab_cons : nullptr, c->cons_n, objective ? c->slab_loss_b : nullptr,
+                    c->slab_n[1], c->xbar[c->xb], c->ld, (int32_t)c->nchs, cons1, loss1, xnorm1, c->stream));
+  // history[G-2]: consensus partials of x_{G-1} (the last mix), loss at xbar_{G-1} (slab A), ||xbar_{G-1}||^2
+  if (two && (cons2 || xnorm2 || loss2))
+    HIPOK(launch_fold(c->dtype, c->lg_cons[par ^ 1], (int64_t)c->lg_ncb * c->n, objective ? c->slab_loss : nullptr,
+                      c->slab_n[0], c->xbar[c->xb ^ 1], c->ld, (int32_t)c->nchs, cons2, loss2, xnorm2, c->stream));
   return DOPT_OK;
 }
 

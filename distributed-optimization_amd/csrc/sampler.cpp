@@ -515,6 +515,7 @@ class ParAdvance {
     segs_.reserve((size_t)nseg_);
     for (int64_t j = 0; j < nseg_; ++j) segs_.emplace_back(new ParSeg());
     snap_ready_.store(1, std::memory_order_release);
+    ahead_ = std::max<int64_t>(4, 4 * (int64_t)threads);
     try {
       prod_ = std::thread([this] { produce(); });
       for (int h = 0; h < threads; ++h) th_.emplace_back([this] { work(); });
@@ -554,6 +555,7 @@ class ParAdvance {
             break;
           }
         ktrue = s->kend;
+        release(j);
         continue;
       }
       // from the true state until it meets the segment's recorded run (or to the segment's end),
@@ -621,6 +623,7 @@ class ParAdvance {
       if (last >= 0) break;
       if (!met) {  // no meeting point (or a segment past the planned ones): the stitch's run is the truth
         ktrue = k;
+        release(j);
         continue;
       }
       for (int64_t e : s->pe)
@@ -629,6 +632,7 @@ class ParAdvance {
           break;
         }
       ktrue = s->kend;
+      release(j);
     }
     stop_.store(true, std::memory_order_release);
     // numpy's state: the key of the block holding the last word, pos just past it (1 .. 624)
@@ -657,10 +661,29 @@ class ParAdvance {
     memcpy(key, snaps_.data() + (size_t)j * kN, sizeof(uint32_t) * kN);
     for (int64_t x = j * seg_; x < b; ++x) twist_key(key);
   }
+  // Segment j is stitched: its k records and permutation ends are dead (its kept values stay while
+  // pieces point into them), and the filter threads may run that much further ahead.
+  void release(int64_t j) {
+    if (j < nseg_) {
+      ParSeg& s = *segs_[(size_t)j];
+      while (!s.done.load(std::memory_order_acquire) && j > 0 && !stop_.load(std::memory_order_acquire)) {
+        // a segment the stitch finished itself may still be filtering: its thread owns the buffers
+        std::this_thread::yield();
+      }
+      std::vector<uint16_t>().swap(s.pre);
+      std::vector<int64_t>().swap(s.pe);
+    }
+    stitched_.store(j + 1, std::memory_order_release);
+  }
   void work() {
     for (;;) {
       const int64_t j = next_.fetch_add(1);
       if (j >= nseg_) return;
+      // bounded run-ahead: at most ahead_ segments past the stitch hold their buffers
+      while (j >= stitched_.load(std::memory_order_acquire) + ahead_) {
+        if (stop_.load(std::memory_order_acquire)) return;
+        std::this_thread::yield();
+      }
       while (snap_count() <= j) {
         if (stop_.load(std::memory_order_acquire)) return;
         std::this_thread::yield();
@@ -722,7 +745,8 @@ class ParAdvance {
   std::vector<std::unique_ptr<std::vector<uint32_t>>> owns_;  // the stitch's kept values (pieces point in)
   std::vector<uint32_t> key0_, snaps_;
   std::vector<std::unique_ptr<ParSeg>> segs_;
-  std::atomic<int64_t> snap_ready_{0}, next_{0};
+  std::atomic<int64_t> snap_ready_{0}, next_{0}, stitched_{0};
+  int64_t ahead_ = 8;  // segments the filter threads may run past the stitch (set from the thread count)
   std::atomic<bool> stop_{false};
   std::thread prod_;
   std::vector<std::thread> th_;
@@ -743,18 +767,53 @@ int64_t uniform_drawing(int64_t n_workers, const int64_t* rows, int64_t max_m, i
   return drawing;
 }
 
-int par_threads() { return (int)env_i64("DOPT_MT_THREADS", std::min(12, std::max(0, affinity_cpus() - 4))); }
+// filter threads: min(12, the rank's CPUs - 4), the CPUs split over the ranks of this node when
+// every rank sees them all (torchrun: LOCAL_WORLD_SIZE ranks, one affinity set)
+int par_threads() {
+  const int64_t local = std::max<int64_t>(1, env_i64("LOCAL_WORLD_SIZE", 1));
+  const int64_t cpus = affinity_cpus() / local;
+  return (int)env_i64("DOPT_MT_THREADS", std::min<int64_t>(12, std::max<int64_t>(0, cpus - 4)));
+}
 
 bool par_worth(int64_t T, int64_t drawing, int64_t m) {  // >= 3 segments of words
   return (double)T * drawing * (m - 1) * 1.38 >= 3.0 * (double)(env_i64("DOPT_MT_SEG_BLOCKS", 4096) * kN);
 }
 }  // namespace
 
+static int choice_rounds_parallel_part(uint32_t key[624], int32_t* pos, int64_t T, int64_t n, const int64_t* rows,
+                                       int64_t b, int32_t* out, int64_t max_m, int64_t drawing, int threads);
+
+// Minibatch draws over many rounds: the parallel filter keeps every kept word's value until the
+// shuffles have read them (~4 bytes per word, ~705 words per permutation of 512), so the rounds go
+// in parts of at most kKeepSegs segments of words each (~330 MB of values per part).
+constexpr int64_t kKeepSegs = 32;
 static int choice_rounds_parallel(uint32_t key[624], int32_t* pos, int64_t T, int64_t n, const int64_t* rows,
                                   int64_t b, int32_t* out, int64_t max_m) {
   const int64_t drawing = uniform_drawing(n, rows, max_m, 3);
   const int threads = par_threads();
   if (drawing <= 0 || threads < 2 || !par_worth(T, drawing, max_m)) return 1;
+  const double words_per_round = (double)drawing * (double)(max_m - 1) * 1.38;
+  const double cap_words = (double)kKeepSegs * (double)env_i64("DOPT_MT_SEG_BLOCKS", 4096) * kN;
+  const int64_t per = std::max<int64_t>(1, (int64_t)(cap_words / std::max(1.0, words_per_round)));
+  uint32_t kl[kN];  // the state advances part by part; numpy's copy only when every part is done
+  int32_t pl = *pos;
+  memcpy(kl, key, sizeof(kl));
+  for (int64_t t0 = 0; t0 < T;) {
+    int64_t tp = std::min(per, T - t0);
+    if (T - t0 - tp > 0 && !par_worth(T - t0 - tp, drawing, max_m)) tp = T - t0;  // no short tail part
+    // (every part is long enough: per rounds hold kKeepSegs segments of words, a merged tail more)
+    const int rc = choice_rounds_parallel_part(kl, &pl, tp, n, rows, b, out + t0 * n * b, max_m, drawing, threads);
+    if (rc) return rc;
+    t0 += tp;
+  }
+  memcpy(key, kl, sizeof(kl));
+  *pos = pl;
+  return DOPT_OK;
+}
+
+static int choice_rounds_parallel_part(uint32_t key[624], int32_t* pos, int64_t T, int64_t n, const int64_t* rows,
+                                       int64_t b, int32_t* out, int64_t max_m, int64_t drawing, int threads) {
+  if (T <= 0) return DOPT_OK;
   uint32_t key1[kN];
   int32_t pos1 = *pos;
   memcpy(key1, key, sizeof(key1));

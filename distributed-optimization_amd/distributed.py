@@ -37,10 +37,27 @@ import _dopt
 
 DEFAULT_TIMEOUT_S = 300.0
 # Column chunks of the complete graph's row-space pass across ranks: each chunk's
-# sums are all-reduced while the next chunk streams, but every chunk boundary costs a launch tail --
-# C5 at RCCL world 1 (round 3): 1 chunk 11.30 ms per round, 4 chunks 11.62 ms, i.e. ~0.1 ms per
-# boundary, more than an 8 MB all-reduce over xGMI is expected to expose.  So one chunk by default.
+# sums are all-reduced while the next chunk streams, but every chunk boundary costs a launch tail.
 RS_CHUNKS = 1
+# The model that picks the chunk count per world size ("Column chunks across ranks"):
+# a round is pass(N) + boundary * (K - 1) + allreduce(S / K, N), where the ring all-reduce of S bytes
+# over N ranks on xGMI costs ALPHA + 2 (N - 1) / N * S / BUSBW and only the last chunk's is exposed.
+AR_ALPHA_S = 30e-6       # per all-reduce latency (8 ranks, ring steps, launch): assumed
+AR_BUSBW = 100e9         # RCCL bus bandwidth for MB-sized messages over xGMI, bytes/s: assumed
+RS_BOUNDARY_S = 0.1e-3   # measured cost of one extra chunk boundary (C5, world 1, round 3)
+
+
+def rs_chunks_for(world, sum_bytes=8 << 20, max_chunks=8):
+    """Chunk count K minimising the modelled exposed time (K - 1) boundaries + the last chunk's
+    all-reduce; 1 at world 1 (nothing to overlap).  With the constants above it is 1 for every
+    world size up to 8: the boundary (0.1 ms) costs more than the all-reduce time it hides."""
+    if world <= 1:
+        return 1
+
+    def exposed(k):
+        return (k - 1) * RS_BOUNDARY_S + AR_ALPHA_S + 2.0 * (world - 1) / world * (sum_bytes / k) / AR_BUSBW
+
+    return min(range(1, max_chunks + 1), key=exposed)
 
 
 class CollectiveError(RuntimeError):
@@ -66,11 +83,12 @@ def init_process_group(backend, timeout=None, **kw):
 
     import torch.distributed as dist
 
+    kw.setdefault("timeout", datetime.timedelta(seconds=timeout if timeout is not None else timeout_seconds()))
     if backend == "nccl" and os.environ.get("DOPT_NCCL_HIPRI", "1") != "0":
         opts = dist.ProcessGroupNCCL.Options()
         opts.is_high_priority_stream = True
+        opts._timeout = kw["timeout"]  # the options carry the job's bound too (no override warning)
         kw["pg_options"] = opts
-    kw.setdefault("timeout", datetime.timedelta(seconds=timeout if timeout is not None else timeout_seconds()))
     dist.init_process_group(backend, **kw)
 
 
@@ -232,6 +250,67 @@ def build_plan(topo, world, rank):
                     w=topo.w[e0:e1].copy())
 
 
+@dataclass
+class ExchangeLayout:
+    """Send / halo buffer rows of the lagged schedule's exchange (round 4): per peer p in rank order
+    (p != rank), p's plan rows, then `ks` rows holding this rank's (send) or p's (halo) float64 column
+    sums of the current iterates (ks = 8 / element bytes: one row of float64, two of float32).  One
+    all-to-all-v per round then moves the halo rows and the sums every rank needs for xbar; every
+    peer gets a block (the sums), so every pair of ranks exchanges each round."""
+    ks: int
+    send_sizes: list        # [world] rows per peer block of the send buffer
+    recv_sizes: list        # [world] rows per peer block of the halo buffer
+    send_rows: np.ndarray   # [n_send] buffer row of plan send slot k
+    halo_rows: np.ndarray   # [n_halo] buffer row of plan halo row j
+    sum_send_row: np.ndarray  # [world] send-buffer row of the sums for peer p (-1: self)
+    sum_recv_row: np.ndarray  # [world] halo-buffer row of peer p's sums (-1: self)
+
+    @property
+    def n_send_rows(self):
+        return int(sum(self.send_sizes))
+
+    @property
+    def n_recv_rows(self):
+        return int(sum(self.recv_sizes))
+
+    def send_ids(self, plan):
+        """Local worker of every send-buffer row, -1 on the sum rows (dopt_set_halo)."""
+        ids = np.full(self.n_send_rows, -1, dtype=np.int32)
+        ids[self.send_rows] = plan.send_ids
+        return ids
+
+    def local_col(self, plan):
+        """The plan's local CSR columns with halo columns moved to their buffer rows."""
+        col = plan.col.astype(np.int64).copy()
+        h = col >= plan.n_local
+        col[h] = plan.n_local + self.halo_rows[col[h] - plan.n_local]
+        return col.astype(np.int32)
+
+
+def exchange_layout(plan, ks):
+    """ExchangeLayout of a HaloPlan with ks sum rows per peer (ks = 0: the plan's rows only)."""
+    W, r = plan.world, plan.rank
+
+    def shift(p):  # sum rows of the peer blocks before peer p's rows
+        p = np.asarray(p)
+        return ks * (p - (p > r))
+
+    send_sizes = [0 if p == r else int(plan.send_off[p + 1] - plan.send_off[p]) + ks for p in range(W)]
+    recv_sizes = [0 if p == r else int(plan.recv_off[p + 1] - plan.recv_off[p]) + ks for p in range(W)]
+    k = np.arange(len(plan.send_ids))
+    send_rows = k + shift(np.searchsorted(plan.send_off, k, side="right") - 1)
+    j = np.arange(plan.n_halo)
+    halo_rows = j + shift(np.searchsorted(plan.recv_off, j, side="right") - 1)
+    ps = np.arange(W)
+    sum_send = np.where(ps == r, -1, plan.send_off[1:] + shift(ps)).astype(np.int64)
+    sum_recv = np.where(ps == r, -1, plan.recv_off[1:] + shift(ps)).astype(np.int64)
+    if ks == 0:
+        sum_send[:] = -1
+        sum_recv[:] = -1
+    return ExchangeLayout(ks, send_sizes, recv_sizes, send_rows.astype(np.int64), halo_rows.astype(np.int64),
+                          sum_send, sum_recv)
+
+
 class HaloExchange:
     """The per-round halo transfer of a HaloPlan: rows send[send_off[p]:send_off[p+1]] go to
     peer p, rows halo[recv_off[p]:recv_off[p+1]] come from peer p.
@@ -248,18 +327,26 @@ class HaloExchange:
     waits on the host with the job's timeout, so a peer that never sends ends this rank with a
     CollectiveError naming it."""
 
-    def __init__(self, plan, send, halo, group=None, device_comm=False):
+    def __init__(self, plan, send, halo, group=None, device_comm=False, layout=None):
+        """layout: an ExchangeLayout (the blocks carry column-sum rows too), or None: the plan's rows."""
         import torch.distributed as dist
 
         self.dist, self.plan, self.group, self.device_comm = dist, plan, group, device_comm
         self.send, self.halo = send, halo
-        self.peers = plan.peers()
         self.rank = plan.rank
         # the RCCL all-to-all: at world > 1, or at world 1 with the collectives forced (the one-GPU
         # box runs the call then, with zero rows or rows to itself)
         self.collective = device_comm and (plan.world > 1 or os.environ.get("DOPT_FORCE_COLLECTIVES") == "1")
-        self.send_sizes = [int(plan.send_off[p + 1] - plan.send_off[p]) for p in range(plan.world)]
-        self.recv_sizes = [int(plan.recv_off[p + 1] - plan.recv_off[p]) for p in range(plan.world)]
+        if layout is None:
+            self.send_sizes = [int(plan.send_off[p + 1] - plan.send_off[p]) for p in range(plan.world)]
+            self.recv_sizes = [int(plan.recv_off[p + 1] - plan.recv_off[p]) for p in range(plan.world)]
+        else:
+            self.send_sizes, self.recv_sizes = list(layout.send_sizes), list(layout.recv_sizes)
+        self.send_off = np.concatenate([[0], np.cumsum(self.send_sizes)]).astype(np.int64)
+        self.recv_off = np.concatenate([[0], np.cumsum(self.recv_sizes)]).astype(np.int64)
+        self.peers = [p for p in range(plan.world) if p != self.rank and (self.send_sizes[p] or self.recv_sizes[p])]
+        self.ns, self.nr = int(self.send_off[-1]), int(self.recv_off[-1])
+        self.what = f"all_to_all_single of {self.ns} rows out / {self.nr} halo rows in (peers {self.peers})"
 
     def disable(self):
         """No exchange at all (complete-graph mixing on every rank: no rows move)."""
@@ -268,10 +355,9 @@ class HaloExchange:
 
     def _ops(self, send, halo):
         """(kind, peer, buffer, rows) for every transfer, sends first per peer, peers ascending."""
-        P = self.plan
         for p in self.peers:
-            s0, s1 = P.send_off[p], P.send_off[p + 1]
-            r0, r1 = P.recv_off[p], P.recv_off[p + 1]
+            s0, s1 = self.send_off[p], self.send_off[p + 1]
+            r0, r1 = self.recv_off[p], self.recv_off[p + 1]
             if s1 > s0:
                 yield "isend", p, send[s0:s1], int(s1 - s0)
             if r1 > r0:
@@ -280,10 +366,9 @@ class HaloExchange:
     def start(self):
         dist = self.dist
         if self.collective:
-            ns, nr = sum(self.send_sizes), sum(self.recv_sizes)
-            w = dist.all_to_all_single(self.halo[:nr], self.send[:ns], output_split_sizes=self.recv_sizes,
+            w = dist.all_to_all_single(self.halo[:self.nr], self.send[:self.ns], output_split_sizes=self.recv_sizes,
                                        input_split_sizes=self.send_sizes, group=self.group, async_op=True)
-            return [(w, f"all_to_all_single of {ns} rows out / {nr} halo rows in (peers {self.peers})")]
+            return [(w, self.what)]
         if not self.peers or self.device_comm:
             return None
         send = self.send.cpu()
@@ -314,7 +399,7 @@ class DistributedDSGD:
         the row count of the objective data (all shards, or the X_full slices loaded with
         Engine.load_objective_data when obj_sep).  `rs_chunks`: column chunks of the row-space
         pass (complete graph), each chunk's sums all-reduced while the next one streams
-        (default: 1 at world size 1, else RS_CHUNKS)."""
+        (default: 1 at world size 1, else rs_chunks_for(world))."""
         self.obj_sep = obj_sep
         import torch
         import torch.distributed as dist
@@ -328,16 +413,21 @@ class DistributedDSGD:
         ld, esz = engine.layout()
         self.ld = ld
         tdt = torch.float32 if esz == 4 else torch.float64
-        self.halo = torch.zeros((max(1, plan.n_halo), ld), dtype=tdt, device=self.dev)
-        self.send = torch.zeros((max(1, len(plan.send_ids)), ld), dtype=tdt, device=self.dev)
+        # CSR mixing: the exchange also carries every rank's column sums (the lagged schedule's
+        # xbar, no all-reduce per round); ks rows of T per peer hold ld float64 sums
+        self.layout = exchange_layout(plan, (8 // esz) if (mean is None and plan.world > 1) else 0)
+        lay = self.layout
+        self.halo = torch.zeros((max(1, lay.n_recv_rows), ld), dtype=tdt, device=self.dev)
+        self.send = torch.zeros((max(1, lay.n_send_rows), ld), dtype=tdt, device=self.dev)
         self.sum = torch.zeros(ld, dtype=torch.float64, device=self.dev)
-        self.exchange = HaloExchange(plan, self.send, self.halo, group, self.device_comm)
-        self.rs_chunks = int(rs_chunks) if rs_chunks else (1 if self._solo() else RS_CHUNKS)
+        self.exchange = HaloExchange(plan, self.send, self.halo, group, self.device_comm, layout=lay)
+        self.rs_chunks = int(rs_chunks) if rs_chunks else (1 if self._solo() else rs_chunks_for(plan.world))
         engine.set_partition(self.n_global, self.rows_global)
         if mean is None:
-            engine.set_halo(plan.n_halo, self.halo.data_ptr(), plan.send_ids, self.send.data_ptr())
-            engine.set_topology(plan.row_ptr, plan.col, plan.w)
-            self._peers = plan.peers()
+            engine.set_halo(lay.n_recv_rows, self.halo.data_ptr(), lay.send_ids(plan), self.send.data_ptr())
+            engine.set_topology(plan.row_ptr, lay.local_col(plan), plan.w)
+            engine.lagged_exchange_layout(plan.world, plan.rank, lay.sum_send_row, lay.sum_recv_row)
+            self._peers = self.exchange.peers
         else:
             engine.set_halo(0, None, np.zeros(0, np.int32), None)
             engine.set_mixing_mean(mean[0], mean[1])
@@ -558,25 +648,31 @@ class DistributedDSGD:
                     pipelined=False):
         """Rounds with CSR mixing whose metrics ride the gradient pass (full shards, or
         minibatches taken inside a pass over every row); history[t] = metrics of x_{t+1}.
-        Round g (counted from the start of the chain; one call = one chain unless pipelined),
-        all on the engine stream except the two transfers:
+        Round g (counted from the start of the chain; one call = one chain unless pipelined):
 
-          exchange(send rows of x_g) ------------------------------------------.
-          colsum(x_g) [+ fold of history[g-2] / loss of history[g-3]] -> all-reduce --.
-          grad(x_g) + loss of every row at xbar_{g-1} ------------------------------+-+-> mix
-                                                      mix: xbar_g, consensus of x_g, x_{g+1},
-                                                           send rows of x_{g+1}
+          exchange: halo rows of x_g + every rank's column sums of x_g (ONE all-to-all-v) ---.
+          lagged_grad: gradient pass of x_g + loss of every row at xbar_{g-1} -------------+--> lagged_mix
+          lagged_mix: xbar_g (rank-ordered sums), consensus of x_g, x_{g+1} and its send rows,
+                      the column sums of x_{g+1} into the send buffer, fold of history[g-2]
 
-        Four kernels per round and no collective between two of them; after the last round
-        of a chain (the tail) xbar_T, the consensus of x_T and one pass for the losses at
-        xbar_{T-1}, xbar_T."""
+        Two kernels, two engine calls and one collective per round (round 4; round 3 had four
+        kernels, two collectives and five engine calls); history row t is complete once round t + 2's
+        mix has folded it.  After the last round of a chain (the tail): one more exchange for the
+        sums of x_T, then xbar_T, the consensus of x_T and one pass for the losses at xbar_{T-1} and
+        xbar_T (dopt_lagged_tail)."""
         torch, eng = self.torch, self.eng
         xnorm = self.plan.rank == 0  # ||xbar||^2 is global already: count it once
         obj_f = _dopt.RUN_OBJECTIVE if objective else 0
         flags = (objective, consensus)
         # every rank makes the same calls, so all see the same chain state
-        cont = pipelined and eng.phase_chain(False) and getattr(self, "_chain", None) is not None \
-            and self._chain["flags"] == flags
+        was_open = pipelined and eng.phase_chain(False) and getattr(self, "_chain", None) is not None
+        if was_open and self._chain["flags"] != flags:
+            # the open chain owes history rows with the other flags: refuse, as the row-space rounds and
+            # dopt_run_dsgd_pipelined on one context do (ADVICE r3); the chain stays open
+            eng.phase_chain(True)
+            raise ValueError("pipelined run: the open chain owes the metrics of its last iterates with other "
+                             "objective / consensus flags; continue or close it (T = 0) with the same flags")
+        cont = was_open
         if not cont:
             if not pipelined and T == 0:
                 return (np.zeros(0) if objective else None), (np.zeros(0) if consensus else None)
@@ -584,6 +680,7 @@ class DistributedDSGD:
         ch = self._chain
         G0, G1 = ch["g"], ch["g"] + T
         tail = not pipelined or T == 0
+        exchange = self.exchange
         with torch.cuda.stream(self.stream):
             cap = max(1, G1)
             if ch["hist"] is None or ch["hist"].shape[0] < cap:  # history rows by global entry, grown by doubling
@@ -598,45 +695,27 @@ class DistributedDSGD:
             def at(e, k, want=True):  # device address of history row e, column k, or None
                 return base + (3 * e + k) * 8 if want and 0 <= e < G1 else None
 
-            def colsum_fold(g):  # column sums of x_g; history[g-2] (consensus, ||xbar||^2), [g-3] (loss)
-                eng.phase_colsum_fold(self.sum.data_ptr(), at(g - 2, 0, consensus), at(g - 2, 2, objective and xnorm),
-                                      at(g - 3, 1, objective))
-
             if not cont:
-                eng.phase_begin(batch)
-                eng.phase_gather()  # send rows of x_0; later rounds get them from the mix kernel
+                eng.lagged_begin(batch)  # send rows and column sums of x_0
+            lagged_grad, lagged_mix = eng.lagged_grad, eng.lagged_mix
             for g in range(G0, G1):
                 h = g - G0
-                pending = self._start_exchange()
-                colsum_fold(g)
-                ar = self._all_reduce_start(self.sum)
-                # the device sampler's counter (sampling='device') and the step size: the gradient
-                # kernel mixes and steps the workers whose rows need no halo (the mix skips them)
-                eng.phase_set_step(t0 + h, eta0)
+                pending = exchange.start()
                 # loss at xbar_{g-1} (history[g-2]); at g = 1 it is the loss of x_0, which no history row
                 # holds -- taken anyway so round 1's gradient dots reduce in the same (paired) butterfly
                 # as the fused single-context round 1, whose pass carries the metrics of x_1
-                eng.phase_grad(batch, lam_grad, obj_f if g >= 1 else 0,
-                               idx=None if idx is None else idx[h])
-                if ar is not None:
-                    ar.wait()
-                self._finish_exchange(pending)
-                eng.phase_mix_lagged(t0 + h, eta0, self.sum.data_ptr(), consensus)
+                lagged_grad(t0 + h, eta0, batch, lam_grad, obj_f if g >= 1 else 0, None if idx is None else idx[h])
+                if pending is not None:
+                    exchange.finish(pending)
+                e = g - 2
+                lagged_mix(t0 + h, eta0, consensus, at(e, 0, consensus), at(e, 2, objective and xnorm),
+                           at(e, 1, objective))
             if tail and G1 > 0:
-                colsum_fold(G1)
-                ar = self._all_reduce_start(self.sum)
-                if ar is not None:
-                    ar.wait()
-                eng.phase_xbar(self.sum.data_ptr())  # xbar_T
-                if consensus:
-                    eng.phase_cons()
-                if objective:  # losses at xbar_T (history[T-1]) and xbar_{T-1} (history[T-2])
-                    eng.phase_loss_pass(G1 >= 2)
-                eng.phase_fold(at(G1 - 1, 0, consensus), at(G1 - 1, 2, objective and xnorm),
-                               at(G1 - 1, 1, objective), 1)
-                if objective and G1 >= 2:
-                    eng.phase_fold(None, None, at(G1 - 2, 1), 0)
-            upto = G1 if tail else max(ch["done"], G1 - 3)  # history rows complete on every rank
+                exchange.finish(exchange.start())  # every rank's column sums of x_T
+                eng.lagged_tail(consensus, objective,
+                                (at(G1 - 1, 0, consensus), at(G1 - 1, 2, objective and xnorm), at(G1 - 1, 1, objective)),
+                                (at(G1 - 2, 0, consensus), at(G1 - 2, 2, objective and xnorm), at(G1 - 2, 1, objective)))
+            upto = G1 if tail else max(ch["done"], G1 - 2)  # history rows complete on every rank
             done = ch["done"]
             if upto > done:
                 self._all_reduce(partials[done:upto])

@@ -37,8 +37,13 @@ extern "C" {
  *      minibatches), dopt_eval_full, dopt_phase_chain / _colsum_fold / _mix_lagged / _cons /
  *      _fold / _loss_pass (lagged multi-GPU schedule), the dopt_rs_phase_* row-space calls; and
  *      one signature change: dopt_rs_phase_begin reports a 64-bit content hash (was a double
- *      checksum). */
-#define DOPT_ABI_VERSION 2
+ *      checksum).
+ *   3  round 4: the lagged multi-GPU schedule with the column sums in the halo exchange
+ *      (dopt_lagged_exchange_layout / _begin / _grad / _mix / _tail) replaces dopt_phase_colsum_fold,
+ *      dopt_phase_mix_lagged, dopt_phase_cons and dopt_phase_loss_pass; dopt_set_halo takes send_ids
+ *      of -1 (rows that carry no worker); the multi-GPU runner internals form the header's last
+ *      section. */
+#define DOPT_ABI_VERSION 3
 
 typedef struct dopt_ctx dopt_ctx;
 
@@ -222,7 +227,35 @@ int dopt_eval_objective(dopt_ctx *ctx, int problem, int64_t n, int64_t d,
                         const double *w, const double *X, const double *y, double reg,
                         double *out);
 
-/* ------------------------------------------------------------------ multi-GPU phases
+int dopt_sync(dopt_ctx *ctx);
+/* Host: raw[T x 3] (summed over ranks) -> history values, the exact formula
+ * the single-GPU path applies. */
+int dopt_finalize_metrics(int problem, int64_t T, const double *raw, int64_t n_workers,
+                          int64_t m_obj, double lam_obj, double f_opt, double *obj_out,
+                          double *cons_out);
+
+/* Full-data objective and gradient at w over every loaded row (or the separate
+ * objective dataset): f = mean loss + reg/2 ||w||^2 (obj_problems.py:3-11 /
+ * :39-44), g = mean_k c_k x_k + reg w (the full-gradient shape of
+ * obj_problems.py:22-36 / :55-69).  One pass over the data; the building block
+ * of the device f(x*) solver (solver.py) that replaces sklearn's saga at sizes
+ * sklearn cannot handle (simulator.py:32-69).  g_out may be NULL (objective only);
+ * column-blocked contexts (rows beyond the row-resident kernel) evaluate the objective only,
+ * with the direct kernels' dots pass (g_out must be NULL there). */
+int dopt_eval_full(dopt_ctx *ctx, const double *w, double reg, double *f_out, double *g_out);
+
+/* Device time of the dominant kernel (the fused round kernel) since the last call:
+ * sampled launches and their summed milliseconds, measured with HIP events on the
+ * engine's stream.  Used by bench.py for the roofline figure.
+ * dopt_set_profiling: 0 = off; k >= 1 = bracket every k-th launch with an event pair
+ * (a pair costs ~30 us of round time on MI355X, so bench.py samples). */
+int dopt_kernel_stats(dopt_ctx *ctx, int64_t *launches, double *total_ms);
+int dopt_set_profiling(dopt_ctx *ctx, int enable);
+
+/* ------------------------------------------------------------------ multi-GPU runner internals
+ * Not a user API: the calls distributed.py (DistributedDSGD / DistributedCentralized) makes to drive
+ * one rank's context through the round phases.  A user runs several GPUs through the drop-in
+ * trainers under torchrun and never calls these.
  * One process per GPU, each context holding a contiguous slice of the workers.
  * The round of trainer.py:161-193 is split into enqueue-only phases on the
  * context's stream, so the caller can interleave the collectives
@@ -285,18 +318,10 @@ int dopt_phase_metrics_pass(dopt_ctx *ctx, uint32_t flags);
 /* Raw sums -> out_dev[3] = (sum of consensus partials, sum of loss terms,
  * ||xbar||^2 if include_xnorm else 0). */
 int dopt_phase_metrics(dopt_ctx *ctx, uint32_t flags, int include_xnorm, double *out_dev);
-/* Lagged schedule (the cross-rank all-reduce of xbar off the critical path; distributed.py):
- * dopt_phase_cons: consensus partials ||x_i - xbar||^2 of the current iterates at the current
- *   average (trainer.py:185), per group of 64 workers.
- * dopt_phase_fold: *cons_out = their sum, *xnorm_out = ||xbar||^2, *loss_out = sum of loss
- *   slab `slab` (slab 0: the last dopt_phase_grad with DOPT_RUN_OBJECTIVE, or the previous
- *   average's loss of a two-point pass; slab 1: the current average's loss of the last pass);
- *   NULL outputs are skipped.
- * dopt_phase_loss_pass: loss of every local objective row at the current average -> slab 1,
- *   and with two_points also at the previous average -> slab 0 (one pass over the rows). */
-int dopt_phase_cons(dopt_ctx *ctx);
+/* dopt_phase_fold: *cons_out = the sum of the consensus slab, *xnorm_out = ||xbar||^2, *loss_out =
+ *   sum of loss slab `slab` (slab 0: the last pass with DOPT_RUN_OBJECTIVE; slab 1: unused outside
+ *   the lagged tail); NULL outputs are skipped (the row-space rounds' history rows). */
 int dopt_phase_fold(dopt_ctx *ctx, double *cons_out, double *xnorm_out, double *loss_out, int slab);
-int dopt_phase_loss_pass(dopt_ctx *ctx, int two_points);
 /* Row-space rounds on a rank's slice (complete graph with one W_ii, quadratic, full shards of
  * 1..64 rows) -- replace the serial phase order of DistributedDSGD for that case
  * (trainer.py:161-193 with the mix of trainer.py:173 through the all-reduced column sums):
@@ -325,15 +350,34 @@ int dopt_rs_phase_cols(dopt_ctx *ctx, int64_t t, double eta0, double lam_grad, c
 int dopt_rs_phase_pass(dopt_ctx *ctx, int32_t chunk, int32_t n_chunks, double *sum_dev, int64_t *col_range);
 int dopt_rs_phase_rows(dopt_ctx *ctx, int64_t t, double eta0, double lam_grad, uint32_t metric_flags);
 int dopt_rs_phase_metrics(dopt_ctx *ctx, uint32_t metric_flags);
-/* dopt_phase_colsum_fold: dopt_phase_colsum, plus (same launch) the fold of the consensus slab
- *   of the last dopt_phase_mix_lagged / dopt_phase_cons, loss slab 0 and ||xbar||^2 of the
- *   current average into the non-NULL outputs.
- * dopt_phase_mix_lagged: dopt_phase_mix, plus xbar of the iterates being mixed from their
- *   all-reduced column sums sum_dev (becomes the current average) and, with consensus, their
- *   per-worker consensus terms -- so no kernel of its own sits between two rounds. */
-int dopt_phase_colsum_fold(dopt_ctx *ctx, double *sum_dev, double *cons_out, double *xnorm_out,
-                           double *loss_out);
-int dopt_phase_mix_lagged(dopt_ctx *ctx, int64_t t, double eta0, const double *sum_dev, int consensus);
+/* The lagged schedule (round 4, ABI version 3; distributed.py DistributedDSGD._run_lagged): one
+ * collective per round -- the halo rows of x_g AND every rank's column sums of x_g in one exchange
+ * (an all-to-all-v: the send / halo buffers hold, per peer in rank order, that peer's rows then
+ * 8 ld bytes of float64 sums) -- and two kernels per round:
+ *   exchange(x_g rows + sums) ----------------------------------------------.
+ *   dopt_lagged_grad: gradient pass of x_g (+ loss of every row at xbar_{g-1}) +--> dopt_lagged_mix
+ * dopt_lagged_exchange_layout: the send-buffer row where the sums for peer p go and the halo-buffer
+ *   row where peer p's sums arrive, p = 0 .. world-1 (-1 for p == rank); after dopt_set_halo, whose
+ *   send_ids are -1 on those rows.
+ * dopt_lagged_begin: dopt_phase_begin + the send rows and this rank's column sums of x_0.
+ * dopt_lagged_grad: dopt_phase_set_step + dopt_phase_grad (replaces the worker loop of
+ *   trainer.py:164-170; interior workers mixed and stepped too).
+ * dopt_lagged_mix: xbar_g = (sum over ranks p in rank order of p's column sums of x_g) / n_global
+ *   (trainer.py:182), the consensus partials of x_g (trainer.py:183-186, with consensus), x_{g+1} =
+ *   W [x_g | halo] - eta g (trainer.py:173-175) and its send rows, this rank's column sums of
+ *   x_{g+1} into the send buffer's sum rows, and into the non-NULL outputs the history row g-2
+ *   (consensus partials of x_{g-1}, the losses of the preceding dopt_lagged_grad, ||xbar_{g-1}||^2).
+ * dopt_lagged_tail: after one more exchange: xbar_G, and the history rows G-1 (cons1 / xnorm1 /
+ *   loss1) and G-2 (cons2 / xnorm2 / loss2) of a chain of G rounds. */
+int dopt_lagged_exchange_layout(dopt_ctx *ctx, int32_t world, int32_t rank, const int64_t *sum_send_row,
+                                const int64_t *sum_recv_row);
+int dopt_lagged_begin(dopt_ctx *ctx, int64_t batch);
+int dopt_lagged_grad(dopt_ctx *ctx, int64_t t, double eta0, int64_t batch, const int32_t *idx, double lam_grad,
+                     uint32_t metric_flags);
+int dopt_lagged_mix(dopt_ctx *ctx, int64_t t, double eta0, int consensus, double *cons_out, double *xnorm_out,
+                    double *loss_out);
+int dopt_lagged_tail(dopt_ctx *ctx, int consensus, int objective, double *cons1, double *xnorm1, double *loss1,
+                     double *cons2, double *xnorm2, double *loss2);
 /* Centralized trainer across ranks (trainer.py:41-71): gradients of the local
  * workers at the shared iterate (fuse_loss: the objective partial of the shared
  * iterate over the same rows, full shards only), local column sums of the
@@ -347,31 +391,6 @@ int dopt_phase_central_step(dopt_ctx *ctx, const double *sum_dev, int64_t t, dou
  * out_dev[3] = (0, sum of loss terms, ||x||^2 if include_xnorm). */
 int dopt_phase_metrics_pass_shared(dopt_ctx *ctx);
 int dopt_phase_metrics_shared(dopt_ctx *ctx, int include_xnorm, double *out_dev);
-int dopt_sync(dopt_ctx *ctx);
-/* Host: raw[T x 3] (summed over ranks) -> history values, the exact formula
- * the single-GPU path applies. */
-int dopt_finalize_metrics(int problem, int64_t T, const double *raw, int64_t n_workers,
-                          int64_t m_obj, double lam_obj, double f_opt, double *obj_out,
-                          double *cons_out);
-
-/* Full-data objective and gradient at w over every loaded row (or the separate
- * objective dataset): f = mean loss + reg/2 ||w||^2 (obj_problems.py:3-11 /
- * :39-44), g = mean_k c_k x_k + reg w (the full-gradient shape of
- * obj_problems.py:22-36 / :55-69).  One pass over the data; the building block
- * of the device f(x*) solver (solver.py) that replaces sklearn's saga at sizes
- * sklearn cannot handle (simulator.py:32-69).  g_out may be NULL (objective only);
- * column-blocked contexts (rows beyond the row-resident kernel) evaluate the objective only,
- * with the direct kernels' dots pass (g_out must be NULL there). */
-int dopt_eval_full(dopt_ctx *ctx, const double *w, double reg, double *f_out, double *g_out);
-
-/* Device time of the dominant kernel (the fused round kernel) since the last call:
- * sampled launches and their summed milliseconds, measured with HIP events on the
- * engine's stream.  Used by bench.py for the roofline figure.
- * dopt_set_profiling: 0 = off; k >= 1 = bracket every k-th launch with an event pair
- * (a pair costs ~30 us of round time on MI355X, so bench.py samples). */
-int dopt_kernel_stats(dopt_ctx *ctx, int64_t *launches, double *total_ms);
-int dopt_set_profiling(dopt_ctx *ctx, int enable);
-
 #ifdef __cplusplus
 }
 #endif

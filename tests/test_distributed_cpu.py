@@ -40,44 +40,69 @@ def _rank_main(rank, world, port, name, n, T, out):
     _rank_main_topo(rank, world, port, _topo(name, n), T, out)
 
 
-def _rank_main_topo(rank, world, port, topo, T, out):
+def _rank_main_topo(rank, world, port, topo, T, out, collective=False):
+    """The round restated in numpy over the product's exchange: the halo plan, its ExchangeLayout
+    (per peer: the plan's rows, then one row of this rank's column sums) and HaloExchange over gloo
+    (per-peer isend / irecv, or with `collective` the all_to_all_single the RCCL path issues).
+    Every round each rank also forms xbar from the ranks' sums in rank order (distributed.py
+    _run_lagged / k_mixcs) and saves it with its final iterates."""
     import torch
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     n = topo.n
     plan = D.build_plan(topo, world, rank)
+    lay = D.exchange_layout(plan, 1)
     shards = _data(n)
-    x = np.zeros((plan.n_local, shards[0][0].shape[1]))
+    d = shards[0][0].shape[1]
+    x = np.zeros((plan.n_local, d))
+    col = lay.local_col(plan)
+    send = torch.zeros((max(1, lay.n_send_rows), d), dtype=torch.float64)
+    halo = torch.zeros((max(1, lay.n_recv_rows), d), dtype=torch.float64)
+    ex = D.HaloExchange(plan, send, halo, layout=lay)
+    ex.collective = collective
+    xbars = []
     for t in range(T):
         g = np.stack([O.gradient("logistic", x[i], *shards[plan.lo + i], CFG) for i in range(plan.n_local)])
-        send = torch.from_numpy(np.ascontiguousarray(x[plan.send_ids]))
-        halo = torch.zeros((plan.n_halo, x.shape[1]), dtype=torch.float64)
-        works = []
-        for p in plan.peers():
-            s0, s1, r0, r1 = plan.send_off[p], plan.send_off[p + 1], plan.recv_off[p], plan.recv_off[p + 1]
-            if s1 > s0:
-                works.append(dist.isend(send[s0:s1].contiguous(), p))
-            if r1 > r0:
-                buf = torch.zeros((r1 - r0, x.shape[1]), dtype=torch.float64)
-                works.append((dist.irecv(buf, p), r0, buf))
-        for w in works:
-            if isinstance(w, tuple):
-                w[0].wait()
-                halo[w[1]:w[1] + w[2].shape[0]] = w[2]
-            else:
-                w.wait()
+        own = x.sum(axis=0)
+        send[lay.send_rows] = torch.from_numpy(np.ascontiguousarray(x[plan.send_ids]))
+        for p in range(world):
+            if lay.sum_send_row[p] >= 0:
+                send[lay.sum_send_row[p]] = torch.from_numpy(own)
+        ex.finish(ex.start())
         H = halo.numpy()
+        tot = 0.0
+        for p in range(world):  # the ranks' sums in rank order (every rank the same bits)
+            tot = tot + (own if p == rank else H[lay.sum_recv_row[p]])
+        xbars.append(tot / n)
         new = np.empty_like(x)
         for i in range(plan.n_local):
-            acc = np.zeros(x.shape[1])
+            acc = np.zeros(d)
             for e in range(plan.row_ptr[i], plan.row_ptr[i + 1]):
-                c = plan.col[e]
+                c = col[e]
                 acc = acc + plan.w[e] * (x[c] if c < plan.n_local else H[c - plan.n_local])
             new[i] = acc
         x = new - np.asarray(O._lr(CFG["learning_rate_eta0"], t)) * g
     np.save(os.path.join(out, f"rank{rank}.npy"), x)
+    np.save(os.path.join(out, f"xbar{rank}.npy"), np.array(xbars))
     dist.destroy_process_group()
+
+
+def _check_ranks(tmp_path, topo, world, T):
+    """Iterates bitwise the oracle's; every rank's per-round xbar the same bits, and the oracle's
+    mean of the iterates to rounding."""
+    n = topo.n
+    got = np.concatenate([np.load(tmp_path / f"rank{r}.npy") for r in range(world)])
+    idx = [[np.arange(7)] * n] * T
+    _, _, ref, _ = O.run_decentralized(_data(n), topo.dense_W(), T, CFG, mixing="sparse", indices=idx)
+    np.testing.assert_array_equal(got, ref)
+    xb = [np.load(tmp_path / f"xbar{r}.npy") for r in range(world)]
+    for r in range(1, world):
+        np.testing.assert_array_equal(xb[r], xb[0])
+    for t in range(T):  # xbar of round t = mean of x_t (x_0 = 0)
+        xt = np.zeros((n, 6)) if t == 0 else O.run_decentralized(_data(n), topo.dense_W(), t, CFG, mixing="sparse",
+                                                                 indices=idx[:t])[2]
+        np.testing.assert_allclose(xb[0][t], xt.mean(axis=0), rtol=1e-12, atol=1e-15)
 
 
 @pytest.mark.parametrize("name,n,world", [("ring", 10, 2), ("grid", 16, 3), ("random_regular", 24, 3),
@@ -86,12 +111,28 @@ def test_partitioned_rounds_match_oracle(tmp_path, name, n, world):
     T = 4
     mp.start_processes(_rank_main, args=(world, _free_port(), name, n, T, str(tmp_path)), nprocs=world,
                        join=True, start_method="fork")
-    got = np.concatenate([np.load(tmp_path / f"rank{r}.npy") for r in range(world)])
+    _check_ranks(tmp_path, _topo(name, n), world, T)
+
+
+@pytest.mark.parametrize("name,n,collective", [("random_regular", 64, False), ("grid", 256, False),
+                                               ("fully_connected", 16, False), ("random_regular", 64, True)])
+def test_eight_ranks_match_oracle(tmp_path, name, n, collective):
+    """the driver's 8-GPU shape on CPU -- 8 gloo ranks, every rank exchanging with
+    all 7 peers each round (halo rows and column sums): a spectrally partitioned random 4-regular
+    graph of 64 workers, the 16 x 16 torus in strips of two torus rows, the complete graph, and the
+    RCCL path's single all_to_all_single per round (over gloo).  Iterates bitwise the oracle's."""
+    world, T = 8, 3
     topo = _topo(name, n)
-    shards = _data(n)
-    idx = [[np.arange(7)] * n] * T
-    _, _, ref, _ = O.run_decentralized(shards, topo.dense_W(), T, CFG, mixing="sparse", indices=idx)
-    np.testing.assert_array_equal(got, ref)
+    if name == "random_regular":
+        topo = TP.relabel(topo, D.partition_order(D.graph_partition(topo, world)))
+    mp.start_processes(_rank_main_topo, args=(world, _free_port(), topo, T, str(tmp_path), collective), nprocs=world,
+                       join=True, start_method="fork")
+    _check_ranks(tmp_path, topo, world, T)
+    for r in range(world):
+        lay = D.exchange_layout(D.build_plan(topo, world, r), 1)
+        assert sum(1 for p in range(world) if p != r and lay.send_sizes[p] > 0) == 7
+    if name == "grid":
+        assert all(D.build_plan(topo, world, r).n_halo == 2 * 16 for r in range(world))
 
 
 def test_plan_structure():
@@ -195,28 +236,34 @@ def test_relabelled_rounds_match_oracle(tmp_path):
     topo = TP.relabel(_topo("random_regular", n), D.partition_order(D.graph_partition(_topo("random_regular", n), world)))
     mp.start_processes(_rank_main_topo, args=(world, _free_port(), topo, T, str(tmp_path)), nprocs=world,
                        join=True, start_method="fork")
-    got = np.concatenate([np.load(tmp_path / f"rank{r}.npy") for r in range(world)])
-    idx = [[np.arange(7)] * n] * T
-    _, _, ref, _ = O.run_decentralized(_data(n), topo.dense_W(), T, CFG, mixing="sparse", indices=idx)
-    np.testing.assert_array_equal(got, ref)
+    _check_ranks(tmp_path, topo, world, T)
 
 
 def _rank_alltoall(rank, world, port, topo, out):
     """HaloExchange's RCCL form (one all_to_all_single per round over the peer-grouped buffers),
-    driven over gloo on CPU tensors: every halo row must arrive holding its global id."""
+    driven over gloo on CPU tensors: every halo row must arrive holding its global id -- in the plain
+    layout and in the lagged schedule's (a sum row per peer, holding the sender's rank + 1000)."""
     import torch
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     plan = D.build_plan(topo, world, rank)
-    send = torch.full((max(1, len(plan.send_ids)), 3), -1.0, dtype=torch.float64)
-    send[:len(plan.send_ids)] = torch.from_numpy((plan.send_ids + plan.lo).astype(np.float64))[:, None]
-    halo = torch.full((max(1, plan.n_halo), 3), -1.0, dtype=torch.float64)
-    ex = D.HaloExchange(plan, send, halo)
-    ex.collective = True  # the device path's call, here on gloo
-    for _ in range(2):  # every round is the same collective; repeated calls reuse the buffers
-        ex.finish(ex.start())
-    np.save(os.path.join(out, f"rank{rank}.npy"), halo[:plan.n_halo].numpy())
+    for ks in (0, 1):
+        lay = D.exchange_layout(plan, ks)
+        send = torch.full((max(1, lay.n_send_rows), 3), -1.0, dtype=torch.float64)
+        send[lay.send_rows] = torch.from_numpy((plan.send_ids + plan.lo).astype(np.float64))[:, None]
+        for p in range(world):
+            if lay.sum_send_row[p] >= 0:
+                send[lay.sum_send_row[p]] = 1000.0 + rank
+        halo = torch.full((max(1, lay.n_recv_rows), 3), -1.0, dtype=torch.float64)
+        ex = D.HaloExchange(plan, send, halo, layout=lay if ks else None)
+        ex.collective = True  # the device path's call, here on gloo
+        for _ in range(2):  # every round is the same collective; repeated calls reuse the buffers
+            ex.finish(ex.start())
+        np.save(os.path.join(out, f"rank{rank}_{ks}.npy"), halo[lay.halo_rows].numpy())
+        np.save(os.path.join(out, f"sums{rank}_{ks}.npy"),
+                np.array([halo[lay.sum_recv_row[p], 0].item() if lay.sum_recv_row[p] >= 0 else -1.0
+                          for p in range(world)]))
     dist.destroy_process_group()
 
 
@@ -235,7 +282,10 @@ def test_alltoall_halo_layout(tmp_path, name, n, world):
                        start_method="fork")
     for r in range(world):
         plan = D.build_plan(topo, world, r)
-        got = np.load(tmp_path / f"rank{r}.npy")
-        np.testing.assert_array_equal(got, np.repeat(plan.halo_ids.astype(np.float64)[:, None], 3, axis=1))
+        for ks in (0, 1):
+            got = np.load(tmp_path / f"rank{r}_{ks}.npy")
+            np.testing.assert_array_equal(got, np.repeat(plan.halo_ids.astype(np.float64)[:, None], 3, axis=1))
+        np.testing.assert_array_equal(np.load(tmp_path / f"sums{r}_1.npy"),
+                                      [-1.0 if p == r else 1000.0 + p for p in range(world)])
     if name == "two_rings":
         assert D.build_plan(topo, world, 2).peers() == []

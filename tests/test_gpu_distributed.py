@@ -220,6 +220,22 @@ def test_partitioned_graph_ranks_match_single_context(tmp_path, monkeypatch, wor
     _compare_single(got, "float64", False, 5, parts=world)
 
 
+def test_eight_ranks_match_single_context(tmp_path, monkeypatch):
+    """the driver's SCALE shape on the one GPU -- 8 gloo ranks x 256 workers of the
+    spectrally partitioned random 4-regular graph (every rank exchanging halo rows and column sums
+    with all 7 peers each round), as a chain of pipelined calls: bitwise one context's iterates."""
+    import torch.multiprocessing as mp
+
+    n, d, m, t = 2048, 100, 32, 6
+    monkeypatch.setenv("DOPT_TEST_PARTITION", "1")
+    monkeypatch.setenv("DOPT_TEST_PIPE", "1")
+    mp.start_processes(_rank_main, args=(8, _free_port(), "float64/x32", str(tmp_path), False, t, "1", n, d, m),
+                       nprocs=8, join=True, start_method="spawn")
+    got = np.load(tmp_path / "dist.npz")
+    assert len(got["obj"]) == len(got["cons"]) == t
+    _compare_single(got, "float64/x32", False, t, n, d, m, parts=8)
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_strong_split_bench_shape_matches_single_context(tmp_path, monkeypatch, world):
     """bench.py's strong-scaling leg in miniature: a FIXED total of workers (1024, d = 1024, the

@@ -546,3 +546,72 @@ def test_rowspace_x32_direct_rounds_from_unequal_starts(monkeypatch):
     assert out[None][3].startswith("void dopt::k_split_step<double, double,"), out[None][3]
     for u, v in zip(out["float32"][:3], out[None][:3]):
         np.testing.assert_allclose(u, v, rtol=1e-12, atol=1e-15 * np.abs(v).max())
+
+
+def _flag_rank(rank, world, port, out):
+    """A pipelined chain continued with other metric flags: the row-space rounds (complete graph,
+    long rows) and the lagged schedule (CSR) both refuse, leave the chain open, and close it with
+    the chain's own flags afterwards."""
+    import os
+
+    import torch  # noqa: F401  (one HIP runtime, loaded before libdopt)
+    import torch.distributed as dist
+
+    import distributed as Dm
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    got = []
+    # row-space: complete graph over rows beyond the row-resident kernel
+    shards = _rs_data(False)
+    n = len(shards)
+    bounds = Dm.partition_bounds(n, world)
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    plan = Dm.HaloPlan(rank, world, bounds, lo, hi, np.zeros(0, np.int64), np.zeros(world + 1, np.int64),
+                       np.zeros(0, np.int32), np.zeros(world + 1, np.int64), None, None, None)
+    eng = _dopt.Engine(0, "float64")
+    mine = shards[lo:hi]
+    off = np.concatenate([[0], np.cumsum([len(s[1]) for s in mine])])
+    eng.load_shards("quadratic", np.vstack([s[0] for s in mine]), np.concatenate([s[1] for s in mine]), off)
+    w_off, diag = TP.fully_connected(n).uniform_offdiag()
+    runs = [(Dm.DistributedDSGD(eng, plan, n, sum(SIZES_D), device=0, mean=(w_off, diag[lo:hi])), max(SIZES_D), eng)]
+    # lagged: a ring over short rows
+    eng2 = _dopt.Engine(0, "float64")
+    top = TP.ring(16)
+    plan2 = Dm.build_plan(top, world, rank)
+    eng2.generate_shards("logistic", plan2.n_local, 20, 8, seed=3, first_worker=plan2.lo)
+    runs.append((Dm.DistributedDSGD(eng2, plan2, 16, 16 * 8, device=0), 8, eng2))
+    for run, b, _ in runs:
+        run.run_pipelined(2, 0.05, b, 2e-3, 1e-3, 0.1)
+        try:
+            run.run_pipelined(1, 0.05, b, 2e-3, 1e-3, 0.1, consensus=False)
+            got.append("ran")
+        except ValueError:
+            got.append("refused")
+        o, c = run.run_pipelined(0, 0.05, b, 2e-3, 1e-3, 0.1)  # closes the open chain: its owed rows
+        got.append(f"closed:{len(o)}")
+    if rank == 0:
+        np.savez(os.path.join(out, "flags.npz"), got=np.array(got))
+    dist.barrier()
+    for _, _, e in runs:
+        e.close()
+    dist.destroy_process_group()
+
+
+def test_pipelined_flag_change_refused_on_both_paths(tmp_path):
+    """continuing an open pipelined chain with other objective / consensus flags raises
+    ValueError on the row-space path AND on the lagged schedule (it used to start a new chain
+    silently there), and the chain then closes with its own flags, returning the rows it owed."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.start_processes(_flag_rank, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    got = list(np.load(tmp_path / "flags.npz")["got"])
+    assert got[0] == "refused" and got[2] == "refused", got
+    assert got[1].startswith("closed:") and got[3].startswith("closed:"), got
+    assert int(got[1].split(":")[1]) >= 1 and int(got[3].split(":")[1]) >= 1, got

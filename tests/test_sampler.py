@@ -276,3 +276,40 @@ def test_parallel_minibatch_draws_match_numpy(monkeypatch, seg, win, rows, T, b)
     st = np.random.get_state()
     assert st[2] == st_ours[2]
     np.testing.assert_array_equal(st[1], st_ours[1])
+
+
+_RSS_PROBE = r"""
+import resource, sys, time
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import _dopt
+_dopt.lib()
+np.random.seed(7)
+base = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+t0 = time.time()
+mode = sys.argv[2]
+if mode == "choice":  # C3 minibatch draws, 256 rounds in one call (the trainer's non-overlapped chunk)
+    _dopt.mt_choice_rounds(256, [512] * 4096, 16)
+else:  # C3 full-shard stream advance, 512 rounds in one call
+    _dopt.mt_advance_rounds(512, [512] * 4096)
+peak = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+print((peak - base) / 1024.0, time.time() - t0)
+"""
+
+
+@pytest.mark.parametrize("mode,cap_mb", [("choice", 900), ("advance", 300)])
+def test_parallel_draw_memory_is_bounded(mode, cap_mb):
+    """the parallel filter keeps at most a bounded number of segments' buffers
+    (run-ahead bound, stitched segments released) and minibatch draws go in parts of at most
+    32 segments of kept values -- a C3-sized call no longer holds ~3 GB.  Run in a fresh process
+    so the peak resident set is this call's (4 filter threads)."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, DOPT_MT_THREADS="4", DOPT_NO_TORCH="1")
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "distributed-optimization_amd")
+    r = subprocess.run([sys.executable, "-c", _RSS_PROBE, pkg, mode], capture_output=True, text=True, env=env,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr
+    grew_mb, secs = (float(v) for v in r.stdout.split())
+    assert grew_mb < cap_mb, (grew_mb, secs)

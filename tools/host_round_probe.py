@@ -2,8 +2,10 @@
 """Host cost per round of the multi-GPU lagged schedule (distributed.py: _run_lagged) at RCCL
 world 1 with the collectives forced (DOPT_FORCE_COLLECTIVES=1), PROBE_WORKERS workers (default
 512, the strong leg's share of N = 4096 at 8 ranks): the Python time spent in each call of the
-round loop, accumulated over PROBE_ROUNDS rounds, against the round's GPU time.  A loop whose host
-time per round exceeds the GPU's leaves the GPU waiting between kernels."""
+round loop (the exchange's start / finish, the two engine calls), accumulated over PROBE_ROUNDS
+rounds, and the whole loop's host time per round (everything but the device), against the round's
+GPU time.  A loop whose host time per round exceeds the GPU's leaves the GPU waiting between
+kernels."""
 import json
 import os
 import sys
@@ -44,20 +46,29 @@ def main():
             return r
         setattr(obj, name, g)
 
-    for name in ("phase_colsum_fold", "phase_set_step", "phase_grad", "phase_mix_lagged"):
+    for name in ("lagged_grad", "lagged_mix"):
         wrap(eng, name)
-    for name in ("_start_exchange", "_finish_exchange", "_all_reduce_start"):
-        wrap(run, name)
+    for name in ("start", "finish"):
+        wrap(run.exchange, name)
     run.run_pipelined(5, 0.05, m, 1e-4, 1e-4, 0.0)
     torch.cuda.synchronize()
     acc.clear()
+    issued = []
+    ar = run._all_reduce
+
+    def mark(*a, **k):  # the first call after the round loop: every round is issued by now
+        issued.append(time.perf_counter())
+        return ar(*a, **k)
+    run._all_reduce = mark
     t0 = time.perf_counter()
     run.run_pipelined(R, 0.05, m, 1e-4, 1e-4, 0.0)
     wall = time.perf_counter() - t0
+    run._all_reduce = ar
     run.run_pipelined(0, 0.05, m, 1e-4, 1e-4, 0.0)
     out = {"workers": n, "rounds": R, "wall_us_per_round": wall / R * 1e6,
            "host_us_per_round": {k: v / R * 1e6 for k, v in sorted(acc.items())},
-           "host_us_per_round_total": sum(acc.values()) / R * 1e6}
+           "host_us_per_round_total": sum(acc.values()) / R * 1e6,
+           "loop_issue_us_per_round": (issued[0] - t0) / R * 1e6 if issued else None}
     print(json.dumps(out))
     eng.close()
     torch.distributed.destroy_process_group()
