@@ -48,8 +48,13 @@ __device__ __forceinline__ typename VT<T>::v rs_ld_nt(const T* p) {
 // (XT = T) and k_rs_pass_x32<...> (float64 arithmetic over float32-stored rows, the C3 headline's
 // layout: the 16-byte chunk is 4 floats, xbar's 4 doubles stay in registers, every product and
 // sum in float64).
-template <typename T, typename XT, bool COLS, int CB, int NBUF>
-__device__ __forceinline__ void rs_pass_body(const RsArgs& a, double* red) {
+// LDOT (round 4): each row's per-lane partial dot goes to LDS (pdot: [64 rows][64 lanes] per wave,
+// lane l's value of row k at slot (l + k) % 64, so the window's read-back is 2-way bank conflicted at
+// worst); after the window, lane k sums row k's 64 partials in lane order -- one LDS store per row
+// instead of a six-step DPP butterfly and its dependency chain per row (a wave per SIMD has nothing
+// else to issue while the chain drains).
+template <typename T, typename XT, bool COLS, int CB, int NBUF, bool LDOT = false>
+__device__ __forceinline__ void rs_pass_body(const RsArgs& a, double* red, double* pdot = nullptr) {
   using V = typename VT<XT>::v;
   constexpr int VN = VT<XT>::n;
   constexpr bool SAME = std::is_same<T, XT>::value;
@@ -183,7 +188,9 @@ __device__ __forceinline__ void rs_pass_body(const RsArgs& a, double* red) {
               for (int e = 0; e < VN; ++e) p += (double)rv[j][e] * xbs[j][e];
             }
           }
-          const double dot = wave_sum_dpp(p);
+          double dot = 0.0;
+          if constexpr (LDOT) pdot[kk * 64 + ((lane + kk) & 63)] = p;
+          else dot = wave_sum_dpp(p);
           if constexpr (COLS) {
             const double cf = readlane_t(cwv, kk);  // wave-uniform
             if constexpr (TACC) {
@@ -199,7 +206,7 @@ __device__ __forceinline__ void rs_pass_body(const RsArgs& a, double* red) {
                 for (int e = 0; e < VN; ++e) acc[j][e] += cf * (double)rv[j][e];
             }
           }
-          st = lane == kk ? dot : st;
+          if constexpr (!LDOT) st = lane == kk ? dot : st;
         };
         if (nw == 64) {
           for (int g0 = 0; g0 < 64; g0 += NBUF) {
@@ -221,6 +228,14 @@ __device__ __forceinline__ void rs_pass_body(const RsArgs& a, double* red) {
           }
         }
         flush();
+        if constexpr (LDOT) {  // row `lane` of the window: its 64 partials in lane order
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          double s0 = 0.0;
+#pragma unroll 8
+          for (int j = 0; j < 64; ++j) s0 += pdot[lane * 64 + ((j + lane) & 63)];
+          st = s0;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // reads done before the next window's stores
+        }
         if (lane < nw) up[w0 + lane] = (T)st;
       }
     }
@@ -257,16 +272,18 @@ __device__ __forceinline__ void rs_pass_body(const RsArgs& a, double* red) {
   }
 }
 
-template <typename T, bool COLS, int CB, int NBUF>
+template <typename T, bool COLS, int CB, int NBUF, bool LDOT = false>
 __global__ __launch_bounds__(NT) void k_rs_pass(const RsArgs a) {
   __shared__ double red[COLS ? NW * 64 * CB * VT<T>::n : 1];
-  rs_pass_body<T, T, COLS, CB, NBUF>(a, red);
+  __shared__ double pdot[LDOT ? NW * 64 * 64 : 1];
+  rs_pass_body<T, T, COLS, CB, NBUF, LDOT>(a, red, pdot + (LDOT ? (threadIdx.x >> 6) * 64 * 64 : 0));
 }
 
-template <bool COLS, int CB, int NBUF>
+template <bool COLS, int CB, int NBUF, bool LDOT = false>
 __global__ __launch_bounds__(NT) void k_rs_pass_x32(const RsArgs a) {
   __shared__ double red[COLS ? NW * 64 * CB * VT<float>::n : 1];
-  rs_pass_body<double, float, COLS, CB, NBUF>(a, red);
+  __shared__ double pdot[LDOT ? NW * 64 * 64 : 1];
+  rs_pass_body<double, float, COLS, CB, NBUF, LDOT>(a, red, pdot + (LDOT ? (threadIdx.x >> 6) * 64 * 64 : 0));
 }
 
 // k_rs_rows: one workgroup per worker (m_i <= 64 rows, lane k = row k).  u_k = sum over the
@@ -805,6 +822,11 @@ static hipError_t rs_pass_shape(const RsArgs& a, dim3 grid, hipStream_t s) {
     else hipLaunchKernelGGL((k_rs_pass<T, COLS, C_, B_>), grid, dim3(NT), 0, s, a);          \
     return hipGetLastError();                                                                  \
   }
+  if (a.ldot && a.cb == 2 && a.nbuf == 8) {  // the default: row dots through LDS (DOPT_RS_LDOT=0: DPP)
+    if constexpr (X32) hipLaunchKernelGGL((k_rs_pass_x32<COLS, 2, 8, true>), grid, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((k_rs_pass<T, COLS, 2, 8, true>), grid, dim3(NT), 0, s, a);
+    return hipGetLastError();
+  }
   RS_SHAPE(2, 8)  // the default; the others: A/B builds (DOPT_RS_CB / DOPT_RS_NBUF)
 #ifdef DOPT_AB
   RS_SHAPE(2, 6)
@@ -836,12 +858,13 @@ hipError_t launch_rs_pass(int dtype, int xdtype, bool cols, const RsArgs& a, hip
   const bool x32 = dtype == 1 && xdtype == 0;
   if (dtype != xdtype && !x32) return hipErrorInvalidValue;
   char buf[112];
+  const bool ld = a.ldot && a.cb == 2 && a.nbuf == 8;
   if (x32)
-    snprintf(buf, sizeof(buf), "void dopt::k_rs_pass_x32<%s, %d, %d>(dopt::RsArgs)", cols ? "true" : "false", a.cb,
-             a.nbuf);
+    snprintf(buf, sizeof(buf), "void dopt::k_rs_pass_x32<%s, %d, %d%s>(dopt::RsArgs)", cols ? "true" : "false", a.cb,
+             a.nbuf, ld ? ", true" : "");
   else
-    snprintf(buf, sizeof(buf), "void dopt::k_rs_pass<%s, %s, %d, %d>(dopt::RsArgs)", rs_tn(dtype),
-             cols ? "true" : "false", a.cb, a.nbuf);
+    snprintf(buf, sizeof(buf), "void dopt::k_rs_pass<%s, %s, %d, %d%s>(dopt::RsArgs)", rs_tn(dtype),
+             cols ? "true" : "false", a.cb, a.nbuf, ld ? ", true" : "");
   if (cols) note_round_kernel(buf);
   if (x32) return cols ? rs_pass_shape<double, true, true>(a, grid, s) : rs_pass_shape<double, true, false>(a, grid, s);
   if (dtype == 0)

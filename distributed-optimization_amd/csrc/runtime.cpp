@@ -239,7 +239,7 @@ struct dopt_ctx {
   bool wdiag_uniform = false;  // complete-graph mixing with one W_ii for every worker
   double wdiag_u = 0.0;
   int64_t min_m = 0;           // smallest shard
-  int rs_wg = 0, rs_nblk = 0, rs_nd = 0, rs_cb = 4, rs_nbuf = 3;
+  int rs_wg = 0, rs_nblk = 0, rs_nd = 0, rs_cb = 4, rs_nbuf = 3, rs_ldot = 1;
   int64_t rs_bcap = 0;
   double* rs_coef = nullptr;   // [rows]
   double* rs_up = nullptr;     // [nblk x rows]
@@ -827,6 +827,7 @@ RsArgs rs_args(dopt_ctx* c) {
   a.nblk = c->rs_nblk;
   a.cb = c->rs_cb;
   a.nbuf = c->rs_nbuf;
+  a.ldot = c->rs_ldot;
   a.coef_row = c->rs_coef;
   a.upart = c->rs_up;
   a.cpart = c->rs_cp;
@@ -864,6 +865,7 @@ int ensure_rs(dopt_ctx* c) {
   // 1 / 8 10.93-11.41, the 2 / 6 row loop 10.87-11.12
   c->rs_cb = (int)ab_knob("DOPT_RS_CB", 2);
   c->rs_nbuf = (int)ab_knob("DOPT_RS_NBUF", 8);
+  c->rs_ldot = (int)ab_knob("DOPT_RS_LDOT", 1);
   const int64_t nblk = (c->nch + 64 * c->rs_cb - 1) / (64 * c->rs_cb);
   int64_t wg = ab_knob("DOPT_RS_WG", (c->rows + 8191) / 8192);  // ~8k rows per row group
   wg = std::max<int64_t>(1, std::min<int64_t>(wg, (c->rows + 255) / 256));

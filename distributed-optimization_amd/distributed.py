@@ -347,6 +347,15 @@ class HaloExchange:
         self.peers = [p for p in range(plan.world) if p != self.rank and (self.send_sizes[p] or self.recv_sizes[p])]
         self.ns, self.nr = int(self.send_off[-1]), int(self.recv_off[-1])
         self.what = f"all_to_all_single of {self.ns} rows out / {self.nr} halo rows in (peers {self.peers})"
+        self._direct = None
+        if self.collective:  # the process group's all-to-all-v, called as dist.all_to_all_single calls it,
+            try:             # minus its per-call argument checks (host cost per round: VERDICT r3 item 3)
+                opts = dist.AllToAllOptions()
+                opts.asyncOp = True
+                pg = group if group is not None else dist.distributed_c10d._get_default_group()
+                self._direct = (pg.alltoall_base, self.halo[:self.nr], self.send[:self.ns], opts)
+            except (AttributeError, RuntimeError):
+                self._direct = None
 
     def disable(self):
         """No exchange at all (complete-graph mixing on every rank: no rows move)."""
@@ -366,6 +375,9 @@ class HaloExchange:
     def start(self):
         dist = self.dist
         if self.collective:
+            if self._direct is not None:
+                fn, out, inp, opts = self._direct
+                return [(fn(out, inp, self.recv_sizes, self.send_sizes, opts), self.what)]
             w = dist.all_to_all_single(self.halo[:self.nr], self.send[:self.ns], output_split_sizes=self.recv_sizes,
                                        input_split_sizes=self.send_sizes, group=self.group, async_op=True)
             return [(w, self.what)]

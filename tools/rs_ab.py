@@ -1,4 +1,4 @@
-"""A/B of the row-space pass shapes (DOPT_RS_CB / DOPT_RS_NBUF / DOPT_RS_WG) at C5 on one GPU:
+"""A/B of the row-space pass shapes (DOPT_RS_CB / DOPT_RS_NBUF / DOPT_RS_WG [/ DOPT_RS_LDOT]) at C5 on one GPU:
 one engine, the shape re-planned by set_mixing_mean, interleaved repetitions; prints the
 round-kernel average (HIP events) and the wall time per round of a pipelined call."""
 import argparse
@@ -33,9 +33,11 @@ def main():
     res = {}
     for rep in range(args.reps):
         for sh in args.shapes.replace("_", " ").split():
-            cb, nb, wg = sh.split(",")
+            parts = sh.split(",")
+            cb, nb, wg = parts[:3]
             os.environ["DOPT_RS_CB"], os.environ["DOPT_RS_NBUF"] = cb, nb
             os.environ["DOPT_RS_WG"] = wg
+            os.environ["DOPT_RS_LDOT"] = parts[3] if len(parts) > 3 else "1"  # row dots through LDS (2,8 only)
             eng.set_mixing_mean(*top.uniform_offdiag())  # re-plans the pass
             eng.set_models(zeros)  # the reference's start (row-space rounds need equal iterates)
             t = time.perf_counter()
