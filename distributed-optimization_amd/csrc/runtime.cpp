@@ -209,6 +209,10 @@ struct dopt_ctx {
   // per-run buffers
   int32_t* idx = nullptr;
   size_t idx_cap = 0;
+  void* idx_pin[2] = {nullptr, nullptr};  // pinned staging of the phase calls' indices (upload_idx_chunk)
+  size_t idx_pin_cap[2] = {0, 0};
+  hipEvent_t idx_ev[2] = {nullptr, nullptr};
+  int idx_slot = 0;
   double* hraw = nullptr;  // [T x 3] raw metric sums per round (cons, loss, ||xbar||^2)
   uint64_t* stamps = nullptr;
   size_t hcap = 0;
@@ -562,14 +566,37 @@ int history(dopt_ctx* c, int64_t h, const void* point, bool cons, bool loss, int
   return DOPT_OK;
 }
 
-int upload_idx_chunk(dopt_ctx* c, const int32_t* idx, int64_t h0, int64_t nr, int64_t b) {
+// Minibatch indices of rounds [h0, h0 + nr) -> c->idx (stream-ordered).  stage: the call returns
+// before the stream runs (the phase API), so the host array may be gone by the time the copy runs
+// -- the indices go through one of two pinned staging buffers (the one whose previous copy has
+// completed) first; the ABI borrows host pointers only for the duration of a call (dopt.h).  Runs
+// (dopt_run_*) copy straight from the caller's array: they synchronise before returning.
+int upload_idx_chunk(dopt_ctx* c, const int32_t* idx, int64_t h0, int64_t nr, int64_t b, bool stage = false) {
   const size_t bytes = (size_t)(nr * c->n * b) * sizeof(int32_t);
   if (bytes > c->idx_cap * sizeof(int32_t) || !c->idx) {
     int rc = dalloc_t(&c->idx, bytes);
     if (rc) return rc;
     c->idx_cap = bytes / sizeof(int32_t);
   }
-  HIPOK(hipMemcpyAsync(c->idx, idx + h0 * c->n * b, bytes, hipMemcpyHostToDevice, c->stream));
+  const int32_t* src = idx + h0 * c->n * b;
+  if (stage && bytes > 0) {
+    const int k = c->idx_slot;
+    c->idx_slot ^= 1;
+    if (!c->idx_ev[k]) HIPOK(hipEventCreateWithFlags(&c->idx_ev[k], hipEventDisableTiming));
+    else HIPOK(hipEventSynchronize(c->idx_ev[k]));  // this buffer's previous copy has run
+    if (bytes > c->idx_pin_cap[k]) {
+      if (c->idx_pin[k]) (void)hipHostFree(c->idx_pin[k]);
+      c->idx_pin[k] = nullptr;
+      c->idx_pin_cap[k] = 0;
+      HIPOK(hipHostMalloc(&c->idx_pin[k], bytes, hipHostMallocDefault));
+      c->idx_pin_cap[k] = bytes;
+    }
+    memcpy(c->idx_pin[k], src, bytes);
+    HIPOK(hipMemcpyAsync(c->idx, c->idx_pin[k], bytes, hipMemcpyHostToDevice, c->stream));
+    HIPOK(hipEventRecord(c->idx_ev[k], c->stream));
+    return DOPT_OK;
+  }
+  HIPOK(hipMemcpyAsync(c->idx, src, bytes, hipMemcpyHostToDevice, c->stream));
   return DOPT_OK;
 }
 
@@ -1228,6 +1255,10 @@ int dopt_destroy(dopt_ctx* c) {
   dfree_t(c->lg_sum_in);
   dfree_t(c->lg_sum_out);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+  for (int k = 0; k < 2; ++k) {
+    if (c->idx_ev[k]) (void)hipEventDestroy(c->idx_ev[k]);
+    if (c->idx_pin[k]) (void)hipHostFree(c->idx_pin[k]);
+  }
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return DOPT_OK;
@@ -2025,7 +2056,7 @@ int dopt_phase_grad(dopt_ctx* c, int64_t batch, const int32_t* idx, double lam_g
   if ((rc = check_run(c, 1, batch, idx, false))) return rc;
   const bool dev = !idx && batch < c->max_m;  // device sampler (check_run)
   if (!c->G && (rc = dalloc(&c->G, (size_t)c->n * c->ld * c->esz))) return rc;
-  if (idx && (rc = upload_idx_chunk(c, idx, 0, 1, batch))) return rc;
+  if (idx && (rc = upload_idx_chunk(c, idx, 0, 1, batch, true))) return rc;
   const bool cons = metric_flags & DOPT_RUN_CONSENSUS, loss = metric_flags & DOPT_RUN_OBJECTIVE;
   const bool bip = (cons || loss) && (dev ? !c->obj_sep : bip_possible(c, batch, idx));
   if ((cons || loss) && ((batch < c->max_m && !bip) || c->obj_sep))
@@ -2129,7 +2160,7 @@ int dopt_phase_grad_shared(dopt_ctx* c, int64_t batch, const int32_t* idx, doubl
   int rc;
   if ((rc = check_run(c, 1, batch, idx, false))) return rc;
   if (!c->G && (rc = dalloc(&c->G, (size_t)c->n * c->ld * c->esz))) return rc;
-  if (idx && (rc = upload_idx_chunk(c, idx, 0, 1, batch))) return rc;
+  if (idx && (rc = upload_idx_chunk(c, idx, 0, 1, batch, true))) return rc;
   if (fuse_loss && (batch < c->max_m || c->obj_sep))
     return fail(DOPT_ERR_UNSUPPORTED, "a fused objective needs full-shard batches over the shard rows");
   RoundArgs a = base_args(c);
