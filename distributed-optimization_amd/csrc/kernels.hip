@@ -1542,23 +1542,33 @@ __device__ void fold_block_rw(const FoldArgs& f, int nch, int vn, double (*red)[
   }
 }
 
-// Column sum of global column `col` over every rank's vector, in rank order (k_mixcs, k_xbar_ranks).
+// Column sum of global column `col` over every rank's vector, in rank order (k_mixcs, k_xbar_ranks);
+// eight ranks' loads in flight at a time (one memory latency for a node of 8 GPUs, not eight).
 template <typename T>
 __device__ __forceinline__ double ranks_sum(const McsArgs& m, const T* halo, int64_t ld, int64_t col) {
   double s = 0.0;
-  for (int p = 0; p < m.world; ++p) {
-    const double v = p == m.rank ? m.own_in[col] : ((const double*)(halo + m.sum_in[p] * ld))[col];
-    s += v;
+  for (int p0 = 0; p0 < m.world; p0 += 8) {
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int p = p0 + k;
+      v[k] = p >= m.world ? 0.0 : p == m.rank ? m.own_in[col] : ((const double*)(halo + m.sum_in[p] * ld))[col];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (p0 + k < m.world) s += v[k];
   }
   return s;
 }
+
+constexpr int kMixcsMaxGroups = 64;  // mixcs_shape keeps ng <= this
 
 template <typename T, int CPB>
 __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __restrict__ G, int n, const McsArgs m,
                                               const FoldArgs fold) {
   using V = typename VT<T>::v;
   constexpr int VN = VT<T>::n;
-  constexpr int MAXE = 6;          // CSR entries held in registers (runtime: max row nnz <= 6)
+  constexpr int MAXE = 6;          // CSR entries held in registers (the rest of a longer row: loaded at use)
   constexpr int BC = 64 * CPB * VN;  // columns of a column block
   __shared__ double red[NW][BC];
   __shared__ int last;
@@ -1604,8 +1614,7 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
       live[u] = i < i_end;
       skip[u] = live[u] && a.interior && a.interior[i];
       e0[u] = live[u] ? a.rp[i] : 0;
-      e1[u] = live[u] ? a.rp[i + 1] : 0;
-      if (e1[u] - e0[u] > MAXE) e1[u] = e0[u] + MAXE;  // (runtime guarantee: never taken)
+      e1[u] = live[u] ? a.rp[i + 1] : 0;  // entries past the first MAXE: loaded at their use
 #pragma unroll
       for (int j = 0; j < CPB; ++j) {
         const int c = cbase + lane + 64 * j;
@@ -1645,6 +1654,12 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
 #pragma unroll
           for (int k = 0; k < MAXE; ++k)
             if (e0[u] + k < e1[u]) acc += ((const T*)a.cw)[e0[u] + k] * r[u][k][j];
+          for (int64_t e = e0[u] + MAXE; e < e1[u]; ++e) {  // longer rows (dense graphs): CSR order
+            const int col = a.ci[e];
+            const T* src = col < a.n_local ? (const T*)a.x_old + (int64_t)col * ld : halo + (int64_t)(col - a.n_local) * ld;
+            const int c = cbase + lane + 64 * j;
+            acc += ((const T*)a.cw)[e] * (c < nch ? *(const V*)(src + (int64_t)c * VN) : V(0));
+          }
           xn[j] = acc - eta * gv[u][j];
         }
       }
@@ -1693,17 +1708,16 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
   for (int t = threadIdx.x; t < BC; t += NT) {
     const int64_t col = colbase + t;
     if (col >= (int64_t)nch * VN) break;
+    // every partial in flight at once (ng <= kMixcsMaxGroups), summed in group order
+    double v[kMixcsMaxGroups];
+#pragma unroll
+    for (int q = 0; q < kMixcsMaxGroups; ++q)
+      v[q] = q < m.ng ? __hip_atomic_load(m.part + (int64_t)q * ld + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : 0.0;
     double s = 0.0;
-    int q = 0;
-    for (; q + 8 <= m.ng; q += 8) {  // eight partials in flight, summed in group order
-      double v[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        v[k] = __hip_atomic_load(m.part + (int64_t)(q + k) * ld + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) s += v[k];
-    }
-    for (; q < m.ng; ++q) s += __hip_atomic_load(m.part + (int64_t)q * ld + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int q = 0; q < kMixcsMaxGroups; ++q)
+      if (q < m.ng) s += v[q];
     m.own_out[col] = s;
     for (int p = 0; p < m.world; ++p)
       if (m.sum_out[p] >= 0) ((double*)((T*)a.send + m.sum_out[p] * ld))[col] = s;
@@ -1717,7 +1731,7 @@ void mixcs_shape(int dtype, int64_t n, int32_t nch, int32_t* ncb, int32_t* r, in
   *ncb = (nch + 64 * CPB - 1) / (64 * CPB);
   // groups of 8 workers, at most 64 groups (the last arriver reads ng partials of its block)
   int64_t rr = 8;
-  while ((n + rr - 1) / rr > 64) rr += 8;
+  while ((n + rr - 1) / rr > kMixcsMaxGroups) rr += 8;
   *r = (int32_t)rr;
   *ng = (int32_t)std::max<int64_t>(1, (n + rr - 1) / rr);
 }

@@ -13,7 +13,7 @@ tail -n 1 gpurun_out/r4_base_bench.json | cut -c 1-600
 for w in 512 4096; do  # early prologue (new default, -1) vs the round-3 default, interleaved in one process
   echo "=== early-prologue A/B, $w workers"
   DOPT_LIB=$PWD/distributed-optimization_amd/libdopt_ab.so timeout -k 10 200 python3 tools/kr_variants.py --mode x32 \
-    --variants -1,161843 --reps 7 --rounds 20 --workers $w > gpurun_out/r4_early_ab_$w.json 2> gpurun_out/r4_early_ab_$w.err \
+    --variants=-1,161843 --reps 7 --rounds 20 --workers $w > gpurun_out/r4_early_ab_$w.json 2> gpurun_out/r4_early_ab_$w.err \
     || { tail -n 20 gpurun_out/r4_early_ab_$w.err; exit 1; }
   cat gpurun_out/r4_early_ab_$w.json
 done
@@ -34,4 +34,9 @@ echo "=== host round probe (512 workers, RCCL world 1, collectives forced)"
 timeout -k 10 200 python3 tools/host_round_probe.py > gpurun_out/r4_host_probe.json 2> gpurun_out/r4_host_probe.err \
   || { tail -n 20 gpurun_out/r4_host_probe.err; exit 1; }
 cat gpurun_out/r4_host_probe.json
+echo "=== SCALE command shape at 8 gloo ranks on this one GPU (VERDICT r3 item 2)"
+timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+  --master-port 29517 bench.py --gpus 8 --backend gloo --workers 256 --strong-workers 2048 --steps 5 --warmup 3 \
+  > gpurun_out/r4_rehearsal8.json 2> gpurun_out/r4_rehearsal8.err || { tail -n 30 gpurun_out/r4_rehearsal8.err; exit 1; }
+tail -n 1 gpurun_out/r4_rehearsal8.json | cut -c 1-400
 echo "=== done"

@@ -28,4 +28,8 @@ DOPT_LIB=$PWD/distributed-optimization_amd/libdopt_ab.so timeout -k 10 300 pytho
   --data-dtype float32 --reps 3 --shapes "2,8,2,1 2,8,2,0" > gpurun_out/r4_c5_ldot.txt 2>&1 \
   || { tail -n 20 gpurun_out/r4_c5_ldot.txt; exit 1; }
 cat gpurun_out/r4_c5_ldot.txt | grep -v amdgpu.ids
+echo "=== C3 profile: kernel stats + FETCH_SIZE / WRITE_SIZE passes (summarised locally into profiles/r4_*)"
+OUT=gpurun_out/prof_r4 bash scripts/profile.sh || exit 1
+echo "=== C5 profile (x32 row-space rounds)"
+OUT=gpurun_out/prof_r4c5 PSTEPS=6 BENCH_ARGS="--config c5" bash scripts/profile.sh || exit 1
 echo "=== done"

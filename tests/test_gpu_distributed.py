@@ -51,7 +51,7 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
     B = int(os.environ.get("DOPT_TEST_BATCH", M))  # B < M: device-drawn minibatches
     if B < M:
         eng.set_sampler("device", seed=31, first_worker=plan.lo)
-    uni = top.uniform_offdiag() if mean else None
+    uni = top.uniform_offdiag() if mean is True else None
     run = Dm.DistributedDSGD(eng, plan, N, N * M, device=0,
                              mean=None if uni is None else (uni[0], uni[1][plan.lo:plan.hi]))
     which = os.environ.get("DOPT_TEST_METRICS", "both")
@@ -84,7 +84,9 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
                                                       ("float64", False, 3, "1", 3),
                                                       ("float64/x32", False, T, "1", 2),
                                                       ("float64/x32", False, T, "0", 2),
-                                                      ("float64/x32", True, T, "1", 2)])
+                                                      ("float64/x32", True, T, "1", 2),
+                                                      ("float64/x32", "csr", T, "1", 2),
+                                                      ("float32", "csr", T, "0", 2)])
 def test_ranks_match_single_context(tmp_path, dtype, mean, T, lagged, world):
     import torch.multiprocessing as mp
 
@@ -96,12 +98,13 @@ def test_ranks_match_single_context(tmp_path, dtype, mean, T, lagged, world):
 
 
 def _topo(mean, n, parts=0):
-    """The test graph; with parts > 0 relabelled by the spectral partition for that many
-    ranks (bench.py's C3 placement)."""
+    """The test graph (mean: the complete graph, mixed through the column sums when True and as CSR
+    rows longer than the mix kernels' register-held entries when "csr"); with parts > 0 relabelled by
+    the spectral partition for that many ranks (bench.py's C3 placement)."""
     import distributed as Dm
     import topology as TP
 
-    if mean:
+    if mean:  # True: column-sum mixing; "csr": the complete graph as CSR rows of n entries
         return TP.fully_connected(n)
     top = TP.random_regular(n, 4, seed=2)
     if parts:
@@ -118,14 +121,14 @@ def _compare_single(got, dtype, mean, T, N=N, D=D, M=M, exact=True, parts=0):
     if B < M:
         eng.set_sampler("device", seed=31)
     top = _topo(mean, N, parts)
-    if mean:
+    if mean is True:
         eng.set_mixing_mean(*top.uniform_offdiag())
     else:
         eng.set_topology(top.row_ptr, top.col, top.w)
     obj, cons, _ = eng.run_dsgd(T, 0.05, B, 1e-3, 1e-3, 0.25)
     x = eng.get_models()
     eng.close()
-    if mean or not exact:  # column sums / split partial dots reduced per rank then across ranks
+    if mean is True or not exact:  # column sums / split partial dots reduced per rank then across ranks
         np.testing.assert_allclose(got["x"], x, rtol=1e-12, atol=1e-15)
     else:
         np.testing.assert_array_equal(got["x"], x)
