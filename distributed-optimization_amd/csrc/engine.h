@@ -108,6 +108,7 @@ struct FoldArgs {
 // column-block partial of the column sums of x_new to part[g]; the last workgroup of a column
 // block to arrive (agent-scope ticket) sums the NG partials in group order into own_out and into
 // the send buffer's sum rows of every peer.  Block 0 folds a history row (FoldArgs).
+constexpr int kMcsKargRanks = 16;  // sum rows of the first ranks passed as kernel arguments
 struct McsArgs {
   double* part;            // [ng x ld] group partials of the column sums of x_new
   unsigned* cnt;           // [ncb] arrival tickets (zero between launches: the last arriver resets)
@@ -119,6 +120,8 @@ struct McsArgs {
   const int64_t* sum_out;  // [world] send-buffer row of the sums of x_new for peer p (-1: self)
   double* cons_part;       // [ncb x n] consensus partial of (column block, worker), or null
   double n_div;            // the mean's divisor (workers on all ranks)
+  int32_t kin[kMcsKargRanks], kout[kMcsKargRanks];  // sum_in / sum_out of ranks < kMcsKargRanks
+  int32_t cut;             // A/B builds, timing only (DOPT_MIXCS_CUT): end the kernel early (0: never)
 };
 
 // Row-space rounds (rowspace.hip): complete graph (uniform W_ii), either objective, full

@@ -962,6 +962,68 @@ __global__ __launch_bounds__(NT) void k_colsum_part(const T* __restrict__ x, int
   }
 }
 
+// sum_{k = threadIdx.x + j NT < cnt} v[k] in fold_block's order -- four accumulators s0..s3 taking
+// k, k + NT, k + 2 NT, k + 3 NT per step of 4 NT, the rest into s0, then (s0 + s1) + (s2 + s3) -- with
+// two steps' loads (and the tail's up to three) issued before their adds: fewer dependent memory
+// round trips in the one-workgroup folds, the same sums bit for bit.
+__device__ __forceinline__ double fold_sum4(const double* v, int64_t cnt) {
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  int64_t k = threadIdx.x;
+  for (; k + 7 * NT < cnt; k += 8 * NT) {
+    double a[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) a[q] = v[k + q * NT];
+    s0 += a[0];
+    s1 += a[1];
+    s2 += a[2];
+    s3 += a[3];
+    s0 += a[4];
+    s1 += a[5];
+    s2 += a[6];
+    s3 += a[7];
+  }
+  for (; k + 3 * NT < cnt; k += 4 * NT) {
+    double a[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[q] = v[k + q * NT];
+    s0 += a[0];
+    s1 += a[1];
+    s2 += a[2];
+    s3 += a[3];
+  }
+  double t[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) t[q] = k + q * NT < cnt ? v[k + q * NT] : 0.0;
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+    if (k + q * NT < cnt) s0 += t[q];
+  return (s0 + s1) + (s2 + s3);
+}
+
+// ||xbar||^2 over nch chunks of vn elements, thread-strided by chunk, in that order; up to four
+// chunks' loads in flight per thread.
+template <typename T>
+__device__ __forceinline__ double fold_xnorm(const T* x, int nch, int vn) {
+  double q = 0.0;
+  for (int c0 = threadIdx.x; c0 < nch; c0 += 4 * NT) {
+    double v[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = c0 + u * NT;
+        v[u][e] = (c < nch && e < vn) ? (double)x[(int64_t)c * vn + e] : 0.0;
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (c0 + u * NT < nch)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (e < vn) q += v[u][e] * v[u][e];
+  }
+  return q;
+}
+
 // The history fold of k_history by one NT-thread block (fixed order): *out_c = sum sc[0:nc],
 // *out_l = sum sl[0:nl], *out_q = ||xbar||^2; null outputs are skipped.
 template <typename T>
@@ -969,29 +1031,9 @@ __device__ void fold_block(const FoldArgs& f, int nch, double (*red)[64 * VT<T>:
   constexpr int VN = VT<T>::n;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double a = 0.0, b = 0.0, q = 0.0;
-  // four independent accumulators per thread (fixed order), so 256 threads keep many loads in
-  // flight instead of one dependent add chain per thread
-  auto sum4 = [&](const double* v, int64_t cnt) {
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-    int64_t k = threadIdx.x;
-    for (; k + 3 * NT < cnt; k += 4 * NT) {
-      s0 += v[k];
-      s1 += v[k + NT];
-      s2 += v[k + 2 * NT];
-      s3 += v[k + 3 * NT];
-    }
-    for (; k < cnt; k += NT) s0 += v[k];
-    return (s0 + s1) + (s2 + s3);
-  };
-  if (f.sc && f.out_c) a = sum4(f.sc, f.nc);
-  if (f.sl && f.out_l) b = sum4(f.sl, f.nl);
-  if (f.xbar && f.out_q)
-    for (int c = threadIdx.x; c < nch; c += NT)
-#pragma unroll
-      for (int e = 0; e < VN; ++e) {
-        const double v = (double)((const T*)f.xbar)[(int64_t)c * VN + e];
-        q += v * v;
-      }
+  if (f.sc && f.out_c) a = fold_sum4(f.sc, f.nc);
+  if (f.sl && f.out_l) b = fold_sum4(f.sl, f.nl);
+  if (f.xbar && f.out_q) q = fold_xnorm<T>((const T*)f.xbar, nch, VN);
   a = wave_sum(a);
   b = wave_sum(b);
   q = wave_sum(q);
@@ -1479,7 +1521,7 @@ hipError_t launch_mix(int dtype, int cpl, const RoundArgs& a, const void* G, int
 
 // ---------------------------------------------------------------------------- lagged mix + column sums
 // k_mixcs (round 4): the lagged schedule's mix (k_mix with a.xsum) with the column sums of the new
-// iterates fused in, so a multi-GPU round is two kernels -- the gradient pass and this -- and the
+// iterates fused in, so a multi-GPU round is the gradient pass, this and k_mixcs_final, and the
 // next round's exchange carries the column sums beside the halo rows (no all-reduce; every rank
 // sums the ranks' vectors in rank order, so all ranks hold the same bits).
 //   block 0: the history fold of McsArgs' caller (FoldArgs; nothing when no output is set);
@@ -1488,38 +1530,21 @@ hipError_t launch_mix(int dtype, int cpl, const RoundArgs& a, const void* G, int
 // once); per worker: xbar of x_old from the rank-ordered sums, the consensus partial of this column
 // block, the mix + step (CSR order and arithmetic of k_mix / k_round: bitwise the same iterates) or,
 // for an interior worker the gradient kernel stepped, its new row read back; the new rows' column
-// sums accumulate per lane in float64 in worker order, meet in LDS in wave order, and go to part[g]
-// as write-through (sc1) stores.  The last arriving workgroup of column block cb (agent-scope
-// ticket, MI355X_MICROARCH.md "Valid forms" row 1: sc1 stores drained by every storing wave before
-// one lane's ticket add, sc1 loads after it; the acquire fence is kept as well) sums part[0..ng) in
-// group order and writes the block's sums to own_out and to every peer's sum rows in the send
-// buffer, then resets the ticket for the next launch.
+// sums accumulate per lane in float64 in worker order, meet in LDS in wave order, and go to part[g];
+// k_mixcs_final (the next launch) sums part[0..ng) of each column block in group order and writes
+// the sums to own_out and to every peer's sum rows in the send buffer.  TICKET (A/B builds,
+// DOPT_MIXCS_TICKET=1): one launch instead -- the partials as write-through (sc1) stores, and the
+// last arriving workgroup of column block cb (agent-scope ticket, MI355X_MICROARCH.md "Valid forms"
+// row 1: sc1 stores drained by every storing wave before one lane's ticket add, sc1 loads after it;
+// the acquire fence kept as well) does k_mixcs_final's sum, then resets the ticket.
 template <int RW>
 __device__ void fold_block_rw(const FoldArgs& f, int nch, int vn, double (*red)[RW]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double a = 0.0, b = 0.0, q = 0.0;
-  auto sum4 = [&](const double* v, int64_t cnt) {  // the fold_block order
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-    int64_t k = threadIdx.x;
-    for (; k + 3 * NT < cnt; k += 4 * NT) {
-      s0 += v[k];
-      s1 += v[k + NT];
-      s2 += v[k + 2 * NT];
-      s3 += v[k + 3 * NT];
-    }
-    for (; k < cnt; k += NT) s0 += v[k];
-    return (s0 + s1) + (s2 + s3);
-  };
-  if (f.sc && f.out_c) a = sum4(f.sc, f.nc);
-  if (f.sl && f.out_l) b = sum4(f.sl, f.nl);
-  if (f.xbar && f.out_q) {
-    for (int c = threadIdx.x; c < nch; c += NT)
-      for (int e = 0; e < vn; ++e) {
-        const int64_t k = (int64_t)c * vn + e;
-        const double v = vn == 2 ? ((const double*)f.xbar)[k] : (double)((const float*)f.xbar)[k];
-        q += v * v;
-      }
-  }
+  if (f.sc && f.out_c) a = fold_sum4(f.sc, f.nc);
+  if (f.sl && f.out_l) b = fold_sum4(f.sl, f.nl);
+  if (f.xbar && f.out_q)
+    q = vn == 2 ? fold_xnorm<double>((const double*)f.xbar, nch, 2) : fold_xnorm<float>((const float*)f.xbar, nch, 4);
   a = wave_sum(a);
   b = wave_sum(b);
   q = wave_sum(q);
@@ -1563,17 +1588,21 @@ __device__ __forceinline__ double ranks_sum(const McsArgs& m, const T* halo, int
 
 constexpr int kMixcsMaxGroups = 64;  // mixcs_shape keeps ng <= this
 
-template <typename T, int CPB>
+template <typename T, int CPB, bool TICKET>
 __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __restrict__ G, int n, const McsArgs m,
                                               const FoldArgs fold) {
   using V = typename VT<T>::v;
   constexpr int VN = VT<T>::n;
-  constexpr int MAXE = 6;          // CSR entries held in registers (the rest of a longer row: loaded at use)
+  constexpr int MAXE = 6;            // CSR entries held in registers (the rest of a longer row: loaded at use)
+  constexpr int MAXS = 2;            // send slots of a row held in registers (the rest: loaded at use)
   constexpr int BC = 64 * CPB * VN;  // columns of a column block
+  constexpr int XR = 2 * NW;         // ranks' sums staged through LDS per pass (two per wave)
+  constexpr int XT = BC / 64;        // columns per lane in the staging
   __shared__ double red[NW][BC];
+  __shared__ double xsum[XR][BC];
   __shared__ int last;
   if (blockIdx.x == 0) {
-    fold_block_rw<BC>(fold, a.nchunks, VN, red);
+    if (m.cut != 3) fold_block_rw<BC>(fold, a.nchunks, VN, red);
     return;
   }
   const int lane = threadIdx.x & 63;
@@ -1583,47 +1612,50 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
   const int64_t ld = a.ld;
   const int nch = a.nchunks;
   const int cbase = cb * 64 * CPB;
+  const int64_t colbase = (int64_t)cbase * VN, ncol = (int64_t)nch * VN;
   const T eta = (T)a.eta;
   const T* halo = (const T*)a.halo;
-  // xbar of x_old at this lane's chunks (as k_colsum_final / k_mix round it: (T)(sum / n))
-  V xb[CPB];
-#pragma unroll
-  for (int j = 0; j < CPB; ++j) {
-    const int c = cbase + lane + 64 * j;
-    xb[j] = V(0);
-    if (c < nch) {
-#pragma unroll
-      for (int e = 0; e < VN; ++e) xb[j][e] = (T)(ranks_sum<T>(m, halo, ld, (int64_t)c * VN + e) / m.n_div);
-      if (g == 0 && wave == 0 && a.xbar_out) *(V*)((T*)a.xbar_out + (int64_t)c * VN) = xb[j];
-    }
-  }
-  double cs[CPB][VN];
-#pragma unroll
-  for (int j = 0; j < CPB; ++j)
-#pragma unroll
-    for (int e = 0; e < VN; ++e) cs[j][e] = 0.0;
   const int i_end = (g + 1) * m.r < n ? (g + 1) * m.r : n;
-  for (int i0 = g * m.r + wave; i0 < i_end; i0 += 2 * NW) {
-    // two workers of this wave: i0 and i0 + NW; every load of both is issued before any use
-    V own[2][CPB], gv[2][CPB], r[2][MAXE][CPB];
-    int64_t e0[2], e1[2];
-    bool live[2], skip[2];
+
+  // Every load of a wave's two workers is issued before any of them is used: (A) the CSR range,
+  // interior flag, send range and own row, (B) the CSR columns, the send slots and the gradient
+  // (or, for an interior worker, the row the gradient kernel stepped), (C) the neighbour rows.
+  V own[2][CPB], gv[2][CPB], r[2][MAXE][CPB];
+  int64_t e0[2], e1[2], s0[2], s1[2];
+  int32_t sl[2][MAXS];
+  bool live[2], skip[2];
+  auto issue = [&](int i0) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int i = i0 + u * NW;
       live[u] = i < i_end;
-      skip[u] = live[u] && a.interior && a.interior[i];
       e0[u] = live[u] ? a.rp[i] : 0;
-      e1[u] = live[u] ? a.rp[i + 1] : 0;  // entries past the first MAXE: loaded at their use
+      e1[u] = live[u] ? a.rp[i + 1] : 0;
+      skip[u] = live[u] && a.interior && a.interior[i];
+      s0[u] = (live[u] && a.sptr) ? a.sptr[i] : 0;
+      s1[u] = (live[u] && a.sptr) ? a.sptr[i + 1] : 0;
+#pragma unroll
+      for (int j = 0; j < CPB; ++j) {
+        const int c = cbase + lane + 64 * j;
+        own[u][j] = (live[u] && c < nch) ? *(const V*)((const T*)a.x_old + (int64_t)i * ld + (int64_t)c * VN) : V(0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = i0 + u * NW;
+#pragma unroll
+      for (int q = 0; q < MAXS; ++q) sl[u][q] = (!skip[u] && s0[u] + q < s1[u]) ? a.sslot[s0[u] + q] : -1;
 #pragma unroll
       for (int j = 0; j < CPB; ++j) {
         const int c = cbase + lane + 64 * j;
         const bool in = live[u] && c < nch;
-        own[u][j] = in ? *(const V*)((const T*)a.x_old + (int64_t)i * ld + (int64_t)c * VN) : V(0);
         // an interior worker's new row (written by the gradient kernel) comes back in gv
         gv[u][j] = !in ? V(0) : skip[u] ? *(const V*)((const T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN)
                                         : *(const V*)(G + (int64_t)i * ld + (int64_t)c * VN);
       }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
 #pragma unroll
       for (int k = 0; k < MAXE; ++k) {
         if (!skip[u] && e0[u] + k < e1[u]) {
@@ -1637,6 +1669,72 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
         }
       }
     }
+  };
+
+  // xbar of x_old at this lane's chunks, (T)(sum / n) of the ranks' column sums added in rank order
+  // (as k_xbar_ranks / k_colsum_final round it).  The ranks' sums of this column block come through
+  // LDS, XR ranks per pass, wave w loading ranks w and w + NW of the pass: a rank's row is read by
+  // one wave, and the first pass's loads are in flight with the first workers' rows.
+  double xv[2][XT];
+  auto xload = [&](int p0) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int p = p0 + wave + k * NW;
+      const double* src = nullptr;
+      if (p < m.world) {
+        const int64_t row = p < kMcsKargRanks ? (int64_t)m.kin[p] : m.sum_in[p];
+        src = p == m.rank ? m.own_in : (const double*)(halo + row * ld);
+      }
+#pragma unroll
+      for (int t = 0; t < XT; ++t) {
+        const int64_t col = colbase + lane + 64 * t;
+        xv[k][t] = (src && col < ncol) ? src[col] : 0.0;
+      }
+    }
+  };
+  double xs[CPB][VN];
+#pragma unroll
+  for (int j = 0; j < CPB; ++j)
+#pragma unroll
+    for (int e = 0; e < VN; ++e) xs[j][e] = 0.0;
+  auto xfold = [&](int p0) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int t = 0; t < XT; ++t) xsum[wave + k * NW][lane + 64 * t] = xv[k][t];
+    __syncthreads();
+    for (int q = 0; q < XR && p0 + q < m.world; ++q)
+#pragma unroll
+      for (int j = 0; j < CPB; ++j)
+#pragma unroll
+        for (int e = 0; e < VN; ++e) xs[j][e] += xsum[q][(lane + 64 * j) * VN + e];
+    __syncthreads();
+  };
+  xload(0);
+  int i0 = g * m.r + wave;
+  issue(i0);
+  xfold(0);
+  for (int p0 = XR; p0 < m.world; p0 += XR) {  // more than XR ranks: further passes
+    xload(p0);
+    xfold(p0);
+  }
+  V xb[CPB];
+#pragma unroll
+  for (int j = 0; j < CPB; ++j) {
+    const int c = cbase + lane + 64 * j;
+#pragma unroll
+    for (int e = 0; e < VN; ++e) xb[j][e] = c < nch ? (T)(xs[j][e] / m.n_div) : T(0);
+    if (c < nch && g == 0 && wave == 0 && a.xbar_out) *(V*)((T*)a.xbar_out + (int64_t)c * VN) = xb[j];
+  }
+  if (m.cut == 2) return;
+
+  double cs[CPB][VN];
+#pragma unroll
+  for (int j = 0; j < CPB; ++j)
+#pragma unroll
+    for (int e = 0; e < VN; ++e) cs[j][e] = 0.0;
+  for (bool first = true; i0 < i_end; i0 += 2 * NW, first = false) {
+    if (!first) issue(i0);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       if (!live[u]) continue;
@@ -1667,7 +1765,6 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
         const double t = wave_sum((double)hsum<T>(dv));
         if (lane == 0) m.cons_part[(int64_t)cb * n + i] = t;
       }
-      const int64_t s0 = (!skip[u] && a.sptr) ? a.sptr[i] : 0, s1 = (!skip[u] && a.sptr) ? a.sptr[i + 1] : 0;
 #pragma unroll
       for (int j = 0; j < CPB; ++j) {
         const int c = cbase + lane + 64 * j;
@@ -1676,23 +1773,30 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
         for (int e = 0; e < VN; ++e) cs[j][e] += (double)xn[j][e];
         if (skip[u]) continue;
         *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = xn[j];
-        for (int64_t q = s0; q < s1; ++q)  // rows peers read next round
+#pragma unroll
+        for (int q = 0; q < MAXS; ++q)  // rows peers read next round
+          if (sl[u][q] >= 0) *(V*)((T*)a.send + (int64_t)sl[u][q] * ld + (int64_t)c * VN) = xn[j];
+        for (int64_t q = s0[u] + MAXS; q < s1[u]; ++q)
           *(V*)((T*)a.send + (int64_t)a.sslot[q] * ld + (int64_t)c * VN) = xn[j];
       }
     }
   }
-  // this group's partial of the column block: waves in order, write-through stores
+  if (m.cut == 1) return;
+  // this group's partial of the column block: waves in order (TICKET: write-through stores)
 #pragma unroll
   for (int j = 0; j < CPB; ++j)
 #pragma unroll
     for (int e = 0; e < VN; ++e) red[wave][(lane + 64 * j) * VN + e] = cs[j][e];
   __syncthreads();
-  const int64_t colbase = (int64_t)cbase * VN;
   for (int t = threadIdx.x; t < BC; t += NT) {
-    if (colbase + t >= (int64_t)nch * VN) break;
+    if (colbase + t >= ncol) break;
     const double s = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
-    __hip_atomic_store(m.part + (int64_t)g * ld + colbase + t, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (TICKET)
+      __hip_atomic_store(m.part + (int64_t)g * ld + colbase + t, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      m.part[(int64_t)g * ld + colbase + t] = s;
   }
+  if (!TICKET || m.cut == 4) return;  // (two launches: k_mixcs_final sums the partials)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1707,7 +1811,7 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
   if (!last) return;
   for (int t = threadIdx.x; t < BC; t += NT) {
     const int64_t col = colbase + t;
-    if (col >= (int64_t)nch * VN) break;
+    if (col >= ncol) break;
     // every partial in flight at once (ng <= kMixcsMaxGroups), summed in group order
     double v[kMixcsMaxGroups];
 #pragma unroll
@@ -1719,10 +1823,40 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
     for (int q = 0; q < kMixcsMaxGroups; ++q)
       if (q < m.ng) s += v[q];
     m.own_out[col] = s;
-    for (int p = 0; p < m.world; ++p)
-      if (m.sum_out[p] >= 0) ((double*)((T*)a.send + m.sum_out[p] * ld))[col] = s;
+    for (int p = 0; p < m.world; ++p) {
+      const int64_t row = p < kMcsKargRanks ? (int64_t)m.kout[p] : m.sum_out[p];
+      if (row >= 0) ((double*)((T*)a.send + row * ld))[col] = s;
+    }
   }
   if (threadIdx.x == 0) __hip_atomic_store(m.cnt + cb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The second launch of the two-kernel k_mixcs (the default): workgroup cb sums the ng group partials
+// of its column block in group order (the last arriver's arithmetic), writes them to own_out and to
+// every peer's sum rows.  The kernel boundary is the hand-off: the single-launch form's write-through
+// stores, agent-scope ticket and acquire cost ~9 us of dependent latency per round at 512 workers
+// (timing-only cuts, profiles/r4_mixcs_cut.txt), the boundary a few.
+template <typename T>
+__global__ __launch_bounds__(NT) void k_mixcs_final(const McsArgs m, int64_t ld, int nch, T* send) {
+  constexpr int VN = VT<T>::n;
+  constexpr int BC = 64 * 2 * VN;  // k_mixcs's column block (CPB = 2)
+  const int64_t colbase = (int64_t)blockIdx.x * BC, ncol = (int64_t)nch * VN;
+  for (int t = threadIdx.x; t < BC; t += NT) {
+    const int64_t col = colbase + t;
+    if (col >= ncol) break;
+    double v[kMixcsMaxGroups];
+#pragma unroll
+    for (int q = 0; q < kMixcsMaxGroups; ++q) v[q] = q < m.ng ? m.part[(int64_t)q * ld + col] : 0.0;
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < kMixcsMaxGroups; ++q)
+      if (q < m.ng) s += v[q];
+    m.own_out[col] = s;
+    for (int p = 0; p < m.world; ++p) {
+      const int64_t row = p < kMcsKargRanks ? (int64_t)m.kout[p] : m.sum_out[p];
+      if (row >= 0) ((double*)(send + row * ld))[col] = s;
+    }
+  }
 }
 
 void mixcs_shape(int dtype, int64_t n, int32_t nch, int32_t* ncb, int32_t* r, int32_t* ng) {
@@ -1741,11 +1875,43 @@ hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_work
   FoldArgs f;
   memset(&f, 0, sizeof(f));
   if (fold) f = *fold;
+  McsArgs mm = m;
+#ifdef DOPT_AB
+  static const int cut = [] {
+    const char* v = getenv("DOPT_MIXCS_CUT");
+    return v ? atoi(v) : 0;
+  }();
+  mm.cut = cut;
+#else
+  mm.cut = 0;
+#endif
+  // one launch with the agent-scope last-arriver hand-off (A/B builds: DOPT_MIXCS_TICKET=1), or two
+  static const bool ticket = [] {
+#ifdef DOPT_AB
+    const char* v = getenv("DOPT_MIXCS_TICKET");
+    return v && atoi(v) != 0;
+#else
+    return false;
+#endif
+  }();
   const dim3 grid(1 + (unsigned)m.ng * (unsigned)m.ncb);
+  if (dtype == 0) {
+    if (ticket)
+      hipLaunchKernelGGL((k_mixcs<float, 2, true>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
+    else
+      hipLaunchKernelGGL((k_mixcs<float, 2, false>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
+  } else {
+    if (ticket)
+      hipLaunchKernelGGL((k_mixcs<double, 2, true>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
+    else
+      hipLaunchKernelGGL((k_mixcs<double, 2, false>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
+  }
+  if (ticket || mm.cut != 0) return hipGetLastError();
+  const dim3 g2((unsigned)m.ncb);
   if (dtype == 0)
-    hipLaunchKernelGGL((k_mixcs<float, 2>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, m, f);
+    hipLaunchKernelGGL(k_mixcs_final<float>, g2, dim3(NT), 0, s, mm, a.ld, a.nchunks, (float*)a.send);
   else
-    hipLaunchKernelGGL((k_mixcs<double, 2>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, m, f);
+    hipLaunchKernelGGL(k_mixcs_final<double>, g2, dim3(NT), 0, s, mm, a.ld, a.nchunks, (double*)a.send);
   return hipGetLastError();
 }
 

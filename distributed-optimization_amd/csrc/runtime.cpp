@@ -2397,7 +2397,8 @@ int dopt_phase_metrics(dopt_ctx* c, uint32_t flags, int include_xnorm, double* o
 // every row at xbar_{g-1}) beside the exchange of x_g's send rows AND every rank's column sums of
 // x_g, then dopt_lagged_mix (k_mixcs: xbar_g from the rank-ordered sums, consensus of x_g, x_{g+1}
 // of the other workers and their send rows, the column sums of x_{g+1} into the send buffer, and
-// the fold of history[g-2]).  Two kernels and one collective per round.
+// the fold of history[g-2]; k_mixcs_final totals the column sums).  Three launches and one
+// collective per round.
 int dopt_lagged_exchange_layout(dopt_ctx* c, int32_t world, int32_t rank, const int64_t* sum_send_row,
                                 const int64_t* sum_recv_row) {
   CHECK_ARG(c && sum_send_row && sum_recv_row, "NULL argument");
@@ -2500,6 +2501,10 @@ McsArgs lagged_args(dopt_ctx* c, const double* own_in, double* own_out, double* 
   m.sum_out = c->lg_sum_out;
   m.cons_part = cons_part;
   m.n_div = (double)n_div(c);
+  for (int p = 0; p < kMcsKargRanks; ++p) {  // the first ranks' rows by value (no dependent load in the kernel)
+    m.kin[p] = p < (int)c->lg_in_h.size() ? (int32_t)c->lg_in_h[p] : -1;
+    m.kout[p] = p < (int)c->lg_out_h.size() ? (int32_t)c->lg_out_h[p] : -1;
+  }
   return m;
 }
 }  // namespace

@@ -667,7 +667,7 @@ class DistributedDSGD:
           lagged_mix: xbar_g (rank-ordered sums), consensus of x_g, x_{g+1} and its send rows,
                       the column sums of x_{g+1} into the send buffer, fold of history[g-2]
 
-        Two kernels, two engine calls and one collective per round (round 4; round 3 had four
+        Three launches, two engine calls and one collective per round (round 4; round 3 had four
         kernels, two collectives and five engine calls); history row t is complete once round t + 2's
         mix has folded it.  After the last round of a chain (the tail): one more exchange for the
         sums of x_T, then xbar_T, the consensus of x_T and one pass for the losses at xbar_{T-1} and

@@ -353,7 +353,7 @@ int dopt_rs_phase_metrics(dopt_ctx *ctx, uint32_t metric_flags);
 /* The lagged schedule (round 4, ABI version 3; distributed.py DistributedDSGD._run_lagged): one
  * collective per round -- the halo rows of x_g AND every rank's column sums of x_g in one exchange
  * (an all-to-all-v: the send / halo buffers hold, per peer in rank order, that peer's rows then
- * 8 ld bytes of float64 sums) -- and two kernels per round:
+ * 8 ld bytes of float64 sums) -- and three launches per round (gradient, k_mixcs, k_mixcs_final):
  *   exchange(x_g rows + sums) ----------------------------------------------.
  *   dopt_lagged_grad: gradient pass of x_g (+ loss of every row at xbar_{g-1}) +--> dopt_lagged_mix
  * dopt_lagged_exchange_layout: the send-buffer row where the sums for peer p go and the halo-buffer
