@@ -161,7 +161,8 @@ struct RsArgs {
   const double* csum;      // [ld] all-reduced column sums C (multi-GPU), or null: sum cpart
   double a1, q, eta, eta_n;  // w_off N, W_ii - w_off - eta mu, eta, eta / N
   int32_t blk0;            // first column block of this pass launch (column-chunked passes)
-  int32_t ldot;            // k_rs_pass: row dots reduced through LDS per 64-row window (1) or by DPP per row (0)
+  int32_t ldot;            // k_rs_pass: row dots through LDS per 64-row window, every lane's partial (1) or lane
+                           // pairs first (2, A/B), or by DPP per row (0)
   // iterates that did not start equal: x_i = c x_i(0) + Z + X_i^T beta_i (else c = 0, pointers null)
   double c;                // the x_i(0) coefficient of the iterates the pass reads (prod of q so far)
   const double* xbar0;     // [ld] mean of the starting iterates

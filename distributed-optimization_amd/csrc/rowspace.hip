@@ -48,12 +48,16 @@ __device__ __forceinline__ typename VT<T>::v rs_ld_nt(const T* p) {
 // (XT = T) and k_rs_pass_x32<...> (float64 arithmetic over float32-stored rows, the C3 headline's
 // layout: the 16-byte chunk is 4 floats, xbar's 4 doubles stay in registers, every product and
 // sum in float64).
-// LDOT (round 4): each row's per-lane partial dot goes to LDS (pdot: [64 rows][64 lanes] per wave,
-// lane l's value of row k at slot (l + k) % 64, so the window's read-back is 2-way bank conflicted at
-// worst); after the window, lane k sums row k's 64 partials in lane order -- one LDS store per row
-// instead of a six-step DPP butterfly and its dependency chain per row (a wave per SIMD has nothing
-// else to issue while the chain drains).
-template <typename T, typename XT, bool COLS, int CB, int NBUF, bool LDOT = false>
+// LDOT (round 4): each row's per-lane partial dot goes to LDS instead of a six-step DPP butterfly and
+// its dependency chain per row (a wave per SIMD has nothing else to issue while the chain drains);
+// after the window, lane k sums row k's partials.  LDOT 1: pdot [64 rows][64 lanes] per wave, lane
+// l's value of row k at slot (l + k) % 64, summed in lane order (32 KiB per wave: 147 KiB per
+// workgroup, one workgroup per CU; the default).  LDOT 2 (A/B, DOPT_RS_LDOT=2): adjacent lanes'
+// partials are first added by one DPP quad swap, and the even lanes store [64 rows][32 pairs] (slot
+// (l/2 + k) % 32), summed in pair order -- 16 KiB per wave, 80 KiB per workgroup with the column-sum
+// LDS, so two workgroups (two waves per SIMD at <= 256 VGPRs) share a CU: 1 % slower than LDOT 1
+// (profiles/r4_c5_ldot2.txt) -- the pass does not want more waves, as no shape A/B has shown.
+template <typename T, typename XT, bool COLS, int CB, int NBUF, int LDOT = 0>
 __device__ __forceinline__ void rs_pass_body(const RsArgs& a, double* red, double* pdot = nullptr) {
   using V = typename VT<XT>::v;
   constexpr int VN = VT<XT>::n;
@@ -189,8 +193,14 @@ __device__ __forceinline__ void rs_pass_body(const RsArgs& a, double* red, doubl
             }
           }
           double dot = 0.0;
-          if constexpr (LDOT) pdot[kk * 64 + ((lane + kk) & 63)] = p;
-          else dot = wave_sum_dpp(p);
+          if constexpr (LDOT == 1) {
+            pdot[kk * 64 + ((lane + kk) & 63)] = p;
+          } else if constexpr (LDOT == 2) {
+            const double pp = dpp_add<0xb1, 0xf, 0xf>(p);  // p[l] + p[l ^ 1] (quad_perm [1,0,3,2])
+            if (!(lane & 1)) pdot[kk * 32 + (((lane >> 1) + kk) & 31)] = pp;
+          } else {
+            dot = wave_sum_dpp(p);
+          }
           if constexpr (COLS) {
             const double cf = readlane_t(cwv, kk);  // wave-uniform
             if constexpr (TACC) {
@@ -206,7 +216,7 @@ __device__ __forceinline__ void rs_pass_body(const RsArgs& a, double* red, doubl
                 for (int e = 0; e < VN; ++e) acc[j][e] += cf * (double)rv[j][e];
             }
           }
-          if constexpr (!LDOT) st = lane == kk ? dot : st;
+          if constexpr (LDOT == 0) st = lane == kk ? dot : st;
         };
         if (nw == 64) {
           for (int g0 = 0; g0 < 64; g0 += NBUF) {
@@ -228,11 +238,12 @@ __device__ __forceinline__ void rs_pass_body(const RsArgs& a, double* red, doubl
           }
         }
         flush();
-        if constexpr (LDOT) {  // row `lane` of the window: its 64 partials in lane order
+        if constexpr (LDOT != 0) {  // row `lane` of the window: its partials in lane (pair) order
+          constexpr int PW = LDOT == 1 ? 64 : 32;
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           double s0 = 0.0;
 #pragma unroll 8
-          for (int j = 0; j < 64; ++j) s0 += pdot[lane * 64 + ((j + lane) & 63)];
+          for (int j = 0; j < PW; ++j) s0 += pdot[lane * PW + ((j + lane) & (PW - 1))];
           st = s0;
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // reads done before the next window's stores
         }
@@ -272,18 +283,20 @@ __device__ __forceinline__ void rs_pass_body(const RsArgs& a, double* red, doubl
   }
 }
 
-template <typename T, bool COLS, int CB, int NBUF, bool LDOT = false>
-__global__ __launch_bounds__(NT) void k_rs_pass(const RsArgs a) {
+template <typename T, bool COLS, int CB, int NBUF, int LDOT = 0>
+__global__ __launch_bounds__(NT, LDOT == 2 ? 2 : 1) void k_rs_pass(const RsArgs a) {
+  constexpr int PWV = LDOT == 1 ? 64 * 64 : LDOT == 2 ? 64 * 32 : 0;  // pdot doubles per wave
   __shared__ double red[COLS ? NW * 64 * CB * VT<T>::n : 1];
-  __shared__ double pdot[LDOT ? NW * 64 * 64 : 1];
-  rs_pass_body<T, T, COLS, CB, NBUF, LDOT>(a, red, pdot + (LDOT ? (threadIdx.x >> 6) * 64 * 64 : 0));
+  __shared__ double pdot[LDOT ? NW * PWV : 1];
+  rs_pass_body<T, T, COLS, CB, NBUF, LDOT>(a, red, pdot + (threadIdx.x >> 6) * PWV);
 }
 
-template <bool COLS, int CB, int NBUF, bool LDOT = false>
-__global__ __launch_bounds__(NT) void k_rs_pass_x32(const RsArgs a) {
+template <bool COLS, int CB, int NBUF, int LDOT = 0>
+__global__ __launch_bounds__(NT, LDOT == 2 ? 2 : 1) void k_rs_pass_x32(const RsArgs a) {  // (LDOT 2: <= 256 VGPRs)
+  constexpr int PWV = LDOT == 1 ? 64 * 64 : LDOT == 2 ? 64 * 32 : 0;
   __shared__ double red[COLS ? NW * 64 * CB * VT<float>::n : 1];
-  __shared__ double pdot[LDOT ? NW * 64 * 64 : 1];
-  rs_pass_body<double, float, COLS, CB, NBUF, LDOT>(a, red, pdot + (LDOT ? (threadIdx.x >> 6) * 64 * 64 : 0));
+  __shared__ double pdot[LDOT ? NW * PWV : 1];
+  rs_pass_body<double, float, COLS, CB, NBUF, LDOT>(a, red, pdot + (threadIdx.x >> 6) * PWV);
 }
 
 // k_rs_rows: one workgroup per worker (m_i <= 64 rows, lane k = row k).  u_k = sum over the
@@ -822,11 +835,23 @@ static hipError_t rs_pass_shape(const RsArgs& a, dim3 grid, hipStream_t s) {
     else hipLaunchKernelGGL((k_rs_pass<T, COLS, C_, B_>), grid, dim3(NT), 0, s, a);          \
     return hipGetLastError();                                                                  \
   }
-  if (a.ldot && a.cb == 2 && a.nbuf == 8) {  // the default: row dots through LDS (DOPT_RS_LDOT=0: DPP)
-    if constexpr (X32) hipLaunchKernelGGL((k_rs_pass_x32<COLS, 2, 8, true>), grid, dim3(NT), 0, s, a);
-    else hipLaunchKernelGGL((k_rs_pass<T, COLS, 2, 8, true>), grid, dim3(NT), 0, s, a);
+  if (a.ldot == 2 && a.cb == 2 && a.nbuf == 8) {  // DOPT_RS_LDOT=2: row dots through LDS, lane pairs first
+    if constexpr (X32) hipLaunchKernelGGL((k_rs_pass_x32<COLS, 2, 8, 2>), grid, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((k_rs_pass<T, COLS, 2, 8, 2>), grid, dim3(NT), 0, s, a);
     return hipGetLastError();
   }
+  if (a.ldot == 1 && a.cb == 2 && a.nbuf == 8) {  // the default: every lane's partial through LDS
+    if constexpr (X32) hipLaunchKernelGGL((k_rs_pass_x32<COLS, 2, 8, 1>), grid, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((k_rs_pass<T, COLS, 2, 8, 1>), grid, dim3(NT), 0, s, a);
+    return hipGetLastError();
+  }
+#ifdef DOPT_AB
+  if (a.ldot == 1 && a.cb == 2 && a.nbuf == 16) {  // 16 rows in flight per wave (one wave per SIMD anyway)
+    if constexpr (X32) hipLaunchKernelGGL((k_rs_pass_x32<COLS, 2, 16, 1>), grid, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((k_rs_pass<T, COLS, 2, 16, 1>), grid, dim3(NT), 0, s, a);
+    return hipGetLastError();
+  }
+#endif
   RS_SHAPE(2, 8)  // the default; the others: A/B builds (DOPT_RS_CB / DOPT_RS_NBUF)
 #ifdef DOPT_AB
   RS_SHAPE(2, 6)
@@ -858,13 +883,15 @@ hipError_t launch_rs_pass(int dtype, int xdtype, bool cols, const RsArgs& a, hip
   const bool x32 = dtype == 1 && xdtype == 0;
   if (dtype != xdtype && !x32) return hipErrorInvalidValue;
   char buf[112];
-  const bool ld = a.ldot && a.cb == 2 && a.nbuf == 8;
+  const int ld = (a.cb == 2 && (a.nbuf == 8 || (a.nbuf == 16 && a.ldot == 1))) ? a.ldot : 0;
+  char lds[8] = "";
+  if (ld) snprintf(lds, sizeof(lds), ", %d", ld);
   if (x32)
     snprintf(buf, sizeof(buf), "void dopt::k_rs_pass_x32<%s, %d, %d%s>(dopt::RsArgs)", cols ? "true" : "false", a.cb,
-             a.nbuf, ld ? ", true" : "");
+             a.nbuf, lds);
   else
     snprintf(buf, sizeof(buf), "void dopt::k_rs_pass<%s, %s, %d, %d%s>(dopt::RsArgs)", rs_tn(dtype),
-             cols ? "true" : "false", a.cb, a.nbuf, ld ? ", true" : "");
+             cols ? "true" : "false", a.cb, a.nbuf, lds);
   if (cols) note_round_kernel(buf);
   if (x32) return cols ? rs_pass_shape<double, true, true>(a, grid, s) : rs_pass_shape<double, true, false>(a, grid, s);
   if (dtype == 0)
