@@ -851,6 +851,11 @@ static hipError_t rs_pass_shape(const RsArgs& a, dim3 grid, hipStream_t s) {
     else hipLaunchKernelGGL((k_rs_pass<T, COLS, 2, 16, 1>), grid, dim3(NT), 0, s, a);
     return hipGetLastError();
   }
+  if (a.ldot == 1 && a.cb == 4 && a.nbuf == 4) {  // 4 KiB blocks: half the blocks, half the row-dot partials
+    if constexpr (X32) hipLaunchKernelGGL((k_rs_pass_x32<COLS, 4, 4, 1>), grid, dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((k_rs_pass<T, COLS, 4, 4, 1>), grid, dim3(NT), 0, s, a);
+    return hipGetLastError();
+  }
 #endif
   RS_SHAPE(2, 8)  // the default; the others: A/B builds (DOPT_RS_CB / DOPT_RS_NBUF)
 #ifdef DOPT_AB
@@ -883,7 +888,8 @@ hipError_t launch_rs_pass(int dtype, int xdtype, bool cols, const RsArgs& a, hip
   const bool x32 = dtype == 1 && xdtype == 0;
   if (dtype != xdtype && !x32) return hipErrorInvalidValue;
   char buf[112];
-  const int ld = (a.cb == 2 && (a.nbuf == 8 || (a.nbuf == 16 && a.ldot == 1))) ? a.ldot : 0;
+  const int ld = ((a.cb == 2 && (a.nbuf == 8 || (a.nbuf == 16 && a.ldot == 1))) || (a.cb == 4 && a.nbuf == 4 && a.ldot == 1))
+                     ? a.ldot : 0;
   char lds[8] = "";
   if (ld) snprintf(lds, sizeof(lds), ", %d", ld);
   if (x32)

@@ -889,12 +889,14 @@ int ensure_rs(dopt_ctx* c) {
   // sums groups x ld) and long row visits matter more than the tail of ~4k 16 MiB workgroups.
   // Round 3 (tiled rows, C5 x32, alternated twice on one box, scripts/r3_rs_shape.sh): the windowed
   // row loop (NBUF dividing 64) at 2 / 8 10.66-10.83 ms, 2 / 4 10.79-10.81, 1 / 16 10.76-10.77,
-  // 1 / 8 10.93-11.41, the 2 / 6 row loop 10.87-11.12
+  // 1 / 8 10.93-11.41, the 2 / 6 row loop 10.87-11.12.  Round 4 (row dots through LDS, LDOT 1, one
+  // workgroup per CU; profiles/r4_c5_shapes.txt, 3 reps interleaved): 1 row group of 16k rows
+  // 10.757-10.762 ms, 2 groups 10.867-10.909, 4 groups 10.924-10.963, 16 rows in flight 10.874-10.895
   c->rs_cb = (int)ab_knob("DOPT_RS_CB", 2);
   c->rs_nbuf = (int)ab_knob("DOPT_RS_NBUF", 8);
   c->rs_ldot = (int)ab_knob("DOPT_RS_LDOT", 1);
   const int64_t nblk = (c->nch + 64 * c->rs_cb - 1) / (64 * c->rs_cb);
-  int64_t wg = ab_knob("DOPT_RS_WG", (c->rows + 8191) / 8192);  // ~8k rows per row group
+  int64_t wg = ab_knob("DOPT_RS_WG", (c->rows + 16383) / 16384);  // ~16k rows per row group
   wg = std::max<int64_t>(1, std::min<int64_t>(wg, (c->rows + 255) / 256));
   int rc;
   c->rs_nblk = (int)nblk;
