@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summary of rocprofv3 SQ counter passes for the round kernels (scripts/r4_c3_sq.sh).
+"""Summary of rocprofv3 SQ counter passes for the round kernels (scripts/r4.sh sq).
 
 Arguments: counter-collection output directories (run_counter_collection.csv), then optionally one
 kernel-trace directory (run_kernel_trace.csv) for each kernel's VGPR / AGPR / LDS / scratch.  Prints,
