@@ -1586,7 +1586,8 @@ __device__ __forceinline__ double ranks_sum(const McsArgs& m, const T* halo, int
   return s;
 }
 
-constexpr int kMixcsMaxGroups = 64;  // mixcs_shape keeps ng <= this
+constexpr int kMixcsBatch = 64;        // group partials loaded per batch (all in flight)
+constexpr int kMixcsMaxGroups = 1024;  // mixcs_shape keeps ng <= this
 
 template <typename T, int CPB, bool TICKET>
 __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __restrict__ G, int n, const McsArgs m,
@@ -1812,16 +1813,19 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
   for (int t = threadIdx.x; t < BC; t += NT) {
     const int64_t col = colbase + t;
     if (col >= ncol) break;
-    // every partial in flight at once (ng <= kMixcsMaxGroups), summed in group order
-    double v[kMixcsMaxGroups];
-#pragma unroll
-    for (int q = 0; q < kMixcsMaxGroups; ++q)
-      v[q] = q < m.ng ? __hip_atomic_load(m.part + (int64_t)q * ld + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                      : 0.0;
+    // the partials in batches of kMixcsBatch in flight, summed in group order
     double s = 0.0;
+    for (int qb = 0; qb < m.ng; qb += kMixcsBatch) {
+      double v[kMixcsBatch];
 #pragma unroll
-    for (int q = 0; q < kMixcsMaxGroups; ++q)
-      if (q < m.ng) s += v[q];
+      for (int q = 0; q < kMixcsBatch; ++q)
+        v[q] = qb + q < m.ng
+                   ? __hip_atomic_load(m.part + (int64_t)(qb + q) * ld + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : 0.0;
+#pragma unroll
+      for (int q = 0; q < kMixcsBatch; ++q)
+        if (qb + q < m.ng) s += v[q];
+    }
     m.own_out[col] = s;
     for (int p = 0; p < m.world; ++p) {
       const int64_t row = p < kMcsKargRanks ? (int64_t)m.kout[p] : m.sum_out[p];
@@ -1831,30 +1835,38 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
   if (threadIdx.x == 0) __hip_atomic_store(m.cnt + cb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The second launch of the two-kernel k_mixcs (the default): workgroup cb sums the ng group partials
-// of its column block in group order (the last arriver's arithmetic), writes them to own_out and to
-// every peer's sum rows.  The kernel boundary is the hand-off: the single-launch form's write-through
-// stores, agent-scope ticket and acquire cost ~9 us of dependent latency per round at 512 workers
-// (timing-only cuts, profiles/r4_mixcs_cut.txt), the boundary a few.
+// The second launch of the two-kernel k_mixcs (the default): the ng group partials of every column,
+// summed per column block -- workgroup (64 columns), wave w summing groups [w ng / 4, (w + 1) ng / 4)
+// in group order with 64 loads in flight, the four waves' sums added in wave order through LDS --
+// to own_out and to every peer's sum rows.  The kernel boundary is the hand-off: the single-launch
+// form's write-through stores, agent-scope ticket and acquire cost ~9 us of dependent latency per
+// round at 512 workers (timing-only cuts, profiles/r4_mixcs_cut.txt), the boundary a few.
 template <typename T>
 __global__ __launch_bounds__(NT) void k_mixcs_final(const McsArgs m, int64_t ld, int nch, T* send) {
   constexpr int VN = VT<T>::n;
-  constexpr int BC = 64 * 2 * VN;  // k_mixcs's column block (CPB = 2)
-  const int64_t colbase = (int64_t)blockIdx.x * BC, ncol = (int64_t)nch * VN;
-  for (int t = threadIdx.x; t < BC; t += NT) {
-    const int64_t col = colbase + t;
-    if (col >= ncol) break;
-    double v[kMixcsMaxGroups];
+  __shared__ double red[NW][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.x * 64 + lane, ncol = (int64_t)nch * VN;
+  const int q0 = (int)((int64_t)m.ng * wave / NW), q1 = (int)((int64_t)m.ng * (wave + 1) / NW);
+  double s = 0.0;
+  if (col < ncol) {
+    for (int qb = q0; qb < q1; qb += kMixcsBatch) {
+      double v[kMixcsBatch];
 #pragma unroll
-    for (int q = 0; q < kMixcsMaxGroups; ++q) v[q] = q < m.ng ? m.part[(int64_t)q * ld + col] : 0.0;
-    double s = 0.0;
+      for (int q = 0; q < kMixcsBatch; ++q) v[q] = qb + q < q1 ? m.part[(int64_t)(qb + q) * ld + col] : 0.0;
 #pragma unroll
-    for (int q = 0; q < kMixcsMaxGroups; ++q)
-      if (q < m.ng) s += v[q];
-    m.own_out[col] = s;
+      for (int q = 0; q < kMixcsBatch; ++q)
+        if (qb + q < q1) s += v[q];
+    }
+  }
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && col < ncol) {
+    const double t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    m.own_out[col] = t;
     for (int p = 0; p < m.world; ++p) {
       const int64_t row = p < kMcsKargRanks ? (int64_t)m.kout[p] : m.sum_out[p];
-      if (row >= 0) ((double*)(send + row * ld))[col] = s;
+      if (row >= 0) ((double*)(send + row * ld))[col] = t;
     }
   }
 }
@@ -1863,8 +1875,13 @@ void mixcs_shape(int dtype, int64_t n, int32_t nch, int32_t* ncb, int32_t* r, in
   constexpr int CPB = 2;
   (void)dtype;
   *ncb = (nch + 64 * CPB - 1) / (64 * CPB);
-  // groups of 8 workers, at most 64 groups (the last arriver reads ng partials of its block)
+  // groups of 8 workers (one iteration of the two-worker loop per wave), up to kMixcsMaxGroups groups:
+  // many short workgroups rather than few long ones -- a wave's workers run one after the other, each
+  // a few dependent memory round trips (A/B builds: DOPT_MIXCS_R forces the group size)
   int64_t rr = 8;
+#ifdef DOPT_AB
+  if (const char* v = getenv("DOPT_MIXCS_R")) rr = std::max(8, atoi(v) / 8 * 8);
+#endif
   while ((n + rr - 1) / rr > kMixcsMaxGroups) rr += 8;
   *r = (int32_t)rr;
   *ng = (int32_t)std::max<int64_t>(1, (n + rr - 1) / rr);
@@ -1907,7 +1924,8 @@ hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_work
       hipLaunchKernelGGL((k_mixcs<double, 2, false>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
   }
   if (ticket || mm.cut != 0) return hipGetLastError();
-  const dim3 g2((unsigned)m.ncb);
+  const int vn = dtype == 0 ? 4 : 2;
+  const dim3 g2((unsigned)(((int64_t)a.nchunks * vn + 63) / 64));
   if (dtype == 0)
     hipLaunchKernelGGL(k_mixcs_final<float>, g2, dim3(NT), 0, s, mm, a.ld, a.nchunks, (float*)a.send);
   else

@@ -93,6 +93,25 @@ for step in "$@"; do
         --output-format csv -d gpurun_out/r4_$tag -o run -- python3 $B > gpurun_out/r4_$tag.log 2>&1 || die mixcs_ab 1
       python3 tools/trace_rounds.py gpurun_out/r4_$tag/run_kernel_trace.csv
     done ;;
+  mixcs_boundary)  # k_mixcs when every worker is mixed in it (DOPT_PHASE_INTERIOR=0: the N = 8 boundary share
+    # is 84 %), 4096 and 512 workers, kernel traces -> profiles/r4_mixcs_boundary.txt
+    for w in 4096 512; do
+      for it in 1 0; do
+        echo "=== $w workers, DOPT_PHASE_INTERIOR=$it"
+        DOPT_PHASE_INTERIOR=$it timeout -s KILL 150 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r4_mb_${w}_$it \
+          -o run -- python3 bench.py --no-cpu-baseline --no-secondary --scaling weak --phase --workers $w --steps 30 \
+          --warmup 3 > gpurun_out/r4_mb_${w}_$it.log 2>&1 || die mixcs_boundary 1
+        python3 tools/trace_rounds.py gpurun_out/r4_mb_${w}_$it/run_kernel_trace.csv
+      done
+    done ;;
+  mixcs_r)  # k_mixcs group size at 4096 workers, every worker mixed in it: R = 8 (default) vs 64 (A/B library)
+    for r in 8 64; do
+      echo "=== DOPT_MIXCS_R=$r, DOPT_PHASE_INTERIOR=0"
+      DOPT_LIB=$AB DOPT_MIXCS_R=$r DOPT_PHASE_INTERIOR=0 timeout -s KILL 150 rocprofv3 --kernel-trace --output-format csv \
+        -d gpurun_out/r4_mr_$r -o run -- python3 bench.py --no-cpu-baseline --no-secondary --scaling weak --phase \
+        --workers 4096 --steps 30 --warmup 3 > gpurun_out/r4_mr_$r.log 2>&1 || die mixcs_r 1
+      python3 tools/trace_rounds.py gpurun_out/r4_mr_$r/run_kernel_trace.csv
+    done ;;
   rehearsal8)  # the SCALE command shape at 8 gloo ranks on this one GPU -> profiles/r4_rehearsal8.json
     echo "=== 8-rank rehearsal"
     timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
