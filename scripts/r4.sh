@@ -137,6 +137,8 @@ for step in "$@"; do
     OUT=gpurun_out/prof_r4 bash scripts/profile.sh || die c3_profile 1 ;;
   c5_profile)  # C5 x32 row-space rounds, same three passes -> profiles/r4_c5x32_*
     OUT=gpurun_out/prof_r4c5 PSTEPS=6 BENCH_ARGS="--config c5" bash scripts/profile.sh || die c5_profile 1 ;;
+  c4_profile)  # C4 (65536 workers, torus, one GPU), same three passes -> profiles/r4_c4_*
+    OUT=gpurun_out/prof_r4c4 PSTEPS=4 BENCH_ARGS="--config c4" bash scripts/profile.sh || die c4_profile 1 ;;
   c5_ldot)  # row dots: every lane through LDS (1) / lane pairs first (2) / DPP (0) -> profiles/r4_c5_ldot2.txt
     rs_ab r4_c5_ldot2 3 "2,8,2,2 2,8,2,1 2,8,2,0" ;;
   c5_shapes)  # rows in flight, row groups, 4 KiB blocks -> profiles/r4_c5_shapes.txt, r4_c5_groups.txt, r4_c5_cb4.txt
