@@ -145,6 +145,11 @@ for step in "$@"; do
     rs_ab r4_c5_shapes 3 "2,8,2,1 2,16,2,1 2,8,4,1 2,8,1,1"
     rs_ab r4_c5_groups 5 "2,8,1,1 2,8,2,1"
     rs_ab r4_c5_cb4 5 "4,4,1,1 2,8,1,1" ;;
+  mainpy)  # the reference's experiment end to end through the drop-in modules (4 trainers x 10^4 rounds)
+    echo "=== main.py"
+    (cd distributed-optimization_amd && MPLBACKEND=Agg timeout -k 10 600 python3 -u -c "import time, runpy; t=time.time(); import matplotlib; matplotlib.use('Agg'); runpy.run_path('main.py', run_name='__main__'); print('main.py wall %.1f s' % (time.time()-t))") \
+      > gpurun_out/r4_mainpy.log 2>&1 || { tail -n 20 gpurun_out/r4_mainpy.log; die mainpy 1; }
+    tail -n 25 gpurun_out/r4_mainpy.log ;;
   diag_trainers)  # the C2 trainers at 1 and 2 gloo ranks vs the fixture, every label (the dense-CSR k_mixcs bug)
     timeout -k 10 300 python3 tools/diag_trainers2.py > gpurun_out/r4_diag.log 2>&1 || die diag_trainers 1
     grep -v "amdgpu.ids\|socket.cpp\|Gloo\|Spectral\|Running\|finished" gpurun_out/r4_diag.log | head -60 ;;
