@@ -90,6 +90,7 @@ _SIGS = {
     "dopt_lagged_grad": ([_P, _I64, _D, _I64, _P, _D, ctypes.c_uint32], ctypes.c_int),
     "dopt_lagged_mix": ([_P, _I64, _D, ctypes.c_int, _P, _P, _P], ctypes.c_int),
     "dopt_lagged_tail": ([_P, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, _P, _P], ctypes.c_int),
+    "dopt_lagged_side_stream": ([_P, _P], ctypes.c_int),
     "dopt_rs_phase_begin": ([_P, ctypes.c_int, _P, _P], ctypes.c_int),
     "dopt_rs_phase_round": ([_P, _I64, _D, _D, ctypes.c_uint32, _P], ctypes.c_int),
     "dopt_rs_phase_cols": ([_P, _I64, _D, _D, _P], ctypes.c_int),
@@ -107,7 +108,7 @@ _SIGS = {
     "dopt_phase_set_step": ([_P, _I64, ctypes.c_double], ctypes.c_int),
 }
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 3  # DOPT_ABI_VERSION of include/dopt.h
+ABI_VERSION = 4  # DOPT_ABI_VERSION of include/dopt.h
 
 
 def lib():
@@ -480,6 +481,11 @@ class Engine:
         rc = lib().dopt_lagged_mix(self._h, t, eta0, 1 if consensus else 0, cons_ptr, xnorm_ptr, loss_ptr)
         if rc:
             check(rc)
+
+    def lagged_side_stream(self, stream_ptr):
+        """dopt_lagged_side_stream: the stream (a hipStream_t as int, or None) that takes each mix's
+        column-sum totals and that the caller issues the exchange on."""
+        check(lib().dopt_lagged_side_stream(self._h, ctypes.c_void_p(stream_ptr or None)))
 
     def lagged_tail(self, consensus, objective, row1, row2):
         """row1 / row2: (cons, xnorm, loss) device addresses of the history rows G-1 / G-2 (None: skip)."""

@@ -1586,7 +1586,8 @@ __device__ __forceinline__ double ranks_sum(const McsArgs& m, const T* halo, int
   return s;
 }
 
-constexpr int kMixcsBatch = 64;        // group partials loaded per batch (all in flight)
+constexpr int kMixcsBatch = 16;        // group partials loaded per batch (all in flight; few VGPRs, so
+                                       // k_mixcs_final fits beside two round-kernel workgroups per CU)
 constexpr int kMixcsMaxGroups = 1024;  // mixcs_shape keeps ng <= this
 
 template <typename T, int CPB, bool TICKET>
@@ -1888,7 +1889,7 @@ void mixcs_shape(int dtype, int64_t n, int32_t nch, int32_t* ncb, int32_t* r, in
 }
 
 hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_workers, const McsArgs& m,
-                        const FoldArgs* fold, hipStream_t s) {
+                        const FoldArgs* fold, hipStream_t s, hipStream_t side, hipEvent_t ev) {
   FoldArgs f;
   memset(&f, 0, sizeof(f));
   if (fold) f = *fold;
@@ -1924,12 +1925,20 @@ hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_work
       hipLaunchKernelGGL((k_mixcs<double, 2, false>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
   }
   if (ticket || mm.cut != 0) return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipStream_t fs = s;
+  if (side && ev) {
+    if ((e = hipEventRecord(ev, s)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(side, ev, 0)) != hipSuccess) return e;
+    fs = side;
+  }
   const int vn = dtype == 0 ? 4 : 2;
   const dim3 g2((unsigned)(((int64_t)a.nchunks * vn + 63) / 64));
   if (dtype == 0)
-    hipLaunchKernelGGL(k_mixcs_final<float>, g2, dim3(NT), 0, s, mm, a.ld, a.nchunks, (float*)a.send);
+    hipLaunchKernelGGL(k_mixcs_final<float>, g2, dim3(NT), 0, fs, mm, a.ld, a.nchunks, (float*)a.send);
   else
-    hipLaunchKernelGGL(k_mixcs_final<double>, g2, dim3(NT), 0, s, mm, a.ld, a.nchunks, (double*)a.send);
+    hipLaunchKernelGGL(k_mixcs_final<double>, g2, dim3(NT), 0, fs, mm, a.ld, a.nchunks, (double*)a.send);
   return hipGetLastError();
 }
 

@@ -196,6 +196,8 @@ struct dopt_ctx {
   // peer at the rows dopt_lagged_exchange_layout names
   int32_t lg_world = 1, lg_rank = 0;
   std::vector<int64_t> lg_in_h, lg_out_h;  // host copies of the sum rows (-1: self)
+  hipStream_t lg_side = nullptr;  // dopt_lagged_side_stream: k_mixcs_final and the exchange go there
+  hipEvent_t lg_side_ev = nullptr;
   int64_t* lg_sum_in = nullptr;            // [world] halo row of peer p's sums
   int64_t* lg_sum_out = nullptr;           // [world] send row of the sums for peer p
   double* lg_own[2] = {nullptr, nullptr};  // [ld] this rank's column sums of x_g (g parity)
@@ -1257,6 +1259,7 @@ int dopt_destroy(dopt_ctx* c) {
   dfree_t(c->lg_sum_in);
   dfree_t(c->lg_sum_out);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+  if (c->lg_side_ev) (void)hipEventDestroy(c->lg_side_ev);
   for (int k = 0; k < 2; ++k) {
     if (c->idx_ev[k]) (void)hipEventDestroy(c->idx_ev[k]);
     if (c->idx_pin[k]) (void)hipHostFree(c->idx_pin[k]);
@@ -2524,7 +2527,20 @@ int dopt_lagged_begin(dopt_ctx* c, int64_t batch) {
                             c->stream, c->lg_own[0]));
   const McsArgs m = lagged_args(c, c->lg_own[0], nullptr, nullptr);
   if (c->lg_world > 1) HIPOK(launch_xbar_ranks(c->dtype, m, c->halo, c->ld, (int32_t)c->nchs, nullptr, c->send, c->stream));
+  if (c->lg_side) {  // the first exchange, issued on the side stream, follows the send rows written here
+    HIPOK(hipEventRecord(c->lg_side_ev, c->stream));
+    HIPOK(hipStreamWaitEvent(c->lg_side, c->lg_side_ev, 0));
+  }
   c->lg = 0;
+  return DOPT_OK;
+}
+
+int dopt_lagged_side_stream(dopt_ctx* c, void* stream) {
+  CHECK_ARG(c, "ctx is NULL");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  if (stream && !c->lg_side_ev) HIPOK(hipEventCreateWithFlags(&c->lg_side_ev, hipEventDisableTiming));
+  c->lg_side = (hipStream_t)stream;
   return DOPT_OK;
 }
 
@@ -2567,7 +2583,7 @@ int dopt_lagged_mix(dopt_ctx* c, int64_t t, double eta0, int consensus, double* 
   f.out_c = cons_out;
   f.out_l = loss_out;
   f.out_q = xnorm_out;
-  HIPOK(launch_mixcs(c->dtype, a, c->G, (int)c->n, m, any ? &f : nullptr, c->stream));
+  HIPOK(launch_mixcs(c->dtype, a, c->G, (int)c->n, m, any ? &f : nullptr, c->stream, c->lg_side, c->lg_side_ev));
   c->xb ^= 1;
   c->cur ^= 1;
   c->lg += 1;

@@ -362,6 +362,10 @@ class HaloExchange:
         self.peers = []
         self.collective = False
 
+    def peers_or_collective(self):
+        """True when start() moves anything (a collective, or host transfers with peers)."""
+        return bool(self.collective or self.peers)
+
     def _ops(self, send, halo):
         """(kind, peer, buffer, rows) for every transfer, sends first per peer, peers ascending."""
         for p in self.peers:
@@ -451,6 +455,14 @@ class DistributedDSGD:
         nch = (ld * esz) // 16
         self._lagged_ok = (mean is None and nch <= 16 * 64 and
                            os.environ.get("DOPT_LAGGED", "1") != "0")
+        # a second stream for each mix's column-sum totals (k_mixcs_final) and the exchange, so the
+        # next gradient kernel does not wait for them -- whenever there is an exchange to order it
+        # (DOPT_LAGGED_SIDE=0: one stream)
+        self.side = None
+        if (self._lagged_ok and not self._solo() and self.exchange.peers_or_collective()
+                and os.environ.get("DOPT_LAGGED_SIDE", "1") != "0"):
+            self.side = torch.cuda.Stream(self.dev)
+        engine.lagged_side_stream(self.side.cuda_stream if self.side is not None else None)
         # the communicator is created by one small collective here, not inside the first round
         # (the halo all-to-all and the all-reduces of the rounds then find it ready)
         if self.device_comm and dist.get_world_size(group) > 1:
@@ -710,9 +722,20 @@ class DistributedDSGD:
             if not cont:
                 eng.lagged_begin(batch)  # send rows and column sums of x_0
             lagged_grad, lagged_mix = eng.lagged_grad, eng.lagged_mix
+            side = self.side
+
+            def start():  # the exchange, on the side stream when there is one (after k_mixcs_final)
+                if side is None:
+                    return exchange.start()
+                with torch.cuda.stream(side):
+                    w = exchange.start()
+                if w is None:  # host transport: the halo rows were written on the side stream
+                    self.stream.wait_stream(side)
+                return w
+
             for g in range(G0, G1):
                 h = g - G0
-                pending = exchange.start()
+                pending = start()
                 # loss at xbar_{g-1} (history[g-2]); at g = 1 it is the loss of x_0, which no history row
                 # holds -- taken anyway so round 1's gradient dots reduce in the same (paired) butterfly
                 # as the fused single-context round 1, whose pass carries the metrics of x_1
@@ -723,7 +746,7 @@ class DistributedDSGD:
                 lagged_mix(t0 + h, eta0, consensus, at(e, 0, consensus), at(e, 2, objective and xnorm),
                            at(e, 1, objective))
             if tail and G1 > 0:
-                exchange.finish(exchange.start())  # every rank's column sums of x_T
+                exchange.finish(start())  # every rank's column sums of x_T
                 eng.lagged_tail(consensus, objective,
                                 (at(G1 - 1, 0, consensus), at(G1 - 1, 2, objective and xnorm), at(G1 - 1, 1, objective)),
                                 (at(G1 - 2, 0, consensus), at(G1 - 2, 2, objective and xnorm), at(G1 - 2, 1, objective)))
@@ -733,6 +756,8 @@ class DistributedDSGD:
                 self._all_reduce(partials[done:upto])
             raw = partials[done:upto].cpu().numpy()
         self.stream.synchronize()
+        if self.side is not None:
+            self.side.synchronize()  # no side-stream work outlives the call
         ch["g"], ch["done"] = G1, upto
         if tail:
             self._chain = None

@@ -42,8 +42,9 @@ extern "C" {
  *      (dopt_lagged_exchange_layout / _begin / _grad / _mix / _tail) replaces dopt_phase_colsum_fold,
  *      dopt_phase_mix_lagged, dopt_phase_cons and dopt_phase_loss_pass; dopt_set_halo takes send_ids
  *      of -1 (rows that carry no worker); the multi-GPU runner internals form the header's last
- *      section. */
-#define DOPT_ABI_VERSION 3
+ *      section.
+ *   4  round 4: dopt_lagged_side_stream (k_mixcs_final and the exchange on a second stream). */
+#define DOPT_ABI_VERSION 4
 
 typedef struct dopt_ctx dopt_ctx;
 
@@ -368,7 +369,12 @@ int dopt_rs_phase_metrics(dopt_ctx *ctx, uint32_t metric_flags);
  *   x_{g+1} into the send buffer's sum rows, and into the non-NULL outputs the history row g-2
  *   (consensus partials of x_{g-1}, the losses of the preceding dopt_lagged_grad, ||xbar_{g-1}||^2).
  * dopt_lagged_tail: after one more exchange: xbar_G, and the history rows G-1 (cons1 / xnorm1 /
- *   loss1) and G-2 (cons2 / xnorm2 / loss2) of a chain of G rounds. */
+ *   loss1) and G-2 (cons2 / xnorm2 / loss2) of a chain of G rounds.
+ * dopt_lagged_side_stream: a second stream (NULL: none) for the column-sum totals of each mix
+ *   (k_mixcs_final, after an event wait on the engine stream) and for the caller's exchange, so the
+ *   next gradient kernel does not wait for them; dopt_lagged_begin makes it wait for x_0's send rows.
+ *   The caller issues the exchange on it and makes the engine stream wait for the exchange (RCCL:
+ *   work.wait() on the engine stream; host transports: a stream wait on the side stream). */
 int dopt_lagged_exchange_layout(dopt_ctx *ctx, int32_t world, int32_t rank, const int64_t *sum_send_row,
                                 const int64_t *sum_recv_row);
 int dopt_lagged_begin(dopt_ctx *ctx, int64_t batch);
@@ -378,6 +384,7 @@ int dopt_lagged_mix(dopt_ctx *ctx, int64_t t, double eta0, int consensus, double
                     double *loss_out);
 int dopt_lagged_tail(dopt_ctx *ctx, int consensus, int objective, double *cons1, double *xnorm1, double *loss1,
                      double *cons2, double *xnorm2, double *loss2);
+int dopt_lagged_side_stream(dopt_ctx *ctx, void *stream);
 /* Centralized trainer across ranks (trainer.py:41-71): gradients of the local
  * workers at the shared iterate (fuse_loss: the objective partial of the shared
  * iterate over the same rows, full shards only), local column sums of the
