@@ -1586,6 +1586,11 @@ __device__ __forceinline__ double ranks_sum(const McsArgs& m, const T* halo, int
   return s;
 }
 
+#ifdef DOPT_AB
+constexpr bool kMixcsAB = true;  // A/B builds: DOPT_MIXCS_CUT (timing-only early exits) and DOPT_MIXCS_TICKET
+#else
+constexpr bool kMixcsAB = false;
+#endif
 constexpr int kMixcsBatch = 16;        // group partials loaded per batch (all in flight; few VGPRs, so
                                        // k_mixcs_final fits beside two round-kernel workgroups per CU)
 constexpr int kMixcsMaxGroups = 1024;  // mixcs_shape keeps ng <= this
@@ -1604,7 +1609,7 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
   __shared__ double xsum[XR][BC];
   __shared__ int last;
   if (blockIdx.x == 0) {
-    if (m.cut != 3) fold_block_rw<BC>(fold, a.nchunks, VN, red);
+    if (!kMixcsAB || m.cut != 3) fold_block_rw<BC>(fold, a.nchunks, VN, red);
     return;
   }
   const int lane = threadIdx.x & 63;
@@ -1728,7 +1733,7 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
     for (int e = 0; e < VN; ++e) xb[j][e] = c < nch ? (T)(xs[j][e] / m.n_div) : T(0);
     if (c < nch && g == 0 && wave == 0 && a.xbar_out) *(V*)((T*)a.xbar_out + (int64_t)c * VN) = xb[j];
   }
-  if (m.cut == 2) return;
+  if (kMixcsAB && m.cut == 2) return;
 
   double cs[CPB][VN];
 #pragma unroll
@@ -1783,7 +1788,7 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
       }
     }
   }
-  if (m.cut == 1) return;
+  if (kMixcsAB && m.cut == 1) return;
   // this group's partial of the column block: waves in order (TICKET: write-through stores)
 #pragma unroll
   for (int j = 0; j < CPB; ++j)
@@ -1798,7 +1803,7 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
     else
       m.part[(int64_t)g * ld + colbase + t] = s;
   }
-  if (!TICKET || m.cut == 4) return;  // (two launches: k_mixcs_final sums the partials)
+  if (!TICKET || (kMixcsAB && m.cut == 4)) return;  // (two launches: k_mixcs_final sums the partials)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1894,37 +1899,31 @@ hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_work
   memset(&f, 0, sizeof(f));
   if (fold) f = *fold;
   McsArgs mm = m;
+  mm.cut = 0;
+  const dim3 grid(1 + (unsigned)m.ng * (unsigned)m.ncb);
 #ifdef DOPT_AB
   static const int cut = [] {
     const char* v = getenv("DOPT_MIXCS_CUT");
     return v ? atoi(v) : 0;
   }();
-  mm.cut = cut;
-#else
-  mm.cut = 0;
-#endif
-  // one launch with the agent-scope last-arriver hand-off (A/B builds: DOPT_MIXCS_TICKET=1), or two
-  static const bool ticket = [] {
-#ifdef DOPT_AB
+  static const bool ticket = [] {  // one launch with the agent-scope last-arriver hand-off
     const char* v = getenv("DOPT_MIXCS_TICKET");
     return v && atoi(v) != 0;
-#else
-    return false;
-#endif
   }();
-  const dim3 grid(1 + (unsigned)m.ng * (unsigned)m.ncb);
-  if (dtype == 0) {
-    if (ticket)
+  mm.cut = cut;
+  if (ticket) {
+    if (dtype == 0)
       hipLaunchKernelGGL((k_mixcs<float, 2, true>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
     else
-      hipLaunchKernelGGL((k_mixcs<float, 2, false>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
-  } else {
-    if (ticket)
       hipLaunchKernelGGL((k_mixcs<double, 2, true>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
-    else
-      hipLaunchKernelGGL((k_mixcs<double, 2, false>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
+    return hipGetLastError();
   }
-  if (ticket || mm.cut != 0) return hipGetLastError();
+#endif
+  if (dtype == 0)
+    hipLaunchKernelGGL((k_mixcs<float, 2, false>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
+  else
+    hipLaunchKernelGGL((k_mixcs<double, 2, false>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
+  if (mm.cut != 0) return hipGetLastError();  // (timing-only cuts: no totals)
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipStream_t fs = s;
