@@ -39,7 +39,9 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
     import distributed as Dm
     import topology as TP
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DOPT_LAGGED=lagged,
+    side = "0" if lagged.endswith("-noside") else "1"  # "1-noside": the lagged schedule on one stream
+    lagged = lagged.split("-")[0]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DOPT_LAGGED=lagged, DOPT_LAGGED_SIDE=side,
                       DOPT_FORCE_COLLECTIVES="1" if backend == "nccl" else "0")
     if backend == "nccl":
         torch.cuda.set_device(0)
@@ -86,6 +88,7 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
                                                       ("float64/x32", False, T, "0", 2),
                                                       ("float64/x32", True, T, "1", 2),
                                                       ("float64/x32", "csr", T, "1", 2),
+                                                      ("float64/x32", False, T, "1-noside", 2),
                                                       ("float32", "csr", T, "0", 2)])
 def test_ranks_match_single_context(tmp_path, dtype, mean, T, lagged, world):
     import torch.multiprocessing as mp
