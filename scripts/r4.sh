@@ -134,7 +134,7 @@ for step in "$@"; do
     python3 tools/sq_summary.py gpurun_out/r4_sq1 gpurun_out/r4_sq2 gpurun_out/r4_sq3 gpurun_out/r4_kt \
       > gpurun_out/r4_c3_sq.txt && cat gpurun_out/r4_c3_sq.txt ;;
   c3_profile)  # C3 kernel stats + FETCH_SIZE / WRITE_SIZE passes -> profiles/r4_kernel_stats.csv, r4_pmc.json
-    OUT=gpurun_out/prof_r4 bash scripts/profile.sh || die c3_profile 1 ;;
+    OUT=gpurun_out/prof_r4 PSTEPS=20 bash scripts/profile.sh || die c3_profile 1 ;;
   c5_profile)  # C5 x32 row-space rounds, same three passes -> profiles/r4_c5x32_*
     OUT=gpurun_out/prof_r4c5 PSTEPS=6 BENCH_ARGS="--config c5" bash scripts/profile.sh || die c5_profile 1 ;;
   c4_profile)  # C4 (65536 workers, torus, one GPU), same three passes -> profiles/r4_c4_*
