@@ -69,6 +69,13 @@ for step in "$@"; do
       bench_step r4sp_phase1_$w 200 --no-cpu-baseline --no-secondary --scaling weak --phase --workers $w --steps 100 \
         --warmup 5
     done ;;
+  strong_mid)  # the strong leg's rank shapes at N = 2 and 4 (2048 / 1024 workers): fused, phase (forced) -> profiles/r4_strong_mid.txt
+    for w in 2048 1024; do
+      bench_step r4sp_fused_$w 200 --no-cpu-baseline --no-secondary --scaling weak --workers $w --steps 100 --warmup 5
+      DOPT_FORCE_COLLECTIVES=1 bench_step r4sp_phase_$w 200 --no-cpu-baseline --no-secondary --scaling weak --phase \
+        --workers $w --steps 100 --warmup 5
+    done
+    bench_step r4sp_fused_4096 200 --no-cpu-baseline --no-secondary --scaling weak --workers 4096 --steps 100 --warmup 5 ;;
   host_probe)  # host time per round at 512 workers, collectives forced / skipped -> profiles/r4_host_probe*.json
     for f in 1 0; do
       echo "=== host probe, DOPT_FORCE_COLLECTIVES=$f"
