@@ -1877,8 +1877,24 @@ __global__ __launch_bounds__(NT) void k_mixcs_final(const McsArgs m, int64_t ld,
   }
 }
 
+// 16-byte chunks per lane of a k_mixcs column block (A/B builds: DOPT_MIXCS_CPB = 2).  One chunk:
+// twice the column blocks, 105 VGPRs (four waves per SIMD instead of two at 192), and, with every
+// worker mixed there, 40.0 vs 48.5 us at 4096 workers and 11.0 vs 13.6 at 512
+// (profiles/r4_mixcs_cpb.txt)
+static int mixcs_cpb() {
+#ifdef DOPT_AB
+  static const int v = [] {
+    const char* e = getenv("DOPT_MIXCS_CPB");
+    return (e && atoi(e) == 2) ? 2 : 1;
+  }();
+  return v;
+#else
+  return 1;
+#endif
+}
+
 void mixcs_shape(int dtype, int64_t n, int32_t nch, int32_t* ncb, int32_t* r, int32_t* ng) {
-  constexpr int CPB = 2;
+  const int CPB = mixcs_cpb();
   (void)dtype;
   *ncb = (nch + 64 * CPB - 1) / (64 * CPB);
   // groups of 8 workers (one iteration of the two-worker loop per wave), up to kMixcsMaxGroups groups:
@@ -1911,18 +1927,33 @@ hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_work
     return v && atoi(v) != 0;
   }();
   mm.cut = cut;
-  if (ticket) {
-    if (dtype == 0)
-      hipLaunchKernelGGL((k_mixcs<float, 2, true>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
-    else
-      hipLaunchKernelGGL((k_mixcs<double, 2, true>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
+  if (ticket) {  // (column blocks of mixcs_cpb() chunks, as the shape was planned)
+    if (mixcs_cpb() == 2) {
+      if (dtype == 0)
+        hipLaunchKernelGGL((k_mixcs<float, 2, true>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
+      else
+        hipLaunchKernelGGL((k_mixcs<double, 2, true>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
+    } else {
+      if (dtype == 0)
+        hipLaunchKernelGGL((k_mixcs<float, 1, true>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
+      else
+        hipLaunchKernelGGL((k_mixcs<double, 1, true>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
+    }
     return hipGetLastError();
   }
 #endif
+#ifdef DOPT_AB
+  if (mixcs_cpb() == 2) {
+    if (dtype == 0)
+      hipLaunchKernelGGL((k_mixcs<float, 2, false>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
+    else
+      hipLaunchKernelGGL((k_mixcs<double, 2, false>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
+  } else
+#endif
   if (dtype == 0)
-    hipLaunchKernelGGL((k_mixcs<float, 2, false>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
+    hipLaunchKernelGGL((k_mixcs<float, 1, false>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
   else
-    hipLaunchKernelGGL((k_mixcs<double, 2, false>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
+    hipLaunchKernelGGL((k_mixcs<double, 1, false>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
   if (mm.cut != 0) return hipGetLastError();  // (timing-only cuts: no totals)
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

@@ -119,6 +119,16 @@ for step in "$@"; do
         --workers 4096 --steps 30 --warmup 3 > gpurun_out/r4_mr_$r.log 2>&1 || die mixcs_r 1
       python3 tools/trace_rounds.py gpurun_out/r4_mr_$r/run_kernel_trace.csv
     done ;;
+  mixcs_cpb)  # k_mixcs column blocks of 1 vs 2 chunks per lane (A/B library), every worker mixed in it, 4096 / 512
+    for w in 4096 512; do
+      for c in 1 2; do
+        echo "=== DOPT_MIXCS_CPB=$c, $w workers, DOPT_PHASE_INTERIOR=0"
+        DOPT_LIB=$AB DOPT_MIXCS_CPB=$c DOPT_PHASE_INTERIOR=0 timeout -s KILL 150 rocprofv3 --kernel-trace --output-format csv \
+          -d gpurun_out/r4_mc_${w}_$c -o run -- python3 bench.py --no-cpu-baseline --no-secondary --scaling weak --phase \
+          --workers $w --steps 30 --warmup 3 > gpurun_out/r4_mc_${w}_$c.log 2>&1 || die mixcs_cpb 1
+        python3 tools/trace_rounds.py gpurun_out/r4_mc_${w}_$c/run_kernel_trace.csv
+      done
+    done ;;
   rehearsal8)  # the SCALE command shape at 8 gloo ranks on this one GPU -> profiles/r4_rehearsal8.json
     echo "=== 8-rank rehearsal"
     timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
