@@ -106,9 +106,11 @@ _SIGS = {
     "dopt_set_sampler": ([_P, ctypes.c_int, ctypes.c_uint64, _I64], ctypes.c_int),
     "dopt_phase_set_round": ([_P, _I64], ctypes.c_int),
     "dopt_phase_set_step": ([_P, _I64, ctypes.c_double], ctypes.c_int),
+    "dopt_phase_interior_count": ([_P, _P], ctypes.c_int),
+    "dopt_host_digest": ([_I32, _P, _P, _I32, _P], ctypes.c_int),
 }
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 4  # DOPT_ABI_VERSION of include/dopt.h
+ABI_VERSION = 5  # DOPT_ABI_VERSION of include/dopt.h
 
 
 def lib():
@@ -156,6 +158,18 @@ def check(rc):
 
 def _ptr(a):
     return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def host_digest(buffers, threads=0):
+    """128-bit content digest (32 hex digits) of C-contiguous host arrays, in order, hashed in 4 MiB
+    chunks on several threads (dopt_host_digest; host code, no GPU needed)."""
+    bufs = [np.ascontiguousarray(b) for b in buffers]
+    n = len(bufs)
+    ptrs = (ctypes.c_void_p * max(1, n))(*[b.ctypes.data if b.nbytes else None for b in bufs])
+    sizes = np.array([b.nbytes for b in bufs] or [0], dtype=np.int64)
+    out = np.zeros(2, dtype=np.uint64)
+    check(lib().dopt_host_digest(n, ptrs, _ptr(sizes), int(threads), _ptr(out)))
+    return f"{int(out[0]):016x}{int(out[1]):016x}"
 
 
 def device_count():
@@ -398,6 +412,12 @@ class Engine:
         ids = np.ascontiguousarray(send_ids, dtype=np.int32)
         check(lib().dopt_set_halo(self._h, int(n_halo), ctypes.c_void_p(halo_ptr) if halo_ptr else None, len(ids),
                                   ctypes.c_void_p(send_ptr) if send_ptr else None, _ptr(ids)))
+
+    def phase_interior_count(self):
+        """Workers this rank's gradient kernel mixes and steps itself (dopt_phase_interior_count)."""
+        n = ctypes.c_int64(0)
+        check(lib().dopt_phase_interior_count(self._h, ctypes.byref(n)))
+        return n.value
 
     def phase_chain(self, mark):
         """dopt_phase_chain: whether the last pipelined phase run left its schedule open (and

@@ -105,19 +105,23 @@ struct FoldArgs {
 // (group g of R workers, column block cb of 64 * CPB state chunks) mixes and steps its workers'
 // slices (interior workers: stepped by the gradient kernel, read back), takes their consensus
 // partials at xbar = (rank-ordered sum of every rank's column sums of x_old) / n, and writes the
-// column-block partial of the column sums of x_new to part[g]; the last workgroup of a column
-// block to arrive (agent-scope ticket) sums the NG partials in group order into own_out and into
-// the send buffer's sum rows of every peer.  Block 0 folds a history row (FoldArgs).
+// column-block partial of the column sums of x_new to part[g].  A second launch, k_mixcs_final (on
+// the side stream when the caller gave one), sums the NG partials in group order into own_out and
+// into the send buffer's sum rows of every peer (the shipped default; A/B builds keep a one-launch
+// form in which the last workgroup of a column block to arrive sums them, DOPT_MIXCS_TICKET).
+// Block 0 folds a history row (FoldArgs).
 constexpr int kMcsKargRanks = 16;  // sum rows of the first ranks passed as kernel arguments
 struct McsArgs {
   double* part;            // [ng x ld] group partials of the column sums of x_new
   unsigned* cnt;           // [ncb] arrival tickets (zero between launches: the last arriver resets)
   int32_t ng, ncb, r;      // worker groups, column blocks, workers per group
-  int32_t world, rank;     // the rank-ordered global sums: p == rank -> own_in, else peer p's rows
+  int32_t world, rank;     // the rank-ordered global sums: rank p's halo rows, or own_in (row -1)
   const double* own_in;    // [ld] this rank's column sums of x_old
   double* own_out;         // [ld] this rank's column sums of x_new
-  const int64_t* sum_in;   // [world] halo-buffer row of peer p's column sums of x_old (-1: self)
-  const int64_t* sum_out;  // [world] send-buffer row of the sums of x_new for peer p (-1: self)
+  // [world] halo-buffer row of rank p's column sums of x_old; -1 for this rank (own_in) unless its
+  // sums travel through the exchange to itself (a self block: RCCL world 1, collectives forced)
+  const int64_t* sum_in;
+  const int64_t* sum_out;  // [world] send-buffer row of the sums of x_new for rank p (-1: none)
   double* cons_part;       // [ncb x n] consensus partial of (column block, worker), or null
   double n_div;            // the mean's divisor (workers on all ranks)
   int32_t kin[kMcsKargRanks], kout[kMcsKargRanks];  // sum_in / sum_out of ranks < kMcsKargRanks

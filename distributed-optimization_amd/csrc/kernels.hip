@@ -1577,7 +1577,10 @@ __device__ __forceinline__ double ranks_sum(const McsArgs& m, const T* halo, int
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int p = p0 + k;
-      v[k] = p >= m.world ? 0.0 : p == m.rank ? m.own_in[col] : ((const double*)(halo + m.sum_in[p] * ld))[col];
+      // p's sums: the halo row they arrived in, or -- this rank, unless its own sums travel through the
+      // exchange too (a self block: RCCL world 1 with the collectives forced) -- own_in
+      const int64_t row = p >= m.world ? -1 : p < kMcsKargRanks ? (int64_t)m.kin[p] : m.sum_in[p];
+      v[k] = p >= m.world ? 0.0 : row < 0 ? m.own_in[col] : ((const double*)(halo + row * ld))[col];
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k)
@@ -1690,7 +1693,7 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
       const double* src = nullptr;
       if (p < m.world) {
         const int64_t row = p < kMcsKargRanks ? (int64_t)m.kin[p] : m.sum_in[p];
-        src = p == m.rank ? m.own_in : (const double*)(halo + row * ld);
+        src = row < 0 ? m.own_in : (const double*)(halo + row * ld);  // (row < 0: this rank, no self block)
       }
 #pragma unroll
       for (int t = 0; t < XT; ++t) {

@@ -195,6 +195,7 @@ struct dopt_ctx {
   // sums of x_g travel beside the halo rows; the send / halo buffers hold one block of sum rows per
   // peer at the rows dopt_lagged_exchange_layout names
   int32_t lg_world = 1, lg_rank = 0;
+  bool lg_self = false;  // a self block in the exchange layout (RCCL world 1, collectives forced)
   std::vector<int64_t> lg_in_h, lg_out_h;  // host copies of the sum rows (-1: self)
   hipStream_t lg_side = nullptr;  // dopt_lagged_side_stream: k_mixcs_final and the exchange go there
   hipEvent_t lg_side_ev = nullptr;
@@ -442,6 +443,7 @@ int set_layout(dopt_ctx* c, int problem, int64_t n, int64_t d) {
   c->send_fresh = false;
   c->lg_world = 1;
   c->lg_rank = 0;
+  c->lg_self = false;
   c->lg_in_h.clear();
   c->lg_out_h.clear();
   return DOPT_OK;
@@ -2026,6 +2028,12 @@ int dopt_phase_gather(dopt_ctx* c) {
   return DOPT_OK;
 }
 
+int dopt_phase_interior_count(dopt_ctx* c, int64_t* n_interior) {
+  CHECK_ARG(c && n_interior, "NULL argument");
+  *n_interior = c->have_topo && !c->mean_mix && c->interior ? c->n_interior : 0;
+  return DOPT_OK;
+}
+
 int dopt_phase_chain(dopt_ctx* c, int mark, int* was_pending) {
   CHECK_ARG(c && was_pending, "NULL argument");
   *was_pending = c->carry_pending ? 1 : 0;
@@ -2408,11 +2416,12 @@ int dopt_lagged_exchange_layout(dopt_ctx* c, int32_t world, int32_t rank, const 
                                 const int64_t* sum_recv_row) {
   CHECK_ARG(c && sum_send_row && sum_recv_row, "NULL argument");
   CHECK_ARG(world >= 1 && rank >= 0 && rank < world, "bad world / rank");
+  CHECK_ARG(world <= 1024, "at most 1024 ranks");
   if (!c->have_data) return fail(DOPT_ERR_STATE, "no shards loaded");
   const int64_t rows = (int64_t)(c->esz == 4 ? 2 : 1);  // rows of T holding ld doubles
   for (int32_t p = 0; p < world; ++p) {
-    if (p == rank) {
-      CHECK_ARG(sum_send_row[p] < 0 && sum_recv_row[p] < 0, "rank %d: no sum rows to itself", rank);
+    if (p == rank && sum_send_row[p] < 0) {  // (a self block -- both rows >= 0 -- is checked below)
+      CHECK_ARG(sum_recv_row[p] < 0, "rank %d: sum rows to itself received but not sent", rank);
       continue;
     }
     CHECK_ARG(sum_send_row[p] >= 0 && sum_recv_row[p] >= 0, "peer %d: sum rows missing", p);
@@ -2430,6 +2439,7 @@ int dopt_lagged_exchange_layout(dopt_ctx* c, int32_t world, int32_t rank, const 
   c->lg_out_h.assign(sum_send_row, sum_send_row + world);
   c->lg_world = world;
   c->lg_rank = rank;
+  c->lg_self = sum_send_row[rank] >= 0;  // this rank's sums go through the exchange to itself too
   return DOPT_OK;
 }
 
@@ -2526,7 +2536,7 @@ int dopt_lagged_begin(dopt_ctx* c, int64_t batch) {
   HIPOK(launch_colsum_final(c->dtype, c->part, c->groups, c->n, c->ld, (int32_t)c->nchs, nullptr, nullptr, 0.0, 0,
                             c->stream, c->lg_own[0]));
   const McsArgs m = lagged_args(c, c->lg_own[0], nullptr, nullptr);
-  if (c->lg_world > 1) HIPOK(launch_xbar_ranks(c->dtype, m, c->halo, c->ld, (int32_t)c->nchs, nullptr, c->send, c->stream));
+  if (c->lg_world > 1 || c->lg_self) HIPOK(launch_xbar_ranks(c->dtype, m, c->halo, c->ld, (int32_t)c->nchs, nullptr, c->send, c->stream));
   if (c->lg_side) {  // the first exchange, issued on the side stream, follows the send rows written here
     HIPOK(hipEventRecord(c->lg_side_ev, c->stream));
     HIPOK(hipStreamWaitEvent(c->lg_side, c->lg_side_ev, 0));

@@ -287,23 +287,30 @@ class ExchangeLayout:
         return col.astype(np.int32)
 
 
-def exchange_layout(plan, ks):
-    """ExchangeLayout of a HaloPlan with ks sum rows per peer (ks = 0: the plan's rows only)."""
+def exchange_layout(plan, ks, self_block=False):
+    """ExchangeLayout of a HaloPlan with ks sum rows per peer (ks = 0: the plan's rows only).
+    self_block: this rank gets a block too -- its own plan rows (if any) and sum rows, sent to itself
+    -- so the one-GPU rehearsal of the RCCL path (world 1, collectives forced) moves real rows
+    through the all-to-all and the mix reads them back from the halo buffer."""
     W, r = plan.world, plan.rank
 
-    def shift(p):  # sum rows of the peer blocks before peer p's rows
+    def shift(p):  # sum rows of the blocks before rank p's rows
         p = np.asarray(p)
-        return ks * (p - (p > r))
+        return ks * (p if self_block else p - (p > r))
 
-    send_sizes = [0 if p == r else int(plan.send_off[p + 1] - plan.send_off[p]) + ks for p in range(W)]
-    recv_sizes = [0 if p == r else int(plan.recv_off[p + 1] - plan.recv_off[p]) + ks for p in range(W)]
+    def block(off, p):
+        return int(off[p + 1] - off[p]) + ks if (p != r or self_block) else 0
+
+    send_sizes = [block(plan.send_off, p) for p in range(W)]
+    recv_sizes = [block(plan.recv_off, p) for p in range(W)]
     k = np.arange(len(plan.send_ids))
     send_rows = k + shift(np.searchsorted(plan.send_off, k, side="right") - 1)
     j = np.arange(plan.n_halo)
     halo_rows = j + shift(np.searchsorted(plan.recv_off, j, side="right") - 1)
     ps = np.arange(W)
-    sum_send = np.where(ps == r, -1, plan.send_off[1:] + shift(ps)).astype(np.int64)
-    sum_recv = np.where(ps == r, -1, plan.recv_off[1:] + shift(ps)).astype(np.int64)
+    mine = (ps == r) & (not self_block)
+    sum_send = np.where(mine, -1, plan.send_off[1:] + shift(ps)).astype(np.int64)
+    sum_recv = np.where(mine, -1, plan.recv_off[1:] + shift(ps)).astype(np.int64)
     if ks == 0:
         sum_send[:] = -1
         sum_recv[:] = -1
@@ -429,9 +436,17 @@ class DistributedDSGD:
         ld, esz = engine.layout()
         self.ld = ld
         tdt = torch.float32 if esz == 4 else torch.float64
-        # CSR mixing: the exchange also carries every rank's column sums (the lagged schedule's
-        # xbar, no all-reduce per round); ks rows of T per peer hold ld float64 sums
-        self.layout = exchange_layout(plan, (8 // esz) if (mean is None and plan.world > 1) else 0)
+        # the lagged schedule: CSR mixing on row-resident contexts (DOPT_LAGGED=0: the serial one)
+        nch = (ld * esz) // 16
+        self._lagged_ok = (mean is None and nch <= 16 * 64 and
+                           os.environ.get("DOPT_LAGGED", "1") != "0")
+        # RCCL at world 1 with the collectives forced (the one-GPU rehearsal): this rank's own sums go
+        # through the all-to-all to itself (a self block), so the side-stream chain carries real data
+        forced = plan.world == 1 and self.device_comm and os.environ.get("DOPT_FORCE_COLLECTIVES") == "1"
+        # the lagged schedule's exchange also carries every rank's column sums (its xbar, no all-reduce
+        # per round); ks rows of T per block hold ld float64 sums.  Other schedules: the plan's rows only
+        ks = (8 // esz) if (self._lagged_ok and (plan.world > 1 or forced)) else 0
+        self.layout = exchange_layout(plan, ks, self_block=forced and ks > 0)
         lay = self.layout
         self.halo = torch.zeros((max(1, lay.n_recv_rows), ld), dtype=tdt, device=self.dev)
         self.send = torch.zeros((max(1, lay.n_send_rows), ld), dtype=tdt, device=self.dev)
@@ -442,7 +457,8 @@ class DistributedDSGD:
         if mean is None:
             engine.set_halo(lay.n_recv_rows, self.halo.data_ptr(), lay.send_ids(plan), self.send.data_ptr())
             engine.set_topology(plan.row_ptr, lay.local_col(plan), plan.w)
-            engine.lagged_exchange_layout(plan.world, plan.rank, lay.sum_send_row, lay.sum_recv_row)
+            if lay.ks > 0:
+                engine.lagged_exchange_layout(plan.world, plan.rank, lay.sum_send_row, lay.sum_recv_row)
             self._peers = self.exchange.peers
         else:
             engine.set_halo(0, None, np.zeros(0, np.int32), None)
@@ -451,10 +467,6 @@ class DistributedDSGD:
             self.exchange.disable()
         self.mean = mean
         engine.set_stream(self.stream.cuda_stream)
-        # the lagged schedule: CSR mixing on row-resident contexts (DOPT_LAGGED=0: the serial one)
-        nch = (ld * esz) // 16
-        self._lagged_ok = (mean is None and nch <= 16 * 64 and
-                           os.environ.get("DOPT_LAGGED", "1") != "0")
         # a second stream for each mix's column-sum totals (k_mixcs_final) and the exchange, so the
         # next gradient kernel does not wait for them -- whenever there is an exchange to order it
         # (DOPT_LAGGED_SIDE=0: one stream)
@@ -654,7 +666,7 @@ class DistributedDSGD:
         x_T and a pass for the last losses); T = 0 runs that tail and closes the chain.  Each
         call returns the GLOBAL (objective, consensus) entries that became complete during it
         -- T of them in the steady state (history[t] is complete once the loss at xbar_t has
-        been folded, three rounds later).  Rounds use learning-rate index t0 + h per call.
+        been folded, two rounds later: round t + 2's mix).  Rounds use learning-rate index t0 + h per call.
         Any other run or dopt_set_models ends a chain (dopt_phase_chain)."""
         rows = self.eng.shard_rows
         bip = (idx is not None and not self.obj_sep and rows is not None and len(rows) > 0 and

@@ -133,8 +133,8 @@ def _hash_algo():
         return "blake2b"
 
 
-_FP_CACHE = {}            # identity of a list of arrays -> (sampled digest, full digest)
-_FP_FULL_BELOW = 64 << 20  # arrays totalling fewer bytes are hashed in full on every call
+_FP_CACHE = {}            # identity of a list of arrays -> (sampled digest, full digest): opt-in only
+_FP_FULL_BELOW = 64 << 20  # with the sampled key, arrays totalling fewer bytes are still hashed in full
 _FP_SAMPLES = 64          # 256-byte pieces per array in the sampled digest
 
 
@@ -157,32 +157,50 @@ def _sampled_digest(arrays):
     return h.hexdigest()
 
 
-def _fingerprint(arrays):
+def _content_digest(arrays):
+    """Every byte of the arrays (dtype and shape too), hashed natively on several threads
+    (dopt_host_digest: C3's 8.6 GB of host shards without one Python thread's ~6 GB/s limit)."""
+    import hashlib
+
+    meta = hashlib.blake2b(repr([(a.dtype.str, a.shape) for a in arrays]).encode(), digest_size=8).hexdigest()
+    return meta + _dopt.host_digest(arrays)
+
+
+def _fingerprint(arrays, sampled=False):
     """Content key of arrays, for the engine cache (it compares data by content, not by id(): ids of
-    freed arrays are reused by CPython, and shards edited in place keep their ids).  Data of 64 MiB
-    or more is hashed in full the first time a list of arrays is seen; later calls with the same
-    arrays (object ids, buffer addresses, shapes, dtypes, strides) re-hash only a sample of each
-    array and reuse the full digest while the sample is unchanged (the drop-in
-    trainer's per-run hash of C3's 8.6 GB of host shards took ~0.5 s).  An in-place edit of such
-    large arrays that touches none of the sampled bytes is not seen: pass fresh arrays, or call
-    trainer.forget_data() after editing them in place."""
+    freed arrays are reused by CPython, and shards edited in place keep their ids, trainer.py's
+    reference semantics being that every run uses the arrays as they are now).  By default every
+    byte is hashed on every call.  sampled=True (trainer config content_key='sampled', an opt-in):
+    data of 64 MiB or more is hashed in full the first time a list of arrays is seen, and later calls
+    with the same arrays (object ids, buffer addresses, shapes, dtypes, strides) re-hash only 64
+    pieces of each array, reusing the full digest while those are unchanged -- an in-place edit
+    that touches none of the sampled bytes is then NOT seen (call trainer.forget_data() after one)."""
     arrays = [np.asarray(a) for a in arrays]
-    if sum(a.nbytes for a in arrays) < _FP_FULL_BELOW:
-        return _full_digest(arrays, _hash_algo())
+    if not sampled or sum(a.nbytes for a in arrays) < _FP_FULL_BELOW:
+        return _content_digest(arrays)
     ident = tuple((id(a), a.__array_interface__["data"][0], a.shape, a.dtype.str, a.strides) for a in arrays)
     samp = _sampled_digest(arrays)
     hit = _FP_CACHE.get(ident)
     if hit is not None and hit[0] == samp:
         return hit[1]
-    full = _full_digest(arrays, _hash_algo())
+    full = _content_digest(arrays)
     if len(_FP_CACHE) >= 16:
         _FP_CACHE.pop(next(iter(_FP_CACHE)))
     _FP_CACHE[ident] = (samp, full)
     return full
 
 
+def _sampled_key(config):
+    """Trainer config content_key: 'full' (default, every byte hashed per run) or 'sampled'."""
+    v = (config or {}).get("content_key", "full")
+    if v not in ("full", "sampled"):
+        raise ValueError(f"content_key must be 'full' or 'sampled', not {v!r}")
+    return v == "sampled"
+
+
 def forget_data():
-    """Drop the cached content digests (after editing large shard arrays in place)."""
+    """Drop the cached content digests of the opt-in sampled key (after editing large shard arrays
+    in place)."""
     _FP_CACHE.clear()
 
 
@@ -241,12 +259,13 @@ def _engine(workers, n_features, config, lo=0, hi=None, X_full=None, y_full=None
     """One resident engine per (device, dtype), holding one data set: reused by the four
     trainers Simulator.run_all builds over the same worker data.  [lo, hi) is the slice of
     workers this process holds (multi-process mode).  Reuse is decided by CONTENT (a hash
-    of the slice's shards), so freed-and-reallocated or edited-in-place arrays reload."""
+    of every byte of the slice's shards), so freed-and-reallocated or edited-in-place arrays reload
+    (with the opt-in content_key='sampled': edits the sample sees)."""
     hi = len(workers) if hi is None else hi
     arrays = [a for w in workers[lo:hi] for a in (w.X_local, w.y_local)]
     dev, dtype = _device(config), config.get("dtype", "float64")
     xdt = _data_dtype(config, n_features, arrays + [X_full, y_full])
-    key = (config["problem_type"], xdt, lo, hi, _fingerprint(arrays))
+    key = (config["problem_type"], xdt, lo, hi, _fingerprint(arrays, _sampled_key(config)))
     eng = _ENGINES.get((dev, dtype))
     if eng is None or eng.data_key != key:
         if eng is not None:
@@ -262,7 +281,7 @@ def _engine(workers, n_features, config, lo=0, hi=None, X_full=None, y_full=None
     return eng
 
 
-def _dist_objective(eng, workers, n_features, X_full, y_full, rank, world):
+def _dist_objective(eng, workers, n_features, X_full, y_full, rank, world, sampled=False):
     """Objective rows for a rank: its own shards when X_full is their union, else its
     array_split slice of X_full.  Returns (want_obj, rows_global, separate)."""
     if X_full is None or y_full is None:
@@ -278,11 +297,11 @@ def _dist_objective(eng, workers, n_features, X_full, y_full, rank, world):
     yf = np.asarray(y_full, dtype=np.float64).reshape(-1)
     parts = np.array_split(np.arange(Xf.shape[0]), world)[rank]
     eng.load_objective_data(Xf[parts], yf[parts])
-    eng.obj_key = ("dist", _fingerprint([X_full, y_full]))
+    eng.obj_key = ("dist", _fingerprint([X_full, y_full], sampled))
     return True, Xf.shape[0], True
 
 
-def _set_objective_data(eng, workers, n_features, X_full, y_full):
+def _set_objective_data(eng, workers, n_features, X_full, y_full, sampled=False):
     """trainer.py:188: the objective is recorded only when X_full and y_full are given.
     When they hold exactly the shard rows (the Simulator case) the objective is fused
     into the round's pass over the shards; otherwise X_full is uploaded separately."""
@@ -291,7 +310,7 @@ def _set_objective_data(eng, workers, n_features, X_full, y_full):
             eng.clear_objective_data()
             eng.obj_key = None
         return False
-    key = _fingerprint([X_full, y_full])  # by content: ids are reused once arrays are freed
+    key = _fingerprint([X_full, y_full], sampled)  # by content: ids are reused once arrays are freed
     if eng.obj_key != key:
         X, y, _ = _pack(workers, n_features, f32=_all_f32(workers))
         if _same_rows(X_full, y_full, X, y):
@@ -535,7 +554,7 @@ class CentralizedTrainer:
             return self._run_distributed(info, int(n_iterations), X_full, y_full, f_opt, lam_grad, reg_param,
                                          start_time, cfg)
         eng = _engine(self.workers, self.n_features, cfg, X_full=X_full, y_full=y_full)
-        want_obj = _set_objective_data(eng, self.workers, self.n_features, X_full, y_full)
+        want_obj = _set_objective_data(eng, self.workers, self.n_features, X_full, y_full, _sampled_key(cfg))
         T = int(n_iterations)
         ck = _Checkpoint(cfg, "centralized", self)
         t_begin, state, t_off = ck.load(T)
@@ -566,7 +585,8 @@ class CentralizedTrainer:
         bounds = distributed.partition_bounds(self.n_workers, world)
         lo, hi = int(bounds[rank]), int(bounds[rank + 1])
         eng = _engine(self.workers, self.n_features, cfg, lo, hi, X_full=X_full, y_full=y_full)
-        want_obj, rows_global, sep = _dist_objective(eng, self.workers, self.n_features, X_full, y_full, rank, world)
+        want_obj, rows_global, sep = _dist_objective(eng, self.workers, self.n_features, X_full, y_full, rank, world,
+                                                    _sampled_key(cfg))
         plan = distributed.HaloPlan(rank, world, bounds, lo, hi, np.zeros(0, np.int64), np.zeros(world + 1, np.int64),
                                     np.zeros(0, np.int32), np.zeros(world + 1, np.int64), None, None, None)
         runner = distributed.DistributedCentralized(eng, plan, self.n_workers, rows_global, device=_device(cfg),
@@ -648,7 +668,7 @@ class DecentralizedTrainer:
             return self._run_distributed(info, int(n_iterations), X_full, y_full, f_opt, lam_grad, reg_param,
                                          start_time)
         eng = _engine(self.workers, self.n_features, cfg, X_full=X_full, y_full=y_full)
-        want_obj = _set_objective_data(eng, self.workers, self.n_features, X_full, y_full)
+        want_obj = _set_objective_data(eng, self.workers, self.n_features, X_full, y_full, _sampled_key(cfg))
         t = self._topo
         uni = t.uniform_offdiag() if self._mean_mixing() else None
         if uni is not None:  # complete graph: w_off (S - x_i) + W_ii x_i, no N^2 neighbour reads
@@ -711,7 +731,8 @@ class DecentralizedTrainer:
         uni = t.uniform_offdiag() if self._mean_mixing() else None
         plan = distributed.build_plan(t, world, rank)
         eng = _engine(self.workers, self.n_features, cfg, plan.lo, plan.hi, X_full=X_full, y_full=y_full)
-        want_obj, rows_global, sep = _dist_objective(eng, self.workers, self.n_features, X_full, y_full, rank, world)
+        want_obj, rows_global, sep = _dist_objective(eng, self.workers, self.n_features, X_full, y_full, rank, world,
+                                                    _sampled_key(cfg))
         ck = _Checkpoint(cfg, "decentralized", self, rank)
         t_begin, state, t_off = ck.load(T)
         x0 = state if state is not None else np.stack([np.asarray(w.x, dtype=np.float64) for w in self.workers])

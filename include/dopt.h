@@ -43,8 +43,11 @@ extern "C" {
  *      dopt_phase_mix_lagged, dopt_phase_cons and dopt_phase_loss_pass; dopt_set_halo takes send_ids
  *      of -1 (rows that carry no worker); the multi-GPU runner internals form the header's last
  *      section.
- *   4  round 4: dopt_lagged_side_stream (k_mixcs_final and the exchange on a second stream). */
-#define DOPT_ABI_VERSION 4
+ *   4  round 4: dopt_lagged_side_stream (k_mixcs_final and the exchange on a second stream).
+ *   5  round 5: dopt_host_digest (threaded content digest of host arrays, the drop-in trainers'
+ *      engine cache key), dopt_phase_interior_count; dopt_lagged_exchange_layout accepts a self
+ *      block (a rank's own column sums routed through the exchange). */
+#define DOPT_ABI_VERSION 5
 
 typedef struct dopt_ctx dopt_ctx;
 
@@ -97,6 +100,13 @@ int dopt_mt_choice_rounds(uint32_t key[624], int32_t *pos, int64_t T, int64_t n_
  * worker.py:27).  Replaces the draws of trainer.py:166 when local_batch_size >= m. */
 int dopt_mt_advance_rounds(uint32_t key[624], int32_t *pos, int64_t T, int64_t n_workers,
                            const int64_t *shard_rows);
+
+/* Content digest (128 bits) of n_arrays host buffers -- ptrs[k] / bytes[k], in order -- hashed in
+ * 4 MiB chunks on `threads` threads (<= 0: min(16, this process's CPUs / LOCAL_WORLD_SIZE)).  The
+ * drop-in trainers key their resident engine on it (trainer._fingerprint: the Worker.X_local /
+ * y_local arrays of worker.py:7-8, compared by content on every run). */
+int dopt_host_digest(int32_t n_arrays, const void *const *ptrs, const int64_t *bytes, int32_t threads,
+                     uint64_t out[2]);
 
 /* ------------------------------------------------------------------ device */
 int dopt_device_count(int *count);
@@ -284,6 +294,10 @@ int dopt_set_halo(dopt_ctx *ctx, int64_t n_halo, void *halo_dev, int64_t n_send,
  * touched the context since); then the mark is set (mark = 1: this run leaves it open) or
  * cleared. */
 int dopt_phase_chain(dopt_ctx *ctx, int mark, int *was_pending);
+/* Workers of this rank's slice that dopt_phase_grad / dopt_lagged_grad mix and step itself (no halo
+ * column in their CSR row, no peer reading their row), as set by dopt_set_topology after
+ * dopt_set_halo; 0 without a halo plan or with column-sum mixing. */
+int dopt_phase_interior_count(dopt_ctx *ctx, int64_t *n_interior);
 /* Start of a run of phases: column-blocked contexts (large d) compute the
  * coefficients of the starting iterates here (full-shard batches). */
 int dopt_phase_begin(dopt_ctx *ctx, int64_t batch);
@@ -358,8 +372,9 @@ int dopt_rs_phase_metrics(dopt_ctx *ctx, uint32_t metric_flags);
  *   exchange(x_g rows + sums) ----------------------------------------------.
  *   dopt_lagged_grad: gradient pass of x_g (+ loss of every row at xbar_{g-1}) +--> dopt_lagged_mix
  * dopt_lagged_exchange_layout: the send-buffer row where the sums for peer p go and the halo-buffer
- *   row where peer p's sums arrive, p = 0 .. world-1 (-1 for p == rank); after dopt_set_halo, whose
- *   send_ids are -1 on those rows.
+ *   row where peer p's sums arrive, p = 0 .. world-1 (-1 for p == rank, or -- a self block, the
+ *   one-GPU rehearsal of the RCCL path at world 1 -- rows for the rank's own sums, which the mix then
+ *   reads back from the halo buffer); after dopt_set_halo, whose send_ids are -1 on those rows.
  * dopt_lagged_begin: dopt_phase_begin + the send rows and this rank's column sums of x_0.
  * dopt_lagged_grad: dopt_phase_set_step + dopt_phase_grad (replaces the worker loop of
  *   trainer.py:164-170; interior workers mixed and stepped too).

@@ -59,8 +59,8 @@ def _rank_main_topo(rank, world, port, topo, T, out, collective=False):
     col = lay.local_col(plan)
     send = torch.zeros((max(1, lay.n_send_rows), d), dtype=torch.float64)
     halo = torch.zeros((max(1, lay.n_recv_rows), d), dtype=torch.float64)
-    ex = D.HaloExchange(plan, send, halo, layout=lay)
-    ex.collective = collective
+    ex = D.HaloExchange(plan, send, halo, layout=lay, device_comm=collective)
+    assert ex.collective == collective and (ex._direct is not None) == collective
     xbars = []
     for t in range(T):
         g = np.stack([O.gradient("logistic", x[i], *shards[plan.lo + i], CFG) for i in range(plan.n_local)])
@@ -256,8 +256,10 @@ def _rank_alltoall(rank, world, port, topo, out):
             if lay.sum_send_row[p] >= 0:
                 send[lay.sum_send_row[p]] = 1000.0 + rank
         halo = torch.full((max(1, lay.n_recv_rows), 3), -1.0, dtype=torch.float64)
-        ex = D.HaloExchange(plan, send, halo, layout=lay if ks else None)
-        ex.collective = True  # the device path's call, here on gloo
+        # the device path's construction (device_comm: the process group's all-to-all-v called directly,
+        # HaloExchange._direct), here on gloo over CPU tensors
+        ex = D.HaloExchange(plan, send, halo, layout=lay if ks else None, device_comm=True)
+        assert ex.collective and ex._direct is not None
         for _ in range(2):  # every round is the same collective; repeated calls reuse the buffers
             ex.finish(ex.start())
         np.save(os.path.join(out, f"rank{rank}_{ks}.npy"), halo[lay.halo_rows].numpy())
@@ -289,3 +291,39 @@ def test_alltoall_halo_layout(tmp_path, name, n, world):
                                       [-1.0 if p == r else 1000.0 + p for p in range(world)])
     if name == "two_rings":
         assert D.build_plan(topo, world, 2).peers() == []
+
+
+def _rank_self_block(rank, world, port, out):
+    """World 1, collectives forced (the one-GPU rehearsal of the RCCL path): a self block -- plan rows
+    sent to the rank itself plus its own sum row -- through the all-to-all-v (over gloo here)."""
+    import torch
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DOPT_FORCE_COLLECTIVES="1")
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    S = np.array([0, 3, 6, 9])
+    plan = D.HaloPlan(0, 1, np.array([0, 12]), 0, 12, S.astype(np.int64), np.array([0, 4]), S.astype(np.int32),
+                      np.array([0, 4]), None, None, None)
+    lay = D.exchange_layout(plan, 1, self_block=True)
+    assert lay.send_sizes == [5] and lay.recv_sizes == [5]
+    assert lay.sum_send_row[0] == 4 and lay.sum_recv_row[0] == 4
+    np.testing.assert_array_equal(lay.send_rows, np.arange(4))
+    np.testing.assert_array_equal(lay.send_ids(plan), [0, 3, 6, 9, -1])
+    send = torch.arange(5 * 3, dtype=torch.float64).reshape(5, 3)
+    halo = torch.full((5, 3), -1.0, dtype=torch.float64)
+    ex = D.HaloExchange(plan, send, halo, layout=lay, device_comm=True)
+    assert ex.collective and ex._direct is not None
+    ex.finish(ex.start())
+    np.save(os.path.join(out, "self.npy"), halo.numpy())
+    dist.destroy_process_group()
+
+
+def test_self_block_exchange_world1(tmp_path):
+    """exchange_layout(self_block=True): the rank's block holds its plan rows, then its sum rows, and
+    the all-to-all copies it onto itself (distributed.DistributedDSGD at RCCL world 1, forced)."""
+    mp.start_processes(_rank_self_block, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True,
+                       start_method="fork")
+    np.testing.assert_array_equal(np.load(tmp_path / "self.npy"), np.arange(15.0).reshape(5, 3))
+    # without the self block a world-1 plan has no rows to move and no sum rows
+    plan = D.build_plan(TP.ring(6), 1, 0)
+    lay = D.exchange_layout(plan, 1)
+    assert lay.send_sizes == [0] and list(lay.sum_send_row) == [-1] and list(lay.sum_recv_row) == [-1]

@@ -48,6 +48,8 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
     dist.init_process_group(backend, rank=rank, world_size=world)
     top = _topo(mean, N, world if os.environ.get("DOPT_TEST_PARTITION") == "1" else 0)
     plan = Dm.build_plan(top, world, rank)
+    if os.environ.get("DOPT_TEST_SELF_HALO") == "1":  # world 1: a third of the rows through the exchange
+        plan = _self_halo_plan(top)
     eng = _engine(dtype)
     eng.generate_shards("logistic", plan.n_local, D, M, seed=9, first_worker=plan.lo)
     B = int(os.environ.get("DOPT_TEST_BATCH", M))  # B < M: device-drawn minibatches
@@ -56,6 +58,10 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
     uni = top.uniform_offdiag() if mean is True else None
     run = Dm.DistributedDSGD(eng, plan, N, N * M, device=0,
                              mean=None if uni is None else (uni[0], uni[1][plan.lo:plan.hi]))
+    info = {"interior": eng.phase_interior_count(), "n_local": plan.n_local, "n_halo": plan.n_halo,
+            "send_sizes": list(run.layout.send_sizes), "recv_sizes": list(run.layout.recv_sizes),
+            "ks": run.layout.ks, "side": run.side is not None, "collective": bool(run.exchange.collective)}
+    np.save(os.path.join(out, f"info{rank}.npy"), np.array([repr(info)]))
     which = os.environ.get("DOPT_TEST_METRICS", "both")
     if os.environ.get("DOPT_TEST_PIPE") == "1":  # a chain of pipelined calls covering T rounds, then the tail
         parts, t = [], 0
@@ -102,11 +108,15 @@ def test_ranks_match_single_context(tmp_path, dtype, mean, T, lagged, world):
 
 def _topo(mean, n, parts=0):
     """The test graph (mean: the complete graph, mixed through the column sums when True and as CSR
-    rows longer than the mix kernels' register-held entries when "csr"); with parts > 0 relabelled by
-    the spectral partition for that many ranks (bench.py's C3 placement)."""
+    rows longer than the mix kernels' register-held entries when "csr"; "torus": the sqrt(n) x sqrt(n)
+    torus of trainer.py:99-108, row-major ids, so contiguous slices are strips of torus rows -- config
+    C4's placement); with parts > 0 relabelled by the spectral partition for that many ranks (bench.py's
+    C3 placement)."""
     import distributed as Dm
     import topology as TP
 
+    if mean == "torus":
+        return TP.grid(n)
     if mean:  # True: column-sum mixing; "csr": the complete graph as CSR rows of n entries
         return TP.fully_connected(n)
     top = TP.random_regular(n, 4, seed=2)
@@ -139,6 +149,58 @@ def _compare_single(got, dtype, mean, T, N=N, D=D, M=M, exact=True, parts=0):
         np.testing.assert_allclose(got["obj"], obj, rtol=1e-12 if dtype != "float32" else 1e-6)
     if len(got["cons"]):
         np.testing.assert_allclose(got["cons"], cons, rtol=1e-12 if dtype != "float32" else 1e-5)
+
+
+def _self_halo_plan(top, every=3):
+    """A world-1 halo plan whose exchange is not empty: every `every`-th worker's row is sent to the
+    rank itself, and the OTHER workers' CSR entries of it read that copy from the halo buffer (same
+    entry order and weights, so the iterates are bitwise one context's) -- on RCCL world 1 with the
+    collectives forced, the mix then depends on rows the all-to-all moved."""
+    import distributed as Dm
+
+    n = top.n
+    S = np.arange(0, n, every)
+    pos = np.full(n, -1, np.int64)
+    pos[S] = np.arange(len(S))
+    rows = np.repeat(np.arange(n), np.diff(top.row_ptr))
+    col = top.col.astype(np.int64).copy()
+    via = (pos[col] >= 0) & (col != rows)
+    col[via] = n + pos[col[via]]
+    return Dm.HaloPlan(0, 1, np.array([0, n]), 0, n, S.astype(np.int64), np.array([0, len(S)]), S.astype(np.int32),
+                       np.array([0, len(S)]), top.row_ptr.astype(np.int64), col.astype(np.int32), top.w.copy())
+
+
+def _info(tmp_path, world):
+    import ast
+
+    return [ast.literal_eval(str(np.load(tmp_path / f"info{r}.npy")[0])) for r in range(world)]
+
+
+@pytest.mark.parametrize("world,dtype,d,m", [(2, "float64", 100, 32), (8, "float64", 100, 32),
+                                             (8, "float64/x32", 1024, 16)])
+def test_torus_strips_ranks_match_single_context(tmp_path, monkeypatch, world, dtype, d, m):
+    """config C4's split -- a torus (trainer.py:99-108) in strips of torus rows, one
+    strip per rank (64 x 64 torus: strips of 32 rows at 2 ranks, 8 at 8 ranks, >= 256 workers per rank so
+    every context launches the headline's kernel instance) -- as a chain of pipelined calls through the
+    device kernels: the strip interiors stepped inside the gradient kernel (dopt_phase_interior_count =
+    64 x (rows - 2)), the two boundary rows mixed in k_mixcs from the halo rows, the column sums riding
+    the all-to-all to all 7 peers.  Iterates bitwise one context's, history rtol 1e-12."""
+    import torch.multiprocessing as mp
+
+    n, t = 4096, 7
+    monkeypatch.setenv("DOPT_TEST_PIPE", "1")
+    mp.start_processes(_rank_main, args=(world, _free_port(), dtype, str(tmp_path), "torus", t, "1", n, d, m),
+                       nprocs=world, join=True, start_method="spawn")
+    got = np.load(tmp_path / "dist.npz")
+    assert len(got["obj"]) == len(got["cons"]) == t
+    info = _info(tmp_path, world)
+    rows = 64 // world
+    for r, it in enumerate(info):
+        assert it["n_local"] == 64 * rows and it["n_halo"] == 2 * 64, it
+        assert it["interior"] == 64 * (rows - 2), it
+        assert it["ks"] > 0 and all(it["send_sizes"][p] > 0 for p in range(world) if p != r), it
+        assert it["side"], it
+    _compare_single(got, dtype, "torus", t, n, d, m)
 
 
 def _trainer_rank(rank, world, port, out):
@@ -412,6 +474,31 @@ def _rccl_self_exchange(rank, world, port, out):
     s.synchronize()
     np.save(os.path.join(out, "ok.npy"), np.array([ok]))
     dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dtype,lagged", [("float64", "1"), ("float64/x32", "1"), ("float64", "1-noside"),
+                                          ("float32", "1")])
+def test_rccl_one_rank_self_exchange_matches_single_context(tmp_path, monkeypatch, dtype, lagged):
+    """the RCCL path at world 1 (collectives forced) with an exchange that moves data -- a
+    third of the workers' rows and the rank's own column sums go through the all-to-all to itself (a
+    self block), and the mix reads them back from the halo buffer.  With the side stream (k_mixcs_final
+    and the exchange on a second stream, ProcessGroupNCCL's stream sync and work.wait() ordering them)
+    or on one stream, as a pipelined chain: iterates bitwise one context's, history rtol 1e-12 -- a
+    missing dependency would mix stale halo rows or column sums."""
+    import torch.multiprocessing as mp
+
+    monkeypatch.setenv("DOPT_TEST_SELF_HALO", "1")
+    monkeypatch.setenv("DOPT_TEST_PIPE", "1")
+    mp.start_processes(_rank_main, args=(1, _free_port(), dtype, str(tmp_path), False, 9, lagged, N, D, M, "nccl"),
+                       nprocs=1, join=True, start_method="spawn")
+    got = np.load(tmp_path / "dist.npz")
+    assert len(got["obj"]) == len(got["cons"]) == 9
+    it = _info(tmp_path, 1)[0]
+    ks = 2 if dtype == "float32" else 1
+    assert it["collective"] and it["ks"] == ks and it["send_sizes"] == [len(range(0, N, 3)) + ks], it
+    assert it["side"] == (lagged == "1"), it
+    assert it["interior"] < N - len(range(0, N, 3)), it  # readers of the halo copies are not interior
+    _compare_single(got, dtype, False, 9)
 
 
 def test_rccl_alltoall_halo_exchange_one_rank(tmp_path):

@@ -309,14 +309,16 @@ def _rs_rank(rank, world, port, out, T, pipe=False, x32=False, chunks=None):
 
 @pytest.mark.parametrize("world,pipe,x32,chunks", [(2, False, False, None), (3, False, False, None),
                                                   (2, True, False, None), (2, True, True, None),
-                                                  (2, False, False, 1), (3, True, True, 16)])
+                                                  (2, False, False, 1), (3, True, True, 16),
+                                                  (8, True, True, None), (8, False, False, 4)])
 def test_rowspace_ranks_vs_oracle(tmp_path, world, pipe, x32, chunks):
     """Row-space rounds across ranks (gloo, contexts sharing the GPU): each rank's pass gives its
     column sums, all-reduced into the replicated average; history and gathered iterates vs the
     oracle at rtol 1e-9 (float64); pipe: the later rounds as a chain of pipelined calls; x32:
     float32-stored rows under float64 arithmetic (k_rs_pass_x32); chunks: the pass in that many
-    column chunks, each chunk's sums all-reduced on their own (default RS_CHUNKS = 4; 16 is more
-    chunks than the pass has column blocks: empty chunks)."""
+    column chunks, each chunk's sums all-reduced on their own (default: distributed.rs_chunks_for; 16
+    is more chunks than the pass has column blocks: empty chunks).  World 8: config
+    C5's rank count, the 13 ragged workers over 8 ranks (1-2 each)."""
     import socket
 
     import torch.multiprocessing as mp
