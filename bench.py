@@ -63,12 +63,18 @@ def pmc_traffic(kernel_name, config="c3"):
                    if re.fullmatch(pat, os.path.basename(f)))
     for f in reversed(files):
         try:
-            rec = json.load(open(f)).get(kernel_name)
+            doc = json.load(open(f))
         except Exception:
             continue
+        rec = doc.get(kernel_name)
         if rec:
-            return rec["hbm_bytes_per_dispatch"], os.path.relpath(f, ROOT)
-    return None, None
+            run = doc.get("_run") or {}
+            # the profiled run itself (one box, one gpurun call): its step time and the trace's average of
+            # the same kernel over that run's timed launches (scripts/pmc_summary.py)
+            same = {"ms_per_step": run.get("ms_per_step"), "kernel_timed_avg_ms_trace": run.get("kernel_timed_avg_ms_trace"),
+                    "kernel_avg_ms_events": run.get("kernel_avg_ms_events"), "steps": run.get("steps")} if run else None
+            return rec["hbm_bytes_per_dispatch"], os.path.relpath(f, ROOT), same
+    return None, None, None
 
 
 # ---------------------------------------------------------------------------- CPU baseline
@@ -722,7 +728,7 @@ def main():
     xesz = 4 if eng.data_dtype == _dopt.F32 else 8
     kname = kernel_name()
     full = {"c3": n == 4096, "c4": n == 65536, "c5": n == 1024}[args.config]  # the profiled shapes
-    traffic, traffic_src = pmc_traffic(kname, args.config) if full and world == 1 else (None, None)
+    traffic, traffic_src, traffic_run = pmc_traffic(kname, args.config) if full and world == 1 else (None, None, None)
     bytes_per_launch = bytes_per_round(eng, n, d, m, kname)
     avg_s = (kr_ms / launches) * 1e-3 if launches else float("nan")
     achieved = bytes_per_launch / avg_s / 1e9 if launches else None
@@ -768,6 +774,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
                      "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
+                     "traffic_source_run": traffic_run,
                      "kernel": kname, "kernel_avg_ms": avg_s * 1e3 if launches else None,
                      "kernel_launches_timed": launches, "event_every": every,
                      "bytes_per_launch": bytes_per_launch},

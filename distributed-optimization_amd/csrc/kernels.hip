@@ -26,6 +26,9 @@
 //
 // No atomics anywhere: every reduction has a fixed order, so runs are bitwise
 // reproducible.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 
 #include "kcommon.h"
@@ -1912,8 +1915,36 @@ void mixcs_shape(int dtype, int64_t n, int32_t nch, int32_t* ncb, int32_t* r, in
   *ng = (int32_t)std::max<int64_t>(1, (n + rr - 1) / rr);
 }
 
+#ifdef DOPT_AB
+// A/B builds, DOPT_HOST_TIMING=1: host time of each HIP call of launch_mixcs, printed at exit (VERDICT r4
+// item 4: where the side stream's host cost per round goes)
+struct MixcsHostTiming {
+  double ns[4] = {0, 0, 0, 0};
+  long calls = 0;
+  bool on = getenv("DOPT_HOST_TIMING") && atoi(getenv("DOPT_HOST_TIMING")) != 0;
+  ~MixcsHostTiming() {
+    if (on && calls)
+      fprintf(stderr, "[dopt] launch_mixcs host us per call over %ld calls: k_mixcs launch %.2f, event record %.2f, "
+              "stream wait %.2f, k_mixcs_final launch %.2f\n", calls, ns[0] / calls / 1e3, ns[1] / calls / 1e3,
+              ns[2] / calls / 1e3, ns[3] / calls / 1e3);
+  }
+};
+static MixcsHostTiming g_mht;
+static inline double mht_now() {
+  return (double)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+#define MHT_MARK(k) do { if (g_mht.on) { const double t_ = mht_now(); g_mht.ns[k] += t_ - mht_t; mht_t = t_; } } while (0)
+#else
+#define MHT_MARK(k) do { } while (0)
+#endif
+
 hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_workers, const McsArgs& m,
                         const FoldArgs* fold, hipStream_t s, hipStream_t side, hipEvent_t ev) {
+#ifdef DOPT_AB
+  double mht_t = g_mht.on ? mht_now() : 0.0;
+  if (g_mht.on) g_mht.calls++;
+#endif
   FoldArgs f;
   memset(&f, 0, sizeof(f));
   if (fold) f = *fold;
@@ -1960,10 +1991,13 @@ hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_work
   if (mm.cut != 0) return hipGetLastError();  // (timing-only cuts: no totals)
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  MHT_MARK(0);
   hipStream_t fs = s;
   if (side && ev) {
     if ((e = hipEventRecord(ev, s)) != hipSuccess) return e;
+    MHT_MARK(1);
     if ((e = hipStreamWaitEvent(side, ev, 0)) != hipSuccess) return e;
+    MHT_MARK(2);
     fs = side;
   }
   const int vn = dtype == 0 ? 4 : 2;
@@ -1972,6 +2006,7 @@ hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_work
     hipLaunchKernelGGL(k_mixcs_final<float>, g2, dim3(NT), 0, fs, mm, a.ld, a.nchunks, (float*)a.send);
   else
     hipLaunchKernelGGL(k_mixcs_final<double>, g2, dim3(NT), 0, fs, mm, a.ld, a.nchunks, (double*)a.send);
+  MHT_MARK(3);
   return hipGetLastError();
 }
 

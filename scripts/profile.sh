@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=${OUT:-gpurun_out/prof}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-B="python -u bench.py --no-cpu-baseline --no-secondary --steps ${PSTEPS:-10} --warmup 1 ${BENCH_ARGS:-}"
+B="python -u bench.py --no-cpu-baseline --no-secondary --steps ${PSTEPS:-10} --warmup ${PWARM:-1} ${BENCH_ARGS:-}"
 run() {  # run <name> <timeout> <args...>
   local name=$1 t=$2; shift 2
   echo "=== $name"; timeout -s KILL "$t" "$@" > "$OUT/$name.log" 2>&1; local rc=$?

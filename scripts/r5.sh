@@ -55,6 +55,35 @@ for step in "$@"; do
     rehearsal8 r5_rehearsal8_c4 900 --config c4 ;;
   rehearsal8_c5)  # C5 over 8 ranks (1024 workers, d = 2^20, complete graph) -> profiles/r5_rehearsal8_c5.json
     rehearsal8 r5_rehearsal8_c5 900 --config c5 ;;
+  c3_profile)  # the driver's shape (--steps 20 --warmup 5) under rocprofv3: kernel trace + stats, FETCH_SIZE, WRITE_SIZE
+    # passes, each printing its bench line -> profiles/r5_kernel_stats.csv, r5_pmc.json (scripts/pmc_summary.py)
+    OUT=gpurun_out/prof_r5 PSTEPS=20 PWARM=5 bash scripts/profile.sh || die c3_profile 1 ;;
+  host_probe)  # host time per round at 512 workers, RCCL world 1 forced, side stream on / off, launch_mixcs's HIP calls
+    # timed (A/B library, DOPT_HOST_TIMING) -> profiles/r5_host_probe.txt
+    for side in 1 0; do
+      echo "=== host probe, DOPT_LAGGED_SIDE=$side"
+      DOPT_LIB=$AB DOPT_HOST_TIMING=1 DOPT_LAGGED_SIDE=$side DOPT_FORCE_COLLECTIVES=1 timeout -k 10 200 \
+        python3 tools/host_round_probe.py > gpurun_out/r5_host_probe_s$side.json 2> gpurun_out/r5_host_probe_s$side.err \
+        || { tail -n 20 gpurun_out/r5_host_probe_s$side.err; die host_probe 1; }
+      cat gpurun_out/r5_host_probe_s$side.json; grep "launch_mixcs host" gpurun_out/r5_host_probe_s$side.err || true
+    done ;;
+  strong_trace)  # kernel traces of the phase path at 512 workers, RCCL world 1 forced (self block) / skipped
+    # -> profiles/r5_strong_trace.txt
+    B="bench.py --no-cpu-baseline --no-secondary --scaling weak --phase --workers 512 --steps 50 --warmup 5"
+    for f in 1 0; do
+      echo "=== trace, DOPT_FORCE_COLLECTIVES=$f"
+      DOPT_FORCE_COLLECTIVES=$f timeout -s KILL 150 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d gpurun_out/r5_st_f$f -o run -- python3 $B > gpurun_out/r5_st_f$f.log 2>&1 || die strong_trace 1
+      python3 tools/trace_rounds.py gpurun_out/r5_st_f$f/run_kernel_trace.csv
+    done ;;
+  strong_proxy)  # fused 4096 / fused 512 / phase 512 (forced) / phase1 512 -> profiles/r5_strong_proxy.txt
+    for w in 4096 512; do
+      bench_step r5sp_fused_$w 200 --no-cpu-baseline --no-secondary --scaling weak --workers $w --steps 100 --warmup 5
+    done
+    DOPT_FORCE_COLLECTIVES=1 bench_step r5sp_phase_512 200 --no-cpu-baseline --no-secondary --scaling weak --phase \
+      --workers 512 --steps 100 --warmup 5
+    bench_step r5sp_phase1_512 200 --no-cpu-baseline --no-secondary --scaling weak --phase --workers 512 --steps 100 \
+      --warmup 5 ;;
   *) echo "unknown step $step"; exit 2 ;;
   esac
 done

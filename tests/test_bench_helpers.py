@@ -42,14 +42,14 @@ CASES = [
 def test_bytes_and_committed_traffic(config, kernel, dt, xdt, n, d, m, gb, prof):
     b = bench.bytes_per_round(_eng(dt, xdt), n, d, m, kernel)
     assert abs(b / 1e9 - gb) < 0.01 * gb, b
-    traffic, src = bench.pmc_traffic(kernel, config)
+    traffic, src, _ = bench.pmc_traffic(kernel, config)
     assert src == prof, src
     assert 1.0 <= traffic / b < 1.02, traffic / b
 
 
 def test_traffic_lookup_is_per_configuration():
     """C3 and C4 launch the same kernel instance: each line reads its own configuration's file."""
-    t3, s3 = bench.pmc_traffic(C3, "c3")
-    t4, s4 = bench.pmc_traffic(C3, "c4")
+    t3, s3, _ = bench.pmc_traffic(C3, "c3")
+    t4, s4, _ = bench.pmc_traffic(C3, "c4")
     assert s3 != s4 and t4 > 10 * t3
-    assert bench.pmc_traffic("void dopt::k_no_such_kernel()", "c5") == (None, None)
+    assert bench.pmc_traffic("void dopt::k_no_such_kernel()", "c5") == (None, None, None)

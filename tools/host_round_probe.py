@@ -50,6 +50,7 @@ def main():
         wrap(eng, name)
     for name in ("start", "finish"):
         wrap(run.exchange, name)
+    wrap(run, "_start_exchange_lagged")  # the exchange call with the stream switch around it
     run.run_pipelined(5, 0.05, m, 1e-4, 1e-4, 0.0)
     torch.cuda.synchronize()
     acc.clear()
@@ -67,7 +68,8 @@ def main():
     run.run_pipelined(0, 0.05, m, 1e-4, 1e-4, 0.0)
     out = {"workers": n, "rounds": R, "wall_us_per_round": wall / R * 1e6,
            "host_us_per_round": {k: v / R * 1e6 for k, v in sorted(acc.items())},
-           "host_us_per_round_total": sum(acc.values()) / R * 1e6,
+           # ("start" -- the process group's all-to-all call -- runs inside _start_exchange_lagged)
+           "host_us_per_round_total": sum(v for k, v in acc.items() if k != "start") / R * 1e6,
            "loop_issue_us_per_round": (issued[0] - t0) / R * 1e6 if issued else None}
     print(json.dumps(out))
     eng.close()
