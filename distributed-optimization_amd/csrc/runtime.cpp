@@ -604,13 +604,25 @@ int upload_idx_chunk(dopt_ctx* c, const int32_t* idx, int64_t h0, int64_t nr, in
   return DOPT_OK;
 }
 
+// Event flags (A/B builds: DOPT_SIDE_EV / DOPT_PROF_EV = dev -- a device-scope release instead of the
+// default system-scope fence, whose L2 writeback and invalidate the following kernels pay)
+unsigned ev_flags(const char* knob, unsigned base) {
+#ifdef DOPT_AB
+  const char* v = getenv(knob);
+  if (v && v[0] == 'd') return base | hipEventReleaseToDevice;
+#else
+  (void)knob;
+#endif
+  return base;
+}
+
 int prof_event(dopt_ctx* c, bool stop) {
   if (!stop) c->prof_skip = (c->prof_seq++ % c->prof_every) != 0;
   if (c->prof_skip) return DOPT_OK;
   const size_t k = (size_t)(2 * c->prof_n + (stop ? 1 : 0));
   while (c->ev.size() <= k) {
     hipEvent_t e;
-    HIPOK(hipEventCreate(&e));
+    HIPOK(hipEventCreateWithFlags(&e, ev_flags("DOPT_PROF_EV", hipEventDefault)));
     c->ev.push_back(e);
   }
   HIPOK(hipEventRecord(c->ev[k], c->stream));
@@ -2549,7 +2561,8 @@ int dopt_lagged_side_stream(dopt_ctx* c, void* stream) {
   CHECK_ARG(c, "ctx is NULL");
   int rc;
   if ((rc = set_device(c))) return rc;
-  if (stream && !c->lg_side_ev) HIPOK(hipEventCreateWithFlags(&c->lg_side_ev, hipEventDisableTiming));
+  if (stream && !c->lg_side_ev)
+    HIPOK(hipEventCreateWithFlags(&c->lg_side_ev, ev_flags("DOPT_SIDE_EV", hipEventDisableTiming)));
   c->lg_side = (hipStream_t)stream;
   return DOPT_OK;
 }

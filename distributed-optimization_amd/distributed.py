@@ -361,7 +361,10 @@ class HaloExchange:
         if self.collective:  # the process group's all-to-all-v, called as dist.all_to_all_single calls it,
             try:             # minus its per-call argument checks (host cost per round: VERDICT r3 item 3)
                 opts = dist.AllToAllOptions()
-                opts.asyncOp = True
+                # asyncOp=False: ProcessGroupNCCL enqueues the all-to-all on the CURRENT stream (the side
+                # stream) instead of its internal one, so no event hop sits between k_mixcs_final and the
+                # RCCL kernel (DOPT_A2A_STREAM=current; default: the process group's stream)
+                opts.asyncOp = not (device_comm and os.environ.get("DOPT_A2A_STREAM", "nccl") == "current")
                 pg = group if group is not None else dist.distributed_c10d._get_default_group()
                 self._direct = (pg.alltoall_base, self.halo[:self.nr], self.send[:self.ns], opts)
             except (AttributeError, RuntimeError):

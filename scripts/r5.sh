@@ -76,6 +76,40 @@ for step in "$@"; do
         -d gpurun_out/r5_st_f$f -o run -- python3 $B > gpurun_out/r5_st_f$f.log 2>&1 || die strong_trace 1
       python3 tools/trace_rounds.py gpurun_out/r5_st_f$f/run_kernel_trace.csv
     done ;;
+  a2a_trace)  # the lagged exchange on the current (side) stream, asyncOp=False (DOPT_A2A_STREAM=current), 512 workers,
+    # RCCL world 1 forced: kernel trace + proxy line -> profiles/r5_a2a_current.txt
+    B="bench.py --no-cpu-baseline --no-secondary --scaling weak --phase --workers 512 --steps 50 --warmup 5"
+    echo "=== trace, DOPT_A2A_STREAM=current"
+    DOPT_A2A_STREAM=current DOPT_FORCE_COLLECTIVES=1 timeout -s KILL 150 rocprofv3 --kernel-trace --stats --output-format csv \
+      -d gpurun_out/r5_st_cur -o run -- python3 $B > gpurun_out/r5_st_cur.log 2>&1 || die a2a_trace 1
+    python3 tools/trace_rounds.py gpurun_out/r5_st_cur/run_kernel_trace.csv
+    python3 tools/trace_window.py gpurun_out/r5_st_cur/run_kernel_trace.csv
+    DOPT_A2A_STREAM=current DOPT_FORCE_COLLECTIVES=1 bench_step r5sp_phase_512_cur 200 --no-cpu-baseline --no-secondary \
+      --scaling weak --phase --workers 512 --steps 100 --warmup 5
+    DOPT_FORCE_COLLECTIVES=1 bench_step r5sp_phase_512_b 200 --no-cpu-baseline --no-secondary --scaling weak --phase \
+      --workers 512 --steps 100 --warmup 5 ;;
+  ev_ab)  # the side stream's hand-off with a device-scope release (DOPT_SIDE_EV=dev), the exchange on the current
+    # stream (DOPT_A2A_STREAM=current), both; the profiling events (DOPT_PROF_EV=dev), A/B library, interleaved twice
+    # -> profiles/r5_ev_ab.txt
+    for rep in 1 2; do
+      for v in "sys nccl" "dev nccl" "sys current" "dev current"; do
+        ev=${v%% *}; st=${v##* }
+        DOPT_LIB=$AB DOPT_SIDE_EV=$ev DOPT_A2A_STREAM=$st DOPT_FORCE_COLLECTIVES=1 bench_step r5ev_${ev}_${st}_$rep 200 \
+          --no-cpu-baseline --no-secondary --scaling weak --phase --workers 512 --steps 100 --warmup 5
+      done
+      for pe in sys dev; do
+        DOPT_LIB=$AB DOPT_PROF_EV=$pe bench_step r5pe_${pe}_$rep 200 --no-cpu-baseline --no-secondary --steps 20 --warmup 5
+      done
+    done
+    for v in dev_nccl dev_current; do
+      echo "=== trace $v"
+      DOPT_LIB=$AB DOPT_SIDE_EV=${v%_*} DOPT_A2A_STREAM=${v#*_} DOPT_FORCE_COLLECTIVES=1 timeout -s KILL 150 rocprofv3 \
+        --kernel-trace --output-format csv -d gpurun_out/r5_st_$v -o run -- python3 bench.py --no-cpu-baseline \
+        --no-secondary --scaling weak --phase --workers 512 --steps 50 --warmup 5 > gpurun_out/r5_st_$v.log 2>&1 \
+        || die ev_ab 1
+      python3 tools/trace_rounds.py gpurun_out/r5_st_$v/run_kernel_trace.csv
+      python3 tools/trace_window.py gpurun_out/r5_st_$v/run_kernel_trace.csv
+    done ;;
   strong_proxy)  # fused 4096 / fused 512 / phase 512 (forced) / phase1 512 -> profiles/r5_strong_proxy.txt
     for w in 4096 512; do
       bench_step r5sp_fused_$w 200 --no-cpu-baseline --no-secondary --scaling weak --workers $w --steps 100 --warmup 5
