@@ -91,6 +91,7 @@ _SIGS = {
     "dopt_lagged_mix": ([_P, _I64, _D, ctypes.c_int, _P, _P, _P], ctypes.c_int),
     "dopt_lagged_tail": ([_P, ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "dopt_lagged_side_stream": ([_P, _P], ctypes.c_int),
+    "dopt_lagged_exchange_issued": ([_P, _P], ctypes.c_int),
     "dopt_rs_phase_begin": ([_P, ctypes.c_int, _P, _P], ctypes.c_int),
     "dopt_rs_phase_round": ([_P, _I64, _D, _D, ctypes.c_uint32, _P], ctypes.c_int),
     "dopt_rs_phase_cols": ([_P, _I64, _D, _D, _P], ctypes.c_int),
@@ -506,6 +507,13 @@ class Engine:
         """dopt_lagged_side_stream: the stream (a hipStream_t as int, or None) that takes each mix's
         column-sum totals and that the caller issues the exchange on."""
         check(lib().dopt_lagged_side_stream(self._h, ctypes.c_void_p(stream_ptr or None)))
+
+    def lagged_exchange_issued(self):
+        """dopt_lagged_exchange_issued: True when the engine stream will wait for the exchange just issued on
+        the side stream by itself (DOPT_LAGGED_SYNC=value), False when the caller must order it."""
+        o = ctypes.c_int(0)
+        check(lib().dopt_lagged_exchange_issued(self._h, ctypes.byref(o)))
+        return bool(o.value)
 
     def lagged_tail(self, consensus, objective, row1, row2):
         """row1 / row2: (cons, xnorm, loss) device addresses of the history rows G-1 / G-2 (None: skip)."""

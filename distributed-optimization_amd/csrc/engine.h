@@ -275,10 +275,13 @@ hipError_t launch_cons(int dtype, const void* x, const void* xbar, int64_t n, in
 hipError_t launch_mix(int dtype, int cpl, const RoundArgs& a, const void* G, int n_workers, hipStream_t s);
 // The lagged mix with fused column sums (McsArgs); fold: the history row folded by block 0
 // (null: none).  xsum / xsum_n of `a` are unused (the rank-ordered sums of m replace them).
-// side != null: k_mixcs_final goes to `side` after an event wait on `ev` (recorded on s), so the next
-// gradient kernel on s need not wait for it (the exchange, issued on `side`, does).
+// side != null: k_mixcs_final goes to `side` after a wait for k_mixcs on s, so the next gradient kernel
+// on s need not wait for it (the exchange, issued on `side`, does): sig != null -- a stream write of seq
+// to *sig on s and a stream wait for *sig >= seq on side (hipStreamWriteValue64 / WaitValue64, signal
+// memory); otherwise an event `ev` recorded on s and waited for on side.
 hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_workers, const McsArgs& m,
-                        const FoldArgs* fold, hipStream_t s, hipStream_t side = nullptr, hipEvent_t ev = nullptr);
+                        const FoldArgs* fold, hipStream_t s, hipStream_t side = nullptr, hipEvent_t ev = nullptr,
+                        uint64_t* sig = nullptr, uint64_t seq = 0);
 // Column-block count / workers per group / groups of k_mixcs for n workers and nch state chunks.
 void mixcs_shape(int dtype, int64_t n, int32_t nch, int32_t* ncb, int32_t* r, int32_t* ng);
 // xbar_out = (T)(rank-ordered sum of the column sums, as k_mixcs forms it / n_div); with send != null

@@ -1940,7 +1940,8 @@ static inline double mht_now() {
 #endif
 
 hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_workers, const McsArgs& m,
-                        const FoldArgs* fold, hipStream_t s, hipStream_t side, hipEvent_t ev) {
+                        const FoldArgs* fold, hipStream_t s, hipStream_t side, hipEvent_t ev, uint64_t* sig,
+                        uint64_t seq) {
 #ifdef DOPT_AB
   double mht_t = g_mht.on ? mht_now() : 0.0;
   if (g_mht.on) g_mht.calls++;
@@ -1993,7 +1994,13 @@ hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_work
   if (e != hipSuccess) return e;
   MHT_MARK(0);
   hipStream_t fs = s;
-  if (side && ev) {
+  if (side && sig) {  // stream memory operations: no event (and no event's cache-wide fence) in either queue
+    if ((e = hipStreamWriteValue64(s, sig, seq, 0)) != hipSuccess) return e;
+    MHT_MARK(1);
+    if ((e = hipStreamWaitValue64(side, sig, seq, hipStreamWaitValueGte, ~0ull)) != hipSuccess) return e;
+    MHT_MARK(2);
+    fs = side;
+  } else if (side && ev) {
     if ((e = hipEventRecord(ev, s)) != hipSuccess) return e;
     MHT_MARK(1);
     if ((e = hipStreamWaitEvent(side, ev, 0)) != hipSuccess) return e;

@@ -199,6 +199,11 @@ struct dopt_ctx {
   std::vector<int64_t> lg_in_h, lg_out_h;  // host copies of the sum rows (-1: self)
   hipStream_t lg_side = nullptr;  // dopt_lagged_side_stream: k_mixcs_final and the exchange go there
   hipEvent_t lg_side_ev = nullptr;
+  // DOPT_LAGGED_SYNC=value: the two streams hand off through stream memory operations on lg_sig (signal
+  // memory): [0] = the last k_mixcs done (engine -> side), [1] = the last exchange done (side -> engine)
+  uint64_t* lg_sig = nullptr;
+  uint64_t lg_mseq = 0, lg_xseq = 0;
+  bool lg_xwait = false;  // the next mix / tail waits for lg_sig[1] >= lg_xseq on the engine stream
   int64_t* lg_sum_in = nullptr;            // [world] halo row of peer p's sums
   int64_t* lg_sum_out = nullptr;           // [world] send row of the sums for peer p
   double* lg_own[2] = {nullptr, nullptr};  // [ld] this rank's column sums of x_g (g parity)
@@ -1274,6 +1279,7 @@ int dopt_destroy(dopt_ctx* c) {
   dfree_t(c->lg_sum_out);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->lg_side_ev) (void)hipEventDestroy(c->lg_side_ev);
+  if (c->lg_sig) (void)hipFree(c->lg_sig);
   for (int k = 0; k < 2; ++k) {
     if (c->idx_ev[k]) (void)hipEventDestroy(c->idx_ev[k]);
     if (c->idx_pin[k]) (void)hipHostFree(c->idx_pin[k]);
@@ -2512,6 +2518,28 @@ int lagged_loss_pass(dopt_ctx* c, int two_points) {
   return DOPT_OK;
 }
 
+// DOPT_LAGGED_SYNC=value (device support permitting): the side stream's hand-offs through stream
+// memory operations instead of events (round 5; the event's system-scope fence and the cross-queue
+// barrier cost ~7-13 us each on the engine stream at 512 workers, profiles/r5_ev_ab.txt)
+bool lagged_value_sync() {
+  static const bool on = [] {
+    const char* v = getenv("DOPT_LAGGED_SYNC");
+    if (!(v && v[0] == 'v')) return false;
+    int dev = 0, ok = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    return hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, dev) == hipSuccess && ok != 0;
+  }();
+  return on;
+}
+
+// The engine stream waits for the exchange the caller issued on the side stream (value sync).
+int lagged_xwait(dopt_ctx* c) {
+  if (!c->lg_xwait) return DOPT_OK;
+  HIPOK(hipStreamWaitValue64(c->stream, c->lg_sig + 1, c->lg_xseq, hipStreamWaitValueGte, ~0ull));
+  c->lg_xwait = false;
+  return DOPT_OK;
+}
+
 McsArgs lagged_args(dopt_ctx* c, const double* own_in, double* own_out, double* cons_part) {
   McsArgs m;
   memset(&m, 0, sizeof(m));
@@ -2554,6 +2582,17 @@ int dopt_lagged_begin(dopt_ctx* c, int64_t batch) {
     HIPOK(hipStreamWaitEvent(c->lg_side, c->lg_side_ev, 0));
   }
   c->lg = 0;
+  c->lg_xwait = false;
+  return DOPT_OK;
+}
+
+int dopt_lagged_exchange_issued(dopt_ctx* c, int* ordered) {
+  CHECK_ARG(c && ordered, "NULL argument");
+  *ordered = 0;
+  if (!c->lg_side || !c->lg_sig) return DOPT_OK;  // event mode: the caller orders the engine stream itself
+  HIPOK(hipStreamWriteValue64(c->lg_side, c->lg_sig + 1, ++c->lg_xseq, 0));
+  c->lg_xwait = true;
+  *ordered = 1;
   return DOPT_OK;
 }
 
@@ -2563,7 +2602,13 @@ int dopt_lagged_side_stream(dopt_ctx* c, void* stream) {
   if ((rc = set_device(c))) return rc;
   if (stream && !c->lg_side_ev)
     HIPOK(hipEventCreateWithFlags(&c->lg_side_ev, ev_flags("DOPT_SIDE_EV", hipEventDisableTiming)));
+  if (stream && lagged_value_sync() && !c->lg_sig) {
+    HIPOK(hipExtMallocWithFlags((void**)&c->lg_sig, 2 * sizeof(uint64_t), hipMallocSignalMemory));
+    HIPOK(hipMemset(c->lg_sig, 0, 2 * sizeof(uint64_t)));
+    c->lg_mseq = c->lg_xseq = 0;
+  }
   c->lg_side = (hipStream_t)stream;
+  c->lg_xwait = false;
   return DOPT_OK;
 }
 
@@ -2606,7 +2651,9 @@ int dopt_lagged_mix(dopt_ctx* c, int64_t t, double eta0, int consensus, double* 
   f.out_c = cons_out;
   f.out_l = loss_out;
   f.out_q = xnorm_out;
-  HIPOK(launch_mixcs(c->dtype, a, c->G, (int)c->n, m, any ? &f : nullptr, c->stream, c->lg_side, c->lg_side_ev));
+  if ((rc = lagged_xwait(c))) return rc;
+  HIPOK(launch_mixcs(c->dtype, a, c->G, (int)c->n, m, any ? &f : nullptr, c->stream, c->lg_side, c->lg_side_ev,
+                     c->lg_side ? c->lg_sig : nullptr, c->lg_side && c->lg_sig ? ++c->lg_mseq : 0));
   c->xb ^= 1;
   c->cur ^= 1;
   c->lg += 1;
@@ -2620,6 +2667,7 @@ int dopt_lagged_tail(dopt_ctx* c, int consensus, int objective, double* cons1, d
   CHECK_ARG(c, "ctx is NULL");
   int rc;
   if ((rc = lagged_ready(c))) return rc;
+  if ((rc = lagged_xwait(c))) return rc;
   const int par = (int)(c->lg & 1);
   // xbar_G from every rank's sums of x_G (the exchange that preceded this call)
   const McsArgs m = lagged_args(c, c->lg_own[par], nullptr, nullptr);

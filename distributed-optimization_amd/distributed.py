@@ -321,6 +321,19 @@ def exchange_layout(plan, ks, self_block=False):
                           sum_send, sum_recv)
 
 
+class _StreamOrdered:
+    """The 'work' of a collective that ProcessGroupNCCL enqueued on the caller's stream (asyncOp=False):
+    wait() makes the current stream wait for that stream's work so far (the host does not block)."""
+
+    def __init__(self, stream):
+        self.stream = stream
+
+    def wait(self, timeout=None):
+        import torch
+
+        torch.cuda.current_stream().wait_stream(self.stream)
+
+
 class HaloExchange:
     """The per-round halo transfer of a HaloPlan: rows send[send_off[p]:send_off[p+1]] go to
     peer p, rows halo[recv_off[p]:recv_off[p+1]] come from peer p.
@@ -337,8 +350,10 @@ class HaloExchange:
     waits on the host with the job's timeout, so a peer that never sends ends this rank with a
     CollectiveError naming it."""
 
-    def __init__(self, plan, send, halo, group=None, device_comm=False, layout=None):
-        """layout: an ExchangeLayout (the blocks carry column-sum rows too), or None: the plan's rows."""
+    def __init__(self, plan, send, halo, group=None, device_comm=False, layout=None, current_stream=None):
+        """layout: an ExchangeLayout (the blocks carry column-sum rows too), or None: the plan's rows.
+        current_stream (RCCL): enqueue the all-to-all on the caller's current stream (asyncOp=False)
+        instead of the process group's internal one (default: DOPT_A2A_STREAM=current)."""
         import torch.distributed as dist
 
         self.dist, self.plan, self.group, self.device_comm = dist, plan, group, device_comm
@@ -364,7 +379,9 @@ class HaloExchange:
                 # asyncOp=False: ProcessGroupNCCL enqueues the all-to-all on the CURRENT stream (the side
                 # stream) instead of its internal one, so no event hop sits between k_mixcs_final and the
                 # RCCL kernel (DOPT_A2A_STREAM=current; default: the process group's stream)
-                opts.asyncOp = not (device_comm and os.environ.get("DOPT_A2A_STREAM", "nccl") == "current")
+                if current_stream is None:
+                    current_stream = os.environ.get("DOPT_A2A_STREAM", "nccl") == "current"
+                opts.asyncOp = not (device_comm and current_stream)
                 pg = group if group is not None else dist.distributed_c10d._get_default_group()
                 self._direct = (pg.alltoall_base, self.halo[:self.nr], self.send[:self.ns], opts)
             except (AttributeError, RuntimeError):
@@ -394,7 +411,12 @@ class HaloExchange:
         if self.collective:
             if self._direct is not None:
                 fn, out, inp, opts = self._direct
-                return [(fn(out, inp, self.recv_sizes, self.send_sizes, opts), self.what)]
+                w = fn(out, inp, self.recv_sizes, self.send_sizes, opts)
+                if w is None:  # asyncOp=False: enqueued on the current stream; finish() orders after it
+                    import torch
+
+                    w = _StreamOrdered(torch.cuda.current_stream())
+                return [(w, self.what)]
             w = dist.all_to_all_single(self.halo[:self.nr], self.send[:self.ns], output_split_sizes=self.recv_sizes,
                                        input_split_sizes=self.send_sizes, group=self.group, async_op=True)
             return [(w, self.what)]
@@ -457,7 +479,11 @@ class DistributedDSGD:
         self.halo = torch.zeros((max(1, lay.n_recv_rows), ld), dtype=tdt, device=self.dev)
         self.send = torch.zeros((max(1, lay.n_send_rows), ld), dtype=tdt, device=self.dev)
         self.sum = torch.zeros(ld, dtype=torch.float64, device=self.dev)
-        self.exchange = HaloExchange(plan, self.send, self.halo, group, self.device_comm, layout=lay)
+        # DOPT_LAGGED_SYNC=value: the lagged schedule's streams hand off through stream memory operations
+        # (the engine's), which needs the all-to-all on the side stream itself (asyncOp=False)
+        self._value_sync_asked = self._lagged_ok and os.environ.get("DOPT_LAGGED_SYNC", "event") == "value"
+        self.exchange = HaloExchange(plan, self.send, self.halo, group, self.device_comm, layout=lay,
+                                     current_stream=True if self._value_sync_asked else None)
         self.rs_chunks = int(rs_chunks) if rs_chunks else (1 if self._solo() else rs_chunks_for(plan.world))
         engine.set_partition(self.n_global, self.rows_global)
         if mean is None:
@@ -511,6 +537,10 @@ class DistributedDSGD:
             w = self.exchange.start()
         finally:
             set_id(**to_eng)
+        # value sync: the engine's next mix / tail makes the engine stream wait for a value written on the side
+        # stream behind the exchange (RCCL on the side stream, or the host transport's halo copy)
+        if self._value_sync_asked and self.eng.lagged_exchange_issued():
+            return None
         if w is None:  # host transport: the halo rows were written on the side stream
             self.stream.wait_stream(side)
         return w

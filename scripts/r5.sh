@@ -110,6 +110,30 @@ for step in "$@"; do
       python3 tools/trace_rounds.py gpurun_out/r5_st_$v/run_kernel_trace.csv
       python3 tools/trace_window.py gpurun_out/r5_st_$v/run_kernel_trace.csv
     done ;;
+  sync_ab)  # the lagged schedule's stream hand-offs by events (default) vs stream memory operations
+    # (DOPT_LAGGED_SYNC=value), 512 and 4096 workers, RCCL world 1 forced, interleaved twice; a trace and the host
+    # probe of the value mode -> profiles/r5_sync_ab.txt
+    for rep in 1 2; do
+      for w in 512 4096; do
+        for sy in event value; do
+          DOPT_LAGGED_SYNC=$sy DOPT_FORCE_COLLECTIVES=1 bench_step r5sy_${sy}_${w}_$rep 200 --no-cpu-baseline \
+            --no-secondary --scaling weak --phase --workers $w --steps 100 --warmup 5
+        done
+      done
+    done
+    echo "=== trace, value sync"
+    DOPT_LAGGED_SYNC=value DOPT_FORCE_COLLECTIVES=1 timeout -s KILL 150 rocprofv3 --kernel-trace --output-format csv \
+      -d gpurun_out/r5_st_value -o run -- python3 bench.py --no-cpu-baseline --no-secondary --scaling weak --phase \
+      --workers 512 --steps 50 --warmup 5 > gpurun_out/r5_st_value.log 2>&1 || die sync_ab 1
+    python3 tools/trace_rounds.py gpurun_out/r5_st_value/run_kernel_trace.csv
+    python3 tools/trace_window.py gpurun_out/r5_st_value/run_kernel_trace.csv
+    echo "=== host probe, value sync"
+    DOPT_LIB=$AB DOPT_HOST_TIMING=1 DOPT_LAGGED_SYNC=value DOPT_FORCE_COLLECTIVES=1 timeout -k 10 200 \
+      python3 tools/host_round_probe.py > gpurun_out/r5_host_probe_value.json 2> gpurun_out/r5_host_probe_value.err \
+      || { tail -n 20 gpurun_out/r5_host_probe_value.err; die sync_ab 1; }
+    cat gpurun_out/r5_host_probe_value.json; grep "launch_mixcs host" gpurun_out/r5_host_probe_value.err || true ;;
+  sync_tests)  # the multi-GPU tests of the value-sync mode (and everything beside them in those files)
+    echo "=== value-sync tests"; tests r5_sync_tests tests/test_gpu_distributed.py -k "value or self_exchange or torus" ;;
   strong_proxy)  # fused 4096 / fused 512 / phase 512 (forced) / phase1 512 -> profiles/r5_strong_proxy.txt
     for w in 4096 512; do
       bench_step r5sp_fused_$w 200 --no-cpu-baseline --no-secondary --scaling weak --workers $w --steps 100 --warmup 5

@@ -39,10 +39,14 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
     import distributed as Dm
     import topology as TP
 
-    side = "0" if lagged.endswith("-noside") else "1"  # "1-noside": the lagged schedule on one stream
-    lagged = lagged.split("-")[0]
+    # "1-noside": the lagged schedule on one stream; "1-value": its streams hand off through stream memory
+    # operations (DOPT_LAGGED_SYNC=value) instead of events
+    opts = lagged.split("-")
+    side = "0" if "noside" in opts else "1"
+    sync = "value" if "value" in opts else "event"
+    lagged = opts[0]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DOPT_LAGGED=lagged, DOPT_LAGGED_SIDE=side,
-                      DOPT_FORCE_COLLECTIVES="1" if backend == "nccl" else "0")
+                      DOPT_LAGGED_SYNC=sync, DOPT_FORCE_COLLECTIVES="1" if backend == "nccl" else "0")
     if backend == "nccl":
         torch.cuda.set_device(0)
     dist.init_process_group(backend, rank=rank, world_size=world)
@@ -95,6 +99,8 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
                                                       ("float64/x32", True, T, "1", 2),
                                                       ("float64/x32", "csr", T, "1", 2),
                                                       ("float64/x32", False, T, "1-noside", 2),
+                                                      ("float64/x32", False, T, "1-value", 2),
+                                                      ("float64", "torus", T, "1-value", 3),
                                                       ("float32", "csr", T, "0", 2)])
 def test_ranks_match_single_context(tmp_path, dtype, mean, T, lagged, world):
     import torch.multiprocessing as mp
@@ -477,7 +483,7 @@ def _rccl_self_exchange(rank, world, port, out):
 
 
 @pytest.mark.parametrize("dtype,lagged", [("float64", "1"), ("float64/x32", "1"), ("float64", "1-noside"),
-                                          ("float32", "1")])
+                                          ("float32", "1"), ("float64", "1-value"), ("float64/x32", "1-value")])
 def test_rccl_one_rank_self_exchange_matches_single_context(tmp_path, monkeypatch, dtype, lagged):
     """the RCCL path at world 1 (collectives forced) with an exchange that moves data -- a
     third of the workers' rows and the rank's own column sums go through the all-to-all to itself (a
@@ -496,7 +502,7 @@ def test_rccl_one_rank_self_exchange_matches_single_context(tmp_path, monkeypatc
     it = _info(tmp_path, 1)[0]
     ks = 2 if dtype == "float32" else 1
     assert it["collective"] and it["ks"] == ks and it["send_sizes"] == [len(range(0, N, 3)) + ks], it
-    assert it["side"] == (lagged == "1"), it
+    assert it["side"] == ("noside" not in lagged), it
     assert it["interior"] < N - len(range(0, N, 3)), it  # readers of the halo copies are not interior
     _compare_single(got, dtype, False, 9)
 
