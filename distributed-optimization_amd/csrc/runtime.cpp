@@ -201,7 +201,7 @@ struct dopt_ctx {
   hipEvent_t lg_side_ev = nullptr;
   // DOPT_LAGGED_SYNC=value: the two streams hand off through stream memory operations on lg_sig (signal
   // memory): [0] = the last k_mixcs done (engine -> side), [1] = the last exchange done (side -> engine)
-  uint64_t* lg_sig = nullptr;
+  uint64_t* lg_sig[2] = {nullptr, nullptr};  // (signal memory: one 8-byte value per allocation)
   uint64_t lg_mseq = 0, lg_xseq = 0;
   bool lg_xwait = false;  // the next mix / tail waits for lg_sig[1] >= lg_xseq on the engine stream
   int64_t* lg_sum_in = nullptr;            // [world] halo row of peer p's sums
@@ -1279,7 +1279,8 @@ int dopt_destroy(dopt_ctx* c) {
   dfree_t(c->lg_sum_out);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->lg_side_ev) (void)hipEventDestroy(c->lg_side_ev);
-  if (c->lg_sig) (void)hipFree(c->lg_sig);
+  for (uint64_t* p : c->lg_sig)
+    if (p) (void)hipFree(p);
   for (int k = 0; k < 2; ++k) {
     if (c->idx_ev[k]) (void)hipEventDestroy(c->idx_ev[k]);
     if (c->idx_pin[k]) (void)hipHostFree(c->idx_pin[k]);
@@ -2535,7 +2536,7 @@ bool lagged_value_sync() {
 // The engine stream waits for the exchange the caller issued on the side stream (value sync).
 int lagged_xwait(dopt_ctx* c) {
   if (!c->lg_xwait) return DOPT_OK;
-  HIPOK(hipStreamWaitValue64(c->stream, c->lg_sig + 1, c->lg_xseq, hipStreamWaitValueGte, ~0ull));
+  HIPOK(hipStreamWaitValue64(c->stream, c->lg_sig[1], c->lg_xseq, hipStreamWaitValueGte, ~0ull));
   c->lg_xwait = false;
   return DOPT_OK;
 }
@@ -2589,8 +2590,8 @@ int dopt_lagged_begin(dopt_ctx* c, int64_t batch) {
 int dopt_lagged_exchange_issued(dopt_ctx* c, int* ordered) {
   CHECK_ARG(c && ordered, "NULL argument");
   *ordered = 0;
-  if (!c->lg_side || !c->lg_sig) return DOPT_OK;  // event mode: the caller orders the engine stream itself
-  HIPOK(hipStreamWriteValue64(c->lg_side, c->lg_sig + 1, ++c->lg_xseq, 0));
+  if (!c->lg_side || !c->lg_sig[1]) return DOPT_OK;  // event mode: the caller orders the engine stream itself
+  HIPOK(hipStreamWriteValue64(c->lg_side, c->lg_sig[1], ++c->lg_xseq, 0));
   c->lg_xwait = true;
   *ordered = 1;
   return DOPT_OK;
@@ -2602,9 +2603,11 @@ int dopt_lagged_side_stream(dopt_ctx* c, void* stream) {
   if ((rc = set_device(c))) return rc;
   if (stream && !c->lg_side_ev)
     HIPOK(hipEventCreateWithFlags(&c->lg_side_ev, ev_flags("DOPT_SIDE_EV", hipEventDisableTiming)));
-  if (stream && lagged_value_sync() && !c->lg_sig) {
-    HIPOK(hipExtMallocWithFlags((void**)&c->lg_sig, 2 * sizeof(uint64_t), hipMallocSignalMemory));
-    HIPOK(hipMemset(c->lg_sig, 0, 2 * sizeof(uint64_t)));
+  if (stream && lagged_value_sync() && !c->lg_sig[0]) {
+    for (uint64_t*& p : c->lg_sig) {
+      HIPOK(hipExtMallocWithFlags((void**)&p, sizeof(uint64_t), hipMallocSignalMemory));
+      HIPOK(hipMemset(p, 0, sizeof(uint64_t)));
+    }
     c->lg_mseq = c->lg_xseq = 0;
   }
   c->lg_side = (hipStream_t)stream;
@@ -2653,7 +2656,7 @@ int dopt_lagged_mix(dopt_ctx* c, int64_t t, double eta0, int consensus, double* 
   f.out_q = xnorm_out;
   if ((rc = lagged_xwait(c))) return rc;
   HIPOK(launch_mixcs(c->dtype, a, c->G, (int)c->n, m, any ? &f : nullptr, c->stream, c->lg_side, c->lg_side_ev,
-                     c->lg_side ? c->lg_sig : nullptr, c->lg_side && c->lg_sig ? ++c->lg_mseq : 0));
+                     c->lg_side ? c->lg_sig[0] : nullptr, c->lg_side && c->lg_sig[0] ? ++c->lg_mseq : 0));
   c->xb ^= 1;
   c->cur ^= 1;
   c->lg += 1;

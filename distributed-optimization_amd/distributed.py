@@ -84,9 +84,6 @@ def init_process_group(backend, timeout=None, **kw):
     import torch.distributed as dist
 
     kw.setdefault("timeout", datetime.timedelta(seconds=timeout if timeout is not None else timeout_seconds()))
-    if backend == "nccl":
-        # the round's buffers live for the whole run: no caching-allocator recordStream per collective
-        os.environ.setdefault("TORCH_NCCL_AVOID_RECORD_STREAMS", "1")
     if backend == "nccl" and os.environ.get("DOPT_NCCL_HIPRI", "1") != "0":
         opts = dist.ProcessGroupNCCL.Options()
         opts.is_high_priority_stream = True
