@@ -2519,19 +2519,26 @@ int lagged_loss_pass(dopt_ctx* c, int two_points) {
   return DOPT_OK;
 }
 
-// DOPT_LAGGED_SYNC=value (device support permitting): the side stream's hand-offs through stream
-// memory operations instead of events (round 5; the event's system-scope fence and the cross-queue
-// barrier cost ~7-13 us each on the engine stream at 512 workers, profiles/r5_ev_ab.txt)
-bool lagged_value_sync() {
-  static const bool on = [] {
+// How the lagged schedule's two streams hand off (DOPT_LAGGED_SYNC; round 5, profiles/r5_sync_ab.txt):
+//   0 "event":  an event recorded on the engine stream after k_mixcs, waited for on the side stream (round 4);
+//   1 "value":  stream memory operations both ways (a write after k_mixcs / after the exchange, a wait on
+//               the other stream) -- on this ROCm they run as small kernels, ~5 us each on either stream;
+//   2 "signal": k_mixcs's last workgroup writes a sequence number the side stream waits for, so nothing
+//               sits between k_mixcs and the next gradient kernel on the engine stream (an event there
+//               costs ~7 us before that kernel starts at 512 workers).
+// 1 and 2 need stream wait values on the device (else 0).
+int lagged_sync_mode() {
+  static const int mode = [] {
     const char* v = getenv("DOPT_LAGGED_SYNC");
-    if (!(v && v[0] == 'v')) return false;
+    const int want = !v ? 0 : v[0] == 'v' ? 1 : v[0] == 's' ? 2 : 0;
+    if (want == 0) return 0;
     int dev = 0, ok = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return false;
-    return hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, dev) == hipSuccess && ok != 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    return (hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, dev) == hipSuccess && ok) ? want : 0;
   }();
-  return on;
+  return mode;
 }
+bool lagged_value_sync() { return lagged_sync_mode() == 1; }
 
 // The engine stream waits for the exchange the caller issued on the side stream (value sync).
 int lagged_xwait(dopt_ctx* c) {
@@ -2590,7 +2597,7 @@ int dopt_lagged_begin(dopt_ctx* c, int64_t batch) {
 int dopt_lagged_exchange_issued(dopt_ctx* c, int* ordered) {
   CHECK_ARG(c && ordered, "NULL argument");
   *ordered = 0;
-  if (!c->lg_side || !c->lg_sig[1]) return DOPT_OK;  // event mode: the caller orders the engine stream itself
+  if (!c->lg_side || !c->lg_sig[1] || !lagged_value_sync()) return DOPT_OK;  // the caller orders the engine stream
   HIPOK(hipStreamWriteValue64(c->lg_side, c->lg_sig[1], ++c->lg_xseq, 0));
   c->lg_xwait = true;
   *ordered = 1;
@@ -2603,7 +2610,7 @@ int dopt_lagged_side_stream(dopt_ctx* c, void* stream) {
   if ((rc = set_device(c))) return rc;
   if (stream && !c->lg_side_ev)
     HIPOK(hipEventCreateWithFlags(&c->lg_side_ev, ev_flags("DOPT_SIDE_EV", hipEventDisableTiming)));
-  if (stream && lagged_value_sync() && !c->lg_sig[0]) {
+  if (stream && lagged_sync_mode() != 0 && !c->lg_sig[0]) {
     for (uint64_t*& p : c->lg_sig) {
       HIPOK(hipExtMallocWithFlags((void**)&p, sizeof(uint64_t), hipMallocSignalMemory));
       HIPOK(hipMemset(p, 0, sizeof(uint64_t)));
@@ -2656,7 +2663,8 @@ int dopt_lagged_mix(dopt_ctx* c, int64_t t, double eta0, int consensus, double* 
   f.out_q = xnorm_out;
   if ((rc = lagged_xwait(c))) return rc;
   HIPOK(launch_mixcs(c->dtype, a, c->G, (int)c->n, m, any ? &f : nullptr, c->stream, c->lg_side, c->lg_side_ev,
-                     c->lg_side ? c->lg_sig[0] : nullptr, c->lg_side && c->lg_sig[0] ? ++c->lg_mseq : 0));
+                     c->lg_side ? c->lg_sig[0] : nullptr, c->lg_side && c->lg_sig[0] ? ++c->lg_mseq : 0,
+                     lagged_sync_mode() == 2));
   c->xb ^= 1;
   c->cur ^= 1;
   c->lg += 1;

@@ -132,8 +132,42 @@ for step in "$@"; do
       python3 tools/host_round_probe.py > gpurun_out/r5_host_probe_value.json 2> gpurun_out/r5_host_probe_value.err \
       || { tail -n 20 gpurun_out/r5_host_probe_value.err; die sync_ab 1; }
     cat gpurun_out/r5_host_probe_value.json; grep "launch_mixcs host" gpurun_out/r5_host_probe_value.err || true ;;
+  cpwait_ab)  # value sync with the stream waits on the command processor (GPU_STREAMOPS_CP_WAIT=1) vs events, 512
+    # workers, forced, interleaved twice; trace + host probe of the CP-wait form -> profiles/r5_sync_ab.txt
+    for rep in 1 2; do
+      DOPT_FORCE_COLLECTIVES=1 bench_step r5cp_event_$rep 200 --no-cpu-baseline --no-secondary --scaling weak --phase \
+        --workers 512 --steps 100 --warmup 5
+      GPU_STREAMOPS_CP_WAIT=1 DOPT_LAGGED_SYNC=value DOPT_FORCE_COLLECTIVES=1 bench_step r5cp_value_$rep 200 \
+        --no-cpu-baseline --no-secondary --scaling weak --phase --workers 512 --steps 100 --warmup 5
+    done
+    echo "=== trace, value sync, CP waits"
+    GPU_STREAMOPS_CP_WAIT=1 DOPT_LAGGED_SYNC=value DOPT_FORCE_COLLECTIVES=1 timeout -s KILL 150 rocprofv3 --kernel-trace \
+      --output-format csv -d gpurun_out/r5_st_cp -o run -- python3 bench.py --no-cpu-baseline --no-secondary \
+      --scaling weak --phase --workers 512 --steps 50 --warmup 5 > gpurun_out/r5_st_cp.log 2>&1 || die cpwait_ab 1
+    python3 tools/trace_rounds.py gpurun_out/r5_st_cp/run_kernel_trace.csv
+    python3 tools/trace_window.py gpurun_out/r5_st_cp/run_kernel_trace.csv
+    GPU_STREAMOPS_CP_WAIT=1 DOPT_LAGGED_SYNC=value DOPT_FORCE_COLLECTIVES=1 timeout -k 10 200 \
+      python3 tools/host_round_probe.py > gpurun_out/r5_host_probe_cp.json 2> gpurun_out/r5_host_probe_cp.err \
+      || { tail -n 20 gpurun_out/r5_host_probe_cp.err; die cpwait_ab 1; }
+    cat gpurun_out/r5_host_probe_cp.json ;;
+  sig_ab)  # event vs signal hand-off (k_mixcs's last workgroup releases a value the side stream waits for), 512 and
+    # 4096 workers, RCCL world 1 forced, interleaved three times; trace of the signal form -> profiles/r5_sig_ab.txt
+    for rep in 1 2 3; do
+      for w in 512 4096; do
+        for sy in event signal; do
+          DOPT_LAGGED_SYNC=$sy DOPT_FORCE_COLLECTIVES=1 bench_step r5sg_${sy}_${w}_$rep 200 --no-cpu-baseline \
+            --no-secondary --scaling weak --phase --workers $w --steps 100 --warmup 5
+        done
+      done
+    done
+    echo "=== trace, signal"
+    DOPT_LAGGED_SYNC=signal DOPT_FORCE_COLLECTIVES=1 timeout -s KILL 150 rocprofv3 --kernel-trace --output-format csv \
+      -d gpurun_out/r5_st_sig -o run -- python3 bench.py --no-cpu-baseline --no-secondary --scaling weak --phase \
+      --workers 512 --steps 50 --warmup 5 > gpurun_out/r5_st_sig.log 2>&1 || die sig_ab 1
+    python3 tools/trace_rounds.py gpurun_out/r5_st_sig/run_kernel_trace.csv
+    python3 tools/trace_window.py gpurun_out/r5_st_sig/run_kernel_trace.csv ;;
   sync_tests)  # the multi-GPU tests of the value-sync mode (and everything beside them in those files)
-    echo "=== value-sync tests"; tests r5_sync_tests tests/test_gpu_distributed.py -k "value or self_exchange or torus" ;;
+    echo "=== value-sync tests"; tests r5_sync_tests tests/test_gpu_distributed.py -k "value or signal or event or self_exchange or torus" ;;
   strong_proxy)  # fused 4096 / fused 512 / phase 512 (forced) / phase1 512 -> profiles/r5_strong_proxy.txt
     for w in 4096 512; do
       bench_step r5sp_fused_$w 200 --no-cpu-baseline --no-secondary --scaling weak --workers $w --steps 100 --warmup 5
