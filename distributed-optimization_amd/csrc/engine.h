@@ -126,8 +126,6 @@ struct McsArgs {
   double n_div;            // the mean's divisor (workers on all ranks)
   int32_t kin[kMcsKargRanks], kout[kMcsKargRanks];  // sum_in / sum_out of ranks < kMcsKargRanks
   int32_t cut;             // A/B builds, timing only (DOPT_MIXCS_CUT): end the kernel early (0: never)
-  uint64_t* sig;           // signal mode: the last workgroup writes seq here (the side stream waits for it)
-  uint64_t seq;
 };
 
 // Row-space rounds (rowspace.hip): complete graph (uniform W_ii), either objective, full
@@ -278,13 +276,12 @@ hipError_t launch_mix(int dtype, int cpl, const RoundArgs& a, const void* G, int
 // The lagged mix with fused column sums (McsArgs); fold: the history row folded by block 0
 // (null: none).  xsum / xsum_n of `a` are unused (the rank-ordered sums of m replace them).
 // side != null: k_mixcs_final goes to `side` after a wait for k_mixcs on s, so the next gradient kernel
-// on s need not wait for it (the exchange, issued on `side`, does).  sig != null (signal memory) with kick:
-// k_mixcs's last workgroup writes seq to *sig and side waits for *sig >= seq (hipStreamWaitValue64) -- no
-// command between k_mixcs and the next gradient kernel on s; sig without kick: a stream write of seq on
-// s and that wait on side; otherwise an event `ev` recorded on s and waited for on side.
+// on s need not wait for it (the exchange, issued on `side`, does).  sig != null (signal memory): a
+// stream write of seq to *sig on s and a stream wait for *sig >= seq on side (hipStreamWriteValue64 /
+// WaitValue64); otherwise an event `ev` recorded on s and waited for on side.
 hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_workers, const McsArgs& m,
                         const FoldArgs* fold, hipStream_t s, hipStream_t side = nullptr, hipEvent_t ev = nullptr,
-                        uint64_t* sig = nullptr, uint64_t seq = 0, bool kick = false);
+                        uint64_t* sig = nullptr, uint64_t seq = 0);
 // Column-block count / workers per group / groups of k_mixcs for n workers and nch state chunks.
 void mixcs_shape(int dtype, int64_t n, int32_t nch, int32_t* ncb, int32_t* r, int32_t* ng);
 // xbar_out = (T)(rank-ordered sum of the column sums, as k_mixcs forms it / n_div); with send != null

@@ -1602,10 +1602,11 @@ constexpr int kMixcsBatch = 16;        // group partials loaded per batch (all i
 constexpr int kMixcsMaxGroups = 1024;  // mixcs_shape keeps ng <= this
 
 // MODE 0: the group partials by plain stores, k_mixcs_final a second launch after a stream hand-off;
-// MODE 1 (A/B builds, DOPT_MIXCS_TICKET): one launch, the last workgroup of a column block sums them;
-// MODE 2 (signal): as 0, and the last workgroup of the launch writes m.seq to *m.sig once every
-// workgroup's stores are released at agent scope -- the side stream's k_mixcs_final waits for that value
-// (a stream wait), so the engine stream carries no event between k_mixcs and the next gradient kernel.
+// MODE 1 (A/B builds, DOPT_MIXCS_TICKET): one launch, the last workgroup of a column block sums them.
+// (Round 5 also tried a MODE in which the launch's last workgroup released a sequence number for the side
+// stream to wait on, so that no event sat on the engine stream: the agent-scope release of every
+// workgroup took k_mixcs from 6 to 35 us and the side stream's spinning wait slowed the gradient kernel
+// beside it; profiles/r5_sync_ab.txt.)
 template <typename T, int CPB, int MODE>
 __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __restrict__ G, int n, const McsArgs m,
                                               const FoldArgs fold) {
@@ -1815,21 +1816,6 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
     else
       m.part[(int64_t)g * ld + colbase + t] = s;
   }
-  if constexpr (MODE == 2) {
-    // every store of this workgroup (new rows, send rows, partials) visible at agent scope, then one arrival;
-    // the last of the ng x ncb arrivals resets the counter and releases the sequence number system-wide
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const unsigned total = (unsigned)m.ng * (unsigned)m.ncb;
-      const unsigned arrived = __hip_atomic_fetch_add(m.cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (arrived == total - 1) {
-        __hip_atomic_store(m.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(m.sig, m.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
-    return;
-  }
   if (!TICKET || (kMixcsAB && m.cut == 4)) return;  // (two launches: k_mixcs_final sums the partials)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
   __syncthreads();
@@ -1962,7 +1948,7 @@ static inline double mht_now() {
 
 hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_workers, const McsArgs& m,
                         const FoldArgs* fold, hipStream_t s, hipStream_t side, hipEvent_t ev, uint64_t* sig,
-                        uint64_t seq, bool kick) {
+                        uint64_t seq) {
 #ifdef DOPT_AB
   double mht_t = g_mht.on ? mht_now() : 0.0;
   if (g_mht.on) g_mht.calls++;
@@ -1998,46 +1984,24 @@ hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_work
     return hipGetLastError();
   }
 #endif
-  bool signal = side && sig && kick && mm.cut == 0;  // the launch itself signals the side stream (MODE 2)
 #ifdef DOPT_AB
   if (mixcs_cpb() == 2) {
-    signal = false;
     if (dtype == 0)
       hipLaunchKernelGGL((k_mixcs<float, 2, 0>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
     else
       hipLaunchKernelGGL((k_mixcs<double, 2, 0>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
   } else
 #endif
-  if (dtype == 0) {
-    if (signal) {
-      mm.sig = sig;
-      mm.seq = seq;
-    }
-    if (signal)
-      hipLaunchKernelGGL((k_mixcs<float, 1, 2>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
-    else
-      hipLaunchKernelGGL((k_mixcs<float, 1, 0>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
-  } else {
-    if (signal) {
-      mm.sig = sig;
-      mm.seq = seq;
-    }
-    if (signal)
-      hipLaunchKernelGGL((k_mixcs<double, 1, 2>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
-    else
-      hipLaunchKernelGGL((k_mixcs<double, 1, 0>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
-  }
+  if (dtype == 0)
+    hipLaunchKernelGGL((k_mixcs<float, 1, 0>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
+  else
+    hipLaunchKernelGGL((k_mixcs<double, 1, 0>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
   if (mm.cut != 0) return hipGetLastError();  // (timing-only cuts: no totals)
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   MHT_MARK(0);
   hipStream_t fs = s;
-  if (signal) {  // the side stream waits for the value the launch's last workgroup writes
-    MHT_MARK(1);
-    if ((e = hipStreamWaitValue64(side, sig, seq, hipStreamWaitValueGte, ~0ull)) != hipSuccess) return e;
-    MHT_MARK(2);
-    fs = side;
-  } else if (side && sig) {  // stream memory operations: no event in either queue (a write on s, a wait on side)
+  if (side && sig) {  // stream memory operations: no event in either queue (a write on s, a wait on side)
     if ((e = hipStreamWriteValue64(s, sig, seq, 0)) != hipSuccess) return e;
     MHT_MARK(1);
     if ((e = hipStreamWaitValue64(side, sig, seq, hipStreamWaitValueGte, ~0ull)) != hipSuccess) return e;

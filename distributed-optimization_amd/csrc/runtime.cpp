@@ -2520,17 +2520,16 @@ int lagged_loss_pass(dopt_ctx* c, int two_points) {
 }
 
 // How the lagged schedule's two streams hand off (DOPT_LAGGED_SYNC; round 5, profiles/r5_sync_ab.txt):
-//   0 "event":  an event recorded on the engine stream after k_mixcs, waited for on the side stream (round 4);
-//   1 "value":  stream memory operations both ways (a write after k_mixcs / after the exchange, a wait on
-//               the other stream) -- on this ROCm they run as small kernels, ~5 us each on either stream;
-//   2 "signal": k_mixcs's last workgroup writes a sequence number the side stream waits for, so nothing
-//               sits between k_mixcs and the next gradient kernel on the engine stream (an event there
-//               costs ~7 us before that kernel starts at 512 workers).
-// 1 and 2 need stream wait values on the device (else 0).
+//   0 "event": an event recorded on the engine stream after k_mixcs, waited for on the side stream, and the
+//              caller's work.wait() on the exchange (round 4; the default: fastest measured);
+//   1 "value": stream memory operations both ways (a write after k_mixcs / after the exchange, a wait on
+//              the other stream); on this ROCm they run as small kernels, ~5 us each on either stream, so
+//              the 512-worker round is ~6 % slower than with events (also with GPU_STREAMOPS_CP_WAIT=1).
+// 1 needs stream wait values on the device (else 0).
 int lagged_sync_mode() {
   static const int mode = [] {
     const char* v = getenv("DOPT_LAGGED_SYNC");
-    const int want = !v ? 0 : v[0] == 'v' ? 1 : v[0] == 's' ? 2 : 0;
+    const int want = (v && v[0] == 'v') ? 1 : 0;
     if (want == 0) return 0;
     int dev = 0, ok = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
@@ -2663,8 +2662,7 @@ int dopt_lagged_mix(dopt_ctx* c, int64_t t, double eta0, int consensus, double* 
   f.out_q = xnorm_out;
   if ((rc = lagged_xwait(c))) return rc;
   HIPOK(launch_mixcs(c->dtype, a, c->G, (int)c->n, m, any ? &f : nullptr, c->stream, c->lg_side, c->lg_side_ev,
-                     c->lg_side ? c->lg_sig[0] : nullptr, c->lg_side && c->lg_sig[0] ? ++c->lg_mseq : 0,
-                     lagged_sync_mode() == 2));
+                     c->lg_side ? c->lg_sig[0] : nullptr, c->lg_side && c->lg_sig[0] ? ++c->lg_mseq : 0));
   c->xb ^= 1;
   c->cur ^= 1;
   c->lg += 1;

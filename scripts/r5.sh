@@ -150,8 +150,9 @@ for step in "$@"; do
       python3 tools/host_round_probe.py > gpurun_out/r5_host_probe_cp.json 2> gpurun_out/r5_host_probe_cp.err \
       || { tail -n 20 gpurun_out/r5_host_probe_cp.err; die cpwait_ab 1; }
     cat gpurun_out/r5_host_probe_cp.json ;;
-  sig_ab)  # event vs signal hand-off (k_mixcs's last workgroup releases a value the side stream waits for), 512 and
-    # 4096 workers, RCCL world 1 forced, interleaved three times; trace of the signal form -> profiles/r5_sig_ab.txt
+  sig_ab)  # event vs signal hand-off (k_mixcs's last workgroup released a value the side stream waited for; the
+    # signal form was removed after this A/B, DOPT_LAGGED_SYNC=signal now runs the event form), 512 and 4096
+    # workers, RCCL world 1 forced, interleaved three times -> profiles/r5_sync_ab.txt
     for rep in 1 2 3; do
       for w in 512 4096; do
         for sy in event signal; do

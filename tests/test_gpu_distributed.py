@@ -39,11 +39,11 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
     import distributed as Dm
     import topology as TP
 
-    # "1-noside": the lagged schedule on one stream; "1-value" / "1-signal": its streams hand off through stream
-    # memory operations / a value k_mixcs's last workgroup writes (DOPT_LAGGED_SYNC) instead of events
+    # "1-noside": the lagged schedule on one stream; "1-value": its streams hand off through stream memory
+    # operations (DOPT_LAGGED_SYNC=value) instead of events
     opts = lagged.split("-")
     side = "0" if "noside" in opts else "1"
-    sync = "value" if "value" in opts else "signal" if "signal" in opts else "event"
+    sync = "value" if "value" in opts else "event"
     lagged = opts[0]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DOPT_LAGGED=lagged, DOPT_LAGGED_SIDE=side,
                       DOPT_LAGGED_SYNC=sync, DOPT_FORCE_COLLECTIVES="1" if backend == "nccl" else "0")
@@ -101,9 +101,7 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
                                                       ("float64/x32", False, T, "1-noside", 2),
                                                       ("float64/x32", False, T, "1-value", 2),
                                                       ("float64", "torus", T, "1-value", 3),
-                                                      ("float64/x32", False, T, "1-signal", 2),
-                                                      ("float32", "torus", T, "1-signal", 3),
-                                                      ("float64", "torus", T, "1-event", 3),
+                                                      ("float32", "torus", T, "1-event", 3),
                                                       ("float32", "csr", T, "0", 2)])
 def test_ranks_match_single_context(tmp_path, dtype, mean, T, lagged, world):
     import torch.multiprocessing as mp
@@ -487,7 +485,6 @@ def _rccl_self_exchange(rank, world, port, out):
 
 @pytest.mark.parametrize("dtype,lagged", [("float64", "1"), ("float64/x32", "1"), ("float64", "1-noside"),
                                           ("float32", "1"), ("float64", "1-value"), ("float64/x32", "1-value"),
-                                          ("float64", "1-signal"), ("float64/x32", "1-signal"),
                                           ("float64", "1-event")])
 def test_rccl_one_rank_self_exchange_matches_single_context(tmp_path, monkeypatch, dtype, lagged):
     """the RCCL path at world 1 (collectives forced) with an exchange that moves data -- a
