@@ -203,7 +203,8 @@ struct dopt_ctx {
   // memory): [0] = the last k_mixcs done (engine -> side), [1] = the last exchange done (side -> engine)
   uint64_t* lg_sig[2] = {nullptr, nullptr};  // (signal memory: one 8-byte value per allocation)
   uint64_t lg_mseq = 0, lg_xseq = 0;
-  bool lg_xwait = false;  // the next mix / tail waits for lg_sig[1] >= lg_xseq on the engine stream
+  bool lg_xwait = false;  // the next mix / tail waits for the exchange (lg_sig[1] >= lg_xseq, or lg_xev)
+  hipEvent_t lg_xev = nullptr;  // recorded on the side stream behind an exchange issued there (event mode)
   int64_t* lg_sum_in = nullptr;            // [world] halo row of peer p's sums
   int64_t* lg_sum_out = nullptr;           // [world] send row of the sums for peer p
   double* lg_own[2] = {nullptr, nullptr};  // [ld] this rank's column sums of x_g (g parity)
@@ -1279,6 +1280,7 @@ int dopt_destroy(dopt_ctx* c) {
   dfree_t(c->lg_sum_out);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->lg_side_ev) (void)hipEventDestroy(c->lg_side_ev);
+  if (c->lg_xev) (void)hipEventDestroy(c->lg_xev);
   for (uint64_t* p : c->lg_sig)
     if (p) (void)hipFree(p);
   for (int k = 0; k < 2; ++k) {
@@ -2542,7 +2544,10 @@ bool lagged_value_sync() { return lagged_sync_mode() == 1; }
 // The engine stream waits for the exchange the caller issued on the side stream (value sync).
 int lagged_xwait(dopt_ctx* c) {
   if (!c->lg_xwait) return DOPT_OK;
-  HIPOK(hipStreamWaitValue64(c->stream, c->lg_sig[1], c->lg_xseq, hipStreamWaitValueGte, ~0ull));
+  if (lagged_value_sync())
+    HIPOK(hipStreamWaitValue64(c->stream, c->lg_sig[1], c->lg_xseq, hipStreamWaitValueGte, ~0ull));
+  else
+    HIPOK(hipStreamWaitEvent(c->stream, c->lg_xev, 0));
   c->lg_xwait = false;
   return DOPT_OK;
 }
@@ -2596,8 +2601,13 @@ int dopt_lagged_begin(dopt_ctx* c, int64_t batch) {
 int dopt_lagged_exchange_issued(dopt_ctx* c, int* ordered) {
   CHECK_ARG(c && ordered, "NULL argument");
   *ordered = 0;
-  if (!c->lg_side || !c->lg_sig[1] || !lagged_value_sync()) return DOPT_OK;  // the caller orders the engine stream
-  HIPOK(hipStreamWriteValue64(c->lg_side, c->lg_sig[1], ++c->lg_xseq, 0));
+  if (!c->lg_side) return DOPT_OK;  // no side stream: the caller orders the engine stream
+  if (lagged_value_sync()) {
+    HIPOK(hipStreamWriteValue64(c->lg_side, c->lg_sig[1], ++c->lg_xseq, 0));
+  } else {  // an event of the context's own (no timing, created once) behind the exchange on the side stream
+    if (!c->lg_xev) HIPOK(hipEventCreateWithFlags(&c->lg_xev, ev_flags("DOPT_SIDE_EV", hipEventDisableTiming)));
+    HIPOK(hipEventRecord(c->lg_xev, c->lg_side));
+  }
   c->lg_xwait = true;
   *ordered = 1;
   return DOPT_OK;

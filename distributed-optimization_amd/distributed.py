@@ -476,11 +476,14 @@ class DistributedDSGD:
         self.halo = torch.zeros((max(1, lay.n_recv_rows), ld), dtype=tdt, device=self.dev)
         self.send = torch.zeros((max(1, lay.n_send_rows), ld), dtype=tdt, device=self.dev)
         self.sum = torch.zeros(ld, dtype=torch.float64, device=self.dev)
-        # DOPT_LAGGED_SYNC=value: the lagged schedule's streams hand off through stream memory operations
-        # (the engine's), which needs the all-to-all on the side stream itself (asyncOp=False)
-        self._value_sync_asked = self._lagged_ok and os.environ.get("DOPT_LAGGED_SYNC", "event") == "value"
+        # The lagged schedule's exchange on the side stream itself (asyncOp=False: no hop through the process
+        # group's stream before RCCL starts, DOPT_A2A_STREAM=current) or on the process group's stream (nccl,
+        # the default); with the former -- always for DOPT_LAGGED_SYNC=value, whose stream memory operations
+        # need it -- the engine orders the engine stream after the exchange itself (dopt_lagged_exchange_issued)
+        sync_value = os.environ.get("DOPT_LAGGED_SYNC", "event") == "value"
+        self._side_issued = self._lagged_ok and (sync_value or os.environ.get("DOPT_A2A_STREAM", "nccl") == "current")
         self.exchange = HaloExchange(plan, self.send, self.halo, group, self.device_comm, layout=lay,
-                                     current_stream=True if self._value_sync_asked else None)
+                                     current_stream=True if self._side_issued else None)
         self.rs_chunks = int(rs_chunks) if rs_chunks else (1 if self._solo() else rs_chunks_for(plan.world))
         engine.set_partition(self.n_global, self.rows_global)
         if mean is None:
@@ -534,9 +537,9 @@ class DistributedDSGD:
             w = self.exchange.start()
         finally:
             set_id(**to_eng)
-        # value sync: the engine's next mix / tail makes the engine stream wait for a value written on the side
-        # stream behind the exchange (RCCL on the side stream, or the host transport's halo copy)
-        if self._value_sync_asked and self.eng.lagged_exchange_issued():
+        # the exchange was enqueued on the side stream (RCCL with asyncOp=False, or the host transport's halo
+        # copy): the engine's next mix / tail makes the engine stream wait for it (an event or a stream value)
+        if self._side_issued and self.eng.lagged_exchange_issued():
             return None
         if w is None:  # host transport: the halo rows were written on the side stream
             self.stream.wait_stream(side)

@@ -400,11 +400,11 @@ int dopt_lagged_mix(dopt_ctx *ctx, int64_t t, double eta0, int consensus, double
 int dopt_lagged_tail(dopt_ctx *ctx, int consensus, int objective, double *cons1, double *xnorm1, double *loss1,
                      double *cons2, double *xnorm2, double *loss2);
 int dopt_lagged_side_stream(dopt_ctx *ctx, void *stream);
-/* Right after the caller has issued a round's exchange on the side stream: with DOPT_LAGGED_SYNC=value
- * (stream memory operations instead of events; the device must support stream wait values) the
- * context writes a sequence number on the side stream and the next dopt_lagged_mix / _tail makes the
- * engine stream wait for it -- *ordered = 1, and the caller does not order the engine stream itself;
- * otherwise *ordered = 0 (the caller orders it, e.g. work.wait() on the engine stream). */
+/* Right after the caller has enqueued a round's exchange ON the side stream (RCCL with asyncOp = false,
+ * or a host transport's halo copy): the context records an event behind it on the side stream (with
+ * DOPT_LAGGED_SYNC=value: writes a sequence number there instead) and the next dopt_lagged_mix / _tail
+ * makes the engine stream wait for it -- *ordered = 1, the caller does not order the engine stream
+ * itself.  *ordered = 0 without a side stream (the caller orders it). */
 int dopt_lagged_exchange_issued(dopt_ctx *ctx, int *ordered);
 /* Centralized trainer across ranks (trainer.py:41-71): gradients of the local
  * workers at the shared iterate (fuse_loss: the objective partial of the shared

@@ -167,8 +167,31 @@ for step in "$@"; do
       --workers 512 --steps 50 --warmup 5 > gpurun_out/r5_st_sig.log 2>&1 || die sig_ab 1
     python3 tools/trace_rounds.py gpurun_out/r5_st_sig/run_kernel_trace.csv
     python3 tools/trace_window.py gpurun_out/r5_st_sig/run_kernel_trace.csv ;;
+  cur_ab)  # the all-to-all on the process group's stream (nccl, default) vs on the side stream with the engine's own
+    # event behind it (current), 512 and 4096 workers, forced, interleaved three times; traces; host probe of
+    # current -> profiles/r5_cur_ab.txt
+    for rep in 1 2 3; do
+      for w in 512 4096; do
+        for st in nccl current; do
+          DOPT_A2A_STREAM=$st DOPT_FORCE_COLLECTIVES=1 bench_step r5cu_${st}_${w}_$rep 200 --no-cpu-baseline \
+            --no-secondary --scaling weak --phase --workers $w --steps 100 --warmup 5
+        done
+      done
+    done
+    for st in nccl current; do
+      echo "=== trace, $st"
+      DOPT_A2A_STREAM=$st DOPT_FORCE_COLLECTIVES=1 timeout -s KILL 150 rocprofv3 --kernel-trace --output-format csv \
+        -d gpurun_out/r5_st_cu_$st -o run -- python3 bench.py --no-cpu-baseline --no-secondary --scaling weak --phase \
+        --workers 512 --steps 50 --warmup 5 > gpurun_out/r5_st_cu_$st.log 2>&1 || die cur_ab 1
+      python3 tools/trace_rounds.py gpurun_out/r5_st_cu_$st/run_kernel_trace.csv
+      python3 tools/trace_window.py gpurun_out/r5_st_cu_$st/run_kernel_trace.csv
+    done
+    DOPT_A2A_STREAM=current DOPT_FORCE_COLLECTIVES=1 timeout -k 10 200 python3 tools/host_round_probe.py \
+      > gpurun_out/r5_host_probe_cur.json 2> gpurun_out/r5_host_probe_cur.err \
+      || { tail -n 20 gpurun_out/r5_host_probe_cur.err; die cur_ab 1; }
+    cat gpurun_out/r5_host_probe_cur.json ;;
   sync_tests)  # the multi-GPU tests of the value-sync mode (and everything beside them in those files)
-    echo "=== value-sync tests"; tests r5_sync_tests tests/test_gpu_distributed.py -k "value or signal or event or self_exchange or torus" ;;
+    echo "=== value-sync tests"; tests r5_sync_tests tests/test_gpu_distributed.py -k "value or current or event or self_exchange or torus" ;;
   strong_proxy)  # fused 4096 / fused 512 / phase 512 (forced) / phase1 512 -> profiles/r5_strong_proxy.txt
     for w in 4096 512; do
       bench_step r5sp_fused_$w 200 --no-cpu-baseline --no-secondary --scaling weak --workers $w --steps 100 --warmup 5

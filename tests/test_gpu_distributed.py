@@ -44,9 +44,11 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
     opts = lagged.split("-")
     side = "0" if "noside" in opts else "1"
     sync = "value" if "value" in opts else "event"
+    a2a = "current" if "current" in opts else "nccl"  # "1-current": the all-to-all on the side stream itself
     lagged = opts[0]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DOPT_LAGGED=lagged, DOPT_LAGGED_SIDE=side,
-                      DOPT_LAGGED_SYNC=sync, DOPT_FORCE_COLLECTIVES="1" if backend == "nccl" else "0")
+                      DOPT_LAGGED_SYNC=sync, DOPT_A2A_STREAM=a2a,
+                      DOPT_FORCE_COLLECTIVES="1" if backend == "nccl" else "0")
     if backend == "nccl":
         torch.cuda.set_device(0)
     dist.init_process_group(backend, rank=rank, world_size=world)
@@ -102,6 +104,7 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
                                                       ("float64/x32", False, T, "1-value", 2),
                                                       ("float64", "torus", T, "1-value", 3),
                                                       ("float32", "torus", T, "1-event", 3),
+                                                      ("float64/x32", "torus", T, "1-current", 2),
                                                       ("float32", "csr", T, "0", 2)])
 def test_ranks_match_single_context(tmp_path, dtype, mean, T, lagged, world):
     import torch.multiprocessing as mp
@@ -485,7 +488,8 @@ def _rccl_self_exchange(rank, world, port, out):
 
 @pytest.mark.parametrize("dtype,lagged", [("float64", "1"), ("float64/x32", "1"), ("float64", "1-noside"),
                                           ("float32", "1"), ("float64", "1-value"), ("float64/x32", "1-value"),
-                                          ("float64", "1-event")])
+                                          ("float64", "1-event"), ("float64", "1-current"),
+                                          ("float64/x32", "1-current")])
 def test_rccl_one_rank_self_exchange_matches_single_context(tmp_path, monkeypatch, dtype, lagged):
     """the RCCL path at world 1 (collectives forced) with an exchange that moves data -- a
     third of the workers' rows and the rank's own column sums go through the all-to-all to itself (a
