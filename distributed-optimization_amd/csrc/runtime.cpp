@@ -610,16 +610,19 @@ int upload_idx_chunk(dopt_ctx* c, const int32_t* idx, int64_t h0, int64_t nr, in
   return DOPT_OK;
 }
 
-// Event flags (A/B builds: DOPT_SIDE_EV / DOPT_PROF_EV = dev -- a device-scope release instead of the
-// default system-scope fence, whose L2 writeback and invalidate the following kernels pay)
-unsigned ev_flags(const char* knob, unsigned base) {
+// Event flags: a device-scope release instead of the system-scope fence (whose L2 writeback and
+// invalidate the following kernels pay) where only this device reads what the event orders.  A/B builds:
+// DOPT_SIDE_EV / DOPT_PROF_EV = dev / sys override the default (round 5, profiles/r5_sync_ab.txt: the
+// sampled profiling events at device scope took the driver-shaped C3 line from 1.2735 / 1.2760 to
+// 1.2707 / 1.2731 ms per round, interleaved; the side stream's hand-off event showed no difference).
+unsigned ev_flags(const char* knob, unsigned base, bool device_default) {
+  bool dev = device_default;
 #ifdef DOPT_AB
-  const char* v = getenv(knob);
-  if (v && v[0] == 'd') return base | hipEventReleaseToDevice;
+  if (const char* v = getenv(knob)) dev = v[0] == 'd';
 #else
   (void)knob;
 #endif
-  return base;
+  return dev ? (base | hipEventReleaseToDevice) : base;
 }
 
 int prof_event(dopt_ctx* c, bool stop) {
@@ -628,7 +631,7 @@ int prof_event(dopt_ctx* c, bool stop) {
   const size_t k = (size_t)(2 * c->prof_n + (stop ? 1 : 0));
   while (c->ev.size() <= k) {
     hipEvent_t e;
-    HIPOK(hipEventCreateWithFlags(&e, ev_flags("DOPT_PROF_EV", hipEventDefault)));
+    HIPOK(hipEventCreateWithFlags(&e, ev_flags("DOPT_PROF_EV", hipEventDefault, true)));
     c->ev.push_back(e);
   }
   HIPOK(hipEventRecord(c->ev[k], c->stream));
@@ -2605,7 +2608,7 @@ int dopt_lagged_exchange_issued(dopt_ctx* c, int* ordered) {
   if (lagged_value_sync()) {
     HIPOK(hipStreamWriteValue64(c->lg_side, c->lg_sig[1], ++c->lg_xseq, 0));
   } else {  // an event of the context's own (no timing, created once) behind the exchange on the side stream
-    if (!c->lg_xev) HIPOK(hipEventCreateWithFlags(&c->lg_xev, ev_flags("DOPT_SIDE_EV", hipEventDisableTiming)));
+    if (!c->lg_xev) HIPOK(hipEventCreateWithFlags(&c->lg_xev, ev_flags("DOPT_SIDE_EV", hipEventDisableTiming, false)));
     HIPOK(hipEventRecord(c->lg_xev, c->lg_side));
   }
   c->lg_xwait = true;
@@ -2618,7 +2621,7 @@ int dopt_lagged_side_stream(dopt_ctx* c, void* stream) {
   int rc;
   if ((rc = set_device(c))) return rc;
   if (stream && !c->lg_side_ev)
-    HIPOK(hipEventCreateWithFlags(&c->lg_side_ev, ev_flags("DOPT_SIDE_EV", hipEventDisableTiming)));
+    HIPOK(hipEventCreateWithFlags(&c->lg_side_ev, ev_flags("DOPT_SIDE_EV", hipEventDisableTiming, false)));
   if (stream && lagged_sync_mode() != 0 && !c->lg_sig[0]) {
     for (uint64_t*& p : c->lg_sig) {
       HIPOK(hipExtMallocWithFlags((void**)&p, sizeof(uint64_t), hipMallocSignalMemory));
