@@ -53,7 +53,7 @@ def _maybe_init_distributed():
 
         import distributed
 
-        local = int(os.environ.get("LOCAL_RANK", "0"))
+        local = int(os.environ.get("DOPT_DEVICE", os.environ.get("LOCAL_RANK", "0")))  # (trainer._device)
         torch.cuda.set_device(local)
         distributed.init_process_group(os.environ.get("DOPT_BACKEND", "nccl"))
 

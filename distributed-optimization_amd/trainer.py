@@ -83,7 +83,9 @@ def _warn_nonfinite(history, config):
 
 
 def _device(config):
-    return int(config.get("device", os.environ.get("LOCAL_RANK", os.environ.get("DOPT_DEVICE", 0))))
+    """The GPU of this process: config 'device', else DOPT_DEVICE (an explicit override, e.g. every rank
+    of a gloo rehearsal on one GPU), else the launcher's LOCAL_RANK, else 0."""
+    return int(config.get("device", os.environ.get("DOPT_DEVICE", os.environ.get("LOCAL_RANK", 0))))
 
 
 def _pack(workers, n_features, f32=False):

@@ -190,6 +190,15 @@ for step in "$@"; do
       > gpurun_out/r5_host_probe_cur.json 2> gpurun_out/r5_host_probe_cur.err \
       || { tail -n 20 gpurun_out/r5_host_probe_cur.err; die cur_ab 1; }
     cat gpurun_out/r5_host_probe_cur.json ;;
+  mainpy8)  # main.py (the reference's experiment: 4 trainers x 10^4 rounds, N = 25) under torch.distributed.run
+    # with 8 gloo ranks sharing the one GPU -> profiles/r5_mainpy8.log (Table II: 5425 / 7214 / 5666 / 5549)
+    echo "=== main.py, 8 ranks"
+    (cd distributed-optimization_amd && MPLBACKEND=Agg DOPT_BACKEND=gloo DOPT_DEVICE=0 timeout -k 10 900 \
+      python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29533 \
+      main.py) > gpurun_out/r5_mainpy8.log 2>&1 || { tail -n 30 gpurun_out/r5_mainpy8.log; die mainpy8 1; }
+    grep -v "amdgpu.ids\|socket.cpp\|Gloo" gpurun_out/r5_mainpy8.log | tail -n 30 ;;
+  trainer8)  # the drop-in trainers at 2 and 8 gloo ranks vs the C2 fixture
+    echo "=== trainers at 8 ranks"; tests r5_trainer8 tests/test_gpu_distributed.py -k trainers_multiprocess_match ;;
   sync_tests)  # the multi-GPU tests of the value-sync mode (and everything beside them in those files)
     echo "=== value-sync tests"; tests r5_sync_tests tests/test_gpu_distributed.py -k "value or current or event or self_exchange or torus" ;;
   strong_proxy)  # fused 4096 / fused 512 / phase 512 (forced) / phase1 512 -> profiles/r5_strong_proxy.txt

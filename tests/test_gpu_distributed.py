@@ -251,14 +251,15 @@ def _trainer_rank(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_trainers_multiprocess_match_reference(tmp_path):
-    """DecentralizedTrainer / CentralizedTrainer under a 2-rank torch.distributed job
-    (each rank holds half of the workers) reproduce the reference's C2 trajectories."""
+@pytest.mark.parametrize("world", [2, 8])
+def test_trainers_multiprocess_match_reference(tmp_path, world):
+    """DecentralizedTrainer / CentralizedTrainer under a torch.distributed job of 2 and 8 ranks (each
+    rank holds its slice of the 10 workers: 1-2 at 8 ranks) reproduce the reference's C2 trajectories."""
     import json
 
     import torch.multiprocessing as mp
 
-    mp.start_processes(_trainer_rank, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True,
+    mp.start_processes(_trainer_rank, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
     got = np.load(tmp_path / "trainers.npz")
     G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
