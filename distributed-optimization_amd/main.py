@@ -45,10 +45,16 @@ def make_config(**overrides):
 
 def _maybe_init_distributed():
     """Under torch.distributed.run (WORLD_SIZE > 1) every rank runs this script; the
-    trainers then split the workers across the ranks' GPUs (trainer.py docstring)."""
+    trainers then split the workers across the ranks' GPUs (trainer.py docstring), every rank
+    computes the same histories, and rank 0 alone prints the report and plots (the reference's
+    single process prints it once).  Returns True on the rank that reports."""
     import os
 
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        if int(os.environ.get("RANK", "0")) != 0:
+            import sys
+
+            sys.stdout = open(os.devnull, "w")
         import torch
 
         import distributed
@@ -56,11 +62,14 @@ def _maybe_init_distributed():
         local = int(os.environ.get("DOPT_DEVICE", os.environ.get("LOCAL_RANK", "0")))  # (trainer._device)
         torch.cuda.set_device(local)
         distributed.init_process_group(os.environ.get("DOPT_BACKEND", "nccl"))
+        return int(os.environ.get("RANK", "0")) == 0
+    return True
 
 
 if __name__ == "__main__":
-    _maybe_init_distributed()
+    reporter = _maybe_init_distributed()
     np.random.seed(203)
     simulator = Simulator(make_config())
     simulator.run_all()
-    simulator.plot_results()
+    if reporter:
+        simulator.plot_results()
