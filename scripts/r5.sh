@@ -199,6 +199,25 @@ for step in "$@"; do
     grep -v "amdgpu.ids\|socket.cpp\|Gloo" gpurun_out/r5_mainpy8.log | tail -n 30 ;;
   trainer8)  # the drop-in trainers at 2 and 8 gloo ranks vs the C2 fixture
     echo "=== trainers at 8 ranks"; tests r5_trainer8 tests/test_gpu_distributed.py -k trainers_multiprocess_match ;;
+  mixrec_ab)  # k_mixcs with the per-worker mix records (default) vs the CSR arrays (DOPT_MIXCS_REC=0, A/B library),
+    # every worker mixed there (DOPT_PHASE_INTERIOR=0) at 4096 and 512 workers, and the strong proxy (512, forced),
+    # kernel traces, interleaved twice -> profiles/r5_mixrec_ab.txt
+    for rep in 1 2; do
+      for w in 4096 512; do
+        for rec in 1 0; do
+          echo "=== rep $rep, $w workers, DOPT_MIXCS_REC=$rec, DOPT_PHASE_INTERIOR=0"
+          DOPT_LIB=$AB DOPT_MIXCS_REC=$rec DOPT_PHASE_INTERIOR=0 timeout -s KILL 150 rocprofv3 --kernel-trace \
+            --output-format csv -d gpurun_out/r5_mr_${w}_${rec}_$rep -o run -- python3 bench.py --no-cpu-baseline \
+            --no-secondary --scaling weak --phase --workers $w --steps 30 --warmup 3 \
+            > gpurun_out/r5_mr_${w}_${rec}_$rep.log 2>&1 || die mixrec_ab 1
+          python3 tools/trace_rounds.py gpurun_out/r5_mr_${w}_${rec}_$rep/run_kernel_trace.csv
+        done
+      done
+      for rec in 1 0; do
+        DOPT_LIB=$AB DOPT_MIXCS_REC=$rec DOPT_FORCE_COLLECTIVES=1 bench_step r5mr_phase_512_${rec}_$rep 200 \
+          --no-cpu-baseline --no-secondary --scaling weak --phase --workers 512 --steps 100 --warmup 5
+      done
+    done ;;
   sync_tests)  # the multi-GPU tests of the value-sync mode (and everything beside them in those files)
     echo "=== value-sync tests"; tests r5_sync_tests tests/test_gpu_distributed.py -k "value or current or event or self_exchange or torus" ;;
   strong_proxy)  # fused 4096 / fused 512 / phase 512 (forced) / phase1 512 -> profiles/r5_strong_proxy.txt
