@@ -126,15 +126,7 @@ struct McsArgs {
   double n_div;            // the mean's divisor (workers on all ranks)
   int32_t kin[kMcsKargRanks], kout[kMcsKargRanks];  // sum_in / sum_out of ranks < kMcsKargRanks
   int32_t cut;             // A/B builds, timing only (DOPT_MIXCS_CUT): end the kernel early (0: never)
-  // per-worker mix records (or null: the CSR arrays): kMixRec int32 each -- columns [0, 6) (-1 past the
-  // row), the entry count, the interior flag, the send slots [8, 10) (-1 past them), their count -- and
-  // mw: [n x 6] weights in T, CSR order.  Built by dopt_set_topology when every row has <= 6 entries and
-  // every worker <= 2 send rows.
-  const int32_t* mrec;
-  const void* mw;
 };
-constexpr int kMixRec = 16;
-constexpr int kMixRecCols = 6, kMixRecSlots = 2;
 
 // Row-space rounds (rowspace.hip): complete graph (uniform W_ii), either objective, full
 // shards of 1..kRsMaxRows rows, iterates that start equal.  x_i = Z + X_i^T beta_i.

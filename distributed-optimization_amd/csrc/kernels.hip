@@ -1613,9 +1613,8 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
   constexpr bool TICKET = MODE == 1;
   using V = typename VT<T>::v;
   constexpr int VN = VT<T>::n;
-  constexpr int MAXE = kMixRecCols;  // CSR entries held in registers (the rest of a longer row: loaded at use)
-  constexpr int MAXS = kMixRecSlots; // send slots of a row held in registers (the rest: loaded at use)
-  static_assert(MAXE + 3 + MAXS <= kMixRec, "mix record layout");
+  constexpr int MAXE = 6;            // CSR entries held in registers (the rest of a longer row: loaded at use)
+  constexpr int MAXS = 2;            // send slots of a row held in registers (the rest: loaded at use)
   constexpr int BC = 64 * CPB * VN;  // columns of a column block
   constexpr int XR = 2 * NW;         // ranks' sums staged through LDS per pass (two per wave)
   constexpr int XT = BC / 64;        // columns per lane in the staging
@@ -1641,13 +1640,8 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
   // Every load of a wave's two workers is issued before any of them is used: (A) the CSR range,
   // interior flag, send range and own row, (B) the CSR columns, the send slots and the gradient
   // (or, for an interior worker, the row the gradient kernel stepped), (C) the neighbour rows.
-  // With the per-worker mix records (m.mrec: columns, entry count, interior flag, send slots in one
-  // 64-byte record; m.mw: the row's weights) the columns come with the first load, so a worker's loads
-  // take two dependent steps instead of three (record -> rows, not row range -> columns -> rows).
   V own[2][CPB], gv[2][CPB], r[2][MAXE][CPB];
   int64_t e0[2], e1[2], s0[2], s1[2];
-  const int32_t* cp[2];  // the worker's CSR columns (entries e0 .. e1 - 1 of cp)
-  const T* wp[2];        // and their weights
   int32_t sl[2][MAXS];
   bool live[2], skip[2];
   auto issue = [&](int i0) {
@@ -1655,24 +1649,11 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
     for (int u = 0; u < 2; ++u) {
       const int i = i0 + u * NW;
       live[u] = i < i_end;
-      if (m.mrec) {
-        const int32_t* rc = m.mrec + (int64_t)(live[u] ? i : 0) * kMixRec;
-        cp[u] = rc;
-        wp[u] = (const T*)m.mw + (int64_t)(live[u] ? i : 0) * MAXE;
-        e0[u] = 0;
-        e1[u] = live[u] ? rc[MAXE] : 0;
-        skip[u] = live[u] && a.interior && rc[MAXE + 1];
-        s0[u] = 0;
-        s1[u] = (live[u] && a.sptr) ? rc[MAXE + 2 + MAXS] : 0;
-      } else {
-        e0[u] = live[u] ? a.rp[i] : 0;
-        e1[u] = live[u] ? a.rp[i + 1] : 0;
-        cp[u] = a.ci + e0[u];
-        wp[u] = (const T*)a.cw + e0[u];
-        skip[u] = live[u] && a.interior && a.interior[i];
-        s0[u] = (live[u] && a.sptr) ? a.sptr[i] : 0;
-        s1[u] = (live[u] && a.sptr) ? a.sptr[i + 1] : 0;
-      }
+      e0[u] = live[u] ? a.rp[i] : 0;
+      e1[u] = live[u] ? a.rp[i + 1] : 0;
+      skip[u] = live[u] && a.interior && a.interior[i];
+      s0[u] = (live[u] && a.sptr) ? a.sptr[i] : 0;
+      s1[u] = (live[u] && a.sptr) ? a.sptr[i + 1] : 0;
 #pragma unroll
       for (int j = 0; j < CPB; ++j) {
         const int c = cbase + lane + 64 * j;
@@ -1683,8 +1664,7 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
     for (int u = 0; u < 2; ++u) {
       const int i = i0 + u * NW;
 #pragma unroll
-      for (int q = 0; q < MAXS; ++q)
-        sl[u][q] = (!skip[u] && s0[u] + q < s1[u]) ? (m.mrec ? cp[u][MAXE + 2 + q] : a.sslot[s0[u] + q]) : -1;
+      for (int q = 0; q < MAXS; ++q) sl[u][q] = (!skip[u] && s0[u] + q < s1[u]) ? a.sslot[s0[u] + q] : -1;
 #pragma unroll
       for (int j = 0; j < CPB; ++j) {
         const int c = cbase + lane + 64 * j;
@@ -1699,7 +1679,7 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
 #pragma unroll
       for (int k = 0; k < MAXE; ++k) {
         if (!skip[u] && e0[u] + k < e1[u]) {
-          const int col = cp[u][k];
+          const int col = a.ci[e0[u] + k];
           const T* src = col < a.n_local ? (const T*)a.x_old + (int64_t)col * ld : halo + (int64_t)(col - a.n_local) * ld;
 #pragma unroll
           for (int j = 0; j < CPB; ++j) {
@@ -1791,7 +1771,7 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
           V acc = V(0);
 #pragma unroll
           for (int k = 0; k < MAXE; ++k)
-            if (e0[u] + k < e1[u]) acc += wp[u][k] * r[u][k][j];
+            if (e0[u] + k < e1[u]) acc += ((const T*)a.cw)[e0[u] + k] * r[u][k][j];
           for (int64_t e = e0[u] + MAXE; e < e1[u]; ++e) {  // longer rows (dense graphs): CSR order
             const int col = a.ci[e];
             const T* src = col < a.n_local ? (const T*)a.x_old + (int64_t)col * ld : halo + (int64_t)(col - a.n_local) * ld;

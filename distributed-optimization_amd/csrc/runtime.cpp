@@ -196,9 +196,6 @@ struct dopt_ctx {
   // peer at the rows dopt_lagged_exchange_layout names
   int32_t lg_world = 1, lg_rank = 0;
   bool lg_self = false;  // a self block in the exchange layout (RCCL world 1, collectives forced)
-  int32_t* mrec = nullptr;  // k_mixcs's per-worker mix records (dopt_set_topology; engine.h McsArgs)
-  void* mw = nullptr;
-  std::vector<int32_t> send_ids_h;  // dopt_set_halo's send_ids (host copy)
   std::vector<int64_t> lg_in_h, lg_out_h;  // host copies of the sum rows (-1: self)
   hipStream_t lg_side = nullptr;  // dopt_lagged_side_stream: k_mixcs_final and the exchange go there
   hipEvent_t lg_side_ev = nullptr;
@@ -1284,8 +1281,6 @@ int dopt_destroy(dopt_ctx* c) {
   dfree_t(c->lg_cnt);
   dfree_t(c->lg_sum_in);
   dfree_t(c->lg_sum_out);
-  dfree_t(c->mrec);
-  dfree(c->mw);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->lg_side_ev) (void)hipEventDestroy(c->lg_side_ev);
   if (c->lg_xev) (void)hipEventDestroy(c->lg_xev);
@@ -1464,53 +1459,6 @@ int dopt_set_topology(dopt_ctx* c, int64_t n_workers, const int64_t* row_ptr, co
     }
     if ((rc = dalloc_t(&c->interior, in.size() * sizeof(int32_t)))) return rc;
     HIPOK(hipMemcpy(c->interior, in.data(), in.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-  }
-  // per-worker mix records for k_mixcs (engine.h McsArgs::mrec): rows of <= 6 entries, <= 2 send rows
-  dfree_t(c->mrec);
-  dfree(c->mw);
-  {
-    int64_t max_send = 0;  // send rows per worker, in dopt_set_halo's sslot order
-    std::vector<std::vector<int32_t>> slots((size_t)n_workers);
-    for (size_t k = 0; k < c->send_ids_h.size(); ++k)
-      if (c->send_ids_h[k] >= 0) slots[(size_t)c->send_ids_h[k]].push_back((int32_t)k);
-    for (const auto& v : slots) max_send = std::max<int64_t>(max_send, (int64_t)v.size());
-    static const bool rec_on = [] {  // A/B builds: DOPT_MIXCS_REC=0 -> the CSR arrays
-#ifdef DOPT_AB
-      const char* v = getenv("DOPT_MIXCS_REC");
-      return !(v && v[0] == '0');
-#else
-      return true;
-#endif
-    }();
-    if (rec_on && mx <= kMixRecCols && max_send <= kMixRecSlots) {
-      std::vector<int32_t> rec((size_t)n_workers * kMixRec, -1);
-      std::vector<double> wd((size_t)n_workers * kMixRecCols, 0.0);
-      for (int64_t i = 0; i < n_workers; ++i) {
-        int32_t* r = rec.data() + (size_t)i * kMixRec;
-        const int64_t e0 = row_ptr[i], ne = row_ptr[i + 1] - e0;
-        for (int64_t k = 0; k < ne; ++k) {
-          r[k] = col[e0 + k];
-          wd[(size_t)i * kMixRecCols + (size_t)k] = w[e0 + k];
-        }
-        r[kMixRecCols] = (int32_t)ne;
-        bool local = (size_t)i >= c->is_send.size() || !c->is_send[(size_t)i];
-        for (int64_t k = 0; k < ne && local; ++k) local = col[e0 + k] < n_workers;
-        r[kMixRecCols + 1] = (c->n_halo > 0 || !c->is_send.empty()) && local ? 1 : 0;
-        const auto& sv = slots[(size_t)i];
-        for (size_t q = 0; q < sv.size(); ++q) r[kMixRecCols + 2 + (int)q] = sv[q];
-        r[kMixRecCols + 2 + kMixRecSlots] = (int32_t)sv.size();
-      }
-      if ((rc = dalloc_t(&c->mrec, rec.size() * sizeof(int32_t)))) return rc;
-      if ((rc = dalloc(&c->mw, (size_t)n_workers * kMixRecCols * c->esz))) return rc;
-      HIPOK(hipMemcpy(c->mrec, rec.data(), rec.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-      if (c->dtype == DOPT_F64) {
-        HIPOK(hipMemcpy(c->mw, wd.data(), wd.size() * sizeof(double), hipMemcpyHostToDevice));
-      } else {  // the weights as the float32 engine stores them (cw: (float)w)
-        std::vector<float> wf(wd.size());
-        for (size_t k = 0; k < wd.size(); ++k) wf[k] = (float)wd[k];
-        HIPOK(hipMemcpy(c->mw, wf.data(), wf.size() * sizeof(float), hipMemcpyHostToDevice));
-      }
-    }
   }
   c->have_topo = true;
   c->mean_mix = false;
@@ -2082,7 +2030,6 @@ int dopt_set_halo(dopt_ctx* c, int64_t n_halo, void* halo_dev, int64_t n_send, v
   std::vector<int64_t> fill(sp.begin(), sp.end() - 1);
   for (int64_t k = 0; k < n_send; ++k)
     if (send_ids[k] >= 0) slot[(size_t)fill[(size_t)send_ids[k]]++] = (int32_t)k;
-  c->send_ids_h.assign(send_ids, send_ids + n_send);
   c->is_send.assign((size_t)c->n, 0);
   for (int64_t k = 0; k < n_send; ++k)
     if (send_ids[k] >= 0) c->is_send[(size_t)send_ids[k]] = 1;
@@ -2624,8 +2571,6 @@ McsArgs lagged_args(dopt_ctx* c, const double* own_in, double* own_out, double* 
   m.sum_out = c->lg_sum_out;
   m.cons_part = cons_part;
   m.n_div = (double)n_div(c);
-  m.mrec = c->mrec;
-  m.mw = c->mw;
   for (int p = 0; p < kMcsKargRanks; ++p) {  // the first ranks' rows by value (no dependent load in the kernel)
     m.kin[p] = p < (int)c->lg_in_h.size() ? (int32_t)c->lg_in_h[p] : -1;
     m.kout[p] = p < (int)c->lg_out_h.size() ? (int32_t)c->lg_out_h[p] : -1;

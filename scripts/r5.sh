@@ -199,7 +199,8 @@ for step in "$@"; do
     grep -v "amdgpu.ids\|socket.cpp\|Gloo" gpurun_out/r5_mainpy8.log | tail -n 30 ;;
   trainer8)  # the drop-in trainers at 2 and 8 gloo ranks vs the C2 fixture
     echo "=== trainers at 8 ranks"; tests r5_trainer8 tests/test_gpu_distributed.py -k trainers_multiprocess_match ;;
-  mixrec_ab)  # k_mixcs with the per-worker mix records (default) vs the CSR arrays (DOPT_MIXCS_REC=0, A/B library),
+  mixrec_ab)  # (historical: the records were reverted after this A/B showed no difference; DOPT_MIXCS_REC is now
+    # ignored) k_mixcs with the per-worker mix records vs the CSR arrays (DOPT_MIXCS_REC=0, A/B library),
     # every worker mixed there (DOPT_PHASE_INTERIOR=0) at 4096 and 512 workers, and the strong proxy (512, forced),
     # kernel traces, interleaved twice -> profiles/r5_mixrec_ab.txt
     for rep in 1 2; do
