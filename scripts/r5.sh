@@ -219,6 +219,16 @@ for step in "$@"; do
           --no-cpu-baseline --no-secondary --scaling weak --phase --workers 512 --steps 100 --warmup 5
       done
     done ;;
+  lb_ab)  # the objective terms in register batches inside the row stream (VAR bit 21, instance 3291187) vs the
+    # deferred terms after it (default 1210419), A/B library, interleaved in one process, 512 / 4096 workers
+    # -> profiles/r5_lb_ab.txt
+    for w in 512 4096 512; do
+      echo "=== in-stream objective batches, $w workers"
+      DOPT_LIB=$AB timeout -k 10 300 python3 tools/kr_variants.py --mode x32 --variants=-1,3291187 --reps 7 \
+        --rounds 20 --workers $w > gpurun_out/r5_lb_ab_$w.json 2> gpurun_out/r5_lb_ab_$w.err \
+        || { tail -n 20 gpurun_out/r5_lb_ab_$w.err; die lb_ab 1; }
+      cat gpurun_out/r5_lb_ab_$w.json
+    done ;;
   sync_tests)  # the multi-GPU tests of the value-sync mode (and everything beside them in those files)
     echo "=== value-sync tests"; tests r5_sync_tests tests/test_gpu_distributed.py -k "value or current or event or self_exchange or torus" ;;
   strong_proxy)  # fused 4096 / fused 512 / phase 512 (forced) / phase1 512 -> profiles/r5_strong_proxy.txt
