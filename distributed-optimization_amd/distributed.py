@@ -527,9 +527,13 @@ class DistributedDSGD:
             return self.exchange.start()
         sw = self._stream_switch
         if sw is None:
-            set_id = self.torch._C._cuda_setStream
-            ids = [dict(stream_id=st.stream_id, device_index=st.device_index, device_type=st.device_type)
-                   for st in (side, self.stream)]
+            set_id = getattr(self.torch._C, "_cuda_setStream", None)
+            if set_id is not None:
+                ids = [dict(stream_id=st.stream_id, device_index=st.device_index, device_type=st.device_type)
+                       for st in (side, self.stream)]
+            else:  # (a torch without the private setter: the public one, same effect)
+                set_id = lambda stream: self.torch.cuda.set_stream(stream)  # noqa: E731
+                ids = [dict(stream=side), dict(stream=self.stream)]
             sw = self._stream_switch = (set_id, ids[0], ids[1])
         set_id, to_side, to_eng = sw
         set_id(**to_side)
