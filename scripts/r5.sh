@@ -229,6 +229,11 @@ for step in "$@"; do
         || { tail -n 20 gpurun_out/r5_lb_ab_$w.err; die lb_ab 1; }
       cat gpurun_out/r5_lb_ab_$w.json
     done ;;
+  round_index)  # are the first rounds of a run slower because of the iterates or of the clocks? two chains from zero
+    # iterates back to back, every round kernel timed -> profiles/r5_round_index.json
+    timeout -s KILL 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r5_ri -o run -- python3 \
+      tools/round_index_probe.py > gpurun_out/r5_round_index.log 2>&1 || { tail -n 20 gpurun_out/r5_round_index.log; die round_index 1; }
+    python3 tools/round_index_probe.py --analyse gpurun_out/r5_ri/run_kernel_trace.csv | tee gpurun_out/r5_round_index.json ;;
   sync_tests)  # the multi-GPU tests of the value-sync mode (and everything beside them in those files)
     echo "=== value-sync tests"; tests r5_sync_tests tests/test_gpu_distributed.py -k "value or current or event or self_exchange or torus" ;;
   strong_proxy)  # fused 4096 / fused 512 / phase 512 (forced) / phase1 512 -> profiles/r5_strong_proxy.txt
