@@ -618,7 +618,10 @@ int upload_idx_chunk(dopt_ctx* c, const int32_t* idx, int64_t h0, int64_t nr, in
 unsigned ev_flags(const char* knob, unsigned base, bool device_default) {
   bool dev = device_default;
 #ifdef DOPT_AB
-  if (const char* v = getenv(knob)) dev = v[0] == 'd';
+  if (const char* v = getenv(knob)) {
+    if (v[0] == 'n') return base | hipEventDisableSystemFence;  // no fence at all (A/B)
+    dev = v[0] == 'd';
+  }
 #else
   (void)knob;
 #endif

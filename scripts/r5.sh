@@ -234,6 +234,15 @@ for step in "$@"; do
     timeout -s KILL 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r5_ri -o run -- python3 \
       tools/round_index_probe.py > gpurun_out/r5_round_index.log 2>&1 || { tail -n 20 gpurun_out/r5_round_index.log; die round_index 1; }
     python3 tools/round_index_probe.py --analyse gpurun_out/r5_ri/run_kernel_trace.csv | tee gpurun_out/r5_round_index.json ;;
+  pe_ab)  # the sampled profiling events' release: device scope (default) / none (hipEventDisableSystemFence) / system,
+    # the no-flag default line's shape (300 rounds, events every 30th launch) and the driver's (20, every 2nd), no
+    # secondary legs, A/B library, interleaved twice -> profiles/r5_pe_ab.txt
+    for rep in 1 2; do
+      for pe in dev nofence sys; do
+        DOPT_LIB=$AB DOPT_PROF_EV=$pe bench_step r5pe2_${pe}_300_$rep 200 --no-cpu-baseline --no-secondary --steps 300 --warmup 3
+        DOPT_LIB=$AB DOPT_PROF_EV=$pe bench_step r5pe2_${pe}_20_$rep 200 --no-cpu-baseline --no-secondary --steps 20 --warmup 5
+      done
+    done ;;
   sync_tests)  # the multi-GPU tests of the value-sync mode (and everything beside them in those files)
     echo "=== value-sync tests"; tests r5_sync_tests tests/test_gpu_distributed.py -k "value or current or event or self_exchange or torus" ;;
   strong_proxy)  # fused 4096 / fused 512 / phase 512 (forced) / phase1 512 -> profiles/r5_strong_proxy.txt
