@@ -612,9 +612,9 @@ int upload_idx_chunk(dopt_ctx* c, const int32_t* idx, int64_t h0, int64_t nr, in
 
 // Event flags: a device-scope release instead of the system-scope fence (whose L2 writeback and
 // invalidate the following kernels pay) where only this device reads what the event orders.  A/B builds:
-// DOPT_SIDE_EV / DOPT_PROF_EV = dev / sys override the default (round 5, profiles/r5_sync_ab.txt: the
-// sampled profiling events at device scope took the driver-shaped C3 line from 1.2735 / 1.2760 to
-// 1.2707 / 1.2731 ms per round, interleaved; the side stream's hand-off event showed no difference).
+// DOPT_SIDE_EV / DOPT_PROF_EV = dev / sys / nofence override the default (round 5, profiles/r5_sync_ab.txt,
+// r5_pe_ab.txt: for the sampled profiling events and the side stream's hand-off alike the scope is within
+// the run-to-run noise; device scope is kept as the one the consumers need).
 unsigned ev_flags(const char* knob, unsigned base, bool device_default) {
   bool dev = device_default;
 #ifdef DOPT_AB
