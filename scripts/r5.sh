@@ -253,6 +253,39 @@ for step in "$@"; do
       --workers 512 --steps 100 --warmup 5
     bench_step r5sp_phase1_512 200 --no-cpu-baseline --no-secondary --scaling weak --phase --workers 512 --steps 100 \
       --warmup 5 ;;
+  strong_long)  # the same four legs in the steady state: ~0.4-0.6 s of rounds each after a ~60 ms warmup,
+    # so the 512-worker legs are not timed inside the post-setup transient (section 5) that a 100-round
+    # 512-worker leg (18 ms) sits in entirely; interleaved twice -> profiles/r5_strong_long.txt
+    for rep in 1 2; do
+      bench_step r5sl_fused_4096_$rep 200 --no-cpu-baseline --no-secondary --scaling weak --workers 4096 \
+        --steps 400 --warmup 50
+      bench_step r5sl_fused_512_$rep 200 --no-cpu-baseline --no-secondary --scaling weak --workers 512 \
+        --steps 3000 --warmup 400
+      DOPT_FORCE_COLLECTIVES=1 bench_step r5sl_phase_512_$rep 200 --no-cpu-baseline --no-secondary --scaling weak \
+        --phase --workers 512 --steps 3000 --warmup 400
+      bench_step r5sl_phase1_512_$rep 200 --no-cpu-baseline --no-secondary --scaling weak --phase --workers 512 \
+        --steps 3000 --warmup 400
+    done ;;
+  handoff_long)  # the hand-off forms of section 6 again in the steady state (512 workers, RCCL world 1 forced,
+    # 3000 rounds after 400): events + side stream (default), one stream (DOPT_LAGGED_SIDE=0), the all-to-all on
+    # the engine's stream (DOPT_A2A_STREAM=current), stream memory operations (DOPT_LAGGED_SYNC=value);
+    # interleaved twice, then a kernel trace of the default -> profiles/r5_handoff_long.txt
+    for rep in 1 2; do
+      for arm in event side0 current value; do
+        case $arm in
+          event) envs="" ;; side0) envs="DOPT_LAGGED_SIDE=0" ;; current) envs="DOPT_A2A_STREAM=current" ;;
+          value) envs="DOPT_LAGGED_SYNC=value" ;;
+        esac
+        ( if [ -n "$envs" ]; then export "$envs"; fi
+          DOPT_FORCE_COLLECTIVES=1 bench_step r5hl_${arm}_$rep 200 --no-cpu-baseline --no-secondary --scaling weak \
+            --phase --workers 512 --steps 3000 --warmup 400 ) || exit 1
+      done
+    done
+    echo "=== trace, default, steady state"
+    DOPT_FORCE_COLLECTIVES=1 timeout -s KILL 150 rocprofv3 --kernel-trace --output-format csv \
+      -d gpurun_out/r5_hl_trace -o run -- python3 bench.py --no-cpu-baseline --no-secondary --scaling weak --phase \
+      --workers 512 --steps 1500 --warmup 400 > gpurun_out/r5_hl_trace.log 2>&1 || die handoff_long 1
+    python3 tools/trace_rounds.py gpurun_out/r5_hl_trace/run_kernel_trace.csv ;;
   *) echo "unknown step $step"; exit 2 ;;
   esac
 done
