@@ -19,9 +19,10 @@ with the reference's legacy RNG stream ('dropin').
 Multi-GPU: `python3 bench.py --gpus N` starts N ranks itself (torch.distributed.run as a
 child process, before anything touches the GPU); under an external torch.distributed.run
 WORLD_SIZE must equal --gpus.  Weak scaling (`value`): ONE random 4-regular graph over
-4096 x N workers, graph-partitioned so each rank owns a contiguous slice; halo rows of the
-iterates move by grouped send/recv (RCCL) while the gradient kernel runs, and the average
-model is all-reduced every round (distributed.py).  Strong scaling (`strong`, N > 1): the
+4096 x N workers, graph-partitioned so each rank owns a contiguous slice; the halo rows of the
+iterates and every rank's column sums (for xbar) move in ONE all-to-all per round (RCCL), issued
+beside the gradient kernel (distributed.py's lagged schedule; C5's complete graph all-reduces the
+column sums instead).  Strong scaling (`strong`, N > 1): the
 metric's literal N = 4096 workers in total over the N ranks, same graph construction.
 
 Prints ONE JSON line on rank 0 (driver contract), with `roofline` for the fused

@@ -245,6 +245,22 @@ for step in "$@"; do
     done ;;
   sync_tests)  # the multi-GPU tests of the value-sync mode (and everything beside them in those files)
     echo "=== value-sync tests"; tests r5_sync_tests tests/test_gpu_distributed.py -k "value or current or event or self_exchange or torus" ;;
+  rank_proxy)  # rank 0 of the 8-rank SCALE run on one GPU (tools/rank_proxy.py: its real plan, boundary share and
+    # send set, the exchange through RCCL to itself) beside the fused 4096-worker round, weak (4096 per rank) and
+    # strong (512 per rank) legs, steady state, interleaved twice -> profiles/r5_rank_proxy.txt
+    for s in weak strong; do
+      st=400; wu=50
+      [ $s = strong ] && { st=3000; wu=400; }
+      echo "=== rank proxy, $s leg, rank 0 of 8"
+      timeout -k 10 400 python3 tools/rank_proxy.py --world 8 --rank 0 --scaling $s --reps 2 --steps $st --warmup $wu \
+        > gpurun_out/r5_rp_$s.json 2> gpurun_out/r5_rp_$s.err || { tail -n 20 gpurun_out/r5_rp_$s.err; die rank_proxy 1; }
+      python3 -c "import json; d=json.load(open('gpurun_out/r5_rp_$s.json')); print('plan', d['plan']); [print(g['leg'], g['workers'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]; print('proxy / fused', [round(x, 4) for x in d['proxy_over_fused']])"
+    done ;;
+  rank_proxy_trace)  # kernel trace of the weak-leg rank proxy (rank 0 of 8, 200 rounds) -> profiles/r5_rank_proxy.txt
+    timeout -s KILL 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5_rpt -o run -- \
+      python3 tools/rank_proxy.py --world 8 --rank 0 --scaling weak --legs proxy --reps 1 --steps 200 --warmup 20 \
+      > gpurun_out/r5_rpt.log 2>&1 || { tail -n 20 gpurun_out/r5_rpt.log; die rank_proxy_trace 1; }
+    python3 tools/trace_rounds.py gpurun_out/r5_rpt/run_kernel_trace.csv ;;
   strong_proxy)  # fused 4096 / fused 512 / phase 512 (forced) / phase1 512 -> profiles/r5_strong_proxy.txt
     for w in 4096 512; do
       bench_step r5sp_fused_$w 200 --no-cpu-baseline --no-secondary --scaling weak --workers $w --steps 100 --warmup 5
