@@ -97,6 +97,7 @@ _SIGS = {
     "dopt_rs_phase_cols": ([_P, _I64, _D, _D, _P], ctypes.c_int),
     "dopt_rs_phase_metrics": ([_P, ctypes.c_uint32], ctypes.c_int),
     "dopt_rs_phase_pass": ([_P, ctypes.c_int32, ctypes.c_int32, _P, _P], ctypes.c_int),
+    "dopt_rs_phase_cols_range": ([_P, _I64, _D, _D, _P, _I64, _I64, ctypes.c_int32], ctypes.c_int),
     "dopt_rs_phase_rows": ([_P, _I64, _D, _D, ctypes.c_uint32], ctypes.c_int),
     "dopt_zero_models": ([_P], ctypes.c_int),
     "dopt_sync": ([_P], ctypes.c_int),
@@ -111,7 +112,7 @@ _SIGS = {
     "dopt_host_digest": ([_I32, _P, _P, _I32, _P], ctypes.c_int),
 }
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 5  # DOPT_ABI_VERSION of include/dopt.h
+ABI_VERSION = 6  # DOPT_ABI_VERSION of include/dopt.h
 
 
 def lib():
@@ -535,6 +536,12 @@ class Engine:
 
     def rs_phase_cols(self, t, eta0, lam_grad, sum_ptr):
         check(lib().dopt_rs_phase_cols(self._h, int(t), float(eta0), float(lam_grad), ctypes.c_void_p(sum_ptr)))
+
+    def rs_phase_cols_range(self, t, eta0, lam_grad, sum_ptr, c0, c1, last):
+        """The average / Z update of round t for the columns [c0, c1) of one pass chunk (last=True on
+        the round's last chunk: the update is complete)."""
+        check(lib().dopt_rs_phase_cols_range(self._h, int(t), float(eta0), float(lam_grad), ctypes.c_void_p(sum_ptr),
+                                             int(c0), int(c1), 1 if last else 0))
 
     def rs_phase_pass(self, chunk, n_chunks, sum_ptr):
         """The row-space pass over column chunk `chunk` of `n_chunks`; returns the column range

@@ -183,7 +183,7 @@ void rs_block_cols(const RsArgs& a, int xdtype, int b0, int b1, int64_t* c0, int
 // 4 initial state (z = v = u, beta = 0), 8 u = 0 without reading upart (zero start)
 hipError_t launch_rs_rows(int dtype, const RsArgs& a, int n_workers, int mode, hipStream_t s);
 int rs_col_blocks(int64_t ld);  // blocks of k_rs_cols / k_rs_init (= RsArgs.nd)
-hipError_t launch_rs_cols(int dtype, const RsArgs& a, hipStream_t s);
+hipError_t launch_rs_cols(int dtype, const RsArgs& a, hipStream_t s, int64_t c0 = 0, int64_t c1 = -1);
 // out[c0:c1) = sum_g cpart[g][c0:c1) (this rank's column sums of those columns).
 hipError_t launch_rs_csum(const RsArgs& a, double* out, hipStream_t s, int64_t c0 = 0, int64_t c1 = -1);
 // History row (cons, loss, ||xbar||^2) of the row-space rounds from the slabs and partials.

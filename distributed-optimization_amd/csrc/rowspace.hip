@@ -414,13 +414,15 @@ __global__ __launch_bounds__(NT) void k_rs_rows(const RsArgs a, int mode) {
 // k_rs_cols: C = sum_g cpart[g] (fixed order; or the all-reduced sums a.csum), then
 // xbar' = (a1 + q) xbar - (eta / N) C, Z' = a1 xbar + q Z, the T copy of xbar' for the next
 // pass and the metrics, and per-block partials of ||D'||^2, D' = Z' - xbar' (+ q c xbar0 for
-// unequal starts).
+// unequal starts).  Columns [e0, e1) (e0 a multiple of NT: block b of the launch is block
+// e0 / NT + b of the whole vector), so a column-chunked round updates each chunk as soon as its
+// all-reduced sums arrive (distributed.py, dopt_rs_phase_cols_range).
 template <typename T>
-__global__ __launch_bounds__(NT) void k_rs_cols(const RsArgs a) {
+__global__ __launch_bounds__(NT) void k_rs_cols(const RsArgs a, int64_t e0, int64_t e1) {
   __shared__ double red[2 * NW];
-  const int64_t e = (int64_t)blockIdx.x * NT + threadIdx.x;
+  const int64_t e = e0 + (int64_t)blockIdx.x * NT + threadIdx.x;
   double dd = 0.0, xx = 0.0;
-  if (e < a.ld) {
+  if (e < e1) {
     double C;
     if (a.csum) {
       C = a.csum[e];
@@ -447,8 +449,9 @@ __global__ __launch_bounds__(NT) void k_rs_cols(const RsArgs a) {
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    a.dpart[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
-    a.dpart[a.nd + blockIdx.x] = ((red[NW] + red[NW + 1]) + red[NW + 2]) + red[NW + 3];  // ||xbar'||^2 (as T)
+    const int64_t b = e0 / NT + blockIdx.x;
+    a.dpart[b] = ((red[0] + red[1]) + red[2]) + red[3];
+    a.dpart[a.nd + b] = ((red[NW] + red[NW + 1]) + red[NW + 2]) + red[NW + 3];  // ||xbar'||^2 (as T)
   }
 }
 
@@ -914,10 +917,13 @@ hipError_t launch_rs_rows(int dtype, const RsArgs& a, int n_workers, int mode, h
 
 int rs_col_blocks(int64_t ld) { return (int)((ld + NT - 1) / NT); }
 
-hipError_t launch_rs_cols(int dtype, const RsArgs& a, hipStream_t s) {
-  const dim3 grid(rs_col_blocks(a.ld));
-  if (dtype == 0) hipLaunchKernelGGL((k_rs_cols<float>), grid, dim3(NT), 0, s, a);
-  else hipLaunchKernelGGL((k_rs_cols<double>), grid, dim3(NT), 0, s, a);
+hipError_t launch_rs_cols(int dtype, const RsArgs& a, hipStream_t s, int64_t c0, int64_t c1) {
+  if (c1 < 0) c1 = a.ld;
+  if (c0 < 0 || c1 > a.ld || c0 % NT != 0 || (c1 != a.ld && c1 % NT != 0)) return hipErrorInvalidValue;
+  if (c1 <= c0) return hipSuccess;
+  const dim3 grid(rs_col_blocks(c1 - c0));
+  if (dtype == 0) hipLaunchKernelGGL((k_rs_cols<float>), grid, dim3(NT), 0, s, a, c0, c1);
+  else hipLaunchKernelGGL((k_rs_cols<double>), grid, dim3(NT), 0, s, a, c0, c1);
   return hipGetLastError();
 }
 

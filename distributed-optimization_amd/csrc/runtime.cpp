@@ -58,6 +58,7 @@ int fail(int code, const char* fmt, ...) {
     if (e_ != hipSuccess) return fail(DOPT_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
 
+constexpr int64_t kRsColsBlock = 256;  // columns per k_rs_cols workgroup (kcommon.h NT)
 constexpr int64_t kTileRowChunks = 64;  // 16-byte data chunks of a row per tile (kcommon.h kTileChunks)
 
 // Launch-shape tuning knobs: read from the environment only in A/B builds (make AB=1); the
@@ -242,6 +243,9 @@ struct dopt_ctx {
   bool rs_live = false;
   bool rs_xs_valid = false;
   bool rs_gram_ok = false;
+  // a column-chunked average update in progress (dopt_rs_phase_cols_range): chunks already updated
+  // hold the next average in xbar[xb ^ 1], which the passes of those chunks read
+  bool rs_sweep = false;
   // unequal starting iterates: x_i = rs_c x_i(0) + Z + X_i^T beta_i, x(0) kept in rs_x0buf and
   // its mean / deviations / row dots in rs_x0d (rs_x0 false: starts that were all equal, rs_c = 0)
   bool rs_x0 = false;
@@ -956,10 +960,17 @@ int rs_sync(dopt_ctx* c) {
   return DOPT_OK;
 }
 
+static int rs_sweep_closed(dopt_ctx* c) {
+  return c->rs_sweep ? fail(DOPT_ERR_STATE, "a column-chunked average update is open: finish it "
+                                            "(dopt_rs_phase_cols_range with last = 1)")
+                     : DOPT_OK;
+}
+
 // Leave row-space mode: xs[cur] holds the iterates, xbar[xb] their average.  An owed metrics
 // entry of a row-space chain is dropped (the direct rounds carry other state).
 int rs_end(dopt_ctx* c) {
   int rc;
+  if ((rc = rs_sweep_closed(c))) return rc;
   if ((rc = rs_sync(c))) return rc;
   if (c->rs_live) c->carry_pending = false;
   c->rs_live = false;
@@ -2304,6 +2315,7 @@ int dopt_rs_phase_begin(dopt_ctx* c, int commit, int* ok, uint64_t* hash) {
   int rc;
   if ((rc = set_device(c))) return rc;
   if (c->rs_live) {  // (an open chain -- dopt_phase_chain -- stays open)
+    if (int rc = rs_sweep_closed(c)) return rc;
     // the replicated part of the state (Z, then the float64 average), bitwise equal on every
     // rank that took the same all-reduced sums
     std::vector<double> zx(2 * (size_t)c->ld);
@@ -2326,6 +2338,7 @@ int dopt_rs_phase_round(dopt_ctx* c, int64_t t, double eta0, double lam_grad, ui
                         double* sum_dev) {
   CHECK_ARG(c && sum_dev, "NULL argument");
   if (!c->rs_live) return fail(DOPT_ERR_STATE, "dopt_rs_phase_begin first");
+  if (int rc = rs_sweep_closed(c)) return rc;
   const int dt = c->dtype == DOPT_F32 ? 0 : 1;
   RsArgs a = rs_args(c);
   rs_round_args(c, a, t, eta0, lam_grad);
@@ -2351,7 +2364,7 @@ int dopt_rs_phase_pass(dopt_ctx* c, int32_t chunk, int32_t n_chunks, double* sum
   CHECK_ARG(n_chunks >= 1 && chunk >= 0 && chunk < n_chunks, "chunk %d of %d", chunk, n_chunks);
   const int dt = c->dtype == DOPT_F32 ? 0 : 1;
   RsArgs a = rs_args(c);
-  a.xbar = c->xbar[c->xb];
+  a.xbar = c->xbar[c->rs_sweep ? c->xb ^ 1 : c->xb];  // (an open chunked update: its chunks come first)
   const int nb = std::min<int>(n_chunks, a.nblk);  // more chunks than blocks: the extra ones are empty
   const int b0 = chunk < nb ? (int)((int64_t)a.nblk * chunk / nb) : a.nblk;
   const int b1 = chunk < nb ? (int)((int64_t)a.nblk * (chunk + 1) / nb) : a.nblk;
@@ -2371,6 +2384,7 @@ int dopt_rs_phase_pass(dopt_ctx* c, int32_t chunk, int32_t n_chunks, double* sum
 int dopt_rs_phase_rows(dopt_ctx* c, int64_t t, double eta0, double lam_grad, uint32_t metric_flags) {
   CHECK_ARG(c, "ctx is NULL");
   if (!c->rs_live) return fail(DOPT_ERR_STATE, "dopt_rs_phase_begin first");
+  if (int rc = rs_sweep_closed(c)) return rc;
   const int dt = c->dtype == DOPT_F32 ? 0 : 1;
   RsArgs a = rs_args(c);
   rs_round_args(c, a, t, eta0, lam_grad);
@@ -2386,6 +2400,7 @@ int dopt_rs_phase_rows(dopt_ctx* c, int64_t t, double eta0, double lam_grad, uin
 int dopt_rs_phase_cols(dopt_ctx* c, int64_t t, double eta0, double lam_grad, const double* sum_dev) {
   CHECK_ARG(c && sum_dev, "NULL argument");
   if (!c->rs_live) return fail(DOPT_ERR_STATE, "dopt_rs_phase_begin first");
+  if (int rc = rs_sweep_closed(c)) return rc;
   const int dt = c->dtype == DOPT_F32 ? 0 : 1;
   RsArgs a = rs_args(c);
   rs_round_args(c, a, t, eta0, lam_grad);
@@ -2396,9 +2411,32 @@ int dopt_rs_phase_cols(dopt_ctx* c, int64_t t, double eta0, double lam_grad, con
   return DOPT_OK;
 }
 
+// The same update for columns [c0, c1) only (a chunk of dopt_rs_phase_pass), so that the next
+// round's pass over that chunk can start while the sums of later chunks are still being reduced;
+// the chunks of one update in any order, the last one with last = 1.
+int dopt_rs_phase_cols_range(dopt_ctx* c, int64_t t, double eta0, double lam_grad, const double* sum_dev,
+                             int64_t c0, int64_t c1, int32_t last) {
+  CHECK_ARG(c && sum_dev, "NULL argument");
+  if (!c->rs_live) return fail(DOPT_ERR_STATE, "dopt_rs_phase_begin first");
+  const int dt = c->dtype == DOPT_F32 ? 0 : 1;
+  RsArgs a = rs_args(c);
+  CHECK_ARG(c0 >= 0 && c0 <= c1 && c1 <= a.ld &&
+                (c0 == c1 || (c0 % kRsColsBlock == 0 && (c1 == a.ld || c1 % kRsColsBlock == 0))),
+            "column range [%lld, %lld) of %lld: a dopt_rs_phase_pass chunk", (long long)c0, (long long)c1,
+            (long long)a.ld);
+  rs_round_args(c, a, t, eta0, lam_grad);
+  a.csum = sum_dev;
+  a.xbar_out = c->xbar[c->xb ^ 1];
+  if (c1 > c0) HIPOK(launch_rs_cols(dt, a, c->stream, c0, c1));
+  c->rs_sweep = last == 0;
+  if (last) c->xb ^= 1;
+  return DOPT_OK;
+}
+
 int dopt_rs_phase_metrics(dopt_ctx* c, uint32_t metric_flags) {
   CHECK_ARG(c, "ctx is NULL");
   if (!c->rs_live) return fail(DOPT_ERR_STATE, "dopt_rs_phase_begin first");
+  if (int rc = rs_sweep_closed(c)) return rc;
   const int dt = c->dtype == DOPT_F32 ? 0 : 1;
   RsArgs a = rs_args(c);
   a.xbar = c->xbar[c->xb];

@@ -437,6 +437,26 @@ class HaloExchange:
             _wait(w, what, self.rank)
 
 
+_STREAMS = {}
+
+
+def _stream(dev, role):
+    """The process's stream `role` (0: the engine's rounds, 1: the lagged schedule's side stream) on device
+    `dev`, created once and shared by every runner of the process (bench.py's strong leg builds a second
+    DistributedDSGD after the weak leg's; a fresh pair of pool streams for it measured slower on the box,
+    tools/rank_proxy.py --reps 2).  Runners of one process are used one at a time; if two were used at
+    once, sharing a stream would order their work, not corrupt it."""
+    import torch
+
+    key = (int(dev.index if dev.index is not None else torch.cuda.current_device()), role)
+    if os.environ.get("DOPT_FRESH_STREAMS") == "1":  # (A/B: a new pair per runner, the round-4 behaviour)
+        return torch.cuda.Stream(dev)
+    st = _STREAMS.get(key)
+    if st is None:
+        st = _STREAMS[key] = torch.cuda.Stream(dev)
+    return st
+
+
 class DistributedDSGD:
     """Drives one rank's engine through the round phases with torch.distributed."""
 
@@ -457,7 +477,7 @@ class DistributedDSGD:
         self.n_global, self.rows_global = int(n_global), int(rows_global)
         self.dev = torch.device("cuda", device)
         self.device_comm = dist.get_backend(group) == "nccl"
-        self.stream = torch.cuda.Stream(self.dev)
+        self.stream = _stream(self.dev, 0)
         ld, esz = engine.layout()
         self.ld = ld
         tdt = torch.float32 if esz == 4 else torch.float64
@@ -506,7 +526,7 @@ class DistributedDSGD:
         self._stream_switch = None
         if (self._lagged_ok and not self._solo() and self.exchange.peers_or_collective()
                 and os.environ.get("DOPT_LAGGED_SIDE", "1") != "0"):
-            self.side = torch.cuda.Stream(self.dev)
+            self.side = _stream(self.dev, 1)
         engine.lagged_side_stream(self.side.cuda_stream if self.side is not None else None)
         # the communicator is created by one small collective here, not inside the first round
         # (the halo all-to-all and the all-reduces of the rounds then find it ready)
@@ -693,22 +713,30 @@ class DistributedDSGD:
                 eng.phase_fold(base if consensus else None, base + 16 if objective and xnorm else None,
                                base + 8 if objective else None, 0)
 
+            # K column chunks, pipelined across rounds: chunk k's sums are all-reduced while the later chunks
+            # stream, and round h's average update of chunk k (which needs those sums) runs just before
+            # round h + 1's pass over chunk k -- so the all-reduce of the last chunk is hidden behind the
+            # next round's first chunks instead of sitting between two passes (K = 1: the serial order
+            # pass, rows, all-reduce, cols).  Every column's arithmetic is the same in either order.
             K = self.rs_chunks
+            sp = self.sum.data_ptr()
+            pend = None  # (round, [(c0, c1, work)] per chunk) whose average update is still to run
             for h in range(T):
                 met = mf and (h > 0 or owed)
-                works = []
-                for k in range(K):  # the sums of column chunk k are all-reduced while chunk k + 1 streams
-                    c0, c1 = eng.rs_phase_pass(k, K, self.sum.data_ptr())
-                    if c1 > c0:
-                        works.append(self._all_reduce_start(self.sum[c0:c1]))
+                cur = []
+                for k in range(K):
+                    if pend is not None:
+                        self._rs_cols_chunk(pend, k, eta0, lam_grad, sp)
+                    c0, c1 = eng.rs_phase_pass(k, K, sp)
+                    cur.append((c0, c1, self._all_reduce_start(self.sum[c0:c1]) if c1 > c0 else None))
+                pend = (t0 + h, cur)
                 eng.rs_phase_rows(t0 + h, eta0, lam_grad, mf if met else 0)
                 if met:
                     fold(e)
                     e += 1
-                for w in works:
-                    if w is not None:
-                        _wait(w, f"all_reduce of a column chunk of the {self.ld} column sums", self.plan.rank)
-                eng.rs_phase_cols(t0 + h, eta0, lam_grad, self.sum.data_ptr())
+            if pend is not None:
+                for k in range(K):
+                    self._rs_cols_chunk(pend, k, eta0, lam_grad, sp)
             if mf and not leave:
                 eng.rs_phase_metrics(mf)
                 fold(e)
@@ -722,6 +750,14 @@ class DistributedDSGD:
             self._rs_flags = mf
         obj, cons = _dopt.finalize_metrics(self.eng.problem, raw, self.n_global, self.rows_global, lam_obj, f_opt)
         return (obj if objective else None), (cons if consensus else None)
+
+    def _rs_cols_chunk(self, pend, k, eta0, lam_grad, sum_ptr):
+        """Round pend[0]'s average / Z update of pass chunk k, once that chunk's all-reduce is done."""
+        t, chunks = pend
+        c0, c1, w = chunks[k]
+        if w is not None:
+            _wait(w, f"all_reduce of column chunk [{c0}, {c1}) of the {self.ld} column sums", self.plan.rank)
+        self.eng.rs_phase_cols_range(t, eta0, lam_grad, sum_ptr, c0, c1, k == len(chunks) - 1)
 
     def run_pipelined(self, T, eta0, batch, lam_grad, lam_obj, f_opt=0.0, t0=0, objective=True, consensus=True,
                       idx=None):
@@ -863,7 +899,7 @@ class DistributedCentralized:
         self.n_global, self.rows_global, self.obj_sep = int(n_global), int(rows_global), obj_sep
         self.dev = torch.device("cuda", device)
         self.device_comm = dist.get_backend(group) == "nccl"
-        self.stream = torch.cuda.Stream(self.dev)
+        self.stream = _stream(self.dev, 0)
         ld, _ = engine.layout()
         self.sum = torch.zeros(ld, dtype=torch.float64, device=self.dev)
         engine.set_partition(self.n_global, self.rows_global)

@@ -46,8 +46,10 @@ extern "C" {
  *   4  round 4: dopt_lagged_side_stream (k_mixcs_final and the exchange on a second stream).
  *   5  round 5: dopt_host_digest (threaded content digest of host arrays, the drop-in trainers'
  *      engine cache key), dopt_phase_interior_count; dopt_lagged_exchange_layout accepts a self
- *      block (a rank's own column sums routed through the exchange). */
-#define DOPT_ABI_VERSION 5
+ *      block (a rank's own column sums routed through the exchange).
+ *   6  round 5: dopt_rs_phase_cols_range (the complete graph's average update per column chunk, so
+ *      the next round's pass over a chunk starts while later chunks' sums are still being reduced). */
+#define DOPT_ABI_VERSION 6
 
 typedef struct dopt_ctx dopt_ctx;
 
@@ -364,6 +366,14 @@ int dopt_rs_phase_cols(dopt_ctx *ctx, int64_t t, double eta0, double lam_grad, c
  *   metric partials of the current iterates; then dopt_rs_phase_cols with the reduced sums. */
 int dopt_rs_phase_pass(dopt_ctx *ctx, int32_t chunk, int32_t n_chunks, double *sum_dev, int64_t *col_range);
 int dopt_rs_phase_rows(dopt_ctx *ctx, int64_t t, double eta0, double lam_grad, uint32_t metric_flags);
+/* dopt_rs_phase_cols_range: dopt_rs_phase_cols for the columns [c0, c1) of one dopt_rs_phase_pass chunk
+ *   (sum_dev[c0:c1) reduced), so round t + 1's pass over that chunk may run before the later chunks'
+ *   sums arrive: until the call with last = 1 the update is open, dopt_rs_phase_pass reads the updated
+ *   chunks' new average, and every other dopt_rs_phase_* call (and leaving row-space mode) fails with
+ *   DOPT_ERR_STATE.  Each chunk once per round, in any order; the round's metrics (dopt_rs_phase_rows)
+ *   after the last. */
+int dopt_rs_phase_cols_range(dopt_ctx *ctx, int64_t t, double eta0, double lam_grad, const double *sum_dev,
+                             int64_t c0, int64_t c1, int32_t last);
 int dopt_rs_phase_metrics(dopt_ctx *ctx, uint32_t metric_flags);
 /* The lagged schedule (round 4, ABI version 3; distributed.py DistributedDSGD._run_lagged): one
  * collective per round -- the halo rows of x_g AND every rank's column sums of x_g in one exchange

@@ -254,8 +254,36 @@ for step in "$@"; do
       echo "=== rank proxy, $s leg, rank 0 of 8"
       timeout -k 10 400 python3 tools/rank_proxy.py --world 8 --rank 0 --scaling $s --reps 2 --steps $st --warmup $wu \
         > gpurun_out/r5_rp_$s.json 2> gpurun_out/r5_rp_$s.err || { tail -n 20 gpurun_out/r5_rp_$s.err; die rank_proxy 1; }
-      python3 -c "import json; d=json.load(open('gpurun_out/r5_rp_$s.json')); print('plan', d['plan']); [print(g['leg'], g['workers'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]; print('proxy / fused', [round(x, 4) for x in d['proxy_over_fused']])"
+      python3 -c "import json; d=json.loads(open('gpurun_out/r5_rp_$s.json').read().strip().splitlines()[-1]); print('plan', d['plan']); [print(g['leg'], g['workers'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]; print('proxy / fused', [round(x, 4) for x in d['proxy_over_fused']])"
     done ;;
+  proxy_ab)  # what the weak-leg rank pays over the fused round: arms of tools/rank_proxy.py (weak, rank 0 of 8), one
+    # process each: default / one stream / RCCL at 8 channels / two runners (the second after the first's legs) with
+    # the box's 4 HW queues per process and with 8 (ARMS overrides the list)
+    for arm in ${ARMS:-default side0 nch8 reps2 hwq8}; do
+      envs=""; extra=""
+      case $arm in
+        side0) envs="DOPT_LAGGED_SIDE=0" ;;
+        nch8) envs="NCCL_MAX_NCHANNELS=8" ;;
+        hwq8) envs="GPU_MAX_HW_QUEUES=8"; extra="--reps 2" ;;
+        reps2) extra="--reps 2" ;;
+        pfirst) extra="--reps 2 --legs proxy,fused" ;;
+        palone) extra="--legs proxy" ;;
+        pfresh) envs="DOPT_FRESH_STREAMS=1"; extra="--reps 2 --legs proxy,fused" ;;
+        nch2) envs="NCCL_MAX_NCHANNELS=2" ;;
+        simple) envs="NCCL_PROTO=Simple" ;;
+      esac
+      echo "=== $arm ($envs $extra)"
+      env $envs timeout -k 10 300 python3 tools/rank_proxy.py --world 8 --rank 0 --scaling weak --reps 1 --steps 300 \
+        --warmup 50 $extra > gpurun_out/r5_pab_$arm.json 2> gpurun_out/r5_pab_$arm.err \
+        || { tail -n 20 gpurun_out/r5_pab_$arm.err; die proxy_ab 1; }
+      grep '^{"leg"' gpurun_out/r5_pab_$arm.err | python3 -c "import json,sys; [print(d['leg'], d['rep'], round(d['value']), round(d['ms_per_round'], 4), round(d['kernel_avg_ms'], 4)) for d in map(json.loads, sys.stdin)]"
+    done ;;
+  proxy_legs_trace)  # kernel trace of two proxy legs in one process (the second runner is slower: why?)
+    timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r5_plt -o run -- \
+      python3 tools/rank_proxy.py --world 8 --rank 0 --scaling weak --legs fused,proxy --reps 2 --steps 200 --warmup 20 \
+      > gpurun_out/r5_plt.log 2>&1 || { tail -n 20 gpurun_out/r5_plt.log; die proxy_legs_trace 1; }
+    grep '^{"leg"' gpurun_out/r5_plt.log || true
+    python3 tools/trace_legs.py gpurun_out/r5_plt/run_kernel_trace.csv ;;
   rank_proxy_trace)  # kernel trace of the weak-leg rank proxy (rank 0 of 8, 200 rounds) -> profiles/r5_rank_proxy.txt
     timeout -s KILL 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5_rpt -o run -- \
       python3 tools/rank_proxy.py --world 8 --rank 0 --scaling weak --legs proxy --reps 1 --steps 200 --warmup 20 \

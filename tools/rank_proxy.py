@@ -94,6 +94,8 @@ def main():
     ap.add_argument("--fused-workers", type=int, default=4096, help="the fused leg's workers (the N = 1 line)")
     ap.add_argument("--legs", default="fused,proxy", help="legs per repetition, in order")
     ap.add_argument("--plan-only", action="store_true")
+    ap.add_argument("--no-force", action="store_true",
+                    help="no collectives at world 1 (the halo slots are never filled): the kernels alone")
     args = ap.parse_args()
 
     n_global = args.workers * args.world if args.scaling == "weak" else args.workers
@@ -106,7 +108,7 @@ def main():
         print(json.dumps(out), flush=True)
         return 0
 
-    os.environ["DOPT_FORCE_COLLECTIVES"] = "1"
+    os.environ["DOPT_FORCE_COLLECTIVES"] = "0" if args.no_force else "1"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     import torch
     import torch.distributed as dist
@@ -143,7 +145,7 @@ def main():
         try:
             eng.generate_shards("logistic", n, d, m, seed=1000, flip=0.05, first_worker=plan.lo)
             run = Dm.DistributedDSGD(eng, sp, n_global, n_global * m, device=0)
-            if not run._lagged_ok or run.layout.ks == 0 or not run.exchange.collective:
+            if not run._lagged_ok or (not args.no_force and (run.layout.ks == 0 or not run.exchange.collective)):
                 raise SystemExit("the proxy did not take the lagged schedule with the RCCL exchange")
             info = {"workers": n, "interior_engine": eng.phase_interior_count(), "side_stream": run.side is not None,
                     "exchange_rows_out": run.layout.n_send_rows, "exchange_rows_in": run.layout.n_recv_rows}
