@@ -188,6 +188,8 @@ hipError_t launch_rs_cols(int dtype, const RsArgs& a, hipStream_t s, int64_t c0 
 hipError_t launch_rs_csum(const RsArgs& a, double* out, hipStream_t s, int64_t c0 = 0, int64_t c1 = -1);
 // History row (cons, loss, ||xbar||^2) of the row-space rounds from the slabs and partials.
 hipError_t launch_rs_hist(const RsArgs& a, int n_workers, double* out, hipStream_t s);
+hipError_t launch_rs_fold(const RsArgs& a, const double* sc, int64_t nc, const double* sl, int64_t nl, double* out_c,
+                          double* out_l, double* out_q, hipStream_t s);
 hipError_t launch_rs_init(int dtype, const RsArgs& a, const void* x0, hipStream_t s);
 hipError_t launch_rs_check(int dtype, const void* x, int64_t n, int64_t ld, int32_t nch, int G, int32_t* flags,
                            int32_t* zflag, hipStream_t s);

@@ -517,6 +517,43 @@ __global__ __launch_bounds__(NT) void k_rs_hist(const RsArgs a, int n, double* o
     for (int k = 0; k < 3; ++k) out[k] = ((red[k][0] + red[k][1]) + red[k][2]) + red[k][3];
 }
 
+// The history fold of a rank's row-space rounds (dopt_phase_fold while row-space mode is live): k_rs_hist
+// with each output optional, the consensus and loss slabs given -- a rank contributes ||xbar||^2 to the
+// all-reduced history row only once across the ranks.  The norm is the sum of k_rs_cols' / k_rs_init's
+// per-block partials, not a one-workgroup pass over the d-vector (launch_fold: 155 us per round at
+// d = 2^20, profiles/r5_rs_chunks.txt).
+__global__ __launch_bounds__(NT) void k_rs_fold(const RsArgs a, const double* sc, int64_t nc, const double* sl,
+                                                int64_t nl, double* out_c, double* out_l, double* out_q) {
+  __shared__ double red[3][NW];
+  auto sum4 = [&](const double* v, int64_t cnt) {
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int64_t k = threadIdx.x;
+    for (; k + 3 * NT < cnt; k += 4 * NT) {
+      s0 += v[k];
+      s1 += v[k + NT];
+      s2 += v[k + 2 * NT];
+      s3 += v[k + 3 * NT];
+    }
+    for (; k < cnt; k += NT) s0 += v[k];
+    return wave_sum((s0 + s1) + (s2 + s3));
+  };
+  const double c = (sc && out_c) ? sum4(sc, nc) : 0.0;
+  const double l = (sl && out_l) ? sum4(sl, nl) : 0.0;
+  const double q = out_q ? sum4(a.dpart + a.nd, a.nd) : 0.0;
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = c;
+    red[1][w] = l;
+    red[2][w] = q;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double* out[3] = {out_c, out_l, out_q};
+    for (int k = 0; k < 3; ++k)
+      if (out[k]) *out[k] = ((red[k][0] + red[k][1]) + red[k][2]) + red[k][3];
+  }
+}
+
 // flags[i * G + g] = 1 when row i of x differs from row 0 on the chunks of group g; zflag[g] = 1
 // when row 0 is nonzero there.
 template <typename T>
@@ -929,6 +966,12 @@ hipError_t launch_rs_cols(int dtype, const RsArgs& a, hipStream_t s, int64_t c0,
 
 hipError_t launch_rs_hist(const RsArgs& a, int n_workers, double* out, hipStream_t s) {
   hipLaunchKernelGGL(k_rs_hist, dim3(1), dim3(NT), 0, s, a, n_workers, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_rs_fold(const RsArgs& a, const double* sc, int64_t nc, const double* sl, int64_t nl, double* out_c,
+                          double* out_l, double* out_q, hipStream_t s) {
+  hipLaunchKernelGGL(k_rs_fold, dim3(1), dim3(NT), 0, s, a, sc, nc, sl, nl, out_c, out_l, out_q);
   return hipGetLastError();
 }
 

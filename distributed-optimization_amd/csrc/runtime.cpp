@@ -2296,6 +2296,11 @@ int dopt_phase_xbar(dopt_ctx* c, const double* sum_dev) {
 int dopt_phase_fold(dopt_ctx* c, double* cons_out, double* xnorm_out, double* loss_out, int slab) {
   CHECK_ARG(c, "ctx is NULL");
   CHECK_ARG(slab == 0 || slab == 1, "slab must be 0 or 1");
+  if (c->rs_live && !c->rs_sweep) {  // row-space rounds: ||xbar||^2 from the average update's block partials
+    HIPOK(launch_rs_fold(rs_args(c), c->slab_cons, c->cons_n, slab ? c->slab_loss_b : c->slab_loss, c->slab_n[slab],
+                         cons_out, loss_out, xnorm_out, c->stream));
+    return DOPT_OK;
+  }
   HIPOK(launch_fold(c->dtype, c->slab_cons, c->cons_n, slab ? c->slab_loss_b : c->slab_loss, c->slab_n[slab],
                     c->xbar[c->xb], c->ld, (int32_t)c->nchs, cons_out, loss_out, xnorm_out, c->stream));
   return DOPT_OK;

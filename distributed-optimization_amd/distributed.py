@@ -36,28 +36,38 @@ import _dopt
 
 
 DEFAULT_TIMEOUT_S = 300.0
-# Column chunks of the complete graph's row-space pass across ranks: each chunk's
-# sums are all-reduced while the next chunk streams, but every chunk boundary costs a launch tail.
+# Column chunks of the complete graph's row-space pass across ranks, pipelined across rounds:
+# chunk k's sums are all-reduced while the later chunks stream, and round h's average update of chunk k runs
+# just before round h + 1's pass over chunk k, so only what the next round's earlier chunks cannot cover of
+# the last chunk's all-reduce stays exposed; every extra chunk costs a launch boundary and a hand-off.
 RS_CHUNKS = 1
-# The model that picks the chunk count per world size ("Column chunks across ranks"):
-# a round is pass(N) + boundary * (K - 1) + allreduce(S / K, N), where the ring all-reduce of S bytes
-# over N ranks on xGMI costs ALPHA + 2 (N - 1) / N * S / BUSBW and only the last chunk's is exposed.
+# The model that picks the chunk count per world size ("Column chunks across ranks"): exposed
+# time (K - 1) * boundary + max(0, allreduce(S / K, N) - (K - 1) / K * pass(N)), where the ring all-reduce of
+# S bytes over N ranks on xGMI costs ALPHA + 2 (N - 1) / N * S / BUSBW (assumed: no multi-GPU run here to
+# measure them on) and the pass of one rank reads 68.7 GB / N at 6.5 TB/s.
 AR_ALPHA_S = 30e-6       # per all-reduce latency (8 ranks, ring steps, launch): assumed
 AR_BUSBW = 100e9         # RCCL bus bandwidth for MB-sized messages over xGMI, bytes/s: assumed
-RS_BOUNDARY_S = 0.1e-3   # measured cost of one extra chunk boundary (C5, world 1, round 3)
+RS_BOUNDARY_S = 15e-6    # one extra chunk (boundary + hand-off), measured at one rank's shape of 8 (128 workers,
+                         # RCCL world 1 forced, K = 2 / 4 vs 1: 0-12 / 13 us per chunk; profiles/r5_rs_chunks.txt)
+RS_PASS_BYTES = 68.72e9  # C5's row bytes per round (all ranks)
+RS_PASS_BW = 6.5e12
 
 
-def rs_chunks_for(world, sum_bytes=8 << 20, max_chunks=8):
-    """Chunk count K minimising the modelled exposed time (K - 1) boundaries + the last chunk's
-    all-reduce; 1 at world 1 (nothing to overlap).  With the constants above it is 1 for every
-    world size up to 8: the boundary (0.1 ms) costs more than the all-reduce time it hides."""
+def rs_chunks_for(world, sum_bytes=8 << 20, max_chunks=8, pass_bytes=RS_PASS_BYTES):
+    """Chunk count K (a power of two: chunks of equal column blocks -- 3 chunks of C5's 2048 blocks cost
+    0.4 ms at world 1) minimising the modelled exposed time; 1 at world 1 (nothing to overlap).  With
+    the constants above it is 2 for 2-8 ranks: the half all-reduce of the last chunk hides behind the
+    next round's first chunk, for one ~15 us boundary."""
     if world <= 1:
         return 1
+    pass_s = pass_bytes / world / RS_PASS_BW
 
     def exposed(k):
-        return (k - 1) * RS_BOUNDARY_S + AR_ALPHA_S + 2.0 * (world - 1) / world * (sum_bytes / k) / AR_BUSBW
+        ar = AR_ALPHA_S + 2.0 * (world - 1) / world * (sum_bytes / k) / AR_BUSBW
+        return (k - 1) * RS_BOUNDARY_S + max(0.0, ar - (k - 1) / k * pass_s)
 
-    return min(range(1, max_chunks + 1), key=exposed)
+    ks = [k for k in (1, 2, 4, 8, 16) if k <= max_chunks]
+    return min(ks, key=exposed)
 
 
 class CollectiveError(RuntimeError):

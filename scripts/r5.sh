@@ -284,6 +284,22 @@ for step in "$@"; do
       > gpurun_out/r5_plt.log 2>&1 || { tail -n 20 gpurun_out/r5_plt.log; die proxy_legs_trace 1; }
     grep '^{"leg"' gpurun_out/r5_plt.log || true
     python3 tools/trace_legs.py gpurun_out/r5_plt/run_kernel_trace.csv ;;
+  rs_chunks)  # C5 across ranks: the column-chunked rounds pipelined across rounds (dopt_rs_phase_cols_range) -- the
+    # row-space GPU tests (incl. the RCCL world-1 bitwise test), then the price of chunking at one rank's shape of 8
+    # (128 workers) and at world 1's (1024), RCCL world 1 forced -> profiles/r5_rs_chunks.txt
+    echo "=== row-space GPU tests"; tests r5_rs_tests tests/test_gpu_rowspace.py
+    for w in 128 1024; do
+      echo "=== chunk proxy, $w workers"
+      timeout -k 10 300 python3 tools/rs_chunk_proxy.py --workers $w --chunks 1,2,3,4 --reps 2 --steps 40 --warmup 5 \
+        > gpurun_out/r5_rsc_$w.json 2> gpurun_out/r5_rsc_$w.err || { tail -n 20 gpurun_out/r5_rsc_$w.err; die rs_chunks 1; }
+      grep '^{"K"' gpurun_out/r5_rsc_$w.err
+    done ;;
+  rs_chunks_trace)  # kernel trace of the C5 rank shape (128 workers, K = 1 and 2) -> profiles/r5_rs_chunks.txt
+    timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r5_rsct -o run -- \
+      python3 tools/rs_chunk_proxy.py --workers 128 --chunks 1,2 --reps 1 --steps 40 --warmup 5 \
+      > gpurun_out/r5_rsct.log 2>&1 || { tail -n 20 gpurun_out/r5_rsct.log; die rs_chunks_trace 1; }
+    grep '^{"K"' gpurun_out/r5_rsct.log || true
+    python3 tools/trace_legs.py gpurun_out/r5_rsct/run_kernel_trace.csv 1 k_rs_rows ;;
   rank_proxy_trace)  # kernel trace of the weak-leg rank proxy (rank 0 of 8, 200 rounds) -> profiles/r5_rank_proxy.txt
     timeout -s KILL 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5_rpt -o run -- \
       python3 tools/rank_proxy.py --world 8 --rank 0 --scaling weak --legs proxy --reps 1 --steps 200 --warmup 20 \

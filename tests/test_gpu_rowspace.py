@@ -265,7 +265,7 @@ def _rs_data(x32):
     return shards
 
 
-def _rs_rank(rank, world, port, out, T, pipe=False, x32=False, chunks=None):
+def _rs_rank(rank, world, port, out, T, pipe=False, x32=False, chunks=None, backend="gloo"):
     import os
 
     import torch  # noqa: F401  (one HIP runtime, loaded before libdopt)
@@ -274,7 +274,11 @@ def _rs_rank(rank, world, port, out, T, pipe=False, x32=False, chunks=None):
     import distributed as Dm
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+        Dm.init_process_group("nccl", rank=rank, world_size=world)
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
     shards = _rs_data(x32)
     n = len(shards)
     bounds = Dm.partition_bounds(n, world)
@@ -340,6 +344,41 @@ def test_rowspace_ranks_vs_oracle(tmp_path, world, pipe, x32, chunks):
     np.testing.assert_allclose(got["obj"], h["objective"], rtol=1e-9)
     np.testing.assert_allclose(got["cons"], h["consensus_error"], rtol=1e-9)
     np.testing.assert_allclose(got["x"], xr, rtol=1e-9, atol=1e-12 * np.abs(xr).max())
+
+
+@pytest.mark.parametrize("chunks,pipe", [(2, True), (3, False), (16, True)])
+def test_rowspace_chunk_pipeline_rccl_one_rank_bitwise(tmp_path, monkeypatch, chunks, pipe):
+    """The column-chunked rounds across ranks, pipelined across rounds (round h's average update of chunk k
+    runs just before round h + 1's pass over chunk k, so a chunk's all-reduce hides behind the next round's
+    earlier chunks; dopt_rs_phase_cols_range), at RCCL world 1 with the collectives forced: history and
+    gathered iterates bitwise those of the unchunked rounds (a one-rank all-reduce is the identity, and every
+    column's arithmetic is the same in either order), as single runs and as a chain of pipelined calls;
+    16 chunks leave some empty.  Also vs the oracle at rtol 1e-9."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    monkeypatch.setenv("DOPT_FORCE_COLLECTIVES", "1")
+    got = {}
+    for K in (1, chunks):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        d = tmp_path / f"k{K}"
+        d.mkdir()
+        mp.start_processes(_rs_rank, args=(1, port, str(d), 7, pipe, True, K, "nccl"), nprocs=1, join=True,
+                           start_method="spawn")
+        got[K] = np.load(d / "rs.npz")
+    for key in ("obj", "cons", "x"):
+        np.testing.assert_array_equal(got[chunks][key], got[1][key])
+    shards = _rs_data(True)
+    n = len(shards)
+    Xf = np.vstack([s[0] for s in shards])
+    yf = np.concatenate([s[1] for s in shards])
+    h, _, xr, _ = O.run_decentralized(shards, TP.fully_connected(n).dense_W(), 7, _cfg(max(SIZES_D)), Xf, yf, 0.1)
+    np.testing.assert_allclose(got[chunks]["obj"], h["objective"], rtol=1e-9)
+    np.testing.assert_allclose(got[chunks]["x"], xr, rtol=1e-9, atol=1e-12 * np.abs(xr).max())
 
 
 def _rs_rank_minibatch(rank, world, port, out):

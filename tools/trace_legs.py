@@ -6,7 +6,9 @@ frequent k_round instance) it prints the round period, the gradient kernel's med
 kernel's median duration, count per round and median start offset from the round's gradient kernel
 start, and the GPU idle time per round.
 
-  python3 tools/trace_legs.py gpurun_out/<dir>/run_kernel_trace.csv [gap_ms]
+  python3 tools/trace_legs.py gpurun_out/<dir>/run_kernel_trace.csv [gap_ms] [round_kernel_substring]
+
+(the rounds of the row-space path: round_kernel_substring = k_rs_rows, one launch per round)
 """
 import collections
 import csv
@@ -27,8 +29,8 @@ def legs(ev, gap_ns):
     return out
 
 
-def leg_stats(ev):
-    counts = collections.Counter(n for _, _, n in ev if "k_round" in n)
+def leg_stats(ev, key="k_round"):
+    counts = collections.Counter(n for _, _, n in ev if key in n)
     if not counts:
         return None
     grad = counts.most_common(1)[0][0]
@@ -67,11 +69,11 @@ def leg_stats(ev):
             "other": {k: (len(v) / n, statistics.median(v), statistics.median(offs[k])) for k, v in other.items()}}
 
 
-def main(path, gap_ms=5.0):
+def main(path, gap_ms=5.0, key="k_round"):
     rows = list(csv.DictReader(open(path)))
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
     for i, leg in enumerate(legs(ev, gap_ms * 1e6)):
-        st = leg_stats(leg)
+        st = leg_stats(leg, key)
         if st is None or st["rounds"] < 5:
             continue
         print(f"leg {i}: {st['rounds']} steady rounds of {st['grad'][:60]}")
@@ -81,4 +83,4 @@ def main(path, gap_ms=5.0):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], float(sys.argv[2]) if len(sys.argv) > 2 else 5.0)
+    main(sys.argv[1], float(sys.argv[2]) if len(sys.argv) > 2 else 5.0, sys.argv[3] if len(sys.argv) > 3 else "k_round")
