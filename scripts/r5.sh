@@ -300,6 +300,13 @@ for step in "$@"; do
       > gpurun_out/r5_rsct.log 2>&1 || { tail -n 20 gpurun_out/r5_rsct.log; die rs_chunks_trace 1; }
     grep '^{"K"' gpurun_out/r5_rsct.log || true
     python3 tools/trace_legs.py gpurun_out/r5_rsct/run_kernel_trace.csv 1 k_rs_rows ;;
+  rank_proxy_c4)  # C4's rank 0 of 8 (a strip of 32 torus rows, 8192 workers, 512 boundary) beside a fused 8192-worker
+    # round (random 4-regular: the same kernel and degree) -> profiles/r5_rank_proxy.txt
+    echo "=== rank proxy, C4 rank 0 of 8"
+    timeout -k 10 400 python3 tools/rank_proxy.py --world 8 --rank 0 --config c4 --fused-workers 8192 --reps 2 \
+      --steps 100 --warmup 20 > gpurun_out/r5_rp_c4.json 2> gpurun_out/r5_rp_c4.err \
+      || { tail -n 20 gpurun_out/r5_rp_c4.err; die rank_proxy_c4 1; }
+    grep '^{"leg"' gpurun_out/r5_rp_c4.err | python3 -c "import json,sys; [print(d['leg'], d['rep'], d['workers'], round(d['value']), round(d['ms_per_round'], 4), round(d['kernel_avg_ms'], 4)) for d in map(json.loads, sys.stdin)]" ;;
   rank_proxy_trace)  # kernel trace of the weak-leg rank proxy (rank 0 of 8, 200 rounds) -> profiles/r5_rank_proxy.txt
     timeout -s KILL 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5_rpt -o run -- \
       python3 tools/rank_proxy.py --world 8 --rank 0 --scaling weak --legs proxy --reps 1 --steps 200 --warmup 20 \

@@ -35,12 +35,16 @@ sys.path.insert(0, os.path.join(ROOT, "distributed-optimization_amd"))
 import numpy as np  # noqa: E402
 
 
-def rank_plan(world, rank, n_global, degree=4):
-    """Rank `rank`'s HaloPlan of the bench's graph (bench.setup_leg: random_regular, seed 0, spectral
-    partition, relabel) and the partition's cut."""
+def rank_plan(world, rank, n_global, degree=4, config="c3"):
+    """Rank `rank`'s HaloPlan of the bench's graph and the partition's cut: C3 (bench.setup_leg: random_regular,
+    seed 0, spectral partition, relabel) or C4 (the 256 x 256 torus in contiguous strips of torus rows)."""
     import distributed as Dm
     import topology
 
+    if config == "c4":
+        top = topology.grid(n_global)
+        part = np.repeat(np.arange(world), np.diff(Dm.partition_bounds(n_global, world)))
+        return Dm.build_plan(top, world, rank), Dm.cut_edges(top, part)
     top = topology.random_regular(n_global, degree, seed=0)
     part = Dm.graph_partition(top, world)
     cut = Dm.cut_edges(top, part)
@@ -85,6 +89,8 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--config", default="c3", choices=["c3", "c4"],
+                    help="c4: the 256 x 256 torus (65536 workers in all) in strips, --workers ignored")
     ap.add_argument("--workers", type=int, default=4096, help="per rank (weak) / in all (strong)")
     ap.add_argument("--d", type=int, default=1024)
     ap.add_argument("--m", type=int, default=512)
@@ -99,10 +105,12 @@ def main():
     args = ap.parse_args()
 
     n_global = args.workers * args.world if args.scaling == "weak" else args.workers
+    if args.config == "c4":
+        n_global = 65536
     t0 = time.perf_counter()
-    plan, cut = rank_plan(args.world, args.rank, n_global)
+    plan, cut = rank_plan(args.world, args.rank, n_global, config=args.config)
     sp = self_plan(plan)
-    out = {"world": args.world, "rank": args.rank, "scaling": args.scaling, "n_global": n_global,
+    out = {"world": args.world, "rank": args.rank, "config": args.config, "scaling": args.scaling, "n_global": n_global,
            "plan_s": time.perf_counter() - t0, "plan": plan_stats(plan, sp, cut)}
     if args.plan_only:
         print(json.dumps(out), flush=True)
