@@ -270,6 +270,14 @@ for step in "$@"; do
         palone) extra="--legs proxy" ;;
         pfresh) envs="DOPT_FRESH_STREAMS=1"; extra="--reps 2 --legs proxy,fused" ;;
         nch2) envs="NCCL_MAX_NCHANNELS=2" ;;
+        palone_w400) extra="--legs proxy --warmup 400" ;;
+        palone_side0) envs="DOPT_LAGGED_SIDE=0"; extra="--legs proxy" ;;
+        palone_nch2) envs="NCCL_MAX_NCHANNELS=2"; extra="--legs proxy" ;;
+        palone_cur) envs="DOPT_A2A_STREAM=current"; extra="--legs proxy" ;;
+        palone_lo) envs="DOPT_NCCL_HIPRI=0"; extra="--legs proxy" ;;
+        palone_serial) envs="DOPT_LAGGED_SIDE=0 DOPT_A2A_STREAM=current"; extra="--legs proxy" ;;
+        fthen_serial) envs="DOPT_LAGGED_SIDE=0 DOPT_A2A_STREAM=current" ;;
+        pfirst_w400) extra="--reps 2 --legs proxy,fused --warmup 400" ;;
         simple) envs="NCCL_PROTO=Simple" ;;
       esac
       echo "=== $arm ($envs $extra)"
