@@ -315,6 +315,17 @@ for step in "$@"; do
       --steps 100 --warmup 20 > gpurun_out/r5_rp_c4.json 2> gpurun_out/r5_rp_c4.err \
       || { tail -n 20 gpurun_out/r5_rp_c4.err; die rank_proxy_c4 1; }
     grep '^{"leg"' gpurun_out/r5_rp_c4.err | python3 -c "import json,sys; [print(d['leg'], d['rep'], d['workers'], round(d['value']), round(d['ms_per_round'], 4), round(d['kernel_avg_ms'], 4)) for d in map(json.loads, sys.stdin)]" ;;
+  rs_wg_ab)  # the row-space pass's row groups at one rank's shape of C5 over 8 (128 workers: 2048 rows, one group of
+    # 2048-row workgroups by default), A/B library, K = 2 -> profiles/r5_rs_chunks.txt
+    for rep in 1 2; do
+      for wg in 1 2 4; do
+        echo "=== DOPT_RS_WG=$wg rep $rep"
+        DOPT_LIB=$AB DOPT_RS_WG=$wg timeout -k 10 300 python3 tools/rs_chunk_proxy.py --workers 128 --chunks 2 --reps 1 \
+          --steps 40 --warmup 5 > gpurun_out/r5_rswg_$wg.json 2> gpurun_out/r5_rswg_$wg.err \
+          || { tail -n 20 gpurun_out/r5_rswg_$wg.err; die rs_wg_ab 1; }
+        grep '^{"K"' gpurun_out/r5_rswg_$wg.err
+      done
+    done ;;
   rank_proxy_trace)  # kernel trace of the weak-leg rank proxy (rank 0 of 8, 200 rounds) -> profiles/r5_rank_proxy.txt
     timeout -s KILL 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5_rpt -o run -- \
       python3 tools/rank_proxy.py --world 8 --rank 0 --scaling weak --legs proxy --reps 1 --steps 200 --warmup 20 \
