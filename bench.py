@@ -656,7 +656,8 @@ def main():
                          "computed on rank 0 and broadcast) or by contiguous id ranges")
     ap.add_argument("--rs-chunks", type=int, default=0,
                     help="C5 across ranks (or --phase): column chunks of the row-space pass, each chunk's sums "
-                         "all-reduced while the next streams (0: distributed.RS_CHUNKS, 1 at world size 1)")
+                         "all-reduced while the next ones stream, each chunk's average update just before the next "
+                         "round's pass over it (0: distributed.rs_chunks_for -- 2 across ranks, 1 at world size 1)")
     ap.add_argument("--pcie", action="store_true",
                     help="C3, 1 GPU: after the timed region, hand the same shards over as host buffers "
                          "(dopt_load_shards, the drop-in boundary) and report the PCIe-inclusive rate in a "

@@ -40,7 +40,6 @@ DEFAULT_TIMEOUT_S = 300.0
 # chunk k's sums are all-reduced while the later chunks stream, and round h's average update of chunk k runs
 # just before round h + 1's pass over chunk k, so only what the next round's earlier chunks cannot cover of
 # the last chunk's all-reduce stays exposed; every extra chunk costs a launch boundary and a hand-off.
-RS_CHUNKS = 1
 # The model that picks the chunk count per world size ("Column chunks across ranks"): exposed
 # time (K - 1) * boundary + max(0, allreduce(S / K, N) - (K - 1) / K * pass(N)), where the ring all-reduce of
 # S bytes over N ranks on xGMI costs ALPHA + 2 (N - 1) / N * S / BUSBW (assumed: no multi-GPU run here to
