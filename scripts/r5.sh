@@ -326,6 +326,9 @@ for step in "$@"; do
         grep '^{"K"' gpurun_out/r5_rswg_$wg.err
       done
     done ;;
+  contig_ab)  # (historical, profiles/r5_rank_proxy.txt call 11: DOPT_CONTIG_ROWS, a contiguous-allocation A/B knob for the
+    # shard rows, showed no difference and was removed)
+    echo "contig_ab: the knob was removed"; exit 2 ;;
   rank_proxy_trace)  # kernel trace of the weak-leg rank proxy (rank 0 of 8, 200 rounds) -> profiles/r5_rank_proxy.txt
     timeout -s KILL 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5_rpt -o run -- \
       python3 tools/rank_proxy.py --world 8 --rank 0 --scaling weak --legs proxy --reps 1 --steps 200 --warmup 20 \
