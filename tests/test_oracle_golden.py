@@ -149,3 +149,27 @@ def test_device_sampler_restatement_uniform_subsets():
     assert idx.shape == (2, 3, 4)
     np.testing.assert_array_equal(idx[1, 1], DS.minibatch(1, 5, 6, 10, 4))
     assert np.all(idx[:, 0, 3] == -1) and np.all(idx[:, 2] == -1)
+
+
+def test_float32_rounded_reference_data_tracks_the_fixtures():
+    """The north star's fp32 tolerance, checked on the restatement: the reference's own C2 data
+    (StandardScaler float64 output, not float32-representable) rounded to float32 -- what the engine's
+    float32 storage of such data computes on -- gives the reference's D-SGD / centralized trajectories
+    within 1e-9 relative (objective) and 1e-7 (consensus) over 400 rounds."""
+    meta, z = _load("c2")
+    cfg = meta["config"]
+    shards, Xf, yf = odata.generate(cfg, order=z["order"])
+    r = [(X.astype(np.float32).astype(np.float64), y) for X, y in shards]
+    Xr = Xf.astype(np.float32).astype(np.float64)
+    assert not np.array_equal(Xr, Xf)
+    T = 400
+    for j, label in enumerate(meta["labels"]):
+        st = ("MT19937", z[f"state{j}_key"], int(z[f"state{j}_pos"]), 0, 0.0)
+        if label == "Centralized":
+            h, _, _ = O.run_centralized(r, T, cfg, Xr, yf, meta["f_opt"], rng_state=st)
+        else:
+            topo = {"D-SGD (Ring)": "ring", "D-SGD (Grid)": "grid", "D-SGD (Fully Connected)": "fully_connected"}[label]
+            W, _ = O.mh_matrix(O.adjacency(topo, cfg["n_workers"]))
+            h, _, _, _ = O.run_decentralized(r, W, T, cfg, Xr, yf, meta["f_opt"], rng_state=st)
+            np.testing.assert_allclose(h["consensus_error"], z[f"L{j}_consensus"][:T], rtol=1e-7)
+        np.testing.assert_allclose(h["objective"], z[f"L{j}_objective"][:T], rtol=1e-9)
