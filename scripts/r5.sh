@@ -276,6 +276,9 @@ for step in "$@"; do
         palone_cur) envs="DOPT_A2A_STREAM=current"; extra="--legs proxy" ;;
         palone_lo) envs="DOPT_NCCL_HIPRI=0"; extra="--legs proxy" ;;
         palone_serial) envs="DOPT_LAGGED_SIDE=0 DOPT_A2A_STREAM=current"; extra="--legs proxy" ;;
+        pre_palone) extra="--legs proxy --prealloc" ;;
+        falone) extra="--legs fused" ;;
+        pre_falone) extra="--legs fused --prealloc" ;;
         fthen_serial) envs="DOPT_LAGGED_SIDE=0 DOPT_A2A_STREAM=current" ;;
         pfirst_w400) extra="--reps 2 --legs proxy,fused --warmup 400" ;;
         simple) envs="NCCL_PROTO=Simple" ;;
@@ -329,6 +332,21 @@ for step in "$@"; do
   contig_ab)  # (historical, profiles/r5_rank_proxy.txt call 11: DOPT_CONTIG_ROWS, a contiguous-allocation A/B knob for the
     # shard rows, showed no difference and was removed)
     echo "contig_ab: the knob was removed"; exit 2 ;;
+  rank_proxy_all)  # every rank of the 8-rank weak and strong legs on one GPU (one process each, the fused leg first
+    # and last): the SCALE time is the max over ranks -> profiles/r5_rank_proxy.txt
+    for sc in weak strong; do
+      st=300; wu=50
+      [ $sc = strong ] && { st=2000; wu=300; }
+      for r in 0 1 2 3 4 5 6 7; do
+        legs=proxy
+        [ $r = 0 ] && legs=fused,proxy
+        [ $r = 7 ] && legs=proxy,fused
+        timeout -k 10 300 python3 tools/rank_proxy.py --world 8 --rank $r --scaling $sc --legs $legs --reps 1 \
+          --steps $st --warmup $wu > gpurun_out/r5_rpa_${sc}_$r.json 2> gpurun_out/r5_rpa_${sc}_$r.err \
+          || { tail -n 20 gpurun_out/r5_rpa_${sc}_$r.err; die rank_proxy_all 1; }
+        python3 -c "import json; d=json.loads(open('gpurun_out/r5_rpa_${sc}_$r.json').read().strip().splitlines()[-1]); p=d['plan']; [print('$sc', 'rank', $r, g['leg'], g['workers'], 'halo', p['halo_rows_in'], 'interior', p['interior'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]"
+      done
+    done ;;
   rank_proxy_trace)  # kernel trace of the weak-leg rank proxy (rank 0 of 8, 200 rounds) -> profiles/r5_rank_proxy.txt
     timeout -s KILL 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5_rpt -o run -- \
       python3 tools/rank_proxy.py --world 8 --rank 0 --scaling weak --legs proxy --reps 1 --steps 200 --warmup 20 \

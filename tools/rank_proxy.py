@@ -100,6 +100,9 @@ def main():
     ap.add_argument("--fused-workers", type=int, default=4096, help="the fused leg's workers (the N = 1 line)")
     ap.add_argument("--legs", default="fused,proxy", help="legs per repetition, in order")
     ap.add_argument("--plan-only", action="store_true")
+    ap.add_argument("--prealloc", action="store_true",
+                    help="first generate (and free) a throwaway engine's shards of the fused leg's size: no rounds run "
+                         "(does the first large allocation of a process behave differently?)")
     ap.add_argument("--no-force", action="store_true",
                     help="no collectives at world 1 (the halo slots are never filled): the kernels alone")
     args = ap.parse_args()
@@ -163,6 +166,11 @@ def main():
             eng.close()
             raise
 
+    if args.prealloc:
+        tmp = _dopt.Engine(0, "float64", data_dtype="float32")
+        tmp.generate_shards("logistic", args.fused_workers, d, m, seed=1000, flip=0.05)
+        tmp.sync()
+        tmp.close()
     legs = []
     for rep in range(args.reps):
         for name in args.legs.split(","):
