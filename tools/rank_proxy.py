@@ -99,7 +99,10 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--fused-workers", type=int, default=4096, help="the fused leg's workers (the N = 1 line)")
     ap.add_argument("--legs", default="fused,proxy", help="legs per repetition, in order")
+    ap.add_argument("--fused-steps", type=int, default=0, help="the fused leg's timed rounds (0: --steps)")
     ap.add_argument("--plan-only", action="store_true")
+    ap.add_argument("--early-streams", action="store_true",
+                    help="create the runners' two shared streams (distributed._stream) before any engine exists")
     ap.add_argument("--prealloc", action="store_true",
                     help="first generate (and free) a throwaway engine's shards of the fused leg's size: no rounds run "
                          "(does the first large allocation of a process behave differently?)")
@@ -166,6 +169,9 @@ def main():
             eng.close()
             raise
 
+    if args.early_streams:
+        Dm._stream(torch.device("cuda", 0), 0)
+        Dm._stream(torch.device("cuda", 0), 1)
     if args.prealloc:
         tmp = _dopt.Engine(0, "float64", data_dtype="float32")
         tmp.generate_shards("logistic", args.fused_workers, d, m, seed=1000, flip=0.05)
@@ -176,12 +182,14 @@ def main():
         for name in args.legs.split(","):
             eng, rounds, flush, info = {"fused": leg_fused, "proxy": leg_proxy}[name]()
             nw = info["workers"]
+            steps = args.fused_steps if (name == "fused" and args.fused_steps > 0) else args.steps
+            warm = min(args.warmup, steps) if name == "fused" and args.fused_steps > 0 else args.warmup
             try:
-                dt, launches, kr_ms, every, obj, cons = bench.timed_leg(eng, rounds, args.steps, args.warmup, nw, d,
+                dt, launches, kr_ms, every, obj, cons = bench.timed_leg(eng, rounds, steps, warm, nw, d,
                                                                         barrier, 0, flush)
             finally:
                 eng.close()
-            legs.append({"leg": name, "rep": rep, "value": nw * args.steps / dt, "ms_per_round": dt / args.steps * 1e3,
+            legs.append({"leg": name, "rep": rep, "value": nw * steps / dt, "ms_per_round": dt / steps * 1e3,
                          "kernel_avg_ms": kr_ms / launches if launches else None, "kernel_launches": launches,
                          "final_objective": float(obj[-1]), **info})
             print(json.dumps(legs[-1]), file=sys.stderr, flush=True)
