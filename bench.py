@@ -524,6 +524,7 @@ def setup_leg(args, config, n_global, world, rank, dev):
                                              rs_chunks=args.rs_chunks or None)
         ld, esz_state = eng.layout()
         lay = runner.layout
+        S.exchange_shape = (list(lay.send_sizes), list(lay.recv_sizes), ld, esz_state)
         S.comm = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
                   "halo_rows_in": int(plan.n_halo), "send_rows_out": int(len(plan.send_ids)),
                   "halo_bytes_in_per_round": int(plan.n_halo) * ld * esz_state,
@@ -579,6 +580,84 @@ def per_rank(world, item):
     out = [None] * world
     dist.all_gather_object(out, item)
     return out
+
+
+def serial_exchange_leg(args, S, world, barrier, dev):
+    """N > 1, after the weak leg, on its engine and shards: the same rounds with the exchange serialised on
+    the engine stream (DOPT_LAGGED_SIDE=0 DOPT_A2A_STREAM=current: the all-to-all between the mix and the next
+    gradient kernel instead of beside it).  On one GPU the RCCL kernel beside the gradient kernel cost that
+    kernel up to ~70 us per round on some boxes (tools/rank_proxy.py) while a serial exchange
+    adds the transfer itself; which form wins with real peers over xGMI only a multi-GPU run can tell, so the
+    scaling run reports both (this one is not `value`)."""
+    import torch
+    import torch.distributed as dist
+
+    import distributed
+
+    keys = ("DOPT_LAGGED_SIDE", "DOPT_A2A_STREAM")
+    old = {k: os.environ.get(k) for k in keys}
+    os.environ.update(DOPT_LAGGED_SIDE="0", DOPT_A2A_STREAM="current")
+    try:
+        runner = distributed.DistributedDSGD(S.eng, S.plan, S.n_global, S.n_global * S.m, device=dev)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    if not runner._lagged_ok:
+        return None
+    eta0, b, lam = S.eta0, S.b, S.lam
+    dt, launches, kr_ms, every, obj, cons = timed_leg(
+        S.eng, lambda k: runner.run_pipelined(k, eta0, b, lam, lam, 0.0), args.steps, args.warmup, S.plan.n_local,
+        S.d, barrier, args.event_every, lambda: runner.run_pipelined(0, eta0, b, lam, lam, 0.0))
+    tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}" if args.backend == "nccl" else "cpu")
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    dt = float(tt.item())
+    return {"value": S.n_global * args.steps / dt, "unit": "worker-iters/s", "ms_per_step": dt / args.steps * 1e3,
+            "kernel_avg_ms": kr_ms / launches if launches else None, "side_stream": runner.side is not None,
+            "final_objective": float(obj[-1]),
+            "form": "the exchange serialised on the engine stream (DOPT_LAGGED_SIDE=0 DOPT_A2A_STREAM=current)"}
+
+
+def transport_probe(args, world, dev, barrier, shape, reps=20, warm=3):
+    """After the timed legs (N > 1): the round's collectives alone on this node's transport, so a scaling
+    run also measures what one GPU per call cannot -- the weak leg's exchange (one all_to_all_single with
+    that leg's per-peer row blocks) and C5's all-reduce of 2^20 float64 column sums (8 MiB; the chunk model
+    of distributed.rs_chunks_for assumes its cost).  Each timed `reps` times back to back after `warm`,
+    bracketed by barrier + sync; the max over ranks."""
+    import torch
+    import torch.distributed as dist
+
+    send_sizes, recv_sizes, ld, esz = shape
+    tdt = torch.float32 if esz == 4 else torch.float64
+    on = f"cuda:{dev}" if args.backend == "nccl" else "cpu"
+    send = torch.zeros((max(1, sum(send_sizes)), ld), dtype=tdt, device=on)
+    recv = torch.zeros((max(1, sum(recv_sizes)), ld), dtype=tdt, device=on)
+    sums = torch.zeros(1 << 20, dtype=torch.float64, device=on)
+
+    def timed(fn):
+        for _ in range(warm):
+            fn()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        barrier()
+        dt = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=on)
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        return float(dt.item()) * 1e3
+
+    a2a = timed(lambda: dist.all_to_all_single(recv[:sum(recv_sizes)], send[:sum(send_sizes)],
+                                               output_split_sizes=recv_sizes, input_split_sizes=send_sizes))
+    ar = timed(lambda: dist.all_reduce(sums))
+    out_bytes = sum(send_sizes) * ld * esz
+    return {"backend": args.backend, "world_size": world, "reps": reps,
+            "alltoall_ms": a2a, "alltoall_bytes_out_per_rank": out_bytes,
+            "alltoall_GBps_out_per_rank": out_bytes / (a2a * 1e-3) / 1e9 if a2a > 0 else None,
+            "allreduce_8MiB_ms": ar,
+            "allreduce_busbw_GBps": 2.0 * (world - 1) / world * (8 << 20) / (ar * 1e-3) / 1e9 if ar > 0 else None,
+            "note": "the weak leg's exchange and C5's column-sum all-reduce alone, after the timed legs"}
 
 
 def strong_leg(args, world, rank, dev, barrier):
@@ -637,6 +716,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-procs", type=int, default=0, help="CPU baseline processes (0: the box's CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-alt-exchange", action="store_true",
+                    help="N > 1: skip the weak leg's second timing with the exchange serialised on the engine stream")
     ap.add_argument("--no-secondary", action="store_true",
                     help="N=1: skip the f64-storage / f32 legs, the f(x*) solver and the drop-in trainer leg")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (gloo: 1-GPU rehearsal)")
@@ -793,6 +874,9 @@ def main():
     if args.config != "c3":
         out["metric"] = f"worker-iters/sec ({args.config.upper()}, secondary config)"
     secondary = rank == 0 and world == 1 and not args.phase and args.config == "c3" and not args.no_secondary
+    if world > 1 and args.config == "c3" and weak and S.flush is not None and not args.no_alt_exchange:
+        log("weak leg again with the exchange serialised on the engine stream (A/B with real peers)")
+        out["weak_serial_exchange"] = serial_exchange_leg(args, S, world, barrier, dev)
     if secondary and b == m:
         log("f(x*): device L-BFGS")
         out["suboptimality"] = suboptimality(eng, lam, float(obj[-1]))
@@ -806,6 +890,9 @@ def main():
     if args.config == "c3" and world > 1 and weak and args.scaling == "both":
         log(f"strong-scaling leg: {args.strong_workers} workers over {world} ranks")
         out["strong"] = strong_leg(args, world, rank, dev, barrier)
+    if world > 1 and getattr(S, "exchange_shape", None) is not None:
+        log("transport probe: the weak leg's all-to-all and an 8 MiB all-reduce alone")
+        out["transport_probe"] = transport_probe(args, world, dev, barrier, S.exchange_shape)
     if secondary and b == m:
         legs = {}
         if not (esz == 8 and xesz == 8):

@@ -34,7 +34,7 @@ tests() {  # tests <name> <pytest args...>
 rehearsal8() {  # rehearsal8 <name> <timeout> <bench.py args...>: the driver's SCALE command shape, 8 gloo ranks
   local name=$1 t=$2; shift 2
   bench_step "$name" "$t" --gpus 8 --backend gloo --steps 20 --warmup 5 "$@"
-  tail -n 1 "gpurun_out/$name.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('comm', d.get('comm')); print('per_rank', [(r['rank'], r['workers']) for r in d.get('per_rank', [])]); s=d.get('strong'); print('strong', None if s is None else (s['value'], s['n_workers_total'], [(r['workers'], r['halo_rows_in'], r['peers']) for r in s['per_rank']]))"
+  tail -n 1 "gpurun_out/$name.json" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('comm', d.get('comm')); print('per_rank', [(r['rank'], r['workers']) for r in d.get('per_rank', [])]); s=d.get('strong'); print('strong', None if s is None else (s['value'], s['n_workers_total'], [(r['workers'], r['halo_rows_in'], r['peers']) for r in s['per_rank']])); print('transport_probe', d.get('transport_probe')); w=d.get('weak_serial_exchange'); print('weak_serial_exchange', None if w is None else (w['value'], w['ms_per_step'], w['side_stream']), 'weak', d['value'], d['ms_per_step'])"
 }
 
 for step in "$@"; do

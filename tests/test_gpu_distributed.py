@@ -490,7 +490,7 @@ def _rccl_self_exchange(rank, world, port, out):
 @pytest.mark.parametrize("dtype,lagged", [("float64", "1"), ("float64/x32", "1"), ("float64", "1-noside"),
                                           ("float32", "1"), ("float64", "1-value"), ("float64/x32", "1-value"),
                                           ("float64", "1-event"), ("float64", "1-current"),
-                                          ("float64/x32", "1-current")])
+                                          ("float64/x32", "1-current"), ("float64", "1-noside-current")])
 def test_rccl_one_rank_self_exchange_matches_single_context(tmp_path, monkeypatch, dtype, lagged):
     """the RCCL path at world 1 (collectives forced) with an exchange that moves data -- a
     third of the workers' rows and the rank's own column sums go through the all-to-all to itself (a
