@@ -277,6 +277,7 @@ for step in "$@"; do
         palone_lo) envs="DOPT_NCCL_HIPRI=0"; extra="--legs proxy" ;;
         palone_serial) envs="DOPT_LAGGED_SIDE=0 DOPT_A2A_STREAM=current"; extra="--legs proxy" ;;
         pre_palone) extra="--legs proxy --prealloc" ;;
+        palone_cur2) envs="DOPT_A2A_STREAM=current"; extra="--legs proxy" ;;
         early_default) extra="--early-streams" ;;
         fshort_palone) extra="--legs fused,proxy --fused-steps 5" ;;
         falone) extra="--legs fused" ;;
