@@ -278,6 +278,9 @@ for step in "$@"; do
         palone_serial) envs="DOPT_LAGGED_SIDE=0 DOPT_A2A_STREAM=current"; extra="--legs proxy" ;;
         pre_palone) extra="--legs proxy --prealloc" ;;
         palone_cur2) envs="DOPT_A2A_STREAM=current"; extra="--legs proxy" ;;
+        palone_simple) envs="NCCL_PROTO=Simple"; extra="--legs proxy" ;;
+        palone_ll) envs="NCCL_PROTO=LL"; extra="--legs proxy" ;;
+        palone_ll128) envs="NCCL_PROTO=LL128"; extra="--legs proxy" ;;
         early_default) extra="--early-streams" ;;
         fshort_palone) extra="--legs fused,proxy --fused-steps 5" ;;
         falone) extra="--legs fused" ;;
