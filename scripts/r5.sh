@@ -353,6 +353,27 @@ for step in "$@"; do
         python3 -c "import json; d=json.loads(open('gpurun_out/r5_rpa_${sc}_$r.json').read().strip().splitlines()[-1]); p=d['plan']; [print('$sc', 'rank', $r, g['leg'], g['workers'], 'halo', p['halo_rows_in'], 'interior', p['interior'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]"
       done
     done ;;
+  proxy_pmc)  # HBM traffic of the weak rank proxy's gradient kernel with the exchange beside it vs serialised
+    # (FETCH_SIZE / WRITE_SIZE passes, proxy alone, 100 rounds) -> profiles/r5_rank_proxy.txt
+    for arm in overlap serial; do
+      envs=""
+      [ $arm = serial ] && envs="DOPT_LAGGED_SIDE=0 DOPT_A2A_STREAM=current"
+      for c in FETCH_SIZE WRITE_SIZE; do
+        echo "=== $arm $c"
+        env $envs timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d gpurun_out/r5_ppmc_${arm}_$c -o run -- \
+          python3 tools/rank_proxy.py --world 8 --rank 0 --scaling weak --legs proxy --reps 1 --steps 100 --warmup 20 \
+          > gpurun_out/r5_ppmc_${arm}_$c.log 2>&1 || { tail -n 20 gpurun_out/r5_ppmc_${arm}_$c.log; die proxy_pmc 1; }
+        python3 - gpurun_out/r5_ppmc_${arm}_$c/run_counter_collection.csv <<'PY'
+import collections, csv, statistics, sys
+v = collections.defaultdict(list)
+for r in csv.DictReader(open(sys.argv[1])):
+    v[r["Kernel_Name"][:70]].append(float(r["Counter_Value"]))
+for k, xs in sorted(v.items(), key=lambda kv: -statistics.median(kv[1])):
+    if len(xs) >= 50:
+        print(f"  {len(xs):5d} dispatches  median {statistics.median(xs[len(xs)//2:]):14.1f} KB  {k}")
+PY
+      done
+    done ;;
   rank_proxy_trace)  # kernel trace of the weak-leg rank proxy (rank 0 of 8, 200 rounds) -> profiles/r5_rank_proxy.txt
     timeout -s KILL 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5_rpt -o run -- \
       python3 tools/rank_proxy.py --world 8 --rank 0 --scaling weak --legs proxy --reps 1 --steps 200 --warmup 20 \
