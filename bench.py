@@ -884,10 +884,13 @@ def main():
     if secondary and b == m:
         log("f(x*): device L-BFGS")
         out["suboptimality"] = suboptimality(eng, lam, float(obj[-1]))
-        log("drop-in trainer leg (legacy RNG stream)")
-        out["dropin"] = dropin_leg(eng, n, d, m, lam, eta0)
-        log("drop-in trainer leg, b = 16 (minibatch indices from the legacy stream)")
-        out["dropin"]["b16"] = dropin_leg(eng, n, d, m, lam, eta0, batch=16)
+        import contextlib
+
+        with contextlib.redirect_stdout(sys.stderr):  # the trainers' reference prints: stdout keeps the one line
+            log("drop-in trainer leg (legacy RNG stream)")
+            out["dropin"] = dropin_leg(eng, n, d, m, lam, eta0)
+            log("drop-in trainer leg, b = 16 (minibatch indices from the legacy stream)")
+            out["dropin"]["b16"] = dropin_leg(eng, n, d, m, lam, eta0, batch=16)
     if args.pcie and world == 1 and args.config == "c3":
         out["pcie"] = pcie_leg(eng, top, n, d, m, b, lam, eta0, args.steps, dt)
     eng.close()
