@@ -923,6 +923,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1 or args.phase:
+        distributed.close_comms()  # the engine's RCCL communicators, before the process group
         dist.destroy_process_group()
     return 0
 

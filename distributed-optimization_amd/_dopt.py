@@ -110,9 +110,16 @@ _SIGS = {
     "dopt_phase_set_step": ([_P, _I64, ctypes.c_double], ctypes.c_int),
     "dopt_phase_interior_count": ([_P, _P], ctypes.c_int),
     "dopt_host_digest": ([_I32, _P, _P, _I32, _P], ctypes.c_int),
+    "dopt_comm_unique_id": ([_P, _I64], ctypes.c_int),
+    "dopt_comm_create": ([_P, _I32, _I32, _I32, _P, _I64], ctypes.c_int),
+    "dopt_comm_check": ([_P], ctypes.c_int),
+    "dopt_comm_destroy": ([_P, _I32], ctypes.c_int),
+    "dopt_comm_library": ([], ctypes.c_char_p),
+    "dopt_lagged_transport": ([_P, _P, _P, _P], ctypes.c_int),
+    "dopt_lagged_exchange": ([_P], ctypes.c_int),
 }
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 6  # DOPT_ABI_VERSION of include/dopt.h
+ABI_VERSION = 7  # DOPT_ABI_VERSION of include/dopt.h
 
 
 def lib():
@@ -172,6 +179,44 @@ def host_digest(buffers, threads=0):
     out = np.zeros(2, dtype=np.uint64)
     check(lib().dopt_host_digest(n, ptrs, _ptr(sizes), int(threads), _ptr(out)))
     return f"{int(out[0]):016x}{int(out[1]):016x}"
+
+
+COMM_ID_BYTES = 128  # DOPT_COMM_ID_BYTES
+
+
+def comm_unique_id():
+    """dopt_comm_unique_id: rank 0's RCCL unique id (bytes) for Comm()."""
+    buf = (ctypes.c_uint8 * COMM_ID_BYTES)()
+    check(lib().dopt_comm_unique_id(buf, COMM_ID_BYTES))
+    return bytes(buf)
+
+
+def comm_library():
+    """dopt_comm_library: path of the RCCL library the transport uses ('' before the first use / none)."""
+    return (lib().dopt_comm_library() or b"").decode()
+
+
+class Comm:
+    """An RCCL communicator the engine drives itself (dopt_comm_create; csrc/transport.cpp): rank `rank` of
+    `world` on `device`, from rank 0's comm_unique_id() -- every rank constructs it with the same id."""
+
+    def __init__(self, world, rank, device, uid):
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError(f"RCCL unique id of {COMM_ID_BYTES} bytes expected, got {len(uid)}")
+        h = ctypes.c_void_p()
+        buf = (ctypes.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
+        check(lib().dopt_comm_create(ctypes.byref(h), int(world), int(rank), int(device), buf, COMM_ID_BYTES))
+        self._h = h
+        self.world, self.rank, self.device = int(world), int(rank), int(device)
+
+    def check(self):
+        """Raise if RCCL reported an asynchronous error on this communicator."""
+        check(lib().dopt_comm_check(self._h))
+
+    def close(self, abort=False):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            check(lib().dopt_comm_destroy(h, 1 if abort else 0))
 
 
 def device_count():
@@ -515,6 +560,24 @@ class Engine:
         o = ctypes.c_int(0)
         check(lib().dopt_lagged_exchange_issued(self._h, ctypes.byref(o)))
         return bool(o.value)
+
+    def lagged_transport(self, comm, send_rows=None, recv_rows=None):
+        """dopt_lagged_transport: route the exchange through `comm` (a Comm; None: detach), blocks of
+        send_rows[p] / recv_rows[p] rows per peer p in rank order."""
+        if comm is None:
+            check(lib().dopt_lagged_transport(self._h, None, None, None))
+            return
+        s = np.ascontiguousarray(send_rows, dtype=np.int64)
+        r = np.ascontiguousarray(recv_rows, dtype=np.int64)
+        if s.shape != (comm.world,) or r.shape != (comm.world,):
+            raise ValueError(f"{comm.world} block sizes per direction expected")
+        check(lib().dopt_lagged_transport(self._h, comm._h, _ptr(s), _ptr(r)))
+
+    def lagged_exchange(self):
+        """dopt_lagged_exchange: the round's exchange through the attached communicator."""
+        rc = lib().dopt_lagged_exchange(self._h)
+        if rc:
+            check(rc)
 
     def lagged_tail(self, consensus, objective, row1, row2):
         """row1 / row2: (cons, xnorm, loss) device addresses of the history rows G-1 / G-2 (None: skip)."""

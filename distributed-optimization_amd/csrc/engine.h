@@ -5,7 +5,24 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+struct dopt_comm;  // transport.cpp: an RCCL communicator (include/dopt.h)
+
 namespace dopt {
+
+// Error text for dopt_last_error from the library's other translation units (runtime.cpp).
+int fail_code(int code, const char* fmt, ...);
+
+// One point-to-point transfer of a round's exchange: `bytes` at byte offset `off` of the send buffer
+// (recv = 0) or of the halo buffer (recv = 1), with rank `peer`.
+struct XpOp {
+  int64_t off, bytes;
+  int32_t peer, recv;
+};
+// The ops as one RCCL group on stream s (transport.cpp).
+int comm_exchange(dopt_comm* c, const XpOp* ops, size_t n_ops, const void* send, void* recv, hipStream_t s);
+int32_t comm_world(const dopt_comm* c);
+int32_t comm_rank(const dopt_comm* c);
+int32_t comm_device(const dopt_comm* c);
 
 // RoundArgs.flags
 enum : int32_t {

@@ -52,6 +52,20 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
+}  // namespace
+
+int dopt::fail_code(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+namespace {
+
 #define HIPOK(expr)                                                                      \
   do {                                                                                   \
     hipError_t e_ = (expr);                                                              \
@@ -206,6 +220,10 @@ struct dopt_ctx {
   uint64_t lg_mseq = 0, lg_xseq = 0;
   bool lg_xwait = false;  // the next mix / tail waits for the exchange (lg_sig[1] >= lg_xseq, or lg_xev)
   hipEvent_t lg_xev = nullptr;  // recorded on the side stream behind an exchange issued there (event mode)
+  // dopt_lagged_transport: the exchange through an RCCL communicator of the caller's (transport.cpp), one
+  // send / receive per non-empty block of the layout, issued by dopt_lagged_exchange
+  dopt_comm* xp = nullptr;
+  std::vector<XpOp> xp_ops;
   int64_t* lg_sum_in = nullptr;            // [world] halo row of peer p's sums
   int64_t* lg_sum_out = nullptr;           // [world] send row of the sums for peer p
   double* lg_own[2] = {nullptr, nullptr};  // [ld] this rank's column sums of x_g (g parity)
@@ -2647,10 +2665,9 @@ int dopt_lagged_begin(dopt_ctx* c, int64_t batch) {
   return DOPT_OK;
 }
 
-int dopt_lagged_exchange_issued(dopt_ctx* c, int* ordered) {
-  CHECK_ARG(c && ordered, "NULL argument");
-  *ordered = 0;
-  if (!c->lg_side) return DOPT_OK;  // no side stream: the caller orders the engine stream
+namespace {
+// An exchange was just enqueued on the side stream: the next mix / tail waits for it.
+int lagged_mark_exchange(dopt_ctx* c) {
   if (lagged_value_sync()) {
     HIPOK(hipStreamWriteValue64(c->lg_side, c->lg_sig[1], ++c->lg_xseq, 0));
   } else {  // an event of the context's own (no timing, created once) behind the exchange on the side stream
@@ -2658,8 +2675,59 @@ int dopt_lagged_exchange_issued(dopt_ctx* c, int* ordered) {
     HIPOK(hipEventRecord(c->lg_xev, c->lg_side));
   }
   c->lg_xwait = true;
+  return DOPT_OK;
+}
+}  // namespace
+
+int dopt_lagged_exchange_issued(dopt_ctx* c, int* ordered) {
+  CHECK_ARG(c && ordered, "NULL argument");
+  *ordered = 0;
+  if (!c->lg_side) return DOPT_OK;  // no side stream: the caller orders the engine stream
+  int rc;
+  if ((rc = lagged_mark_exchange(c))) return rc;
   *ordered = 1;
   return DOPT_OK;
+}
+
+int dopt_lagged_transport(dopt_ctx* c, dopt_comm* comm, const int64_t* send_rows, const int64_t* recv_rows) {
+  CHECK_ARG(c, "ctx is NULL");
+  c->xp = nullptr;
+  c->xp_ops.clear();
+  if (!comm) return DOPT_OK;
+  CHECK_ARG(send_rows && recv_rows, "NULL argument");
+  CHECK_ARG(comm_device(comm) == c->device, "communicator on device %d, context on device %d", comm_device(comm),
+            c->device);
+  const int32_t world = comm_world(comm), rank = comm_rank(comm);
+  CHECK_ARG(c->lg_world == world && c->lg_rank == rank,
+            "communicator of rank %d of %d, exchange layout of rank %d of %d (dopt_lagged_exchange_layout first)",
+            rank, world, c->lg_rank, c->lg_world);
+  const int64_t row = c->ld * (int64_t)c->esz;
+  int64_t so = 0, ro = 0;
+  std::vector<XpOp> ops;
+  for (int32_t p = 0; p < world; ++p) {
+    CHECK_ARG(send_rows[p] >= 0 && recv_rows[p] >= 0, "peer %d: negative block size", p);
+    if (send_rows[p] > 0) ops.push_back(XpOp{so * row, send_rows[p] * row, p, 0});
+    if (recv_rows[p] > 0) ops.push_back(XpOp{ro * row, recv_rows[p] * row, p, 1});
+    so += send_rows[p];
+    ro += recv_rows[p];
+  }
+  CHECK_ARG(so <= std::max<int64_t>(c->n_send, 0) && ro <= c->n_halo,
+            "blocks of %lld send / %lld halo rows past the buffers (%lld / %lld; dopt_set_halo first)", (long long)so,
+            (long long)ro, (long long)c->n_send, (long long)c->n_halo);
+  CHECK_ARG((so == 0 || c->send) && (ro == 0 || c->halo), "send / halo buffer missing");
+  c->xp = comm;
+  c->xp_ops = std::move(ops);
+  return DOPT_OK;
+}
+
+int dopt_lagged_exchange(dopt_ctx* c) {
+  CHECK_ARG(c, "ctx is NULL");
+  if (!c->xp) return fail(DOPT_ERR_STATE, "no transport (dopt_lagged_transport first)");
+  int rc;
+  if ((rc = comm_exchange(c->xp, c->xp_ops.data(), c->xp_ops.size(), c->send, c->halo,
+                          c->lg_side ? c->lg_side : c->stream)))
+    return rc;
+  return c->lg_side ? lagged_mark_exchange(c) : DOPT_OK;  // (one stream: ordered by the stream itself)
 }
 
 int dopt_lagged_side_stream(dopt_ctx* c, void* stream) {

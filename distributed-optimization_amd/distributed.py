@@ -447,6 +447,49 @@ class HaloExchange:
 
 
 _STREAMS = {}
+_COMMS = {}
+
+
+def transport_kind():
+    """The lagged schedule's exchange over RCCL: "rccl" -- the engine's own communicator, RCCL sends and
+    receives issued by dopt_lagged_exchange on the side stream (ABI 7, csrc/transport.cpp: 4.5-6 us of host
+    time per round against 22 us for the process group's alltoall_base, profiles/r5_rccl_probe.txt) -- or
+    "pg": torch's process group all-to-all-v (rounds 3-4).  DOPT_TRANSPORT overrides."""
+    v = os.environ.get("DOPT_TRANSPORT", "rccl").strip().lower()
+    if v not in ("rccl", "pg"):
+        raise ValueError(f"DOPT_TRANSPORT={v!r}: 'rccl' or 'pg'")
+    return v
+
+
+def _comm(group, dev):
+    """The process's engine-driven RCCL communicator over `group` on device `dev` (created once, collectively:
+    rank 0's unique id is broadcast over the group's process group; every runner of the process shares it)."""
+    import torch
+    import torch.distributed as dist
+
+    key = (None if group is None else id(group), int(dev.index))
+    c = _COMMS.get(key)
+    if c is not None:
+        return c
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    buf = torch.zeros(_dopt.COMM_ID_BYTES, dtype=torch.uint8, device=dev)
+    if rank == 0:
+        buf.copy_(torch.frombuffer(bytearray(_dopt.comm_unique_id()), dtype=torch.uint8))
+    src = 0 if group is None else dist.get_global_rank(group, 0)
+    dist.broadcast(buf, src=src, group=group)
+    if not _COMMS:
+        import atexit
+
+        atexit.register(close_comms)
+    c = _COMMS[key] = _dopt.Comm(world, rank, int(dev.index), bytes(buf.cpu().numpy().tobytes()))
+    return c
+
+
+def close_comms(abort=False):
+    """Destroy the engine-driven communicators (before the process group; bench.py and main.py call it)."""
+    while _COMMS:
+        _, c = _COMMS.popitem()
+        c.close(abort)
 
 
 def _stream(dev, role):
@@ -537,6 +580,14 @@ class DistributedDSGD:
                 and os.environ.get("DOPT_LAGGED_SIDE", "1") != "0"):
             self.side = _stream(self.dev, 1)
         engine.lagged_side_stream(self.side.cuda_stream if self.side is not None else None)
+        # the engine's own RCCL communicator for the lagged exchange (dopt_lagged_exchange), RCCL only
+        self.comm = None
+        if (self.device_comm and self._lagged_ok and mean is None and self.exchange.collective
+                and transport_kind() == "rccl"):
+            self.comm = _comm(group, self.dev)
+            engine.lagged_transport(self.comm, lay.send_sizes, lay.recv_sizes)
+        else:
+            engine.lagged_transport(None)
         # the communicator is created by one small collective here, not inside the first round
         # (the halo all-to-all and the all-reduces of the rounds then find it ready)
         if self.device_comm and dist.get_world_size(group) > 1:
@@ -551,6 +602,9 @@ class DistributedDSGD:
         k_mixcs_final), with the engine stream current again afterwards.  The current stream is switched
         through torch._C._cuda_setStream with the two streams' cached ids (what torch.cuda.stream's
         context manager does, without its per-call Python: VERDICT r4 item 4, host cost per round)."""
+        if self.comm is not None:  # the engine issues it on the side stream and orders the engine stream after it
+            self.eng.lagged_exchange()
+            return None
         side = self.side
         if side is None:
             return self.exchange.start()
@@ -580,6 +634,31 @@ class DistributedDSGD:
 
     def _finish_exchange(self, works):
         self.exchange.finish(works)
+
+    def _sync(self, stream):
+        """stream.synchronize(), bounded like the process group's collectives when the engine's own
+        communicator has exchanges in it: a peer that never joins ends this rank with CollectiveError
+        (the communicator aborted) within timeout_seconds() instead of a hang."""
+        if self.comm is None:
+            stream.synchronize()
+            return
+        import time
+
+        t0 = time.monotonic()
+        last = t0
+        while not stream.query():
+            now = time.monotonic()
+            if now - last > 1.0:
+                last = now
+                try:
+                    self.comm.check()
+                except RuntimeError as e:
+                    raise CollectiveError(f"rank {self.plan.rank}: the engine's RCCL exchange failed: {e}") from e
+                if now - t0 > timeout_seconds():
+                    self.comm.close(abort=True)
+                    _COMMS.clear()
+                    raise CollectiveError(f"rank {self.plan.rank}: the engine's RCCL exchange "
+                                          f"({self.exchange.what}) did not finish in {timeout_seconds():.0f} s")
 
     def _solo(self):
         """One rank: the reductions are identities and are skipped, unless
@@ -869,9 +948,9 @@ class DistributedDSGD:
             if upto > done:
                 self._all_reduce(partials[done:upto])
             raw = partials[done:upto].cpu().numpy()
-        self.stream.synchronize()
+        self._sync(self.stream)
         if self.side is not None:
-            self.side.synchronize()  # no side-stream work outlives the call
+            self._sync(self.side)  # no side-stream work outlives the call
         ch["g"], ch["done"] = G1, upto
         if tail:
             self._chain = None

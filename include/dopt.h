@@ -48,10 +48,14 @@ extern "C" {
  *      engine cache key), dopt_phase_interior_count; dopt_lagged_exchange_layout accepts a self
  *      block (a rank's own column sums routed through the exchange).
  *   6  round 5: dopt_rs_phase_cols_range (the complete graph's average update per column chunk, so
- *      the next round's pass over a chunk starts while later chunks' sums are still being reduced). */
-#define DOPT_ABI_VERSION 6
+ *      the next round's pass over a chunk starts while later chunks' sums are still being reduced).
+ *   7  round 5: the engine-driven RCCL transport (dopt_comm_*, dopt_lagged_transport,
+ *      dopt_lagged_exchange): the lagged schedule's exchange as RCCL sends / receives issued by the
+ *      engine on its side stream, without the process group's per-call cost. */
+#define DOPT_ABI_VERSION 7
 
 typedef struct dopt_ctx dopt_ctx;
+typedef struct dopt_comm dopt_comm; /* an RCCL communicator the engine drives itself (ABI 7) */
 
 /* status codes */
 #define DOPT_OK 0
@@ -416,6 +420,31 @@ int dopt_lagged_side_stream(dopt_ctx *ctx, void *stream);
  * makes the engine stream wait for it -- *ordered = 1, the caller does not order the engine stream
  * itself.  *ordered = 0 without a side stream (the caller orders it). */
 int dopt_lagged_exchange_issued(dopt_ctx *ctx, int *ordered);
+/* Engine-driven RCCL transport (ABI 7; csrc/transport.cpp).  It replaces, for the lagged schedule's
+ * per-round exchange, the caller's process-group all-to-all-v (torch.distributed all_to_all_single in
+ * distributed.py HaloExchange: ~22 us of host time per call, 36-40 us with its wait, against 4.5-6 us for
+ * RCCL's own group of sends and receives -- profiles/r5_rccl_probe.txt).
+ * dopt_comm_unique_id: rank 0's RCCL unique id (DOPT_COMM_ID_BYTES bytes), which the caller hands to every
+ *   rank (the job's existing process group broadcasts it).
+ * dopt_comm_create: RCCL communicator of rank `rank` of `world` on `device`; collective -- every rank
+ *   calls it with the same id.  dopt_comm_destroy (abort = 1: without waiting for pending work, after a
+ *   peer failed); dopt_comm_check: DOPT_ERR_COMM if RCCL reported an asynchronous error.
+ * dopt_comm_library: the path of the RCCL library in use (the process's copy when one is loaded).
+ * dopt_lagged_transport: route the context's exchange through comm (NULL: detach): per peer p in rank
+ *   order, send_rows[p] rows of the send buffer go to p and recv_rows[p] rows of the halo buffer come
+ *   from p (the blocks of the all-to-all-v layout; the rank's own block at world 1 with a self block);
+ *   after dopt_set_halo and dopt_lagged_exchange_layout, whose rank and world must match comm's.
+ * dopt_lagged_exchange: the round's exchange as one RCCL group on the side stream (the engine stream
+ *   without one), ordered before the next dopt_lagged_mix / _tail as dopt_lagged_exchange_issued orders
+ *   the caller's; where the caller would have issued its all-to-all. */
+#define DOPT_COMM_ID_BYTES 128
+int dopt_comm_unique_id(uint8_t *id_out, int64_t n);
+int dopt_comm_create(dopt_comm **out, int32_t world, int32_t rank, int32_t device, const uint8_t *id, int64_t n);
+int dopt_comm_check(dopt_comm *comm);
+int dopt_comm_destroy(dopt_comm *comm, int32_t abort);
+const char *dopt_comm_library(void);
+int dopt_lagged_transport(dopt_ctx *ctx, dopt_comm *comm, const int64_t *send_rows, const int64_t *recv_rows);
+int dopt_lagged_exchange(dopt_ctx *ctx);
 /* Centralized trainer across ranks (trainer.py:41-71): gradients of the local
  * workers at the shared iterate (fuse_loss: the objective partial of the shared
  * iterate over the same rows, full shards only), local column sums of the

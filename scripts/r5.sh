@@ -420,6 +420,33 @@ PY
       -d gpurun_out/r5_hl_trace -o run -- python3 bench.py --no-cpu-baseline --no-secondary --scaling weak --phase \
       --workers 512 --steps 1500 --warmup 400 > gpurun_out/r5_hl_trace.log 2>&1 || die handoff_long 1
     python3 tools/trace_rounds.py gpurun_out/r5_hl_trace/run_kernel_trace.csv ;;
+  transport_ab)  # the engine's own RCCL communicator (dopt_lagged_exchange, DOPT_TRANSPORT=rccl) vs the process
+    # group's all-to-all-v (pg): the RCCL GPU tests, the host cost per round at 512 workers, and the rank proxy's
+    # weak / strong legs, interleaved twice -> profiles/r5_transport.txt
+    timeout -k 10 400 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_distributed.py \
+      -k "rccl" > gpurun_out/r5_transport_tests.txt 2>&1 || { tail -n 30 gpurun_out/r5_transport_tests.txt; die transport_ab 1; }
+    tail -n 2 gpurun_out/r5_transport_tests.txt
+    for rep in 1 2; do
+      for tr in rccl pg; do
+        echo "=== host probe, DOPT_TRANSPORT=$tr (rep $rep)"
+        DOPT_LIB=$AB DOPT_HOST_TIMING=1 DOPT_TRANSPORT=$tr DOPT_FORCE_COLLECTIVES=1 timeout -k 10 200 \
+          python3 tools/host_round_probe.py > gpurun_out/r5_tr_host_$tr.json 2> gpurun_out/r5_tr_host_$tr.err \
+          || { tail -n 20 gpurun_out/r5_tr_host_$tr.err; die transport_ab 1; }
+        cat gpurun_out/r5_tr_host_$tr.json
+      done
+    done
+    for rep in 1 2; do
+      for s in strong weak; do
+        st=400; wu=50
+        [ $s = strong ] && { st=3000; wu=400; }
+        for tr in rccl pg; do
+          echo "=== rank proxy, $s leg, rank 0 of 8, DOPT_TRANSPORT=$tr (rep $rep)"
+          DOPT_TRANSPORT=$tr timeout -k 10 300 python3 tools/rank_proxy.py --world 8 --rank 0 --scaling $s --steps $st \
+            --warmup $wu > gpurun_out/r5_tr_rp.json 2> gpurun_out/r5_tr_rp.err || { tail -n 20 gpurun_out/r5_tr_rp.err; die transport_ab 1; }
+          python3 -c "import json; d=json.loads(open('gpurun_out/r5_tr_rp.json').read().strip().splitlines()[-1]); [print(g['leg'], g['workers'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]; print('proxy / fused', [round(x, 4) for x in d['proxy_over_fused']])"
+        done
+      done
+    done ;;
   *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -45,9 +45,12 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
     side = "0" if "noside" in opts else "1"
     sync = "value" if "value" in opts else "event"
     a2a = "current" if "current" in opts else "nccl"  # "1-current": the all-to-all on the side stream itself
+    # "1-pg": the exchange through the process group's all-to-all-v instead of the engine's own RCCL
+    # communicator (dopt_lagged_exchange, the default)
+    transport = "pg" if "pg" in opts else "rccl"
     lagged = opts[0]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DOPT_LAGGED=lagged, DOPT_LAGGED_SIDE=side,
-                      DOPT_LAGGED_SYNC=sync, DOPT_A2A_STREAM=a2a,
+                      DOPT_LAGGED_SYNC=sync, DOPT_A2A_STREAM=a2a, DOPT_TRANSPORT=transport,
                       DOPT_FORCE_COLLECTIVES="1" if backend == "nccl" else "0")
     if backend == "nccl":
         torch.cuda.set_device(0)
@@ -66,7 +69,8 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
                              mean=None if uni is None else (uni[0], uni[1][plan.lo:plan.hi]))
     info = {"interior": eng.phase_interior_count(), "n_local": plan.n_local, "n_halo": plan.n_halo,
             "send_sizes": list(run.layout.send_sizes), "recv_sizes": list(run.layout.recv_sizes),
-            "ks": run.layout.ks, "side": run.side is not None, "collective": bool(run.exchange.collective)}
+            "ks": run.layout.ks, "side": run.side is not None, "collective": bool(run.exchange.collective),
+            "native": run.comm is not None}
     np.save(os.path.join(out, f"info{rank}.npy"), np.array([repr(info)]))
     which = os.environ.get("DOPT_TEST_METRICS", "both")
     if os.environ.get("DOPT_TEST_PIPE") == "1":  # a chain of pipelined calls covering T rounds, then the tail
@@ -489,15 +493,18 @@ def _rccl_self_exchange(rank, world, port, out):
 
 @pytest.mark.parametrize("dtype,lagged", [("float64", "1"), ("float64/x32", "1"), ("float64", "1-noside"),
                                           ("float32", "1"), ("float64", "1-value"), ("float64/x32", "1-value"),
-                                          ("float64", "1-event"), ("float64", "1-current"),
-                                          ("float64/x32", "1-current"), ("float64", "1-noside-current")])
+                                          ("float64", "1-pg"), ("float64/x32", "1-pg"), ("float64", "1-pg-value"),
+                                          ("float64", "1-pg-current"), ("float64/x32", "1-pg-current"),
+                                          ("float64", "1-noside-pg-current")])
 def test_rccl_one_rank_self_exchange_matches_single_context(tmp_path, monkeypatch, dtype, lagged):
     """the RCCL path at world 1 (collectives forced) with an exchange that moves data -- a
     third of the workers' rows and the rank's own column sums go through the all-to-all to itself (a
     self block), and the mix reads them back from the halo buffer.  With the side stream (k_mixcs_final
     and the exchange on a second stream, ProcessGroupNCCL's stream sync and work.wait() ordering them)
     or on one stream, as a pipelined chain: iterates bitwise one context's, history rtol 1e-12 -- a
-    missing dependency would mix stale halo rows or column sums."""
+    missing dependency would mix stale halo rows or column sums.  The exchange goes through the engine's
+    own RCCL communicator (dopt_lagged_exchange: sends and receives on the side stream) or, "-pg", through
+    the process group's all-to-all-v."""
     import torch.multiprocessing as mp
 
     monkeypatch.setenv("DOPT_TEST_SELF_HALO", "1")
@@ -510,6 +517,7 @@ def test_rccl_one_rank_self_exchange_matches_single_context(tmp_path, monkeypatc
     ks = 2 if dtype == "float32" else 1
     assert it["collective"] and it["ks"] == ks and it["send_sizes"] == [len(range(0, N, 3)) + ks], it
     assert it["side"] == ("noside" not in lagged), it
+    assert it["native"] == ("pg" not in lagged), it
     assert it["interior"] < N - len(range(0, N, 3)), it  # readers of the halo copies are not interior
     _compare_single(got, dtype, False, 9)
 

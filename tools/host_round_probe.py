@@ -66,13 +66,15 @@ def main():
     wall = time.perf_counter() - t0
     run._all_reduce = ar
     run.run_pipelined(0, 0.05, m, 1e-4, 1e-4, 0.0)
-    out = {"workers": n, "rounds": R, "wall_us_per_round": wall / R * 1e6,
+    out = {"workers": n, "rounds": R, "transport": "rccl (engine)" if run.comm is not None else "process group", "wall_us_per_round": wall / R * 1e6,
            "host_us_per_round": {k: v / R * 1e6 for k, v in sorted(acc.items())},
-           # ("start" -- the process group's all-to-all call -- runs inside _start_exchange_lagged)
+           # ("start" -- the process group's all-to-all call -- runs inside _start_exchange_lagged; with the
+           # engine's own communicator that call is dopt_lagged_exchange and start / finish are not used)
            "host_us_per_round_total": sum(v for k, v in acc.items() if k != "start") / R * 1e6,
            "loop_issue_us_per_round": (issued[0] - t0) / R * 1e6 if issued else None}
     print(json.dumps(out))
     eng.close()
+    distributed.close_comms()
     torch.distributed.destroy_process_group()
 
 

@@ -198,6 +198,7 @@ def main():
     out.update({"steps": args.steps, "warmup": args.warmup, "legs": legs,
                 "proxy_over_fused": [b / a for a, b in zip(f, p)], "kernel": bench.kernel_name()})
     print(json.dumps(out), flush=True)
+    Dm.close_comms()
     dist.destroy_process_group()
     return 0
 
