@@ -531,3 +531,61 @@ def test_rccl_alltoall_halo_exchange_one_rank(tmp_path):
     mp.start_processes(_rccl_self_exchange, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True,
                        start_method="spawn")
     assert np.load(tmp_path / "ok.npy")[0]
+
+
+def _transport_errors(rank, world, port, out):
+    """The engine-driven transport's argument and state checks (ABI 7), on a world-1 communicator."""
+    import torch
+
+    import _dopt
+
+    torch.cuda.set_device(0)
+    res = {"library": _dopt.comm_library()}
+    eng = _dopt.Engine(0, "float64")
+    eng.generate_shards("logistic", 8, 16, 4, seed=3)
+    comm = _dopt.Comm(1, 0, 0, _dopt.comm_unique_id())
+    res["library"] = _dopt.comm_library()
+
+    def err(f):
+        try:
+            f()
+        except (ValueError, RuntimeError) as e:
+            return type(e).__name__ + ": " + str(e)
+        return None
+
+    res["no_transport"] = err(eng.lagged_exchange)
+    res["no_buffers"] = err(lambda: eng.lagged_transport(comm, [4], [4]))  # before dopt_set_halo
+    res["bad_shape"] = err(lambda: eng.lagged_transport(comm, [1, 1], [1, 1]))
+    send = torch.zeros((3, 16), dtype=torch.float64, device="cuda")
+    halo = torch.zeros((3, 16), dtype=torch.float64, device="cuda")
+    eng.set_halo(3, halo.data_ptr(), np.array([0, 1, 2], np.int32), send.data_ptr())
+    res["past_buffers"] = err(lambda: eng.lagged_transport(comm, [4], [3]))
+    res["negative"] = err(lambda: eng.lagged_transport(comm, [-1], [3]))
+    res["ok"] = err(lambda: eng.lagged_transport(comm, [3], [3]))
+    res["detach"] = err(lambda: eng.lagged_transport(None))
+    res["after_detach"] = err(eng.lagged_exchange)
+    comm.check()
+    comm.close()
+    eng.close()
+    np.save(os.path.join(out, "res.npy"), np.array([repr(res)]))
+
+
+def test_engine_transport_checks(tmp_path):
+    """dopt_lagged_transport / dopt_lagged_exchange refuse what they cannot do, with the reason: no transport
+    attached (DOPT_ERR_STATE), blocks past the send / halo buffers or negative (ValueError), a block list of
+    the wrong length; the RCCL library is the copy torch loaded (one RCCL in the process)."""
+    import ast
+
+    import torch.multiprocessing as mp
+
+    mp.start_processes(_transport_errors, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True,
+                       start_method="spawn")
+    res = ast.literal_eval(str(np.load(tmp_path / "res.npy")[0]))
+    assert "torch" in res["library"] and "rccl" in res["library"], res
+    assert "no transport" in res["no_transport"], res
+    assert res["no_buffers"].startswith("ValueError") and "past the buffers" in res["no_buffers"], res
+    assert res["bad_shape"].startswith("ValueError"), res
+    assert res["past_buffers"].startswith("ValueError") and "past the buffers" in res["past_buffers"], res
+    assert res["negative"].startswith("ValueError") and "negative" in res["negative"], res
+    assert res["ok"] is None and res["detach"] is None, res
+    assert "no transport" in res["after_detach"], res
