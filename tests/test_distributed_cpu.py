@@ -421,3 +421,68 @@ def test_rs_chunks_model(monkeypatch):
     monkeypatch.setattr(D, "RS_BOUNDARY_S", 1e-6)
     monkeypatch.setattr(D, "AR_BUSBW", 5e9)
     assert D.rs_chunks_for(8, pass_bytes=4e9) > 2
+
+
+class _Stream:
+    def __init__(self, done_after):
+        self.n, self.done_after, self.synced = 0, done_after, False
+
+    def query(self):
+        self.n += 1
+        return self.n > self.done_after
+
+    def synchronize(self):
+        self.synced = True
+
+
+class _Comm:
+    def __init__(self, error=None):
+        self.error, self.checks, self.closed = error, 0, None
+
+    def check(self):
+        self.checks += 1
+        if self.error:
+            raise RuntimeError(self.error)
+
+    def close(self, abort=False):
+        self.closed = "abort" if abort else "destroy"
+
+
+def test_engine_transport_wait_is_bounded(monkeypatch):
+    """With the engine's own RCCL communicator (no process-group watchdog) a chain's final wait polls the
+    stream: done -> returns; RCCL's asynchronous error -> CollectiveError; past DOPT_PG_TIMEOUT -> the
+    communicator aborted and CollectiveError naming the rank and the exchange.  Without the communicator
+    it is the stream's own synchronize()."""
+    import types
+
+    import time
+
+    fake = types.SimpleNamespace(plan=types.SimpleNamespace(rank=3),
+                                 exchange=types.SimpleNamespace(what="all_to_all_single of 5 rows"), comm=None)
+    s = _Stream(0)
+    D.DistributedDSGD._sync(fake, s)
+    assert s.synced
+    fake.comm = _Comm()
+    s = _Stream(5)
+    D.DistributedDSGD._sync(fake, s)
+    assert not s.synced and s.n == 6
+    clock = iter(np.arange(0.0, 1e4, 0.75))
+    monkeypatch.setattr(time, "monotonic", lambda: float(next(clock)))
+    fake.comm = _Comm(error="unhandled system error")
+    with pytest.raises(D.CollectiveError, match="rank 3: the engine's RCCL exchange failed"):
+        D.DistributedDSGD._sync(fake, _Stream(10 ** 9))
+    monkeypatch.setenv("DOPT_PG_TIMEOUT", "5")
+    fake.comm = _Comm()
+    with pytest.raises(D.CollectiveError, match="all_to_all_single of 5 rows.*did not finish in 5 s"):
+        D.DistributedDSGD._sync(fake, _Stream(10 ** 9))
+    assert fake.comm.closed == "abort" and fake.comm.checks >= 3
+
+
+def test_transport_kind(monkeypatch):
+    monkeypatch.delenv("DOPT_TRANSPORT", raising=False)
+    assert D.transport_kind() == "rccl"
+    monkeypatch.setenv("DOPT_TRANSPORT", "PG")
+    assert D.transport_kind() == "pg"
+    monkeypatch.setenv("DOPT_TRANSPORT", "mpi")
+    with pytest.raises(ValueError):
+        D.transport_kind()
