@@ -467,7 +467,8 @@ def _comm(group, dev):
     import torch
     import torch.distributed as dist
 
-    key = (None if group is None else id(group), int(dev.index))
+    # keyed by the group's member ranks (a group object that is gone cannot alias a new one's id)
+    key = (None if group is None else tuple(dist.get_process_group_ranks(group)), int(dev.index))
     c = _COMMS.get(key)
     if c is not None:
         return c

@@ -436,7 +436,9 @@ int dopt_lagged_exchange_issued(dopt_ctx *ctx, int *ordered);
  *   after dopt_set_halo and dopt_lagged_exchange_layout, whose rank and world must match comm's.
  * dopt_lagged_exchange: the round's exchange as one RCCL group on the side stream (the engine stream
  *   without one), ordered before the next dopt_lagged_mix / _tail as dopt_lagged_exchange_issued orders
- *   the caller's; where the caller would have issued its all-to-all. */
+ *   the caller's; where the caller would have issued its all-to-all.
+ * A context keeps the communicator it was given: destroy a communicator only after the contexts using it
+ * are closed or detached (dopt_lagged_transport(ctx, NULL, ...)) and their streams are idle. */
 #define DOPT_COMM_ID_BYTES 128
 int dopt_comm_unique_id(uint8_t *id_out, int64_t n);
 int dopt_comm_create(dopt_comm **out, int32_t world, int32_t rank, int32_t device, const uint8_t *id, int64_t n);
