@@ -400,6 +400,18 @@ PY
       bench_step r5sl_phase1_512_$rep 200 --no-cpu-baseline --no-secondary --scaling weak --phase --workers 512 \
         --steps 3000 --warmup 400
     done ;;
+  strong_long_tr)  # strong_long's legs with the engine's own RCCL communicator (default) and the process group's
+    # all-to-all (DOPT_TRANSPORT=pg) for the forced 512-worker phase round, interleaved twice -> profiles/r5_transport.txt
+    for rep in 1 2; do
+      bench_step r5slt_fused_4096_$rep 200 --no-cpu-baseline --no-secondary --scaling weak --workers 4096 \
+        --steps 400 --warmup 50
+      bench_step r5slt_fused_512_$rep 200 --no-cpu-baseline --no-secondary --scaling weak --workers 512 \
+        --steps 3000 --warmup 400
+      DOPT_FORCE_COLLECTIVES=1 bench_step r5slt_phase_512_rccl_$rep 200 --no-cpu-baseline --no-secondary --scaling weak \
+        --phase --workers 512 --steps 3000 --warmup 400
+      DOPT_TRANSPORT=pg DOPT_FORCE_COLLECTIVES=1 bench_step r5slt_phase_512_pg_$rep 200 --no-cpu-baseline --no-secondary \
+        --scaling weak --phase --workers 512 --steps 3000 --warmup 400
+    done ;;
   handoff_long)  # the hand-off forms of section 6 again in the steady state (512 workers, RCCL world 1 forced,
     # 3000 rounds after 400): events + side stream (default), one stream (DOPT_LAGGED_SIDE=0), the all-to-all on
     # the engine's stream (DOPT_A2A_STREAM=current), stream memory operations (DOPT_LAGGED_SYNC=value);
