@@ -532,7 +532,9 @@ def setup_leg(args, config, n_global, world, rank, dev):
                   "peers": [int(p) for p in runner._peers]}
         if S.mean is None:  # the lagged schedule: the column sums ride the halo all-to-all
             S.comm.update({"collectives_per_round": 1 if world > 1 else 0,
-                           "exchange": "one all_to_all_single per round: halo rows + every rank's column sums",
+                           "exchange": ("one RCCL group of per-peer sends / receives per round, issued by the engine "
+                                        "(dopt_lagged_exchange)" if runner.comm is not None else
+                                        "one all_to_all_single per round") + ": halo rows + every rank's column sums",
                            "colsum_bytes_per_peer_per_round": lay.ks * ld * esz_state,
                            "exchange_bytes_out_per_round": lay.n_send_rows * ld * esz_state})
         else:
