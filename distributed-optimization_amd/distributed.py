@@ -473,11 +473,23 @@ def _comm(group, dev):
     if c is not None:
         return c
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    buf = torch.zeros(_dopt.COMM_ID_BYTES, dtype=torch.uint8, device=dev)
+    # one byte of status ahead of the id: rank 0's failure reaches every rank instead of leaving them in the
+    # broadcast until the timeout
+    buf = torch.zeros(1 + _dopt.COMM_ID_BYTES, dtype=torch.uint8, device=dev)
+    err = None
     if rank == 0:
-        buf.copy_(torch.frombuffer(bytearray(_dopt.comm_unique_id()), dtype=torch.uint8))
+        try:
+            buf[1:].copy_(torch.frombuffer(bytearray(_dopt.comm_unique_id()), dtype=torch.uint8))
+        except RuntimeError as e:
+            err = e
+            buf[0] = 1
     src = 0 if group is None else dist.get_global_rank(group, 0)
     dist.broadcast(buf, src=src, group=group)
+    if err is not None:
+        raise err
+    if int(buf[0].item()) != 0:
+        raise RuntimeError("rank 0 could not create the engine's RCCL communicator id (DOPT_TRANSPORT=pg avoids it)")
+    buf = buf[1:]
     if not _COMMS:
         import atexit
 
