@@ -960,10 +960,11 @@ class DistributedDSGD:
             done = ch["done"]
             if upto > done:
                 self._all_reduce(partials[done:upto])
-            raw = partials[done:upto].cpu().numpy()
+        # the streams drained first (bounded: _sync), then the history rows copied out
         self._sync(self.stream)
         if self.side is not None:
             self._sync(self.side)  # no side-stream work outlives the call
+        raw = partials[done:upto].cpu().numpy()
         ch["g"], ch["done"] = G1, upto
         if tail:
             self._chain = None
