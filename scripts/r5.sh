@@ -432,6 +432,12 @@ PY
       -d gpurun_out/r5_hl_trace -o run -- python3 bench.py --no-cpu-baseline --no-secondary --scaling weak --phase \
       --workers 512 --steps 1500 --warmup 400 > gpurun_out/r5_hl_trace.log 2>&1 || die handoff_long 1
     python3 tools/trace_rounds.py gpurun_out/r5_hl_trace/run_kernel_trace.csv ;;
+  rccl_probe)  # host cost of RCCL's own group of sends / receives (tools/rccl_probe, built here beforehand:
+    # hipcc -O2 -o tools/rccl_probe tools/rccl_probe.cpp -I/opt/rocm/include/rccl -L/opt/rocm/lib -lrccl) vs the
+    # process group's all-to-all (tools/pg_a2a_probe.py), same sizes -> the head of profiles/r5_transport.txt
+    timeout -k 10 120 ./tools/rccl_probe > gpurun_out/r5_rccl_probe.txt 2>&1 || { tail -n 20 gpurun_out/r5_rccl_probe.txt; die rccl_probe 1; }
+    timeout -k 10 150 python3 tools/pg_a2a_probe.py >> gpurun_out/r5_rccl_probe.txt 2>&1 || { tail -n 20 gpurun_out/r5_rccl_probe.txt; die rccl_probe 1; }
+    grep -E "^bytes|^pg alltoall" gpurun_out/r5_rccl_probe.txt ;;
   transport_ab)  # the engine's own RCCL communicator (dopt_lagged_exchange, DOPT_TRANSPORT=rccl) vs the process
     # group's all-to-all-v (pg): the RCCL GPU tests, the host cost per round at 512 workers, and the rank proxy's
     # weak / strong legs, interleaved twice -> profiles/r5_transport.txt
