@@ -30,6 +30,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -2720,14 +2721,50 @@ int dopt_lagged_transport(dopt_ctx* c, dopt_comm* comm, const int64_t* send_rows
   return DOPT_OK;
 }
 
+#ifdef DOPT_AB
+// A/B builds, DOPT_HOST_TIMING=1: host time of dopt_lagged_exchange's RCCL group and hand-off record, and of
+// dopt_lagged_mix's wait for the exchange, printed at exit
+namespace {
+struct XpHostTiming {
+  double ns[3] = {0, 0, 0};
+  long calls[3] = {0, 0, 0};
+  bool on = getenv("DOPT_HOST_TIMING") && atoi(getenv("DOPT_HOST_TIMING")) != 0;
+  ~XpHostTiming() {
+    if (on && calls[0])
+      fprintf(stderr, "[dopt] lagged exchange host us per call: RCCL group %.2f, hand-off record %.2f (%ld calls); "
+              "engine wait for the exchange %.2f (%ld calls)\n", ns[0] / calls[0] / 1e3, ns[1] / calls[0] / 1e3,
+              calls[0], calls[2] ? ns[2] / calls[2] / 1e3 : 0.0, calls[2]);
+  }
+};
+XpHostTiming g_xht;
+double xht_now() {
+  return (double)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+}  // namespace
+#define XHT_BEGIN() const double xht_t0 = g_xht.on ? xht_now() : 0.0
+#define XHT_END(k) do { if (g_xht.on) { g_xht.ns[k] += xht_now() - xht_t0; g_xht.calls[k]++; } } while (0)
+#else
+#define XHT_BEGIN() do { } while (0)
+#define XHT_END(k) do { } while (0)
+#endif
+
 int dopt_lagged_exchange(dopt_ctx* c) {
   CHECK_ARG(c, "ctx is NULL");
   if (!c->xp) return fail(DOPT_ERR_STATE, "no transport (dopt_lagged_transport first)");
   int rc;
-  if ((rc = comm_exchange(c->xp, c->xp_ops.data(), c->xp_ops.size(), c->send, c->halo,
-                          c->lg_side ? c->lg_side : c->stream)))
-    return rc;
-  return c->lg_side ? lagged_mark_exchange(c) : DOPT_OK;  // (one stream: ordered by the stream itself)
+  {
+    XHT_BEGIN();
+    if ((rc = comm_exchange(c->xp, c->xp_ops.data(), c->xp_ops.size(), c->send, c->halo,
+                            c->lg_side ? c->lg_side : c->stream)))
+      return rc;
+    XHT_END(0);
+  }
+  if (!c->lg_side) return DOPT_OK;  // (one stream: ordered by the stream itself)
+  XHT_BEGIN();
+  rc = lagged_mark_exchange(c);
+  XHT_END(1);
+  return rc;
 }
 
 int dopt_lagged_side_stream(dopt_ctx* c, void* stream) {
@@ -2787,7 +2824,11 @@ int dopt_lagged_mix(dopt_ctx* c, int64_t t, double eta0, int consensus, double* 
   f.out_c = cons_out;
   f.out_l = loss_out;
   f.out_q = xnorm_out;
-  if ((rc = lagged_xwait(c))) return rc;
+  {
+    XHT_BEGIN();
+    if ((rc = lagged_xwait(c))) return rc;
+    XHT_END(2);
+  }
   HIPOK(launch_mixcs(c->dtype, a, c->G, (int)c->n, m, any ? &f : nullptr, c->stream, c->lg_side, c->lg_side_ev,
                      c->lg_side ? c->lg_sig[0] : nullptr, c->lg_side && c->lg_sig[0] ? ++c->lg_mseq : 0));
   c->xb ^= 1;
