@@ -486,3 +486,25 @@ def test_transport_kind(monkeypatch):
     monkeypatch.setenv("DOPT_TRANSPORT", "mpi")
     with pytest.raises(ValueError):
         D.transport_kind()
+
+
+@pytest.mark.parametrize("name,n,world,relabel", [("random_regular", 1024, 8, True), ("grid", 1024, 8, False),
+                                                  ("ring", 64, 8, False), ("random_regular", 96, 3, False)])
+def test_exchange_blocks_pair_up_across_ranks(name, n, world, relabel):
+    """The engine's RCCL transport (dopt_lagged_transport) issues one send of send_sizes[p] rows to each peer
+    p and one receive of recv_sizes[p] rows from it; RCCL point-to-point needs every send matched by a receive
+    of the same size on the peer, or the exchange hangs.  So across all ranks of a job, with and without the
+    column-sum rows: rank a's send block for b == rank b's receive block from a, and no rank sends to itself
+    at world > 1 (C3's spectrally partitioned random-regular graph and C4's torus -- the reference's 'grid' -- in strips at 8 ranks)."""
+    topo = _topo(name, n)
+    if relabel:
+        topo = TP.relabel(topo, D.partition_order(D.graph_partition(topo, world)))
+    plans = [D.build_plan(topo, world, r) for r in range(world)]
+    for ks in (0, 1, 2):
+        lays = [D.exchange_layout(p, ks) for p in plans]
+        for a in range(world):
+            assert lays[a].send_sizes[a] == 0 and lays[a].recv_sizes[a] == 0
+            for b in range(world):
+                assert lays[a].send_sizes[b] == lays[b].recv_sizes[a], (ks, a, b)
+                if ks:
+                    assert a == b or lays[a].send_sizes[b] >= ks  # every pair exchanges the sum rows
