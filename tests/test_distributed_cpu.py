@@ -495,7 +495,8 @@ def test_exchange_blocks_pair_up_across_ranks(name, n, world, relabel):
     p and one receive of recv_sizes[p] rows from it; RCCL point-to-point needs every send matched by a receive
     of the same size on the peer, or the exchange hangs.  So across all ranks of a job, with and without the
     column-sum rows: rank a's send block for b == rank b's receive block from a, and no rank sends to itself
-    at world > 1 (C3's spectrally partitioned random-regular graph and C4's torus -- the reference's 'grid' -- in strips at 8 ranks)."""
+    at world > 1 (C3's spectrally partitioned random-regular graph and C4's torus -- the reference's 'grid' --
+    in strips at 8 ranks)."""
     topo = _topo(name, n)
     if relabel:
         topo = TP.relabel(topo, D.partition_order(D.graph_partition(topo, world)))
