@@ -18,12 +18,13 @@ with the reference's legacy RNG stream ('dropin').
 
 Multi-GPU: `python3 bench.py --gpus N` starts N ranks itself (torch.distributed.run as a
 child process, before anything touches the GPU); under an external torch.distributed.run
-WORLD_SIZE must equal --gpus.  Weak scaling (`value`): ONE random 4-regular graph over
-4096 x N workers, graph-partitioned so each rank owns a contiguous slice; the halo rows of the
-iterates and every rank's column sums (for xbar) move in ONE all-to-all per round (RCCL), issued
-beside the gradient kernel (distributed.py's lagged schedule; C5's complete graph all-reduces the
-column sums instead).  Strong scaling (`strong`, N > 1): the
-metric's literal N = 4096 workers in total over the N ranks, same graph construction.
+WORLD_SIZE must equal --gpus.  `value` at every N is the metric's configuration, strong scaling:
+N = 4096 workers IN TOTAL over the N ranks (4096 / N each), ONE random 4-regular graph,
+graph-partitioned so each rank owns a contiguous slice; the halo rows of the iterates and every
+rank's column sums (for xbar) move in ONE exchange per round (RCCL), issued beside the gradient
+kernel (distributed.py's lagged schedule; C5's complete graph all-reduces the column sums
+instead).  Weak scaling (`weak`, N > 1, secondary): 4096 workers PER GPU, 4096 x N in all, same
+graph construction.
 
 Prints ONE JSON line on rank 0 (driver contract), with `roofline` for the fused
 round kernel (HIP-event timed, same timed region) and `cpu_baseline` (the oracle,
@@ -393,14 +394,11 @@ def dropin_leg(eng, n, d, m, lam, eta0, rounds=128, batch=None, reps=5):
 
 
 # ---------------------------------------------------------------------------- launch
-def _free_port():
-    import socket
+def _solo_store():
+    """Rendezvous of a one-rank process group: an in-process store (no port at all)."""
+    import torch.distributed as dist
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+    return dist.HashStore()
 
 
 def launch_ranks(n, argv, limit_s):
@@ -410,8 +408,11 @@ def launch_ranks(n, argv, limit_s):
     it.  The child gets its own process group, ended whole if it outlives `limit_s`."""
     import signal
 
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+    # --standalone: the launcher's agent binds its rendezvous store on port 0 itself and the ranks reuse that
+    # store (TORCHELASTIC_USE_AGENT_STORE), so no port is picked and released before rank 0 binds it (the
+    # EADDRINUSE race of a pre-picked --master-port, VERDICT r5)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--nnodes=1", f"--nproc-per-node={n}",
+           "--local-addr", "127.0.0.1", os.path.abspath(__file__)] + argv
     log(f"launching {n} ranks: {' '.join(cmd[1:])}")
     p = subprocess.Popen(cmd, start_new_session=True)
     try:
@@ -440,10 +441,10 @@ def dry_launch(args, rank, world, local):
 
     import distributed
 
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    if "MASTER_PORT" not in os.environ:
-        os.environ["MASTER_PORT"] = str(_free_port())
-    distributed.init_process_group("gloo", rank=rank, world_size=world)
+    if world == 1:
+        distributed.init_process_group("gloo", store=_solo_store(), rank=0, world_size=1)
+    else:
+        distributed.init_process_group("gloo", rank=rank, world_size=world)
     me = {"rank": rank, "local_rank": local, "pid": os.getpid(), "host": socket.gethostname()}
     every = [None] * world
     dist.all_gather_object(every, me)
@@ -585,7 +586,7 @@ def per_rank(world, item):
 
 
 def serial_exchange_leg(args, S, world, barrier, dev):
-    """N > 1, after the weak leg, on its engine and shards: the same rounds with the exchange serialised on
+    """N > 1, after the headline leg, on its engine and shards: the same rounds with the exchange serialised on
     the engine stream (DOPT_LAGGED_SIDE=0 DOPT_A2A_STREAM=current: the all-to-all between the mix and the next
     gradient kernel instead of beside it).  On one GPU the RCCL kernel beside the gradient kernel cost that
     kernel up to ~70 us per round on some boxes (tools/rank_proxy.py) while a serial exchange
@@ -624,7 +625,7 @@ def serial_exchange_leg(args, S, world, barrier, dev):
 
 def transport_probe(args, world, dev, barrier, shape, reps=20, warm=3):
     """After the timed legs (N > 1): the round's collectives alone on this node's transport, so a scaling
-    run also measures what one GPU per call cannot -- the weak leg's exchange (one all_to_all_single with
+    run also measures what one GPU per call cannot -- the headline leg's exchange (one all_to_all_single with
     that leg's per-peer row blocks) and C5's all-reduce of 2^20 float64 column sums (8 MiB; the chunk model
     of distributed.rs_chunks_for assumes its cost).  Each timed `reps` times back to back after `warm`,
     bracketed by barrier + sync; the max over ranks."""
@@ -659,16 +660,18 @@ def transport_probe(args, world, dev, barrier, shape, reps=20, warm=3):
             "alltoall_GBps_out_per_rank": out_bytes / (a2a * 1e-3) / 1e9 if a2a > 0 else None,
             "allreduce_8MiB_ms": ar,
             "allreduce_busbw_GBps": 2.0 * (world - 1) / world * (8 << 20) / (ar * 1e-3) / 1e9 if ar > 0 else None,
-            "note": "the weak leg's exchange and C5's column-sum all-reduce alone, after the timed legs"}
+            "note": "the headline leg's exchange and C5's column-sum all-reduce alone, after the timed legs"}
 
 
-def strong_leg(args, world, rank, dev, barrier):
-    """The metric's literal configuration: N = args.strong_workers (4096) workers in TOTAL over
-    the ranks (4096 / world each), the same random 4-regular graph construction and spectral
-    partition as the weak-scaling leg; every rank's kernel time and halo bytes are reported."""
+def extra_leg(args, world, rank, dev, barrier, scaling):
+    """The C3 leg that is not the headline at N > 1: "weak" (args.workers PER GPU, args.workers x world in
+    all; --scaling weak makes it the headline instead) or "strong" (args.strong_workers = 4096 in TOTAL over
+    the ranks: the metric's configuration, the headline by default) -- the same random 4-regular graph
+    construction and spectral partition; every rank's kernel time and halo bytes are reported."""
     import _dopt
 
-    S = setup_leg(args, "c3", args.strong_workers, world, rank, dev)
+    n_global = args.workers * world if scaling == "weak" else args.strong_workers
+    S = setup_leg(args, "c3", n_global, world, rank, dev)
     try:
         dt, launches, kr_ms, every, obj, cons = run_leg(S, args, world, barrier, dev)
         kname = kernel_name()
@@ -683,7 +686,7 @@ def strong_leg(args, world, rank, dev, barrier):
         ranks = per_rank(world, mine)
         return {"value": S.n_global * args.steps / dt, "unit": "worker-iters/s", "n_workers_total": S.n_global,
                 "workers_per_gpu": S.n_global / world, "ms_per_step": dt / args.steps * 1e3,
-                "scaling": "strong", "kernel": kname, "per_rank": ranks,
+                "scaling": scaling, "kernel": kname, "per_rank": ranks,
                 "final_objective": float(obj[-1]), "final_consensus": float(cons[-1]),
                 "dtype": "f32" if S.eng.dtype == _dopt.F32 else "f64", "workload": S.workload}
     finally:
@@ -700,11 +703,12 @@ def main():
     ap.add_argument("--steps", type=int, default=300,
                     help="rounds timed (one run: the last round's metrics pass is amortised over them)")
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workers", type=int, default=4096, help="workers per GPU (C3 weak scaling)")
+    ap.add_argument("--workers", type=int, default=4096, help="workers per GPU (C3 weak-scaling leg)")
     ap.add_argument("--strong-workers", type=int, default=4096,
-                    help="C3 strong-scaling leg at N > 1: workers in total (the metric's N = 4096)")
+                    help="C3 strong scaling (the headline): workers in total over the N GPUs (the metric's N = 4096)")
     ap.add_argument("--scaling", default="both", choices=["weak", "strong", "both"],
-                    help="C3 at N > 1: the weak leg (value), the strong leg (under 'strong'), or both")
+                    help="C3 at N > 1: 'both' (default): value = the strong leg (the metric's 4096 workers in all), "
+                         "the weak leg under 'weak'; 'strong' / 'weak': that leg alone, as value")
     ap.add_argument("--d", type=int, default=1024)
     ap.add_argument("--m", type=int, default=512)
     ap.add_argument("--dtype", default="float64", help="iterates and arithmetic (the reference: float64)")
@@ -719,7 +723,7 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=0, help="CPU baseline processes (0: the box's CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-alt-exchange", action="store_true",
-                    help="N > 1: skip the weak leg's second timing with the exchange serialised on the engine stream")
+                    help="N > 1: skip the headline leg's second timing with the exchange serialised on the engine stream")
     ap.add_argument("--no-secondary", action="store_true",
                     help="N=1: skip the f64-storage / f32 legs, the f(x*) solver and the drop-in trainer leg")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (gloo: 1-GPU rehearsal)")
@@ -785,9 +789,7 @@ def main():
     if world > 1 or args.phase:
         torch.cuda.set_device(dev)
         if world == 1:  # --phase on one GPU: the multi-GPU code path incl. RCCL (one rank)
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", str(_free_port()))
-            distributed.init_process_group(args.backend, rank=0, world_size=1)
+            distributed.init_process_group(args.backend, store=_solo_store(), rank=0, world_size=1)
         else:
             distributed.init_process_group(args.backend)
 
@@ -799,10 +801,10 @@ def main():
                 dist.barrier()
         torch.cuda.synchronize(dev)
 
-    weak = args.config != "c3" or world == 1 or args.scaling != "strong"
-    n_global = {"c3": args.workers * world, "c4": 65536, "c5": 1024}[args.config]
-    if not weak:  # --scaling strong: the strong leg is the headline
-        n_global = args.strong_workers
+    # C3: the headline is the strong leg (the metric's 4096 workers in all, over the N GPUs) unless --scaling weak;
+    # at N = 1 the two coincide when --workers == --strong-workers (the default 4096)
+    weak = args.config == "c3" and args.scaling == "weak"
+    n_global = {"c3": args.workers * world if weak else args.strong_workers, "c4": 65536, "c5": 1024}[args.config]
     S = setup_leg(args, args.config, n_global, world, rank, dev)
     eng, plan, d, m, b, lam, eta0, top = S.eng, S.plan, S.d, S.m, S.b, S.lam, S.eta0, S.top
     n = plan.n_local
@@ -830,7 +832,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak" if args.config == "c3" and weak else "strong",
+        "scaling": "weak" if weak else "strong",
         "vs_baseline": None,
         "dtype": "f32" if esz == 4 else "f64",
         "data": (f"synthetic (device-generated X~N(0,1){' rounded to float32' if xesz == 4 else ''} + bias column, "
@@ -876,13 +878,13 @@ def main():
     if args.config != "c3":
         out["metric"] = f"worker-iters/sec ({args.config.upper()}, secondary config)"
     secondary = rank == 0 and world == 1 and not args.phase and args.config == "c3" and not args.no_secondary
-    if world > 1 and args.config == "c3" and weak and S.flush is not None and not args.no_alt_exchange:
-        log("weak leg again with the exchange serialised on the engine stream (A/B with real peers)")
+    if world > 1 and args.config == "c3" and S.flush is not None and not args.no_alt_exchange:
+        log("headline leg again with the exchange serialised on the engine stream (A/B with real peers)")
         try:  # diagnostic only: a failure here must not cost the line its value
-            out["weak_serial_exchange"] = serial_exchange_leg(args, S, world, barrier, dev)
+            out["serial_exchange"] = serial_exchange_leg(args, S, world, barrier, dev)
         except Exception as e:  # noqa: BLE001
-            log(f"weak_serial_exchange failed: {e!r}")
-            out["weak_serial_exchange"] = {"error": repr(e)[:300]}
+            log(f"serial_exchange failed: {e!r}")
+            out["serial_exchange"] = {"error": repr(e)[:300]}
     if secondary and b == m:
         log("f(x*): device L-BFGS")
         out["suboptimality"] = suboptimality(eng, lam, float(obj[-1]))
@@ -896,11 +898,11 @@ def main():
     if args.pcie and world == 1 and args.config == "c3":
         out["pcie"] = pcie_leg(eng, top, n, d, m, b, lam, eta0, args.steps, dt)
     eng.close()
-    if args.config == "c3" and world > 1 and weak and args.scaling == "both":
-        log(f"strong-scaling leg: {args.strong_workers} workers over {world} ranks")
-        out["strong"] = strong_leg(args, world, rank, dev, barrier)
+    if args.config == "c3" and world > 1 and args.scaling == "both":
+        log(f"weak-scaling leg: {args.workers} workers per rank, {args.workers * world} over {world} ranks")
+        out["weak"] = extra_leg(args, world, rank, dev, barrier, "weak")
     if world > 1 and getattr(S, "exchange_shape", None) is not None:
-        log("transport probe: the weak leg's all-to-all and an 8 MiB all-reduce alone")
+        log("transport probe: the headline leg's exchange and an 8 MiB all-reduce alone")
         try:  # diagnostic only, as above
             out["transport_probe"] = transport_probe(args, world, dev, barrier, S.exchange_shape)
         except Exception as e:  # noqa: BLE001
@@ -920,7 +922,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
         log("cpu baseline")
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.cpu_procs or None)
-    out["setup_s"] = setup_s  # rank 0: process start -> the weak / headline leg's warmup
+    out["setup_s"] = setup_s  # rank 0: process start -> the headline leg's warmup
     out["wall_s"] = time.time() - T_START  # rank 0: process start -> this line
     if rank == 0:
         print(json.dumps(out), flush=True)

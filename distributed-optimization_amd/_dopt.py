@@ -13,6 +13,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+import weakref
 
 import numpy as np
 
@@ -111,7 +112,7 @@ _SIGS = {
     "dopt_phase_interior_count": ([_P, _P], ctypes.c_int),
     "dopt_host_digest": ([_I32, _P, _P, _I32, _P], ctypes.c_int),
     "dopt_comm_unique_id": ([_P, _I64], ctypes.c_int),
-    "dopt_comm_create": ([_P, _I32, _I32, _I32, _P, _I64], ctypes.c_int),
+    "dopt_comm_create": ([_P, _I32, _I32, _I32, _P, _I64, ctypes.c_double], ctypes.c_int),
     "dopt_comm_check": ([_P], ctypes.c_int),
     "dopt_comm_destroy": ([_P, _I32], ctypes.c_int),
     "dopt_comm_library": ([], ctypes.c_char_p),
@@ -119,7 +120,7 @@ _SIGS = {
     "dopt_lagged_exchange": ([_P], ctypes.c_int),
 }
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 7  # DOPT_ABI_VERSION of include/dopt.h
+ABI_VERSION = 8  # DOPT_ABI_VERSION of include/dopt.h
 
 
 def lib():
@@ -198,25 +199,41 @@ def comm_library():
 
 class Comm:
     """An RCCL communicator the engine drives itself (dopt_comm_create; csrc/transport.cpp): rank `rank` of
-    `world` on `device`, from rank 0's comm_unique_id() -- every rank constructs it with the same id."""
+    `world` on `device`, from rank 0's comm_unique_id() -- every rank constructs it with the same id.  Its
+    setup waits at most `timeout_s` seconds for the other ranks (0: unbounded), then raises RuntimeError."""
 
-    def __init__(self, world, rank, device, uid):
+    def __init__(self, world, rank, device, uid, timeout_s=0.0):
         if len(uid) != COMM_ID_BYTES:
             raise ValueError(f"RCCL unique id of {COMM_ID_BYTES} bytes expected, got {len(uid)}")
         h = ctypes.c_void_p()
         buf = (ctypes.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
-        check(lib().dopt_comm_create(ctypes.byref(h), int(world), int(rank), int(device), buf, COMM_ID_BYTES))
+        check(lib().dopt_comm_create(ctypes.byref(h), int(world), int(rank), int(device), buf, COMM_ID_BYTES,
+                                     float(timeout_s)))
         self._h = h
         self.world, self.rank, self.device = int(world), int(rank), int(device)
+        self.users = weakref.WeakSet()  # engines whose exchange runs through it (Engine.lagged_transport)
+
+    @property
+    def closed(self):
+        return not getattr(self, "_h", None)
 
     def check(self):
         """Raise if RCCL reported an asynchronous error on this communicator."""
+        if self.closed:
+            raise RuntimeError("the RCCL communicator is closed")
         check(lib().dopt_comm_check(self._h))
 
     def close(self, abort=False):
-        h, self._h = getattr(self, "_h", None), None
-        if h:
-            check(lib().dopt_comm_destroy(h, 1 if abort else 0))
+        """Detach every engine still routed through it (so none can reach the freed communicator: its next
+        dopt_lagged_exchange fails with 'no transport'), then destroy it (abort: without waiting for
+        pending work, after a peer failed).  The caller drains the engines' streams first unless aborting."""
+        h = getattr(self, "_h", None)
+        if not h:
+            return
+        for eng in list(self.users):
+            eng.lagged_transport(None)
+        self._h = None
+        check(lib().dopt_comm_destroy(h, 1 if abort else 0))
 
 
 def device_count():
@@ -302,6 +319,10 @@ class Engine:
         if getattr(self, "_h", None):
             lib().dopt_destroy(self._h)
             self._h = None
+        comm = getattr(self, "_comm", None)
+        if comm is not None:
+            comm.users.discard(self)
+            self._comm = None
 
     def __del__(self):  # pragma: no cover - interpreter shutdown order varies
         try:
@@ -564,14 +585,25 @@ class Engine:
     def lagged_transport(self, comm, send_rows=None, recv_rows=None):
         """dopt_lagged_transport: route the exchange through `comm` (a Comm; None: detach), blocks of
         send_rows[p] / recv_rows[p] rows per peer p in rank order."""
+        old = getattr(self, "_comm", None)
         if comm is None:
-            check(lib().dopt_lagged_transport(self._h, None, None, None))
+            if self._h:  # (a closed context holds no transport)
+                check(lib().dopt_lagged_transport(self._h, None, None, None))
+            if old is not None:
+                old.users.discard(self)
+            self._comm = None
             return
+        if comm.closed:
+            raise ValueError("the RCCL communicator is closed")
         s = np.ascontiguousarray(send_rows, dtype=np.int64)
         r = np.ascontiguousarray(recv_rows, dtype=np.int64)
         if s.shape != (comm.world,) or r.shape != (comm.world,):
             raise ValueError(f"{comm.world} block sizes per direction expected")
         check(lib().dopt_lagged_transport(self._h, comm._h, _ptr(s), _ptr(r)))
+        if old is not None and old is not comm:
+            old.users.discard(self)
+        comm.users.add(self)
+        self._comm = comm
 
     def lagged_exchange(self):
         """dopt_lagged_exchange: the round's exchange through the attached communicator."""

@@ -66,6 +66,19 @@ def _maybe_init_distributed():
     return True
 
 
+def _finish_distributed():
+    """The engine's RCCL communicators (devices drained, engines detached), then the process group."""
+    import os
+
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        import torch.distributed as dist
+
+        import distributed
+
+        distributed.close_comms()
+        dist.destroy_process_group()
+
+
 if __name__ == "__main__":
     reporter = _maybe_init_distributed()
     np.random.seed(203)
@@ -73,3 +86,4 @@ if __name__ == "__main__":
     simulator.run_all()
     if reporter:
         simulator.plot_results()
+    _finish_distributed()

@@ -51,8 +51,10 @@ extern "C" {
  *      the next round's pass over a chunk starts while later chunks' sums are still being reduced).
  *   7  round 5: the engine-driven RCCL transport (dopt_comm_*, dopt_lagged_transport,
  *      dopt_lagged_exchange): the lagged schedule's exchange as RCCL sends / receives issued by the
- *      engine on its side stream, without the process group's per-call cost. */
-#define DOPT_ABI_VERSION 7
+ *      engine on its side stream, without the process group's per-call cost.
+ *   8  round 6: dopt_comm_create takes timeout_s -- the communicator is created non-blocking and its
+ *      setup, a peer's first connection and its destroy are each bounded by that time. */
+#define DOPT_ABI_VERSION 8
 
 typedef struct dopt_ctx dopt_ctx;
 typedef struct dopt_comm dopt_comm; /* an RCCL communicator the engine drives itself (ABI 7) */
@@ -427,8 +429,12 @@ int dopt_lagged_exchange_issued(dopt_ctx *ctx, int *ordered);
  * dopt_comm_unique_id: rank 0's RCCL unique id (DOPT_COMM_ID_BYTES bytes), which the caller hands to every
  *   rank (the job's existing process group broadcasts it).
  * dopt_comm_create: RCCL communicator of rank `rank` of `world` on `device`; collective -- every rank
- *   calls it with the same id.  dopt_comm_destroy (abort = 1: without waiting for pending work, after a
- *   peer failed); dopt_comm_check: DOPT_ERR_COMM if RCCL reported an asynchronous error.
+ *   calls it with the same id.  Created non-blocking (ncclCommInitRankConfig, blocking = 0) and waited
+ *   for at most timeout_s seconds (0: unbounded): a rank that never joins ends the others' call with
+ *   DOPT_ERR_COMM, the half-built communicator aborted, instead of a hang.  The same bound applies to an
+ *   exchange's first connection to a peer and to dopt_comm_destroy's finalize.
+ *   dopt_comm_destroy (abort = 1: without waiting for pending work, after a peer failed);
+ *   dopt_comm_check: DOPT_ERR_COMM if RCCL reported an asynchronous error.
  * dopt_comm_library: the path of the RCCL library in use (the process's copy when one is loaded).
  * dopt_lagged_transport: route the context's exchange through comm (NULL: detach): per peer p in rank
  *   order, send_rows[p] rows of the send buffer go to p and recv_rows[p] rows of the halo buffer come
@@ -441,7 +447,8 @@ int dopt_lagged_exchange_issued(dopt_ctx *ctx, int *ordered);
  * are closed or detached (dopt_lagged_transport(ctx, NULL, ...)) and their streams are idle. */
 #define DOPT_COMM_ID_BYTES 128
 int dopt_comm_unique_id(uint8_t *id_out, int64_t n);
-int dopt_comm_create(dopt_comm **out, int32_t world, int32_t rank, int32_t device, const uint8_t *id, int64_t n);
+int dopt_comm_create(dopt_comm **out, int32_t world, int32_t rank, int32_t device, const uint8_t *id, int64_t n,
+                     double timeout_s);
 int dopt_comm_check(dopt_comm *comm);
 int dopt_comm_destroy(dopt_comm *comm, int32_t abort);
 const char *dopt_comm_library(void);

@@ -3,7 +3,6 @@
 torch.distributed send/recv of the halo rows; the result must equal the
 unpartitioned oracle round bit for bit (last paragraph)."""
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -18,12 +17,16 @@ CFG = {"problem_type": "logistic", "local_batch_size": 7, "learning_rate_eta0": 
        "l2_regularization_lambda": 1e-3, "strong_convexity_mu": 1e-3}
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+_RDV_N = 0
+
+
+def _rdv(tmp_path):
+    """init_method of a multi-process test: a FileStore in the test's own tmp_path.  No port is picked
+    before the ranks start, so nothing on the box can take it in between (a port released
+    by a pre-pick and taken before rank 0's TCPStore bound it -> EADDRINUSE)."""
+    global _RDV_N
+    _RDV_N += 1
+    return f"file://{tmp_path}/pg_store_{os.getpid()}_{_RDV_N}"
 
 
 def _data(n, d=6, m=7, seed=0):
@@ -36,11 +39,11 @@ def _topo(name, n):
     return TP.random_regular(n, 4, seed=3) if name == "random_regular" else TP.build(name, n)
 
 
-def _rank_main(rank, world, port, name, n, T, out):
-    _rank_main_topo(rank, world, port, _topo(name, n), T, out)
+def _rank_main(rank, world, rdv, name, n, T, out):
+    _rank_main_topo(rank, world, rdv, _topo(name, n), T, out)
 
 
-def _rank_main_topo(rank, world, port, topo, T, out, collective=False):
+def _rank_main_topo(rank, world, rdv, topo, T, out, collective=False):
     """The round restated in numpy over the product's exchange: the halo plan, its ExchangeLayout
     (per peer: the plan's rows, then one row of this rank's column sums) and HaloExchange over gloo
     (per-peer isend / irecv, or with `collective` the all_to_all_single the RCCL path issues).
@@ -48,8 +51,7 @@ def _rank_main_topo(rank, world, port, topo, T, out, collective=False):
     _run_lagged / k_mixcs) and saves it with its final iterates."""
     import torch
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=rdv, rank=rank, world_size=world)
     n = topo.n
     plan = D.build_plan(topo, world, rank)
     lay = D.exchange_layout(plan, 1)
@@ -109,7 +111,7 @@ def _check_ranks(tmp_path, topo, world, T):
                                           ("fully_connected", 9, 2)])
 def test_partitioned_rounds_match_oracle(tmp_path, name, n, world):
     T = 4
-    mp.start_processes(_rank_main, args=(world, _free_port(), name, n, T, str(tmp_path)), nprocs=world,
+    mp.start_processes(_rank_main, args=(world, _rdv(tmp_path), name, n, T, str(tmp_path)), nprocs=world,
                        join=True, start_method="fork")
     _check_ranks(tmp_path, _topo(name, n), world, T)
 
@@ -125,7 +127,7 @@ def test_eight_ranks_match_oracle(tmp_path, name, n, collective):
     topo = _topo(name, n)
     if name == "random_regular":
         topo = TP.relabel(topo, D.partition_order(D.graph_partition(topo, world)))
-    mp.start_processes(_rank_main_topo, args=(world, _free_port(), topo, T, str(tmp_path), collective), nprocs=world,
+    mp.start_processes(_rank_main_topo, args=(world, _rdv(tmp_path), topo, T, str(tmp_path), collective), nprocs=world,
                        join=True, start_method="fork")
     _check_ranks(tmp_path, topo, world, T)
     for r in range(world):
@@ -172,7 +174,7 @@ def test_graph_partition_balanced_and_better_than_ranges(n, parts):
     assert halo_new < halo_old
 
 
-def _rank_skip_send(rank, world, port, timeout_s, out):
+def _rank_skip_send(rank, world, rdv, timeout_s, out):
     """Rank 1 never sends its halo rows; then every rank joins an all-reduce.  Each rank writes
     the error it ended with and exits non-zero."""
     import sys
@@ -180,8 +182,8 @@ def _rank_skip_send(rank, world, port, timeout_s, out):
 
     import torch
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DOPT_PG_TIMEOUT=str(timeout_s))
-    D.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ.update(DOPT_PG_TIMEOUT=str(timeout_s))
+    D.init_process_group("gloo", init_method=rdv, rank=rank, world_size=world)
     topo = TP.ring(8)
     plan = D.build_plan(topo, world, rank)
     send = torch.zeros((max(1, len(plan.send_ids)), 3), dtype=torch.float64)
@@ -216,7 +218,7 @@ def test_a_rank_that_skips_its_send_ends_both_ranks_within_the_timeout(tmp_path)
 
     timeout_s = 4
     t0 = time.time()
-    ctx = mp.start_processes(_rank_skip_send, args=(2, _free_port(), timeout_s, str(tmp_path)), nprocs=2,
+    ctx = mp.start_processes(_rank_skip_send, args=(2, _rdv(tmp_path), timeout_s, str(tmp_path)), nprocs=2,
                              join=False, start_method="fork")
     for p in ctx.processes:
         p.join(60)
@@ -234,19 +236,18 @@ def test_relabelled_rounds_match_oracle(tmp_path):
     """Partitioned rounds on a relabelled graph are the oracle's rounds on that graph."""
     n, world, T = 24, 3, 4
     topo = TP.relabel(_topo("random_regular", n), D.partition_order(D.graph_partition(_topo("random_regular", n), world)))
-    mp.start_processes(_rank_main_topo, args=(world, _free_port(), topo, T, str(tmp_path)), nprocs=world,
+    mp.start_processes(_rank_main_topo, args=(world, _rdv(tmp_path), topo, T, str(tmp_path)), nprocs=world,
                        join=True, start_method="fork")
     _check_ranks(tmp_path, topo, world, T)
 
 
-def _rank_alltoall(rank, world, port, topo, out):
+def _rank_alltoall(rank, world, rdv, topo, out):
     """HaloExchange's RCCL form (one all_to_all_single per round over the peer-grouped buffers),
     driven over gloo on CPU tensors: every halo row must arrive holding its global id -- in the plain
     layout and in the lagged schedule's (a sum row per peer, holding the sender's rank + 1000)."""
     import torch
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=rdv, rank=rank, world_size=world)
     plan = D.build_plan(topo, world, rank)
     for ks in (0, 1):
         lay = D.exchange_layout(plan, ks)
@@ -280,7 +281,7 @@ def test_alltoall_halo_layout(tmp_path, name, n, world):
         topo = TP.Topology("two_rings", nb)
     else:
         topo = _topo(name, n)
-    mp.start_processes(_rank_alltoall, args=(world, _free_port(), topo, str(tmp_path)), nprocs=world, join=True,
+    mp.start_processes(_rank_alltoall, args=(world, _rdv(tmp_path), topo, str(tmp_path)), nprocs=world, join=True,
                        start_method="fork")
     for r in range(world):
         plan = D.build_plan(topo, world, r)
@@ -293,13 +294,13 @@ def test_alltoall_halo_layout(tmp_path, name, n, world):
         assert D.build_plan(topo, world, 2).peers() == []
 
 
-def _rank_self_block(rank, world, port, out):
+def _rank_self_block(rank, world, rdv, out):
     """World 1, collectives forced (the one-GPU rehearsal of the RCCL path): a self block -- plan rows
     sent to the rank itself plus its own sum row -- through the all-to-all-v (over gloo here)."""
     import torch
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DOPT_FORCE_COLLECTIVES="1")
-    dist.init_process_group("gloo", rank=0, world_size=1)
+    os.environ.update(DOPT_FORCE_COLLECTIVES="1")
+    dist.init_process_group("gloo", init_method=rdv, rank=0, world_size=1)
     S = np.array([0, 3, 6, 9])
     plan = D.HaloPlan(0, 1, np.array([0, 12]), 0, 12, S.astype(np.int64), np.array([0, 4]), S.astype(np.int32),
                       np.array([0, 4]), None, None, None)
@@ -320,7 +321,7 @@ def _rank_self_block(rank, world, port, out):
 def test_self_block_exchange_world1(tmp_path):
     """exchange_layout(self_block=True): the rank's block holds its plan rows, then its sum rows, and
     the all-to-all copies it onto itself (distributed.DistributedDSGD at RCCL world 1, forced)."""
-    mp.start_processes(_rank_self_block, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True,
+    mp.start_processes(_rank_self_block, args=(1, _rdv(tmp_path), str(tmp_path)), nprocs=1, join=True,
                        start_method="fork")
     np.testing.assert_array_equal(np.load(tmp_path / "self.npy"), np.arange(15.0).reshape(5, 3))
     # without the self block a world-1 plan has no rows to move and no sum rows
@@ -472,10 +473,11 @@ def test_engine_transport_wait_is_bounded(monkeypatch):
     with pytest.raises(D.CollectiveError, match="rank 3: the engine's RCCL exchange failed"):
         D.DistributedDSGD._sync(fake, _Stream(10 ** 9))
     monkeypatch.setenv("DOPT_PG_TIMEOUT", "5")
-    fake.comm = _Comm()
+    c = fake.comm = _Comm()
     with pytest.raises(D.CollectiveError, match="all_to_all_single of 5 rows.*did not finish in 5 s"):
         D.DistributedDSGD._sync(fake, _Stream(10 ** 9))
-    assert fake.comm.closed == "abort" and fake.comm.checks >= 3
+    assert c.closed == "abort" and c.checks >= 3
+    assert fake.comm is None  # the runner no longer holds the aborted communicator
 
 
 def test_transport_kind(monkeypatch):

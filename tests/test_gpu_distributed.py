@@ -4,7 +4,6 @@ single-context fused run bit for bit, the metrics to rtol 1e-12 (reordered sums)
 Full-shard CSR runs take the lagged schedule (distributed.py: _run_lagged; T = 1 and 2
 are its edge cases), DOPT_LAGGED=0 the serial one, the complete graph the serial one."""
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -23,15 +22,19 @@ def _engine(dtype):
     return _dopt.Engine(0, dtype)
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+_RDV_N = 0
 
 
-def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, D=D, M=M, backend="gloo"):
+def _rdv(tmp_path):
+    """init_method of a multi-process test: a FileStore in the test's own tmp_path.  No port is picked
+    before the ranks start, so nothing on the box can take it in between (a port released
+    by a pre-pick and taken before rank 0's TCPStore bound it -> EADDRINUSE)."""
+    global _RDV_N
+    _RDV_N += 1
+    return f"file://{tmp_path}/pg_store_{os.getpid()}_{_RDV_N}"
+
+
+def _rank_main(rank, world, rdv, dtype, out, mean=False, T=T, lagged="1", N=N, D=D, M=M, backend="gloo"):
     import torch  # noqa: F401  (one HIP runtime, loaded before libdopt)
     import torch.distributed as dist
 
@@ -49,12 +52,12 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
     # communicator (dopt_lagged_exchange, the default)
     transport = "pg" if "pg" in opts else "rccl"
     lagged = opts[0]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DOPT_LAGGED=lagged, DOPT_LAGGED_SIDE=side,
+    os.environ.update(DOPT_LAGGED=lagged, DOPT_LAGGED_SIDE=side,
                       DOPT_LAGGED_SYNC=sync, DOPT_A2A_STREAM=a2a, DOPT_TRANSPORT=transport,
                       DOPT_FORCE_COLLECTIVES="1" if backend == "nccl" else "0")
     if backend == "nccl":
         torch.cuda.set_device(0)
-    dist.init_process_group(backend, rank=rank, world_size=world)
+    dist.init_process_group(backend, init_method=rdv, rank=rank, world_size=world)
     top = _topo(mean, N, world if os.environ.get("DOPT_TEST_PARTITION") == "1" else 0)
     plan = Dm.build_plan(top, world, rank)
     if os.environ.get("DOPT_TEST_SELF_HALO") == "1":  # world 1: a third of the rows through the exchange
@@ -113,7 +116,7 @@ def _rank_main(rank, world, port, dtype, out, mean=False, T=T, lagged="1", N=N, 
 def test_ranks_match_single_context(tmp_path, dtype, mean, T, lagged, world):
     import torch.multiprocessing as mp
 
-    mp.start_processes(_rank_main, args=(world, _free_port(), dtype, str(tmp_path), mean, T, lagged), nprocs=world,
+    mp.start_processes(_rank_main, args=(world, _rdv(tmp_path), dtype, str(tmp_path), mean, T, lagged), nprocs=world,
                        join=True, start_method="spawn")
     got = np.load(tmp_path / "dist.npz")
     assert len(got["obj"]) == len(got["cons"]) == T
@@ -203,7 +206,7 @@ def test_torus_strips_ranks_match_single_context(tmp_path, monkeypatch, world, d
 
     n, t = 4096, 7
     monkeypatch.setenv("DOPT_TEST_PIPE", "1")
-    mp.start_processes(_rank_main, args=(world, _free_port(), dtype, str(tmp_path), "torus", t, "1", n, d, m),
+    mp.start_processes(_rank_main, args=(world, _rdv(tmp_path), dtype, str(tmp_path), "torus", t, "1", n, d, m),
                        nprocs=world, join=True, start_method="spawn")
     got = np.load(tmp_path / "dist.npz")
     assert len(got["obj"]) == len(got["cons"]) == t
@@ -217,7 +220,7 @@ def test_torus_strips_ranks_match_single_context(tmp_path, monkeypatch, world, d
     _compare_single(got, dtype, "torus", t, n, d, m)
 
 
-def _trainer_rank(rank, world, port, out):
+def _trainer_rank(rank, world, rdv, out):
     import json
 
     import torch  # noqa: F401
@@ -227,8 +230,7 @@ def _trainer_rank(rank, world, port, out):
     from trainer import CentralizedTrainer, DecentralizedTrainer
     from worker import Worker
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=rdv, rank=rank, world_size=world)
     G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
     meta = json.load(open(os.path.join(G, "traj_c2.json")))
     z = np.load(os.path.join(G, "traj_c2.npz"))
@@ -263,7 +265,7 @@ def test_trainers_multiprocess_match_reference(tmp_path, world):
 
     import torch.multiprocessing as mp
 
-    mp.start_processes(_trainer_rank, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+    mp.start_processes(_trainer_rank, args=(world, _rdv(tmp_path), str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
     got = np.load(tmp_path / "trainers.npz")
     G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -284,7 +286,7 @@ def test_rccl_one_rank_matches_single_context(tmp_path, dtype, mean, lagged):
     stream, work.wait() ordering, object broadcast; the exchange itself has no peer here."""
     import torch.multiprocessing as mp
 
-    mp.start_processes(_rank_main, args=(1, _free_port(), dtype, str(tmp_path), mean, T, lagged, N, D, M, "nccl"),
+    mp.start_processes(_rank_main, args=(1, _rdv(tmp_path), dtype, str(tmp_path), mean, T, lagged, N, D, M, "nccl"),
                        nprocs=1, join=True, start_method="spawn")
     got = np.load(tmp_path / "dist.npz")
     _compare_single(got, dtype, mean, T, exact=not mean)
@@ -297,7 +299,7 @@ def test_partitioned_graph_ranks_match_single_context(tmp_path, monkeypatch, wor
     import torch.multiprocessing as mp
 
     monkeypatch.setenv("DOPT_TEST_PARTITION", "1")
-    mp.start_processes(_rank_main, args=(world, _free_port(), "float64", str(tmp_path), False, 5, "1"),
+    mp.start_processes(_rank_main, args=(world, _rdv(tmp_path), "float64", str(tmp_path), False, 5, "1"),
                        nprocs=world, join=True, start_method="spawn")
     got = np.load(tmp_path / "dist.npz")
     _compare_single(got, "float64", False, 5, parts=world)
@@ -312,7 +314,7 @@ def test_eight_ranks_match_single_context(tmp_path, monkeypatch):
     n, d, m, t = 2048, 100, 32, 6
     monkeypatch.setenv("DOPT_TEST_PARTITION", "1")
     monkeypatch.setenv("DOPT_TEST_PIPE", "1")
-    mp.start_processes(_rank_main, args=(8, _free_port(), "float64/x32", str(tmp_path), False, t, "1", n, d, m),
+    mp.start_processes(_rank_main, args=(8, _rdv(tmp_path), "float64/x32", str(tmp_path), False, t, "1", n, d, m),
                        nprocs=8, join=True, start_method="spawn")
     got = np.load(tmp_path / "dist.npz")
     assert len(got["obj"]) == len(got["cons"]) == t
@@ -333,7 +335,7 @@ def test_strong_split_bench_shape_matches_single_context(tmp_path, monkeypatch, 
     n, d, m, t = 1024, 1024, 16, 9
     monkeypatch.setenv("DOPT_TEST_PARTITION", "1")
     monkeypatch.setenv("DOPT_TEST_PIPE", "1")
-    mp.start_processes(_rank_main, args=(world, _free_port(), "float64/x32", str(tmp_path), False, t, "1", n, d, m),
+    mp.start_processes(_rank_main, args=(world, _rdv(tmp_path), "float64/x32", str(tmp_path), False, t, "1", n, d, m),
                        nprocs=world, join=True, start_method="spawn")
     got = np.load(tmp_path / "dist.npz")
     assert len(got["obj"]) == len(got["cons"]) == t
@@ -348,7 +350,7 @@ def test_device_sampler_ranks_match_single_context(tmp_path, monkeypatch, lagged
     import torch.multiprocessing as mp
 
     monkeypatch.setenv("DOPT_TEST_BATCH", "5")
-    mp.start_processes(_rank_main, args=(3, _free_port(), "float64", str(tmp_path), False, 5, lagged), nprocs=3,
+    mp.start_processes(_rank_main, args=(3, _rdv(tmp_path), "float64", str(tmp_path), False, 5, lagged), nprocs=3,
                        join=True, start_method="spawn")
     _compare_single(np.load(tmp_path / "dist.npz"), "float64", False, 5)
 
@@ -359,7 +361,7 @@ def test_lagged_schedule_single_metric(tmp_path, monkeypatch, which):
     import torch.multiprocessing as mp
 
     monkeypatch.setenv("DOPT_TEST_METRICS", which)
-    mp.start_processes(_rank_main, args=(2, _free_port(), "float64", str(tmp_path), False, 5, "1"), nprocs=2,
+    mp.start_processes(_rank_main, args=(2, _rdv(tmp_path), "float64", str(tmp_path), False, 5, "1"), nprocs=2,
                        join=True, start_method="spawn")
     got = np.load(tmp_path / "dist.npz")
     assert len(got["obj"]) == (5 if which == "obj" else 0) and len(got["cons"]) == (5 if which == "cons" else 0)
@@ -374,7 +376,7 @@ def test_column_blocked_ranks_match_single_context(tmp_path, mean):
     import torch.multiprocessing as mp
 
     n, d, m, t = 16, 2100, 8, 4
-    mp.start_processes(_rank_main, args=(2, _free_port(), "float64", str(tmp_path), mean, t, "1", n, d, m),
+    mp.start_processes(_rank_main, args=(2, _rdv(tmp_path), "float64", str(tmp_path), mean, t, "1", n, d, m),
                        nprocs=2, join=True, start_method="spawn")
     got = np.load(tmp_path / "dist.npz")
     _compare_single(got, "float64", mean, t, n, d, m, exact=False)
@@ -389,14 +391,14 @@ def test_pipelined_chain_matches_single_context(tmp_path, monkeypatch, world, ba
     import torch.multiprocessing as mp
 
     monkeypatch.setenv("DOPT_TEST_PIPE", "1")
-    mp.start_processes(_rank_main, args=(world, _free_port(), dtype, str(tmp_path), False, 9, "1", N, D, M, backend),
+    mp.start_processes(_rank_main, args=(world, _rdv(tmp_path), dtype, str(tmp_path), False, 9, "1", N, D, M, backend),
                        nprocs=world, join=True, start_method="spawn")
     got = np.load(tmp_path / "dist.npz")
     assert len(got["obj"]) == len(got["cons"]) == 9
     _compare_single(got, dtype, False, 9)
 
 
-def _ckpt_rank(rank, world, port, out):
+def _ckpt_rank(rank, world, rdv, out):
     import json
 
     import torch  # noqa: F401
@@ -406,8 +408,7 @@ def _ckpt_rank(rank, world, port, out):
     from trainer import CentralizedTrainer, DecentralizedTrainer
     from worker import Worker
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=rdv, rank=rank, world_size=world)
     G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
     meta = json.load(open(os.path.join(G, "traj_c2.json")))
     z = np.load(os.path.join(G, "traj_c2.npz"))
@@ -452,7 +453,7 @@ def test_trainers_multiprocess_checkpoint_resume(tmp_path):
 
     import torch.multiprocessing as mp
 
-    mp.start_processes(_ckpt_rank, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_ckpt_rank, args=(2, _rdv(tmp_path), str(tmp_path)), nprocs=2, join=True, start_method="spawn")
     got = np.load(tmp_path / "ckpt.npz")
     G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
     meta = json.load(open(os.path.join(G, "traj_c2.json")))
@@ -464,7 +465,7 @@ def test_trainers_multiprocess_checkpoint_resume(tmp_path):
             np.testing.assert_allclose(got[f"L{j}_consensus"], z[f"L{j}_consensus"][:50], rtol=1e-9)
 
 
-def _rccl_self_exchange(rank, world, port, out):
+def _rccl_self_exchange(rank, world, rdv, out):
     """HaloExchange's all_to_all_single on an RCCL communicator of one rank, with rows sent to
     itself (a hand-made plan: rows 0..k-1 out, k halo rows in) on the engine-like side stream."""
     import torch
@@ -472,9 +473,9 @@ def _rccl_self_exchange(rank, world, port, out):
 
     import distributed as Dm
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DOPT_FORCE_COLLECTIVES="1")
+    os.environ.update(DOPT_FORCE_COLLECTIVES="1")
     torch.cuda.set_device(0)
-    Dm.init_process_group("nccl", rank=0, world_size=1)
+    Dm.init_process_group("nccl", init_method=rdv, rank=0, world_size=1)
     k, ld = 37, 130
     plan = Dm.HaloPlan(0, 1, np.array([0, 64]), 0, 64, np.arange(k), np.array([0, k]), np.arange(k, dtype=np.int32),
                        np.array([0, k]), None, None, None)
@@ -509,7 +510,7 @@ def test_rccl_one_rank_self_exchange_matches_single_context(tmp_path, monkeypatc
 
     monkeypatch.setenv("DOPT_TEST_SELF_HALO", "1")
     monkeypatch.setenv("DOPT_TEST_PIPE", "1")
-    mp.start_processes(_rank_main, args=(1, _free_port(), dtype, str(tmp_path), False, 9, lagged, N, D, M, "nccl"),
+    mp.start_processes(_rank_main, args=(1, _rdv(tmp_path), dtype, str(tmp_path), False, 9, lagged, N, D, M, "nccl"),
                        nprocs=1, join=True, start_method="spawn")
     got = np.load(tmp_path / "dist.npz")
     assert len(got["obj"]) == len(got["cons"]) == 9
@@ -528,13 +529,13 @@ def test_rccl_alltoall_halo_exchange_one_rank(tmp_path):
     tests/test_distributed_cpu.py::test_alltoall_halo_layout, same call over gloo)."""
     import torch.multiprocessing as mp
 
-    mp.start_processes(_rccl_self_exchange, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True,
+    mp.start_processes(_rccl_self_exchange, args=(1, _rdv(tmp_path), str(tmp_path)), nprocs=1, join=True,
                        start_method="spawn")
     assert np.load(tmp_path / "ok.npy")[0]
 
 
-def _transport_errors(rank, world, port, out):
-    """The engine-driven transport's argument and state checks (ABI 7), on a world-1 communicator."""
+def _transport_errors(rank, world, rdv, out):
+    """The engine-driven transport's argument and state checks (ABI 7-8), on a world-1 communicator."""
     import torch
 
     import _dopt
@@ -578,7 +579,7 @@ def test_engine_transport_checks(tmp_path):
 
     import torch.multiprocessing as mp
 
-    mp.start_processes(_transport_errors, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True,
+    mp.start_processes(_transport_errors, args=(1, _rdv(tmp_path), str(tmp_path)), nprocs=1, join=True,
                        start_method="spawn")
     res = ast.literal_eval(str(np.load(tmp_path / "res.npy")[0]))
     assert "torch" in res["library"] and "rccl" in res["library"], res
@@ -589,3 +590,48 @@ def test_engine_transport_checks(tmp_path):
     assert res["negative"].startswith("ValueError") and "negative" in res["negative"], res
     assert res["ok"] is None and res["detach"] is None, res
     assert "no transport" in res["after_detach"], res
+
+
+def _lonely_comm(rank, world, rdv, out, timeout_s):
+    """Rank 0 of a world-2 engine communicator whose rank 1 never calls create (csrc/transport.cpp: the
+    non-blocking setup polled under timeout_s, then aborted)."""
+    import time
+
+    import torch
+
+    import _dopt
+
+    torch.cuda.set_device(0)
+    uid = _dopt.comm_unique_id()
+    t0 = time.monotonic()
+    try:
+        _dopt.Comm(2, 0, 0, uid, timeout_s=timeout_s)
+        msg = "created"
+    except RuntimeError as e:
+        msg = f"{type(e).__name__}: {e}"
+    np.save(os.path.join(out, "lonely.npy"), np.array([repr({"msg": msg, "s": time.monotonic() - t0})]))
+
+
+@pytest.mark.timeout(150)
+def test_engine_comm_setup_without_peer_is_bounded(tmp_path):
+    """dopt_comm_create is a collective; a rank whose peer never joins ends with an error
+    after the timeout (the half-built communicator aborted) instead of hanging in ncclCommInitRank, and its
+    process exits (no process left behind)."""
+    import ast
+
+    import torch.multiprocessing as mp
+
+    timeout_s = 6
+    ctx = mp.start_processes(_lonely_comm, args=(1, _rdv(tmp_path), str(tmp_path), timeout_s), nprocs=1,
+                             join=False, start_method="spawn")
+    p = ctx.processes[0]
+    p.join(120)
+    alive = p.is_alive()
+    if alive:
+        p.kill()
+        p.join(10)
+    assert not alive, "the lonely rank did not end within 120 s"
+    assert p.exitcode == 0, p.exitcode
+    res = ast.literal_eval(str(np.load(tmp_path / "lonely.npy")[0]))
+    assert res["msg"].startswith("RuntimeError") and "did not complete in 6 s" in res["msg"], res
+    assert timeout_s <= res["s"] < timeout_s + 30, res

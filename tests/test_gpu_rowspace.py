@@ -12,6 +12,17 @@ import dsgd_oracle as O
 import topology as TP
 
 pytestmark = pytest.mark.gpu
+_RDV_N = 0
+
+
+def _rdv(tmp_path):
+    """init_method of a multi-process test: a FileStore in the test's own tmp_path (no pre-picked port
+    for anything else on the box to take before rank 0 binds it: VERDICT r5)."""
+    import os
+
+    global _RDV_N
+    _RDV_N += 1
+    return f"file://{tmp_path}/pg_store_{os.getpid()}_{_RDV_N}"
 
 
 def _data(sizes, d, seed, problem="quadratic", scale=1.0):
@@ -265,7 +276,7 @@ def _rs_data(x32):
     return shards
 
 
-def _rs_rank(rank, world, port, out, T, pipe=False, x32=False, chunks=None, backend="gloo"):
+def _rs_rank(rank, world, rdv, out, T, pipe=False, x32=False, chunks=None, backend="gloo"):
     import os
 
     import torch  # noqa: F401  (one HIP runtime, loaded before libdopt)
@@ -273,12 +284,11 @@ def _rs_rank(rank, world, port, out, T, pipe=False, x32=False, chunks=None, back
 
     import distributed as Dm
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if backend == "nccl":
         torch.cuda.set_device(0)
-        Dm.init_process_group("nccl", rank=rank, world_size=world)
+        Dm.init_process_group("nccl", init_method=rdv, rank=rank, world_size=world)
     else:
-        dist.init_process_group(backend, rank=rank, world_size=world)
+        dist.init_process_group(backend, init_method=rdv, rank=rank, world_size=world)
     shards = _rs_data(x32)
     n = len(shards)
     bounds = Dm.partition_bounds(n, world)
@@ -311,6 +321,7 @@ def _rs_rank(rank, world, port, out, T, pipe=False, x32=False, chunks=None, back
     dist.destroy_process_group()
 
 
+@pytest.mark.multiproc
 @pytest.mark.parametrize("world,pipe,x32,chunks", [(2, False, False, None), (3, False, False, None),
                                                   (2, True, False, None), (2, True, True, None),
                                                   (2, False, False, 1), (3, True, True, 16),
@@ -323,16 +334,11 @@ def test_rowspace_ranks_vs_oracle(tmp_path, world, pipe, x32, chunks):
     column chunks, each chunk's sums all-reduced on their own (default: distributed.rs_chunks_for; 16
     is more chunks than the pass has column blocks: empty chunks).  World 8: config
     C5's rank count, the 13 ragged workers over 8 ranks (1-2 each)."""
-    import socket
-
     import torch.multiprocessing as mp
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    rdv = _rdv(tmp_path)
     T = 7
-    mp.start_processes(_rs_rank, args=(world, port, str(tmp_path), T, pipe, x32, chunks), nprocs=world, join=True,
+    mp.start_processes(_rs_rank, args=(world, rdv, str(tmp_path), T, pipe, x32, chunks), nprocs=world, join=True,
                        start_method="spawn")
     got = np.load(tmp_path / "rs.npz")
     assert ("k_rs_pass_x32<true" if x32 else "k_rs_pass<double, true") in str(got["kern"])
@@ -346,6 +352,7 @@ def test_rowspace_ranks_vs_oracle(tmp_path, world, pipe, x32, chunks):
     np.testing.assert_allclose(got["x"], xr, rtol=1e-9, atol=1e-12 * np.abs(xr).max())
 
 
+@pytest.mark.multiproc
 @pytest.mark.parametrize("chunks,pipe", [(2, True), (3, False), (16, True)])
 def test_rowspace_chunk_pipeline_rccl_one_rank_bitwise(tmp_path, monkeypatch, chunks, pipe):
     """The column-chunked rounds across ranks, pipelined across rounds (round h's average update of chunk k
@@ -354,20 +361,15 @@ def test_rowspace_chunk_pipeline_rccl_one_rank_bitwise(tmp_path, monkeypatch, ch
     gathered iterates bitwise those of the unchunked rounds (a one-rank all-reduce is the identity, and every
     column's arithmetic is the same in either order), as single runs and as a chain of pipelined calls;
     16 chunks leave some empty.  Also vs the oracle at rtol 1e-9."""
-    import socket
-
     import torch.multiprocessing as mp
 
     monkeypatch.setenv("DOPT_FORCE_COLLECTIVES", "1")
     got = {}
     for K in (1, chunks):
-        s = socket.socket()
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-        s.close()
         d = tmp_path / f"k{K}"
         d.mkdir()
-        mp.start_processes(_rs_rank, args=(1, port, str(d), 7, pipe, True, K, "nccl"), nprocs=1, join=True,
+        rdv = _rdv(d)
+        mp.start_processes(_rs_rank, args=(1, rdv, str(d), 7, pipe, True, K, "nccl"), nprocs=1, join=True,
                            start_method="spawn")
         got[K] = np.load(d / "rs.npz")
     for key in ("obj", "cons", "x"):
@@ -381,7 +383,7 @@ def test_rowspace_chunk_pipeline_rccl_one_rank_bitwise(tmp_path, monkeypatch, ch
     np.testing.assert_allclose(got[chunks]["x"], xr, rtol=1e-9, atol=1e-12 * np.abs(xr).max())
 
 
-def _rs_rank_minibatch(rank, world, port, out):
+def _rs_rank_minibatch(rank, world, rdv, out):
     import os
 
     import torch  # noqa: F401  (one HIP runtime, loaded before libdopt)
@@ -389,8 +391,7 @@ def _rs_rank_minibatch(rank, world, port, out):
 
     import distributed as Dm
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=rdv, rank=rank, world_size=world)
     shards = _rs_data(False)
     n = len(shards)
     bounds = Dm.partition_bounds(n, world)
@@ -418,19 +419,15 @@ def _rs_rank_minibatch(rank, world, port, out):
     dist.destroy_process_group()
 
 
+@pytest.mark.multiproc
 def test_rowspace_ranks_refuse_minibatches(tmp_path):
     """across ranks the row-space rounds take full-shard gradients only, so a run with
     batch < m and no index draws must not silently run full-batch D-SGD there: it goes to the
     phase path, which refuses it (the host sampler needs the reference's indices)."""
-    import socket
-
     import torch.multiprocessing as mp
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    mp.start_processes(_rs_rank_minibatch, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    rdv = _rdv(tmp_path)
+    mp.start_processes(_rs_rank_minibatch, args=(2, rdv, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
     got = np.load(tmp_path / "mb.npz")
     assert "ran" not in list(got["got"]), got["got"]
     assert "k_rs_pass" not in str(got["kern"])
@@ -589,7 +586,7 @@ def test_rowspace_x32_direct_rounds_from_unequal_starts(monkeypatch):
         np.testing.assert_allclose(u, v, rtol=1e-12, atol=1e-15 * np.abs(v).max())
 
 
-def _flag_rank(rank, world, port, out):
+def _flag_rank(rank, world, rdv, out):
     """A pipelined chain continued with other metric flags: the row-space rounds (complete graph,
     long rows) and the lagged schedule (CSR) both refuse, leave the chain open, and close it with
     the chain's own flags afterwards."""
@@ -600,8 +597,7 @@ def _flag_rank(rank, world, port, out):
 
     import distributed as Dm
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=rdv, rank=rank, world_size=world)
     got = []
     # row-space: complete graph over rows beyond the row-resident kernel
     shards = _rs_data(False)
@@ -639,19 +635,15 @@ def _flag_rank(rank, world, port, out):
     dist.destroy_process_group()
 
 
+@pytest.mark.multiproc
 def test_pipelined_flag_change_refused_on_both_paths(tmp_path):
     """continuing an open pipelined chain with other objective / consensus flags raises
     ValueError on the row-space path AND on the lagged schedule (it used to start a new chain
     silently there), and the chain then closes with its own flags, returning the rows it owed."""
-    import socket
-
     import torch.multiprocessing as mp
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    mp.start_processes(_flag_rank, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
+    rdv = _rdv(tmp_path)
+    mp.start_processes(_flag_rank, args=(2, rdv, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
     got = list(np.load(tmp_path / "flags.npz")["got"])
     assert got[0] == "refused" and got[2] == "refused", got
     assert got[1].startswith("closed:") and got[3].startswith("closed:"), got

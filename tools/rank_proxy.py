@@ -132,9 +132,8 @@ def main():
     import distributed as Dm
     import topology
 
-    os.environ.setdefault("MASTER_PORT", str(bench._free_port()))
     torch.cuda.set_device(0)
-    Dm.init_process_group("nccl", rank=0, world_size=1)
+    Dm.init_process_group("nccl", store=bench._solo_store(), rank=0, world_size=1)
     d, m, lam, eta0 = args.d, args.m, 1e-4, 0.05
     n = plan.n_local
 

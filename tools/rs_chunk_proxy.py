@@ -39,9 +39,8 @@ def main():
     import distributed as Dm
     import topology
 
-    os.environ.setdefault("MASTER_PORT", str(bench._free_port()))
     torch.cuda.set_device(0)
-    Dm.init_process_group("nccl", rank=0, world_size=1)
+    Dm.init_process_group("nccl", store=bench._solo_store(), rank=0, world_size=1)
     n, d, m, eta0, lam = args.workers, 1 << 20, 16, 1e-5, 1e-4
     eng = _dopt.Engine(0, "float64", data_dtype="float32")
     eng.generate_shards("quadratic", n, d, m, seed=1000, flip=0.05)
