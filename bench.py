@@ -587,7 +587,7 @@ def per_rank(world, item):
 
 def serial_exchange_leg(args, S, world, barrier, dev):
     """N > 1, after the headline leg, on its engine and shards: the same rounds with the exchange serialised on
-    the engine stream (DOPT_LAGGED_SIDE=0 DOPT_A2A_STREAM=current: the all-to-all between the mix and the next
+    the engine stream (DOPT_LAGGED_SIDE=0: the exchange between the mix and the next
     gradient kernel instead of beside it).  On one GPU the RCCL kernel beside the gradient kernel cost that
     kernel up to ~70 us per round on some boxes (tools/rank_proxy.py) while a serial exchange
     adds the transfer itself; which form wins with real peers over xGMI only a multi-GPU run can tell, so the
@@ -597,9 +597,9 @@ def serial_exchange_leg(args, S, world, barrier, dev):
 
     import distributed
 
-    keys = ("DOPT_LAGGED_SIDE", "DOPT_A2A_STREAM")
+    keys = ("DOPT_LAGGED_SIDE",)
     old = {k: os.environ.get(k) for k in keys}
-    os.environ.update(DOPT_LAGGED_SIDE="0", DOPT_A2A_STREAM="current")
+    os.environ.update(DOPT_LAGGED_SIDE="0")
     try:
         runner = distributed.DistributedDSGD(S.eng, S.plan, S.n_global, S.n_global * S.m, device=dev)
     finally:
@@ -620,7 +620,7 @@ def serial_exchange_leg(args, S, world, barrier, dev):
     return {"value": S.n_global * args.steps / dt, "unit": "worker-iters/s", "ms_per_step": dt / args.steps * 1e3,
             "kernel_avg_ms": kr_ms / launches if launches else None, "side_stream": runner.side is not None,
             "final_objective": float(obj[-1]),
-            "form": "the exchange serialised on the engine stream (DOPT_LAGGED_SIDE=0 DOPT_A2A_STREAM=current)"}
+            "form": "the exchange serialised on the engine stream (DOPT_LAGGED_SIDE=0)"}
 
 
 def transport_probe(args, world, dev, barrier, shape, reps=20, warm=3):

@@ -576,8 +576,9 @@ class Engine:
         check(lib().dopt_lagged_side_stream(self._h, ctypes.c_void_p(stream_ptr or None)))
 
     def lagged_exchange_issued(self):
-        """dopt_lagged_exchange_issued: True when the engine stream will wait for the exchange just issued on
-        the side stream by itself (DOPT_LAGGED_SYNC=value), False when the caller must order it."""
+        """dopt_lagged_exchange_issued: after the caller issued an exchange on the side stream, True when the
+        engine stream will wait for it (an event the context records there), False without a side stream
+        (the caller orders the engine stream)."""
         o = ctypes.c_int(0)
         check(lib().dopt_lagged_exchange_issued(self._h, ctypes.byref(o)))
         return bool(o.value)

@@ -124,13 +124,11 @@ struct FoldArgs {
 // partials at xbar = (rank-ordered sum of every rank's column sums of x_old) / n, and writes the
 // column-block partial of the column sums of x_new to part[g].  A second launch, k_mixcs_final (on
 // the side stream when the caller gave one), sums the NG partials in group order into own_out and
-// into the send buffer's sum rows of every peer (the shipped default; A/B builds keep a one-launch
-// form in which the last workgroup of a column block to arrive sums them, DOPT_MIXCS_TICKET).
+// into the send buffer's sum rows of every peer.
 // Block 0 folds a history row (FoldArgs).
 constexpr int kMcsKargRanks = 16;  // sum rows of the first ranks passed as kernel arguments
 struct McsArgs {
   double* part;            // [ng x ld] group partials of the column sums of x_new
-  unsigned* cnt;           // [ncb] arrival tickets (zero between launches: the last arriver resets)
   int32_t ng, ncb, r;      // worker groups, column blocks, workers per group
   int32_t world, rank;     // the rank-ordered global sums: rank p's halo rows, or own_in (row -1)
   const double* own_in;    // [ld] this rank's column sums of x_old
@@ -142,7 +140,6 @@ struct McsArgs {
   double* cons_part;       // [ncb x n] consensus partial of (column block, worker), or null
   double n_div;            // the mean's divisor (workers on all ranks)
   int32_t kin[kMcsKargRanks], kout[kMcsKargRanks];  // sum_in / sum_out of ranks < kMcsKargRanks
-  int32_t cut;             // A/B builds, timing only (DOPT_MIXCS_CUT): end the kernel early (0: never)
 };
 
 // Row-space rounds (rowspace.hip): complete graph (uniform W_ii), either objective, full
@@ -295,12 +292,10 @@ hipError_t launch_mix(int dtype, int cpl, const RoundArgs& a, const void* G, int
 // The lagged mix with fused column sums (McsArgs); fold: the history row folded by block 0
 // (null: none).  xsum / xsum_n of `a` are unused (the rank-ordered sums of m replace them).
 // side != null: k_mixcs_final goes to `side` after a wait for k_mixcs on s, so the next gradient kernel
-// on s need not wait for it (the exchange, issued on `side`, does).  sig != null (signal memory): a
-// stream write of seq to *sig on s and a stream wait for *sig >= seq on side (hipStreamWriteValue64 /
-// WaitValue64); otherwise an event `ev` recorded on s and waited for on side.
+// on s need not wait for it (the exchange, issued on `side`, does): an event `ev` recorded on s and
+// waited for on side.
 hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_workers, const McsArgs& m,
-                        const FoldArgs* fold, hipStream_t s, hipStream_t side = nullptr, hipEvent_t ev = nullptr,
-                        uint64_t* sig = nullptr, uint64_t seq = 0);
+                        const FoldArgs* fold, hipStream_t s, hipStream_t side = nullptr, hipEvent_t ev = nullptr);
 // Column-block count / workers per group / groups of k_mixcs for n workers and nch state chunks.
 void mixcs_shape(int dtype, int64_t n, int32_t nch, int32_t* ncb, int32_t* r, int32_t* ng);
 // xbar_out = (T)(rank-ordered sum of the column sums, as k_mixcs forms it / n_div); with send != null

@@ -65,7 +65,7 @@ __device__ __forceinline__ typename VT<T>::v ld_nt(const T* p) {
 // CPB = 16-byte chunks per lane per column block (a block is 64 * CPB chunks of every row).
 // One barrier per block: the waves' gradient partials go to a double-buffered LDS
 // slot, every wave folds them and forms the new block itself (wave 0 stores it).
-// Round 2 (C5, float32, interleaved A/B, tools/split_ab.py): the block's mix before its
+// Round 2 (C5, float32, interleaved A/B build): the block's mix before its
 // barrier 14.93 -> 14.60 ms; all of the next block's loads in flight through the barrier
 // (PF, unrolled by two over fixed register sets, branch-free loads so the compiler's waits
 // stay partial) 14.60 -> 14.24; 1/16 as a multiply 14.24 -> ~14.0 (5.5 TB/s, 69 %).
@@ -73,10 +73,9 @@ __device__ __forceinline__ typename VT<T>::v ld_nt(const T* p) {
 // flight per CU, where ~90 KB are needed at the loaded latency (the dots-only kernel, 32
 // VGPRs, 8 waves / SIMD, streams the same rows at 85 %).  Not kept: 2 chunks per lane with
 // PF (166 VGPRs, 13.90 vs 13.99), a column-per-wave kernel without barriers that re-reads
-// the rows from L2 for the dots (k_split_colwave, DOPT_SPLIT_COLWAVE: 17.6 ms).
+// the rows from L2 for the dots (k_split_colwave: 17.6 ms).
 // CPB > 1 keeps 2-4x the bytes in flight per wave between two barriers but costs
-// occupancy (C5: CPB 1 / 2 / 4 = 85 / 115 / 169 VGPRs, 15.1 / 15.5 / 16.7 ms): default 1,
-// DOPT_SPLIT_CPB selects 2 or 4 for A/B runs.  Not kept either: own / xbar / column sums
+// occupancy (C5: CPB 1 / 2 / 4 = 85 / 115 / 169 VGPRs, 15.1 / 15.5 / 16.7 ms): 1.  Not kept either: own / xbar / column sums
 // loaded once per workgroup and shared through LDS instead of by every wave (15.22 vs
 // 15.14 ms).  The kernel waits on memory 78 % of its wave cycles (SQ_WAIT_ANY) at 42 %
 // VALU issue per SIMD.
@@ -309,314 +308,6 @@ __global__ __launch_bounds__(NT) void k_split_step(const RoundArgs a) {
   }
 }
 
-#ifdef DOPT_AB  // A/B-only kernels (make AB=1): measured slower than k_split_step, kept for the record
-// LDS-DMA form of the prefetching step (DOPT_SPLIT_GLDS = D, complete-graph D-SGD steps with
-// the column sums in T, <= 16 rows per worker).  Every load of the block walk is a
-// global_load_lds_dwordx4 (1 KiB per wave instruction, no VGPR destination), so D blocks ahead
-// stay in flight per wave without costing registers: each wave streams its 4 rows' segments
-// into a private D-slot LDS ring; the own-iterate, column-sum and xbar segments go to a
-// workgroup ring of D + 1 slots, one piece per wave (waves 0 / 1 / 2), read by all after the
-// block's barrier.  The waits are counted by hand (s_waitcnt vmcnt(N), N = the loads and stores
-// this wave issued after the block's own; no ordinary global load is in the loop, so hipcc adds
-// no wait of its own), and the block barrier is LDS-only.  Arithmetic is the prefetching
-// kernel's, operation for operation (bitwise the same iterates and partial dots; tested).
-// Measured slower than the register-prefetch kernel at C5 (D = 2 / 3: 15.16 / 15.03 vs 13.32
-// ms, 3 / 2 workgroups per CU by LDS): kept as the A/B knob the write-bound finding rests on.
-__device__ __forceinline__ void vm_wait(int n) {  // s_waitcnt vmcnt(n), n wave-uniform
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;  // never less safe
-  }
-}
-
-// One global_load_lds_dwordx4 (nt: the bytes are read once) into LDS at lds_base + 16 * lane, in
-// inline asm: the builtin form makes hipcc wait vmcnt(0) before every LDS read it cannot prove
-// disjoint from a DMA in flight (all of them, with ring slots indexed at run time).  M0 is set
-// and restored in the same statement (the compiler does not preserve it around asm).
-template <typename V>
-__device__ __forceinline__ void glds16(const V* src, V* lds_base) {
-  const unsigned dst = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds_base;
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(src), "s"(dst)
-               : "memory");
-}
-
-template <typename T, bool ZNEXT, bool MET, int D>
-__global__ __launch_bounds__(NT) void k_split_glds(const RoundArgs a) {
-  using V = typename VT<T>::v;
-  constexpr int VN = VT<T>::n;
-  constexpr int RPW = 4;
-  constexpr int NSM = MET ? 3 : 2;  // workgroup pieces per block: own, column sums (, xbar)
-  __shared__ V rws[NW][D][RPW][64];  // per-wave ring: this wave's rows' segments
-  __shared__ V sml[D + 1][NSM][64];  // workgroup ring: own / sums / xbar segments
-  __shared__ V gred[2][NW][64];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int i = blockIdx.x, grp = blockIdx.y, G = gridDim.y;
-  const int nch = a.nchunks, nblk = (nch + 63) / 64;
-  const BlockWalk bw(a, grp, G, nblk);
-  const int nloc = bw.b1 > bw.b0 ? (bw.b1 - bw.b0 + bw.st - 1) / bw.st : 0;
-  const int64_t ld = a.ld;
-  const int64_t row0 = a.off[i], m = a.off[i + 1] - row0;
-  const int64_t nb = a.idx ? (a.b < m ? a.b : m) : m;  // <= NW * RPW (host-checked)
-  const T* __restrict__ X = (const T*)a.X;
-  const T* own_p = (const T*)a.x_old + (int64_t)i * ld;
-  const T* sums = (sizeof(T) == 8 && !a.colsum_t) ? (const T*)(const void*)a.colsum : (const T*)a.colsum_t;
-  const T* piece = wave == 0 ? own_p : wave == 1 ? sums : (const T*)a.xbar;  // waves < NSM
-  int64_t rowp[RPW];
-  T coef[RPW];
-  double zacc[RPW], uacc[RPW];
-#pragma unroll
-  for (int r = 0; r < RPW; ++r) {
-    const int k = wave + NW * r;
-    const bool ok = k < nb;
-    const int64_t lr = ok ? (a.idx ? (int64_t)a.idx[(int64_t)i * a.b + k] : (int64_t)k) : 0;
-    // wave-uniform values read into SGPRs here: the wait for their loads lands before the first
-    // LDS-DMA (hipcc drains every DMA in flight at the first use of an ordinary load's result)
-    rowp[r] = readlane_t<int64_t>((row0 + lr) * ld, 0);  // absent rows re-read the first row (coef 0)
-    coef[r] = readlane_t<T>(ok ? ((const T*)a.coef)[(int64_t)i * a.bcap + k] : T(0), 0);
-    zacc[r] = 0.0;
-    uacc[r] = 0.0;
-  }
-  double cacc = 0.0;
-  const T inv_eta = (T)a.eta, lam = (T)a.lam;
-  const bool pow2 = nb > 0 && (nb & (nb - 1)) == 0;
-  const T inv_nb = nb > 0 ? T(1) / (T)nb : T(0);
-  const double wii = readlane_t<double>((double)((const T*)a.wdiag)[i], 0);
-  // branch-free issue: a block past the walk re-reads the last block, lanes past the row the
-  // row's last chunk, so every wave issues the same loads each block and the counts are static
-  auto chunk_of = [&](int j) {
-    const int cb = bw.b0 + j * bw.st;
-    const int cbc = cb < bw.b1 ? cb : bw.b1 - 1;
-    const int c0 = cbc * 64 + lane;
-    return (int64_t)(c0 < nch ? c0 : nch - 1) * VN;
-  };
-  auto issue_rows = [&](int j) {
-    const int64_t off = chunk_of(j);
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) glds16<V>((const V*)(X + rowp[r] + off), &rws[wave][j % D][r][0]);
-  };
-  auto issue_small = [&](int j) {
-    if (wave < NSM) glds16<V>((const V*)(piece + chunk_of(j)), &sml[j % (D + 1)][wave][0]);
-  };
-  const int s_cnt = wave < NSM ? 1 : 0;  // this wave's loads / stores per block
-  const int t_cnt = wave == 0 ? 1 : 0;
-  if (nloc > 0) {
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-      issue_rows(j);
-      issue_small(j);
-    }
-  }
-  for (int j = 0; j < nloc; ++j) {
-    const int cb = bw.b0 + j * bw.st;
-    const int c = cb * 64 + lane;
-    const bool in = c < nch;
-    // issued after block j's loads: blocks j+1 .. j+D-1 (RPW + s each) and the stores of blocks
-    // j-D+1 .. j-1 that exist
-    vm_wait((D - 1) * (RPW + s_cnt) + t_cnt * (j < D - 1 ? j : D - 1));
-    V rw[RPW];
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) rw[r] = rws[wave][j % D][r][lane];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read: refill it
-    issue_rows(j + D);
-    V gp = V(0);
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) gp += coef[r] * rw[r];  // absent rows: coef 0
-    gred[j & 1][wave][lane] = gp;
-    lds_barrier();  // every wave's pieces of block j have landed (each waited for its own)
-    const int sl = j % (D + 1);
-    const V own = sml[sl][0][lane];
-    const V sv = sml[sl][1][lane];
-    V xb = V(0);
-    if (MET) xb = sml[sl][2][lane];
-    V g = V(0);
-    if (nb > 0) {
-      const V gs = gred[j & 1][0][lane] + gred[j & 1][1][lane] + gred[j & 1][2][lane] + gred[j & 1][3][lane];
-      g = (pow2 ? gs * inv_nb : gs / (T)nb) + lam * own;
-    }
-    V mixv;
-#pragma unroll
-    for (int e = 0; e < VN; ++e) {
-      const double x = (double)own[e];
-      mixv[e] = (T)(a.w_off * ((double)sv[e] - x) + wii * x);
-    }
-    const V xn = mixv - inv_eta * g;
-    if (wave == 0) {  // every block: the store count stays static (lanes past the row rewrite nothing)
-      if (in) *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = xn;
-    }
-    // slot (j + D) % (D + 1) held block j - 1, which every wave finished reading before this barrier
-    issue_small(j + D);
-    if (ZNEXT && in) {
-#pragma unroll
-      for (int r = 0; r < RPW; ++r) zacc[r] += (double)hsum<T>(rw[r] * xn);
-    }
-    if (MET && in) {
-#pragma unroll
-      for (int r = 0; r < RPW; ++r) uacc[r] += (double)hsum<T>(rw[r] * xb);
-      if (wave == 0) {
-        const V dv = own - xb;
-        cacc += (double)hsum<T>(dv * dv);
-      }
-    }
-  }
-  vm_wait(0);  // no LDS-DMA may land after the workgroup's LDS is handed to the next one
-#pragma unroll
-  for (int r = 0; r < RPW; ++r) {
-    const int k = wave + NW * r;
-    const int64_t slot = ((int64_t)i * a.bcap + k) * G + grp;
-    if (ZNEXT) {
-      const double z = wave_sum_dpp(zacc[r]);
-      if (lane == 0 && k < nb) a.zpart[slot] = z;
-    }
-    if (MET) {
-      const double u = wave_sum_dpp(uacc[r]);
-      if (lane == 0 && k < nb) a.upart[slot] = u;
-    }
-  }
-  if (MET && wave == 0) {
-    const double cs = wave_sum_dpp(cacc);
-    if (lane == 0) a.cpart[(int64_t)i * G + grp] = cs;
-  }
-}
-
-// Column-per-wave form of the column-blocked step (DOPT_SPLIT_COLWAVE, <= 16 rows per worker):
-// every wave owns whole 64-chunk blocks of the workgroup's walk (wave w takes every NW-th
-// block) and ALL of the worker's rows.  Pass 1 streams the rows (cached loads) into the
-// gradient chunk, the wave forms and stores x_i' itself; pass 2 re-reads the same rows --
-// just fetched, so L2 hits -- for the next round's dots and the metric dots.  No barrier and
-// no cross-wave exchange per block, no mix / division repeated by four waves; the waves'
-// per-row dot partials meet in LDS once, after the walk.
-template <typename T, bool ZNEXT, bool MET>
-__global__ __launch_bounds__(NT) void k_split_colwave(const RoundArgs a) {
-  using V = typename VT<T>::v;
-  constexpr int VN = VT<T>::n;
-  constexpr int R = 16;  // rows per worker (host-checked)
-  constexpr int RB = 4;  // row loads in flight per wave and pass step
-  __shared__ double dred[NW][2][R];
-  __shared__ double cred[NW];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int i = blockIdx.x, grp = blockIdx.y, G = gridDim.y;
-  const int nch = a.nchunks, nblk = (nch + 63) / 64;
-  const BlockWalk bw(a, grp, G, nblk);
-  const int64_t ld = a.ld;
-  const int64_t row0 = a.off[i], m = a.off[i + 1] - row0;
-  const int nb = (int)(a.idx ? (a.b < m ? a.b : m) : m);  // <= R
-  const T* __restrict__ X = (const T*)a.X;
-  const bool shared = (a.flags & F_SHARED) != 0;
-  const bool gout = (a.flags & F_GOUT) != 0;
-  const T* own_p = shared ? (const T*)a.w_shared : (const T*)a.x_old + (int64_t)i * ld;
-  int64_t rowp[R];
-  T coef[R];
-  double zacc[R], uacc[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const bool ok = r < nb;
-    const int lr = ok ? (a.idx ? a.idx[(int64_t)i * a.b + r] : r) : 0;
-    // wave-uniform: kept in SGPRs (the VGPRs go to the per-row dot accumulators)
-    rowp[r] = (row0 + __builtin_amdgcn_readfirstlane(lr)) * ld;  // absent rows: row 0, coefficient 0
-    const T cf = ok ? ((const T*)a.coef)[(int64_t)i * a.bcap + r] : T(0);
-    if constexpr (sizeof(T) == 4) {
-      coef[r] = __builtin_bit_cast(T, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, cf)));
-    } else {
-      coef[r] = readlane_t(cf, 0);
-    }
-    zacc[r] = 0.0;
-    uacc[r] = 0.0;
-  }
-  double cacc = 0.0;
-  const T inv_eta = (T)a.eta, lam = (T)a.lam;
-  // 1 / nb when nb is a power of two: x * 2^-k is x / 2^k exactly (one rounding of the same value)
-  const bool pow2 = nb > 0 && (nb & (nb - 1)) == 0;
-  const T inv_nb = nb > 0 ? T(1) / (T)nb : T(0);
-  for (int cb = bw.b0 + wave * bw.st; cb < bw.b1; cb += NW * bw.st) {
-    const int c0 = cb * 64 + lane;
-    const bool in = c0 < nch;
-    const int c = in ? c0 : nch - 1;
-    const V own = *(const V*)(own_p + (int64_t)c * VN);
-    V xb = V(0);
-    if (MET) xb = *(const V*)((const T*)a.xbar + (int64_t)c * VN);
-    V g = V(0);
-#pragma unroll
-    for (int r0 = 0; r0 < R; r0 += RB) {
-      if (r0 >= nb) break;
-      V x[RB];
-#pragma unroll
-      for (int k = 0; k < RB; ++k) x[k] = *(const V*)(X + rowp[r0 + k] + (int64_t)c * VN);
-#pragma unroll
-      for (int k = 0; k < RB; ++k) g += coef[r0 + k] * x[k];
-    }
-    if (nb > 0) g = (pow2 ? g * inv_nb : g / (T)nb) + lam * own;
-    V xn = V(0);
-    if (gout) {
-      if (in) *(V*)((T*)a.g_out + (int64_t)i * ld + (int64_t)c * VN) = g;
-    } else {
-      xn = mix_chunk<T, T>(a, i, c, own) - inv_eta * g;
-      if (in) *(V*)((T*)a.x_new + (int64_t)i * ld + (int64_t)c * VN) = xn;
-    }
-    if (!in) {
-      xn = V(0);
-      xb = V(0);
-    }
-    if (ZNEXT || MET) {
-#pragma unroll
-      for (int r0 = 0; r0 < R; r0 += RB) {
-        if (r0 >= nb) break;
-        V x[RB];
-#pragma unroll
-        for (int k = 0; k < RB; ++k) x[k] = ld_nt<T>(X + rowp[r0 + k] + (int64_t)c * VN);
-#pragma unroll
-        for (int k = 0; k < RB; ++k) {
-          if (ZNEXT) zacc[r0 + k] += (double)hsum<T>(x[k] * xn);
-          if (MET) uacc[r0 + k] += (double)hsum<T>(x[k] * xb);
-        }
-      }
-    }
-    if (MET && in) {
-      const V dv = own - xb;
-      cacc += (double)hsum<T>(dv * dv);
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    double z = 0.0, u = 0.0;
-    if (ZNEXT) z = wave_sum_dpp(zacc[r]);
-    if (MET) u = wave_sum_dpp(uacc[r]);
-    if (lane == 0) {
-      dred[wave][0][r] = z;
-      dred[wave][1][r] = u;
-    }
-  }
-  if (MET) {
-    const double cs = wave_sum_dpp(cacc);
-    if (lane == 0) cred[wave] = cs;
-  }
-  __syncthreads();
-  if ((int)threadIdx.x < nb) {
-    const int r = threadIdx.x;
-    const int64_t slot = ((int64_t)i * a.bcap + r) * G + grp;
-    if (ZNEXT) a.zpart[slot] = ((dred[0][0][r] + dred[1][0][r]) + dred[2][0][r]) + dred[3][0][r];
-    if (MET) a.upart[slot] = ((dred[0][1][r] + dred[1][1][r]) + dred[2][1][r]) + dred[3][1][r];
-  }
-  if (MET && threadIdx.x == 0) a.cpart[(int64_t)i * G + grp] = ((cred[0] + cred[1]) + cred[2]) + cred[3];
-}
-
-#endif  // DOPT_AB
 
 template <typename T, typename S, int MODE, int RPW>
 __global__ __launch_bounds__(NT) void k_split_dots(const RoundArgs a) {
@@ -714,20 +405,6 @@ __global__ __launch_bounds__(NT) void k_split_coef(const RoundArgs a, int mode) 
   }
 }
 
-// Launch-shape knobs are read only by A/B builds (make AB=1, -DDOPT_AB): the default build uses
-// the measured defaults and ignores the environment.
-#ifdef DOPT_AB
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
-#else
-static int env_int(const char*, int dflt) { return dflt; }
-#endif
-
-// contiguous block ranges per column-block group, or every G-th block (A/B DOPT_SPLIT_CONTIG;
-// default: C5 13.91 vs 14.02 ms contiguous, won 4 of 4 interleaved reps)
-static int split_contig() { return env_int("DOPT_SPLIT_CONTIG", 0) != 0; }
 
 static void note_split(const char* kernel, int dtype, int xdtype, const char* params) {
   char buf[160];
@@ -744,7 +421,7 @@ static const char* tf(bool b) { return b ? "true" : "false"; }
 static bool split_types_ok(int dtype, int xdtype) { return dtype == xdtype || (dtype == 1 && xdtype == 0); }
 
 template <typename T, typename S>
-static void split_step_t(bool znext, bool met, bool small, bool pf, int cpb, dim3 grid, const RoundArgs& a2,
+static void split_step_t(bool znext, bool met, bool small, bool pf, dim3 grid, const RoundArgs& a2,
                          hipStream_t s) {
 #define SPLIT_STEP2(R_, P_, C_)                                                                                    \
   if (znext && met) hipLaunchKernelGGL((k_split_step<T, S, R_, true, true, P_, C_>), grid, dim3(NT), 0, s, a2);     \
@@ -752,11 +429,6 @@ static void split_step_t(bool znext, bool met, bool small, bool pf, int cpb, dim
   else if (met) hipLaunchKernelGGL((k_split_step<T, S, R_, false, true, P_, C_>), grid, dim3(NT), 0, s, a2);        \
   else hipLaunchKernelGGL((k_split_step<T, S, R_, false, false, P_, C_>), grid, dim3(NT), 0, s, a2);
   if (small) {
-#ifdef DOPT_AB
-    if (cpb == 4) { SPLIT_STEP2(4, false, 4) return; }
-    if (cpb == 2 && pf) { SPLIT_STEP2(4, true, 2) return; }
-    if (cpb == 2) { SPLIT_STEP2(4, false, 2) return; }
-#endif
     if (pf) { SPLIT_STEP2(4, true, 1) } else { SPLIT_STEP2(4, false, 1) }
   } else {
     if (pf) { SPLIT_STEP2(16, true, 1) } else { SPLIT_STEP2(16, false, 1) }
@@ -772,55 +444,19 @@ hipError_t launch_split_step(int dtype, int xdtype, bool znext, bool met, const 
   const dim3 grid(n_workers, a.groups);
   const bool small = a.b_rows <= 4 * NW;  // rows per worker this step touches
   RoundArgs a2 = a;
-  a2.contig = split_contig();
-  // the block's mix before its barrier (A/B DOPT_SPLIT_EARLYMIX=0: after it)
-  if (env_int("DOPT_SPLIT_EARLYMIX", 1) != 0) a2.flags |= F_EARLYMIX;
+  // every G-th column block per group (contiguous ranges measured 13.91 vs 14.02 ms at C5, round 2)
+  a2.contig = 0;
+  // the block's mix before its barrier
+  a2.flags |= F_EARLYMIX;
   // the next block's loads in flight through the block's barrier: complete-graph D-SGD steps with
-  // the column sums in T (default on: C5 14.60 -> 14.24 ms, and 13.99 with the exact 1/16,
-  // interleaved A/B; DOPT_SPLIT_PREFETCH=0 in A/B builds)
-  const bool pf = env_int("DOPT_SPLIT_PREFETCH", 1) != 0 && (a.flags & F_MEAN) && !(a.flags & F_GOUT) &&
-                  (dtype == 1 ? a.colsum != nullptr : a.colsum_t != nullptr);
-#ifdef DOPT_AB
-  // DOPT_SPLIT_GLDS = D (2 or 3): the LDS-DMA kernel with D blocks in flight per wave, where the
-  // prefetching kernel would run with <= 16 rows (same element types only)
-  const int glds = env_int("DOPT_SPLIT_GLDS", 0);
-  if (pf && small && (glds == 2 || glds == 3) && dtype == xdtype && a.xrows == 0) {  // row-major rows only
-#define GLDS2(T_, D_)                                                                                 \
-  if (znext && met) hipLaunchKernelGGL((k_split_glds<T_, true, true, D_>), grid, dim3(NT), 0, s, a2); \
-  else if (znext) hipLaunchKernelGGL((k_split_glds<T_, true, false, D_>), grid, dim3(NT), 0, s, a2);  \
-  else if (met) hipLaunchKernelGGL((k_split_glds<T_, false, true, D_>), grid, dim3(NT), 0, s, a2);    \
-  else hipLaunchKernelGGL((k_split_glds<T_, false, false, D_>), grid, dim3(NT), 0, s, a2);
-    char nm[160];
-    snprintf(nm, sizeof(nm), "void dopt::k_split_glds<%s, %s, %s, %d>(dopt::RoundArgs)", dtype == 0 ? "float" : "double",
-             tf(znext), tf(met), glds);
-    note_round_kernel(nm);
-#define GLDS(T_) if (glds == 2) { GLDS2(T_, 2) } else { GLDS2(T_, 3) }
-    if (dtype == 0) { GLDS(float) } else { GLDS(double) }
-#undef GLDS
-#undef GLDS2
-    return hipGetLastError();
-  }
-  // DOPT_SPLIT_COLWAVE=1: the column-per-wave kernel for <= 16 rows (same element types only)
-  if (small && env_int("DOPT_SPLIT_COLWAVE", 0) == 1 && dtype == xdtype && a.xrows == 0) {
-#define COLWAVE(T_)                                                                                       \
-  if (znext && met) hipLaunchKernelGGL((k_split_colwave<T_, true, true>), grid, dim3(NT), 0, s, a2);       \
-  else if (znext) hipLaunchKernelGGL((k_split_colwave<T_, true, false>), grid, dim3(NT), 0, s, a2);        \
-  else if (met) hipLaunchKernelGGL((k_split_colwave<T_, false, true>), grid, dim3(NT), 0, s, a2);          \
-  else hipLaunchKernelGGL((k_split_colwave<T_, false, false>), grid, dim3(NT), 0, s, a2);
-    if (dtype == 0) { COLWAVE(float) } else { COLWAVE(double) }
-#undef COLWAVE
-    return hipGetLastError();
-  }
-#endif
-  // CPB: 16-byte chunks per lane per block (A/B DOPT_SPLIT_CPB = 2 / 4; default 1)
-  int cpb = env_int("DOPT_SPLIT_CPB", 1);
-  if (!small || (pf && cpb > 2) || (a.nchunks + 64 * cpb - 1) / (64 * cpb) < 2 * a.groups) cpb = 1;
-  snprintf(params, sizeof(params), "%d, %s, %s, %s, %d", small ? 4 : 16, tf(znext), tf(met),
-           tf(small ? (cpb == 4 ? false : pf) : pf), small ? cpb : 1);
+  // the column sums in T (C5 14.60 -> 14.24 ms, and 13.99 with the exact 1/16, interleaved A/B)
+  const bool pf = (a.flags & F_MEAN) && !(a.flags & F_GOUT) && (dtype == 1 ? a.colsum != nullptr : a.colsum_t != nullptr);
+  // one 16-byte chunk per lane per block (2 / 4 were measured slower, round 3)
+  snprintf(params, sizeof(params), "%d, %s, %s, %s, 1", small ? 4 : 16, tf(znext), tf(met), tf(pf));
   note_split("k_split_step", dtype, xdtype, params);
-  if (dtype == 0) split_step_t<float, float>(znext, met, small, pf, cpb, grid, a2, s);
-  else if (xdtype == 0) split_step_t<double, float>(znext, met, small, pf, cpb, grid, a2, s);
-  else split_step_t<double, double>(znext, met, small, pf, cpb, grid, a2, s);
+  if (dtype == 0) split_step_t<float, float>(znext, met, small, pf, grid, a2, s);
+  else if (xdtype == 0) split_step_t<double, float>(znext, met, small, pf, grid, a2, s);
+  else split_step_t<double, double>(znext, met, small, pf, grid, a2, s);
   return hipGetLastError();
 }
 
@@ -839,7 +475,7 @@ hipError_t launch_split_dots(int dtype, int xdtype, int mode, const RoundArgs& a
   const dim3 grid(n_workers, a.groups);
   const bool small = a.b_rows <= 4 * NW;  // <= 16 rows: one 4-row chunk per wave, high occupancy
   RoundArgs a2 = a;
-  a2.contig = split_contig();
+  a2.contig = 0;  // every G-th column block per group, as in launch_split_step
   if (dtype == 0) split_dots_t<float, float>(mode, small, grid, a2, s);
   else if (xdtype == 0) split_dots_t<double, float>(mode, small, grid, a2, s);
   else split_dots_t<double, double>(mode, small, grid, a2, s);
@@ -1495,10 +1131,8 @@ __global__ __launch_bounds__(NT) void k_mix(const RoundArgs a, const T* __restri
 
 template <typename T>
 static hipError_t launch_mix_t(int cpl, const RoundArgs& a, const T* G, int n, hipStream_t s) {
-  // A/B builds: DOPT_MIX_ONEWAVE=1, one wave per worker for rows of 8 / 16 chunks per lane
-  const bool one = env_int("DOPT_MIX_ONEWAVE", 0) == 1;
   const dim3 grid((n + NW - 1) / NW);
-  if (!one && (cpl == 8 || cpl == 16)) {
+  if (cpl == 8 || cpl == 16) {  // rows of 8 / 16 chunks per lane: several waves per worker
     const int wpw = cpl / 4;
     const dim3 g2(((int64_t)n * wpw + NW - 1) / NW);
     if (wpw == 2) hipLaunchKernelGGL((k_mix<T, 4, 2>), g2, dim3(NT), 0, s, a, G, n);
@@ -1535,11 +1169,9 @@ hipError_t launch_mix(int dtype, int cpl, const RoundArgs& a, const void* G, int
 // for an interior worker the gradient kernel stepped, its new row read back; the new rows' column
 // sums accumulate per lane in float64 in worker order, meet in LDS in wave order, and go to part[g];
 // k_mixcs_final (the next launch) sums part[0..ng) of each column block in group order and writes
-// the sums to own_out and to every peer's sum rows in the send buffer.  TICKET (A/B builds,
-// DOPT_MIXCS_TICKET=1): one launch instead -- the partials as write-through (sc1) stores, and the
-// last arriving workgroup of column block cb (agent-scope ticket, MI355X_MICROARCH.md "Valid forms"
-// row 1: sc1 stores drained by every storing wave before one lane's ticket add, sc1 loads after it;
-// the acquire fence kept as well) does k_mixcs_final's sum, then resets the ticket.
+// the sums to own_out and to every peer's sum rows in the send buffer.  (Round 4 measured a one-launch
+// form -- the last arriving workgroup of a column block summing write-through partials after an
+// agent-scope ticket -- at ~9 us more per round at 512 workers than the second launch)
 template <int RW>
 __device__ void fold_block_rw(const FoldArgs& f, int nch, int vn, double (*red)[RW]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1592,25 +1224,18 @@ __device__ __forceinline__ double ranks_sum(const McsArgs& m, const T* halo, int
   return s;
 }
 
-#ifdef DOPT_AB
-constexpr bool kMixcsAB = true;  // A/B builds: DOPT_MIXCS_CUT (timing-only early exits) and DOPT_MIXCS_TICKET
-#else
-constexpr bool kMixcsAB = false;
-#endif
 constexpr int kMixcsBatch = 16;        // group partials loaded per batch (all in flight; few VGPRs, so
                                        // k_mixcs_final fits beside two round-kernel workgroups per CU)
 constexpr int kMixcsMaxGroups = 1024;  // mixcs_shape keeps ng <= this
 
-// MODE 0: the group partials by plain stores, k_mixcs_final a second launch after a stream hand-off;
-// MODE 1 (A/B builds, DOPT_MIXCS_TICKET): one launch, the last workgroup of a column block sums them.
-// (Round 5 also tried a MODE in which the launch's last workgroup released a sequence number for the side
+// The group partials by plain stores; k_mixcs_final, a second launch after a stream hand-off, sums them.
+// (Round 5 also tried a form in which the launch's last workgroup released a sequence number for the side
 // stream to wait on, so that no event sat on the engine stream: the agent-scope release of every
 // workgroup took k_mixcs from 6 to 35 us and the side stream's spinning wait slowed the gradient kernel
 // beside it; profiles/r5_sync_ab.txt.)
-template <typename T, int CPB, int MODE>
+template <typename T, int CPB>
 __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __restrict__ G, int n, const McsArgs m,
                                               const FoldArgs fold) {
-  constexpr bool TICKET = MODE == 1;
   using V = typename VT<T>::v;
   constexpr int VN = VT<T>::n;
   constexpr int MAXE = 6;            // CSR entries held in registers (the rest of a longer row: loaded at use)
@@ -1620,9 +1245,8 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
   constexpr int XT = BC / 64;        // columns per lane in the staging
   __shared__ double red[NW][BC];
   __shared__ double xsum[XR][BC];
-  __shared__ int last;
   if (blockIdx.x == 0) {
-    if (!kMixcsAB || m.cut != 3) fold_block_rw<BC>(fold, a.nchunks, VN, red);
+    fold_block_rw<BC>(fold, a.nchunks, VN, red);
     return;
   }
   const int lane = threadIdx.x & 63;
@@ -1746,7 +1370,6 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
     for (int e = 0; e < VN; ++e) xb[j][e] = c < nch ? (T)(xs[j][e] / m.n_div) : T(0);
     if (c < nch && g == 0 && wave == 0 && a.xbar_out) *(V*)((T*)a.xbar_out + (int64_t)c * VN) = xb[j];
   }
-  if (kMixcsAB && m.cut == 2) return;
 
   double cs[CPB][VN];
 #pragma unroll
@@ -1801,8 +1424,7 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
       }
     }
   }
-  if (kMixcsAB && m.cut == 1) return;
-  // this group's partial of the column block: waves in order (TICKET: write-through stores)
+  // this group's partial of the column block: waves in order
 #pragma unroll
   for (int j = 0; j < CPB; ++j)
 #pragma unroll
@@ -1810,51 +1432,11 @@ __global__ __launch_bounds__(NT) void k_mixcs(const RoundArgs a, const T* __rest
   __syncthreads();
   for (int t = threadIdx.x; t < BC; t += NT) {
     if (colbase + t >= ncol) break;
-    const double s = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
-    if constexpr (TICKET)
-      __hip_atomic_store(m.part + (int64_t)g * ld + colbase + t, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-      m.part[(int64_t)g * ld + colbase + t] = s;
+    m.part[(int64_t)g * ld + colbase + t] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
   }
-  if (!TICKET || (kMixcsAB && m.cut == 4)) return;  // (two launches: k_mixcs_final sums the partials)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned ticket = __hip_atomic_fetch_add(m.cnt + cb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = ticket == (unsigned)(m.ng - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!last) return;
-  for (int t = threadIdx.x; t < BC; t += NT) {
-    const int64_t col = colbase + t;
-    if (col >= ncol) break;
-    // the partials in batches of kMixcsBatch in flight, summed in group order
-    double s = 0.0;
-    for (int qb = 0; qb < m.ng; qb += kMixcsBatch) {
-      double v[kMixcsBatch];
-#pragma unroll
-      for (int q = 0; q < kMixcsBatch; ++q)
-        v[q] = qb + q < m.ng
-                   ? __hip_atomic_load(m.part + (int64_t)(qb + q) * ld + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                   : 0.0;
-#pragma unroll
-      for (int q = 0; q < kMixcsBatch; ++q)
-        if (qb + q < m.ng) s += v[q];
-    }
-    m.own_out[col] = s;
-    for (int p = 0; p < m.world; ++p) {
-      const int64_t row = p < kMcsKargRanks ? (int64_t)m.kout[p] : m.sum_out[p];
-      if (row >= 0) ((double*)((T*)a.send + row * ld))[col] = s;
-    }
-  }
-  if (threadIdx.x == 0) __hip_atomic_store(m.cnt + cb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The second launch of the two-kernel k_mixcs (the default): the ng group partials of every column,
+// The second launch of k_mixcs: the ng group partials of every column,
 // summed per column block -- workgroup (64 columns), wave w summing groups [w ng / 4, (w + 1) ng / 4)
 // in group order with 64 loads in flight, the four waves' sums added in wave order through LDS --
 // to own_out and to every peer's sum rows.  The kernel boundary is the hand-off: the single-launch
@@ -1890,128 +1472,41 @@ __global__ __launch_bounds__(NT) void k_mixcs_final(const McsArgs m, int64_t ld,
   }
 }
 
-// 16-byte chunks per lane of a k_mixcs column block (A/B builds: DOPT_MIXCS_CPB = 2).  One chunk:
-// twice the column blocks, 105 VGPRs (four waves per SIMD instead of two at 192), and, with every
-// worker mixed there, 40.0 vs 48.5 us at 4096 workers and 11.0 vs 13.6 at 512
-// (profiles/r4_mixcs_cpb.txt)
-static int mixcs_cpb() {
-#ifdef DOPT_AB
-  static const int v = [] {
-    const char* e = getenv("DOPT_MIXCS_CPB");
-    return (e && atoi(e) == 2) ? 2 : 1;
-  }();
-  return v;
-#else
-  return 1;
-#endif
-}
+// One 16-byte chunk per lane of a k_mixcs column block: twice the column blocks of two chunks, 105 VGPRs
+// (four waves per SIMD instead of two at 192), and, with every worker mixed there, 40.0 vs 48.5 us at 4096
+// workers and 11.0 vs 13.6 at 512 (profiles/r4_mixcs_cpb.txt)
+constexpr int kMixcsCpb = 1;
 
 void mixcs_shape(int dtype, int64_t n, int32_t nch, int32_t* ncb, int32_t* r, int32_t* ng) {
-  const int CPB = mixcs_cpb();
+  constexpr int CPB = kMixcsCpb;
   (void)dtype;
   *ncb = (nch + 64 * CPB - 1) / (64 * CPB);
   // groups of 8 workers (one iteration of the two-worker loop per wave), up to kMixcsMaxGroups groups:
   // many short workgroups rather than few long ones -- a wave's workers run one after the other, each
-  // a few dependent memory round trips (A/B builds: DOPT_MIXCS_R forces the group size)
+  // a few dependent memory round trips (profiles/r4_mixcs_groups.txt)
   int64_t rr = 8;
-#ifdef DOPT_AB
-  if (const char* v = getenv("DOPT_MIXCS_R")) rr = std::max(8, atoi(v) / 8 * 8);
-#endif
   while ((n + rr - 1) / rr > kMixcsMaxGroups) rr += 8;
   *r = (int32_t)rr;
   *ng = (int32_t)std::max<int64_t>(1, (n + rr - 1) / rr);
 }
 
-#ifdef DOPT_AB
-// A/B builds, DOPT_HOST_TIMING=1: host time of each HIP call of launch_mixcs, printed at exit (VERDICT r4
-// item 4: where the side stream's host cost per round goes)
-struct MixcsHostTiming {
-  double ns[4] = {0, 0, 0, 0};
-  long calls = 0;
-  bool on = getenv("DOPT_HOST_TIMING") && atoi(getenv("DOPT_HOST_TIMING")) != 0;
-  ~MixcsHostTiming() {
-    if (on && calls)
-      fprintf(stderr, "[dopt] launch_mixcs host us per call over %ld calls: k_mixcs launch %.2f, event record %.2f, "
-              "stream wait %.2f, k_mixcs_final launch %.2f\n", calls, ns[0] / calls / 1e3, ns[1] / calls / 1e3,
-              ns[2] / calls / 1e3, ns[3] / calls / 1e3);
-  }
-};
-static MixcsHostTiming g_mht;
-static inline double mht_now() {
-  return (double)std::chrono::duration_cast<std::chrono::nanoseconds>(
-             std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-#define MHT_MARK(k) do { if (g_mht.on) { const double t_ = mht_now(); g_mht.ns[k] += t_ - mht_t; mht_t = t_; } } while (0)
-#else
-#define MHT_MARK(k) do { } while (0)
-#endif
-
 hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_workers, const McsArgs& m,
-                        const FoldArgs* fold, hipStream_t s, hipStream_t side, hipEvent_t ev, uint64_t* sig,
-                        uint64_t seq) {
-#ifdef DOPT_AB
-  double mht_t = g_mht.on ? mht_now() : 0.0;
-  if (g_mht.on) g_mht.calls++;
-#endif
+                        const FoldArgs* fold, hipStream_t s, hipStream_t side, hipEvent_t ev) {
   FoldArgs f;
   memset(&f, 0, sizeof(f));
   if (fold) f = *fold;
-  McsArgs mm = m;
-  mm.cut = 0;
+  const McsArgs& mm = m;
   const dim3 grid(1 + (unsigned)m.ng * (unsigned)m.ncb);
-#ifdef DOPT_AB
-  static const int cut = [] {
-    const char* v = getenv("DOPT_MIXCS_CUT");
-    return v ? atoi(v) : 0;
-  }();
-  static const bool ticket = [] {  // one launch with the agent-scope last-arriver hand-off
-    const char* v = getenv("DOPT_MIXCS_TICKET");
-    return v && atoi(v) != 0;
-  }();
-  mm.cut = cut;
-  if (ticket) {  // (column blocks of mixcs_cpb() chunks, as the shape was planned)
-    if (mixcs_cpb() == 2) {
-      if (dtype == 0)
-        hipLaunchKernelGGL((k_mixcs<float, 2, 1>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
-      else
-        hipLaunchKernelGGL((k_mixcs<double, 2, 1>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
-    } else {
-      if (dtype == 0)
-        hipLaunchKernelGGL((k_mixcs<float, 1, 1>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
-      else
-        hipLaunchKernelGGL((k_mixcs<double, 1, 1>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
-    }
-    return hipGetLastError();
-  }
-#endif
-#ifdef DOPT_AB
-  if (mixcs_cpb() == 2) {
-    if (dtype == 0)
-      hipLaunchKernelGGL((k_mixcs<float, 2, 0>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
-    else
-      hipLaunchKernelGGL((k_mixcs<double, 2, 0>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
-  } else
-#endif
   if (dtype == 0)
-    hipLaunchKernelGGL((k_mixcs<float, 1, 0>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
+    hipLaunchKernelGGL((k_mixcs<float, kMixcsCpb>), grid, dim3(NT), 0, s, a, (const float*)G, n_workers, mm, f);
   else
-    hipLaunchKernelGGL((k_mixcs<double, 1, 0>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
-  if (mm.cut != 0) return hipGetLastError();  // (timing-only cuts: no totals)
+    hipLaunchKernelGGL((k_mixcs<double, kMixcsCpb>), grid, dim3(NT), 0, s, a, (const double*)G, n_workers, mm, f);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  MHT_MARK(0);
   hipStream_t fs = s;
-  if (side && sig) {  // stream memory operations: no event in either queue (a write on s, a wait on side)
-    if ((e = hipStreamWriteValue64(s, sig, seq, 0)) != hipSuccess) return e;
-    MHT_MARK(1);
-    if ((e = hipStreamWaitValue64(side, sig, seq, hipStreamWaitValueGte, ~0ull)) != hipSuccess) return e;
-    MHT_MARK(2);
-    fs = side;
-  } else if (side && ev) {
+  if (side && ev) {  // k_mixcs_final on the side stream, after an event on the engine stream
     if ((e = hipEventRecord(ev, s)) != hipSuccess) return e;
-    MHT_MARK(1);
     if ((e = hipStreamWaitEvent(side, ev, 0)) != hipSuccess) return e;
-    MHT_MARK(2);
     fs = side;
   }
   const int vn = dtype == 0 ? 4 : 2;
@@ -2020,7 +1515,6 @@ hipError_t launch_mixcs(int dtype, const RoundArgs& a, const void* G, int n_work
     hipLaunchKernelGGL(k_mixcs_final<float>, g2, dim3(NT), 0, fs, mm, a.ld, a.nchunks, (float*)a.send);
   else
     hipLaunchKernelGGL(k_mixcs_final<double>, g2, dim3(NT), 0, fs, mm, a.ld, a.nchunks, (double*)a.send);
-  MHT_MARK(3);
   return hipGetLastError();
 }
 

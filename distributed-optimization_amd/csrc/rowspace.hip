@@ -52,7 +52,7 @@ __device__ __forceinline__ typename VT<T>::v rs_ld_nt(const T* p) {
 // its dependency chain per row (a wave per SIMD has nothing else to issue while the chain drains);
 // after the window, lane k sums row k's partials.  LDOT 1: pdot [64 rows][64 lanes] per wave, lane
 // l's value of row k at slot (l + k) % 64, summed in lane order (32 KiB per wave: 147 KiB per
-// workgroup, one workgroup per CU; the default).  LDOT 2 (A/B, DOPT_RS_LDOT=2): adjacent lanes'
+// workgroup, one workgroup per CU; the default).  LDOT 2 (measured in an A/B build): adjacent lanes'
 // partials are first added by one DPP quad swap, and the even lanes store [64 rows][32 pairs] (slot
 // (l/2 + k) % 32), summed in pair order -- 16 KiB per wave, 80 KiB per workgroup with the column-sum
 // LDS, so two workgroups (two waves per SIMD at <= 256 VGPRs) share a CU: 1 % slower than LDOT 1
@@ -865,50 +865,16 @@ __global__ __launch_bounds__(64) void k_rs_x0_fold(const RsArgs a, const double*
 // ---------------------------------------------------------------------------- launchers
 static const char* rs_tn(int dtype) { return dtype == 0 ? "float" : "double"; }
 
-// Pass shapes (RsArgs.cb / nbuf, picked by the runtime; DOPT_RS_CB / DOPT_RS_NBUF for A/B runs).
-// X32: float64 arithmetic over float32-stored rows (k_rs_pass_x32).
+// The pass shape the runtime picks (RsArgs.cb / nbuf / ldot: 2 / 8 / 1; the other shapes
+// were measured in round 3-4 A/B builds, removed in round 6).  X32: float64 arithmetic over float32-stored
+// rows (k_rs_pass_x32).
 template <typename T, bool X32, bool COLS>
 static hipError_t rs_pass_shape(const RsArgs& a, dim3 grid, hipStream_t s) {
-#define RS_SHAPE(C_, B_)                                                                       \
-  if (a.cb == C_ && a.nbuf == B_) {                                                            \
-    if constexpr (X32) hipLaunchKernelGGL((k_rs_pass_x32<COLS, C_, B_>), grid, dim3(NT), 0, s, a); \
-    else hipLaunchKernelGGL((k_rs_pass<T, COLS, C_, B_>), grid, dim3(NT), 0, s, a);          \
-    return hipGetLastError();                                                                  \
-  }
-  if (a.ldot == 2 && a.cb == 2 && a.nbuf == 8) {  // DOPT_RS_LDOT=2: row dots through LDS, lane pairs first
-    if constexpr (X32) hipLaunchKernelGGL((k_rs_pass_x32<COLS, 2, 8, 2>), grid, dim3(NT), 0, s, a);
-    else hipLaunchKernelGGL((k_rs_pass<T, COLS, 2, 8, 2>), grid, dim3(NT), 0, s, a);
-    return hipGetLastError();
-  }
-  if (a.ldot == 1 && a.cb == 2 && a.nbuf == 8) {  // the default: every lane's partial through LDS
+  if (a.ldot == 1 && a.cb == 2 && a.nbuf == 8) {  // every lane's partial through LDS
     if constexpr (X32) hipLaunchKernelGGL((k_rs_pass_x32<COLS, 2, 8, 1>), grid, dim3(NT), 0, s, a);
     else hipLaunchKernelGGL((k_rs_pass<T, COLS, 2, 8, 1>), grid, dim3(NT), 0, s, a);
     return hipGetLastError();
   }
-#ifdef DOPT_AB
-  if (a.ldot == 1 && a.cb == 2 && a.nbuf == 16) {  // 16 rows in flight per wave (one wave per SIMD anyway)
-    if constexpr (X32) hipLaunchKernelGGL((k_rs_pass_x32<COLS, 2, 16, 1>), grid, dim3(NT), 0, s, a);
-    else hipLaunchKernelGGL((k_rs_pass<T, COLS, 2, 16, 1>), grid, dim3(NT), 0, s, a);
-    return hipGetLastError();
-  }
-  if (a.ldot == 1 && a.cb == 4 && a.nbuf == 4) {  // 4 KiB blocks: half the blocks, half the row-dot partials
-    if constexpr (X32) hipLaunchKernelGGL((k_rs_pass_x32<COLS, 4, 4, 1>), grid, dim3(NT), 0, s, a);
-    else hipLaunchKernelGGL((k_rs_pass<T, COLS, 4, 4, 1>), grid, dim3(NT), 0, s, a);
-    return hipGetLastError();
-  }
-#endif
-  RS_SHAPE(2, 8)  // the default; the others: A/B builds (DOPT_RS_CB / DOPT_RS_NBUF)
-#ifdef DOPT_AB
-  RS_SHAPE(2, 6)
-  RS_SHAPE(4, 2)
-  RS_SHAPE(4, 3)
-  RS_SHAPE(2, 3)
-  RS_SHAPE(2, 4)
-  RS_SHAPE(1, 8)
-  RS_SHAPE(1, 12)
-  RS_SHAPE(1, 16)
-#endif
-#undef RS_SHAPE
   return hipErrorInvalidValue;
 }
 

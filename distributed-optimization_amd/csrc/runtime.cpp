@@ -76,18 +76,6 @@ namespace {
 constexpr int64_t kRsColsBlock = 256;  // columns per k_rs_cols workgroup (kcommon.h NT)
 constexpr int64_t kTileRowChunks = 64;  // 16-byte data chunks of a row per tile (kcommon.h kTileChunks)
 
-// Launch-shape tuning knobs: read from the environment only in A/B builds (make AB=1); the
-// shipped library uses the measured defaults whatever the environment holds.
-int64_t ab_knob(const char* name, int64_t dflt) {
-#ifdef DOPT_AB
-  const char* v = getenv(name);
-  return v ? atoll(v) : dflt;
-#else
-  (void)name;
-  return dflt;
-#endif
-}
-
 #define CHECK_ARG(cond, ...)                          \
   do {                                                \
     if (!(cond)) return fail(DOPT_ERR_INVALID, __VA_ARGS__); \
@@ -215,12 +203,8 @@ struct dopt_ctx {
   std::vector<int64_t> lg_in_h, lg_out_h;  // host copies of the sum rows (-1: self)
   hipStream_t lg_side = nullptr;  // dopt_lagged_side_stream: k_mixcs_final and the exchange go there
   hipEvent_t lg_side_ev = nullptr;
-  // DOPT_LAGGED_SYNC=value: the two streams hand off through stream memory operations on lg_sig (signal
-  // memory): [0] = the last k_mixcs done (engine -> side), [1] = the last exchange done (side -> engine)
-  uint64_t* lg_sig[2] = {nullptr, nullptr};  // (signal memory: one 8-byte value per allocation)
-  uint64_t lg_mseq = 0, lg_xseq = 0;
-  bool lg_xwait = false;  // the next mix / tail waits for the exchange (lg_sig[1] >= lg_xseq, or lg_xev)
-  hipEvent_t lg_xev = nullptr;  // recorded on the side stream behind an exchange issued there (event mode)
+  bool lg_xwait = false;  // the next mix / tail waits for the exchange (lg_xev)
+  hipEvent_t lg_xev = nullptr;  // recorded on the side stream behind an exchange issued there
   // dopt_lagged_transport: the exchange through an RCCL communicator of the caller's (transport.cpp), one
   // send / receive per non-empty block of the layout, issued by dopt_lagged_exchange
   dopt_comm* xp = nullptr;
@@ -230,7 +214,6 @@ struct dopt_ctx {
   double* lg_own[2] = {nullptr, nullptr};  // [ld] this rank's column sums of x_g (g parity)
   double* lg_cons[2] = {nullptr, nullptr}; // [ncb x n] consensus partials of x_g (g parity)
   double* lg_part = nullptr;               // [ng x ld] group partials of k_mixcs
-  unsigned* lg_cnt = nullptr;              // [ncb] k_mixcs tickets
   int32_t lg_ncb = 0, lg_r = 0, lg_ng = 0;
   int64_t lg_alloc_n = -1, lg_alloc_ld = -1;
   int64_t lg = 0;                          // rounds of the current lagged chain
@@ -449,7 +432,7 @@ int set_layout(dopt_ctx* c, int problem, int64_t n, int64_t d) {
   // (k_rs_pass_x32) or the direct column-blocked kernels (k_split_*<double, float, ...>)
   if (c->split) {  // enough workgroups to fill 256 CUs several times over
     const int64_t nblk = (nch + 63) / 64;
-    const int64_t target = std::max<int64_t>(1, ab_knob("DOPT_SPLIT_WGS", 4096));  // workgroups per launch
+    const int64_t target = std::max<int64_t>(1, 4096);  // workgroups per launch
     c->split_groups = (int)std::max<int64_t>(1, std::min<int64_t>(nblk, (target + n - 1) / n));
   }
   c->problem = problem;
@@ -488,11 +471,8 @@ int ensure_hist(dopt_ctx* c, int64_t T) {
   return DOPT_OK;
 }
 
-// fp32 complete-graph mixing reads the column sums as T (A/B builds: DOPT_MEAN_SUMS_T=0, as float64)
-bool sums_t_enabled(dopt_ctx* c) {
-  if (c->dtype != DOPT_F32) return false;
-  return ab_knob("DOPT_MEAN_SUMS_T", 1) != 0;
-}
+// fp32 complete-graph mixing reads the column sums as T (measured faster than reading them as float64)
+bool sums_t_enabled(dopt_ctx* c) { return c->dtype == DOPT_F32; }
 
 // The T copy of the sums the next mix reads (after every producer of S / S_ext).
 int refresh_sums_t(dopt_ctx* c) {
@@ -633,23 +613,10 @@ int upload_idx_chunk(dopt_ctx* c, const int32_t* idx, int64_t h0, int64_t nr, in
   return DOPT_OK;
 }
 
-// Event flags: a device-scope release instead of the system-scope fence (whose L2 writeback and
-// invalidate the following kernels pay) where only this device reads what the event orders.  A/B builds:
-// DOPT_SIDE_EV / DOPT_PROF_EV = dev / sys / nofence override the default (round 5, profiles/r5_sync_ab.txt,
-// r5_pe_ab.txt: for the sampled profiling events and the side stream's hand-off alike the scope is within
-// the run-to-run noise; device scope is kept as the one the consumers need).
-unsigned ev_flags(const char* knob, unsigned base, bool device_default) {
-  bool dev = device_default;
-#ifdef DOPT_AB
-  if (const char* v = getenv(knob)) {
-    if (v[0] == 'n') return base | hipEventDisableSystemFence;  // no fence at all (A/B)
-    dev = v[0] == 'd';
-  }
-#else
-  (void)knob;
-#endif
-  return dev ? (base | hipEventReleaseToDevice) : base;
-}
+// The sampled profiling events release to device scope instead of the system-scope fence (whose L2
+// writeback and invalidate the following kernels pay): only this device reads what they order (round 5,
+// profiles/r5_pe_ab.txt: within the run-to-run noise either way).
+constexpr unsigned kProfEventFlags = hipEventDefault | hipEventReleaseToDevice;
 
 int prof_event(dopt_ctx* c, bool stop) {
   if (!stop) c->prof_skip = (c->prof_seq++ % c->prof_every) != 0;
@@ -657,7 +624,7 @@ int prof_event(dopt_ctx* c, bool stop) {
   const size_t k = (size_t)(2 * c->prof_n + (stop ? 1 : 0));
   while (c->ev.size() <= k) {
     hipEvent_t e;
-    HIPOK(hipEventCreateWithFlags(&e, ev_flags("DOPT_PROF_EV", hipEventDefault, true)));
+    HIPOK(hipEventCreateWithFlags(&e, kProfEventFlags));
     c->ev.push_back(e);
   }
   HIPOK(hipEventRecord(c->ev[k], c->stream));
@@ -933,8 +900,8 @@ constexpr int kRsCheckGroups = 16;  // column groups of the equal-start check
 
 int ensure_rs(dopt_ctx* c) {
   if (c->rs_wg > 0) return DOPT_OK;
-  // pass shape (A/B builds: DOPT_RS_CB / DOPT_RS_NBUF pick the compiled pairs in rowspace.hip)
-  // C5 float32 (tools/rs_ab.py, interleaved on one box, round ms): CB / NBUF / row groups
+  // pass shape, measured in A/B builds:
+  // C5 float32 (round-3 A/B build, interleaved on one box, round ms): CB / NBUF / row groups
   // 2 / 6 / 2 11.22, 2 / 4 / 2 11.50, 1 / 8 / 4 11.46-11.84, 2 / 6 / 4 11.33-11.57, 4 / 2 / 4 12.36,
   // 1 / 8 / 16 12.36, 4 / 2 / 16 13.1-13.2: the partial sums' writes (dots nblk x rows, column
   // sums groups x ld) and long row visits matter more than the tail of ~4k 16 MiB workgroups.
@@ -943,11 +910,11 @@ int ensure_rs(dopt_ctx* c) {
   // 1 / 8 10.93-11.41, the 2 / 6 row loop 10.87-11.12.  Round 4 (row dots through LDS, LDOT 1, one
   // workgroup per CU; profiles/r4_c5_shapes.txt, 3 reps interleaved): 1 row group of 16k rows
   // 10.757-10.762 ms, 2 groups 10.867-10.909, 4 groups 10.924-10.963, 16 rows in flight 10.874-10.895
-  c->rs_cb = (int)ab_knob("DOPT_RS_CB", 2);
-  c->rs_nbuf = (int)ab_knob("DOPT_RS_NBUF", 8);
-  c->rs_ldot = (int)ab_knob("DOPT_RS_LDOT", 1);
+  c->rs_cb = 2;
+  c->rs_nbuf = 8;
+  c->rs_ldot = 1;
   const int64_t nblk = (c->nch + 64 * c->rs_cb - 1) / (64 * c->rs_cb);
-  int64_t wg = ab_knob("DOPT_RS_WG", (c->rows + 16383) / 16384);  // ~16k rows per row group
+  int64_t wg = (c->rows + 16383) / 16384;  // ~16k rows per row group
   wg = std::max<int64_t>(1, std::min<int64_t>(wg, (c->rows + 255) / 256));
   int rc;
   c->rs_nblk = (int)nblk;
@@ -1311,14 +1278,11 @@ int dopt_destroy(dopt_ctx* c) {
   dfree_t(c->rs_grow);
   dfree_t(c->rs_flags);
   for (double** p : {&c->lg_own[0], &c->lg_own[1], &c->lg_cons[0], &c->lg_cons[1], &c->lg_part}) dfree_t(*p);
-  dfree_t(c->lg_cnt);
   dfree_t(c->lg_sum_in);
   dfree_t(c->lg_sum_out);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->lg_side_ev) (void)hipEventDestroy(c->lg_side_ev);
   if (c->lg_xev) (void)hipEventDestroy(c->lg_xev);
-  for (uint64_t* p : c->lg_sig)
-    if (p) (void)hipFree(p);
   for (int k = 0; k < 2; ++k) {
     if (c->idx_ev[k]) (void)hipEventDestroy(c->idx_ev[k]);
     if (c->idx_pin[k]) (void)hipHostFree(c->idx_pin[k]);
@@ -2555,8 +2519,6 @@ int lagged_ready(dopt_ctx* c) {
     if ((rc = dalloc_t(&c->lg_cons[k], (size_t)std::max<int64_t>(1, c->lg_ncb * c->n) * sizeof(double)))) return rc;
   }
   if ((rc = dalloc_t(&c->lg_part, (size_t)c->lg_ng * c->ld * sizeof(double)))) return rc;
-  if ((rc = dalloc_t(&c->lg_cnt, (size_t)std::max(16, c->lg_ncb) * sizeof(unsigned)))) return rc;
-  HIPOK(hipMemsetAsync(c->lg_cnt, 0, (size_t)std::max(16, c->lg_ncb) * sizeof(unsigned), c->stream));
   c->lg_alloc_n = c->n;
   c->lg_alloc_ld = c->ld;
   return DOPT_OK;
@@ -2589,33 +2551,14 @@ int lagged_loss_pass(dopt_ctx* c, int two_points) {
   return DOPT_OK;
 }
 
-// How the lagged schedule's two streams hand off (DOPT_LAGGED_SYNC; round 5, profiles/r5_sync_ab.txt):
-//   0 "event": an event recorded on the engine stream after k_mixcs, waited for on the side stream, and the
-//              caller's work.wait() on the exchange (round 4; the default: fastest measured);
-//   1 "value": stream memory operations both ways (a write after k_mixcs / after the exchange, a wait on
-//              the other stream); on this ROCm they run as small kernels, ~5 us each on either stream, so
-//              the 512-worker round is ~6 % slower than with events (also with GPU_STREAMOPS_CP_WAIT=1).
-// 1 needs stream wait values on the device (else 0).
-int lagged_sync_mode() {
-  static const int mode = [] {
-    const char* v = getenv("DOPT_LAGGED_SYNC");
-    const int want = (v && v[0] == 'v') ? 1 : 0;
-    if (want == 0) return 0;
-    int dev = 0, ok = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    return (hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, dev) == hipSuccess && ok) ? want : 0;
-  }();
-  return mode;
-}
-bool lagged_value_sync() { return lagged_sync_mode() == 1; }
-
-// The engine stream waits for the exchange the caller issued on the side stream (value sync).
+// How the lagged schedule's two streams hand off (round 5, profiles/r5_sync_ab.txt): an event recorded on
+// the engine stream after k_mixcs, waited for on the side stream, and an event behind the exchange on the
+// side stream that the next mix waits for -- the fastest of the forms measured (stream memory operations,
+// ~5 us each as small kernels on this ROCm, made the 512-worker round ~6 % slower).
+// The engine stream waits for the exchange issued on the side stream.
 int lagged_xwait(dopt_ctx* c) {
   if (!c->lg_xwait) return DOPT_OK;
-  if (lagged_value_sync())
-    HIPOK(hipStreamWaitValue64(c->stream, c->lg_sig[1], c->lg_xseq, hipStreamWaitValueGte, ~0ull));
-  else
-    HIPOK(hipStreamWaitEvent(c->stream, c->lg_xev, 0));
+  HIPOK(hipStreamWaitEvent(c->stream, c->lg_xev, 0));
   c->lg_xwait = false;
   return DOPT_OK;
 }
@@ -2624,7 +2567,6 @@ McsArgs lagged_args(dopt_ctx* c, const double* own_in, double* own_out, double* 
   McsArgs m;
   memset(&m, 0, sizeof(m));
   m.part = c->lg_part;
-  m.cnt = c->lg_cnt;
   m.ng = c->lg_ng;
   m.ncb = c->lg_ncb;
   m.r = c->lg_r;
@@ -2669,12 +2611,9 @@ int dopt_lagged_begin(dopt_ctx* c, int64_t batch) {
 namespace {
 // An exchange was just enqueued on the side stream: the next mix / tail waits for it.
 int lagged_mark_exchange(dopt_ctx* c) {
-  if (lagged_value_sync()) {
-    HIPOK(hipStreamWriteValue64(c->lg_side, c->lg_sig[1], ++c->lg_xseq, 0));
-  } else {  // an event of the context's own (no timing, created once) behind the exchange on the side stream
-    if (!c->lg_xev) HIPOK(hipEventCreateWithFlags(&c->lg_xev, ev_flags("DOPT_SIDE_EV", hipEventDisableTiming, false)));
-    HIPOK(hipEventRecord(c->lg_xev, c->lg_side));
-  }
+  // an event of the context's own (no timing, created once) behind the exchange on the side stream
+  if (!c->lg_xev) HIPOK(hipEventCreateWithFlags(&c->lg_xev, hipEventDisableTiming));
+  HIPOK(hipEventRecord(c->lg_xev, c->lg_side));
   c->lg_xwait = true;
   return DOPT_OK;
 }
@@ -2721,49 +2660,17 @@ int dopt_lagged_transport(dopt_ctx* c, dopt_comm* comm, const int64_t* send_rows
   return DOPT_OK;
 }
 
-#ifdef DOPT_AB
-// A/B builds, DOPT_HOST_TIMING=1: host time of dopt_lagged_exchange's RCCL group and hand-off record, and of
-// dopt_lagged_mix's wait for the exchange, printed at exit
-namespace {
-struct XpHostTiming {
-  double ns[3] = {0, 0, 0};
-  long calls[3] = {0, 0, 0};
-  bool on = getenv("DOPT_HOST_TIMING") && atoi(getenv("DOPT_HOST_TIMING")) != 0;
-  ~XpHostTiming() {
-    if (on && calls[0])
-      fprintf(stderr, "[dopt] lagged exchange host us per call: RCCL group %.2f, hand-off record %.2f (%ld calls); "
-              "engine wait for the exchange %.2f (%ld calls)\n", ns[0] / calls[0] / 1e3, ns[1] / calls[0] / 1e3,
-              calls[0], calls[2] ? ns[2] / calls[2] / 1e3 : 0.0, calls[2]);
-  }
-};
-XpHostTiming g_xht;
-double xht_now() {
-  return (double)std::chrono::duration_cast<std::chrono::nanoseconds>(
-             std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-}  // namespace
-#define XHT_BEGIN() const double xht_t0 = g_xht.on ? xht_now() : 0.0
-#define XHT_END(k) do { if (g_xht.on) { g_xht.ns[k] += xht_now() - xht_t0; g_xht.calls[k]++; } } while (0)
-#else
-#define XHT_BEGIN() do { } while (0)
-#define XHT_END(k) do { } while (0)
-#endif
-
 int dopt_lagged_exchange(dopt_ctx* c) {
   CHECK_ARG(c, "ctx is NULL");
   if (!c->xp) return fail(DOPT_ERR_STATE, "no transport (dopt_lagged_transport first)");
   int rc;
   {
-    XHT_BEGIN();
     if ((rc = comm_exchange(c->xp, c->xp_ops.data(), c->xp_ops.size(), c->send, c->halo,
                             c->lg_side ? c->lg_side : c->stream)))
       return rc;
-    XHT_END(0);
   }
   if (!c->lg_side) return DOPT_OK;  // (one stream: ordered by the stream itself)
-  XHT_BEGIN();
   rc = lagged_mark_exchange(c);
-  XHT_END(1);
   return rc;
 }
 
@@ -2772,14 +2679,7 @@ int dopt_lagged_side_stream(dopt_ctx* c, void* stream) {
   int rc;
   if ((rc = set_device(c))) return rc;
   if (stream && !c->lg_side_ev)
-    HIPOK(hipEventCreateWithFlags(&c->lg_side_ev, ev_flags("DOPT_SIDE_EV", hipEventDisableTiming, false)));
-  if (stream && lagged_sync_mode() != 0 && !c->lg_sig[0]) {
-    for (uint64_t*& p : c->lg_sig) {
-      HIPOK(hipExtMallocWithFlags((void**)&p, sizeof(uint64_t), hipMallocSignalMemory));
-      HIPOK(hipMemset(p, 0, sizeof(uint64_t)));
-    }
-    c->lg_mseq = c->lg_xseq = 0;
-  }
+    HIPOK(hipEventCreateWithFlags(&c->lg_side_ev, hipEventDisableTiming));
   c->lg_side = (hipStream_t)stream;
   c->lg_xwait = false;
   return DOPT_OK;
@@ -2825,12 +2725,9 @@ int dopt_lagged_mix(dopt_ctx* c, int64_t t, double eta0, int consensus, double* 
   f.out_l = loss_out;
   f.out_q = xnorm_out;
   {
-    XHT_BEGIN();
     if ((rc = lagged_xwait(c))) return rc;
-    XHT_END(2);
   }
-  HIPOK(launch_mixcs(c->dtype, a, c->G, (int)c->n, m, any ? &f : nullptr, c->stream, c->lg_side, c->lg_side_ev,
-                     c->lg_side ? c->lg_sig[0] : nullptr, c->lg_side && c->lg_sig[0] ? ++c->lg_mseq : 0));
+  HIPOK(launch_mixcs(c->dtype, a, c->G, (int)c->n, m, any ? &f : nullptr, c->stream, c->lg_side, c->lg_side_ev));
   c->xb ^= 1;
   c->cur ^= 1;
   c->lg += 1;

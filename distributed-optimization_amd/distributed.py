@@ -84,7 +84,7 @@ def init_process_group(backend, timeout=None, **kw):
     """torch.distributed.init_process_group with a bounded collective timeout (`timeout`
     seconds, default timeout_seconds()); for "nccl" (RCCL) with high-priority internal
     streams, so the halo send/recv and the all-reduce of a round get CU slots ahead of the
-    4096-workgroup gradient kernel they overlap (DOPT_NCCL_HIPRI=0: default priority).
+    4096-workgroup gradient kernel they overlap.
     With RCCL the watchdog aborts a rank whose collective exceeds the timeout (the work, its
     sequence number and op type in the message) and the launcher ends the other ranks; with
     gloo the waiting call raises, which the transport below turns into CollectiveError."""
@@ -93,7 +93,7 @@ def init_process_group(backend, timeout=None, **kw):
     import torch.distributed as dist
 
     kw.setdefault("timeout", datetime.timedelta(seconds=timeout if timeout is not None else timeout_seconds()))
-    if backend == "nccl" and os.environ.get("DOPT_NCCL_HIPRI", "1") != "0":
+    if backend == "nccl":
         opts = dist.ProcessGroupNCCL.Options()
         opts.is_high_priority_stream = True
         opts._timeout = kw["timeout"]  # the options carry the job's bound too (no override warning)
@@ -356,10 +356,8 @@ class HaloExchange:
     waits on the host with the job's timeout, so a peer that never sends ends this rank with a
     CollectiveError naming it."""
 
-    def __init__(self, plan, send, halo, group=None, device_comm=False, layout=None, current_stream=None):
-        """layout: an ExchangeLayout (the blocks carry column-sum rows too), or None: the plan's rows.
-        current_stream (RCCL): enqueue the all-to-all on the caller's current stream (asyncOp=False)
-        instead of the process group's internal one (default: DOPT_A2A_STREAM=current)."""
+    def __init__(self, plan, send, halo, group=None, device_comm=False, layout=None):
+        """layout: an ExchangeLayout (the blocks carry column-sum rows too), or None: the plan's rows."""
         import torch.distributed as dist
 
         self.dist, self.plan, self.group, self.device_comm = dist, plan, group, device_comm
@@ -382,12 +380,8 @@ class HaloExchange:
         if self.collective:  # the process group's all-to-all-v, called as dist.all_to_all_single calls it,
             try:             # minus its per-call argument checks (host cost per round: VERDICT r3 item 3)
                 opts = dist.AllToAllOptions()
-                # asyncOp=False: ProcessGroupNCCL enqueues the all-to-all on the CURRENT stream (the side
-                # stream) instead of its internal one, so no event hop sits between k_mixcs_final and the
-                # RCCL kernel (DOPT_A2A_STREAM=current; default: the process group's stream)
-                if current_stream is None:
-                    current_stream = os.environ.get("DOPT_A2A_STREAM", "nccl") == "current"
-                opts.asyncOp = not (device_comm and current_stream)
+                # on the process group's stream, behind the current stream's work (the round-5 A/B against
+                # asyncOp=False on the current stream: the engine then waited ~24 us longer per round)
                 pg = group if group is not None else dist.distributed_c10d._get_default_group()
                 self._direct = (pg.alltoall_base, self.halo[:self.nr], self.send[:self.ns], opts)
             except (AttributeError, RuntimeError):
@@ -528,8 +522,6 @@ def _stream(dev, role):
     import torch
 
     key = (int(dev.index if dev.index is not None else torch.cuda.current_device()), role)
-    if os.environ.get("DOPT_FRESH_STREAMS") == "1":  # (A/B: a new pair per runner, the round-4 behaviour)
-        return torch.cuda.Stream(dev)
     st = _STREAMS.get(key)
     if st is None:
         st = _STREAMS[key] = torch.cuda.Stream(dev)
@@ -575,14 +567,7 @@ class DistributedDSGD:
         self.halo = torch.zeros((max(1, lay.n_recv_rows), ld), dtype=tdt, device=self.dev)
         self.send = torch.zeros((max(1, lay.n_send_rows), ld), dtype=tdt, device=self.dev)
         self.sum = torch.zeros(ld, dtype=torch.float64, device=self.dev)
-        # The lagged schedule's exchange on the side stream itself (asyncOp=False: no hop through the process
-        # group's stream before RCCL starts, DOPT_A2A_STREAM=current) or on the process group's stream (nccl,
-        # the default); with the former -- always for DOPT_LAGGED_SYNC=value, whose stream memory operations
-        # need it -- the engine orders the engine stream after the exchange itself (dopt_lagged_exchange_issued)
-        sync_value = os.environ.get("DOPT_LAGGED_SYNC", "event") == "value"
-        self._side_issued = self._lagged_ok and (sync_value or os.environ.get("DOPT_A2A_STREAM", "nccl") == "current")
-        self.exchange = HaloExchange(plan, self.send, self.halo, group, self.device_comm, layout=lay,
-                                     current_stream=True if self._side_issued else None)
+        self.exchange = HaloExchange(plan, self.send, self.halo, group, self.device_comm, layout=lay)
         if rs_chunks:
             self.rs_chunks = int(rs_chunks)
         elif self._solo() or mean is None:
@@ -661,13 +646,9 @@ class DistributedDSGD:
             w = self.exchange.start()
         finally:
             set_id(**to_eng)
-        # the exchange was enqueued on the side stream (RCCL with asyncOp=False, or the host transport's halo
-        # copy): the engine's next mix / tail makes the engine stream wait for it (an event or a stream value).
-        # Only then: the process group's own all-to-all (the fallback without _direct) runs on its internal
-        # stream, which an event on the side stream does not cover -- its work is waited on instead
-        if self._side_issued and (w is None or isinstance(w[0][0], _StreamOrdered)) and self.eng.lagged_exchange_issued():
-            return None
-        if w is None:  # host transport: the halo rows were written on the side stream
+        # the process group's all-to-all runs on its internal stream: finish() waits on its work; the host
+        # transport wrote the halo rows on the side stream, which the engine stream then waits for
+        if w is None:
             self.stream.wait_stream(side)
         return w
 

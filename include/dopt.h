@@ -416,11 +416,11 @@ int dopt_lagged_mix(dopt_ctx *ctx, int64_t t, double eta0, int consensus, double
 int dopt_lagged_tail(dopt_ctx *ctx, int consensus, int objective, double *cons1, double *xnorm1, double *loss1,
                      double *cons2, double *xnorm2, double *loss2);
 int dopt_lagged_side_stream(dopt_ctx *ctx, void *stream);
-/* Right after the caller has enqueued a round's exchange ON the side stream (RCCL with asyncOp = false,
- * or a host transport's halo copy): the context records an event behind it on the side stream (with
- * DOPT_LAGGED_SYNC=value: writes a sequence number there instead) and the next dopt_lagged_mix / _tail
- * makes the engine stream wait for it -- *ordered = 1, the caller does not order the engine stream
- * itself.  *ordered = 0 without a side stream (the caller orders it). */
+/* Right after the caller has enqueued a round's exchange ON the side stream (a transport of its own that
+ * runs on the stream it is issued on, or a host transport's halo copy): the context records an event
+ * behind it on the side stream and the next dopt_lagged_mix / _tail makes the engine stream wait for it --
+ * *ordered = 1, the caller does not order the engine stream itself.  *ordered = 0 without a side stream
+ * (the caller orders it). */
 int dopt_lagged_exchange_issued(dopt_ctx *ctx, int *ordered);
 /* Engine-driven RCCL transport (ABI 7; csrc/transport.cpp).  It replaces, for the lagged schedule's
  * per-round exchange, the caller's process-group all-to-all-v (torch.distributed all_to_all_single in

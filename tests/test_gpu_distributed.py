@@ -42,18 +42,13 @@ def _rank_main(rank, world, rdv, dtype, out, mean=False, T=T, lagged="1", N=N, D
     import distributed as Dm
     import topology as TP
 
-    # "1-noside": the lagged schedule on one stream; "1-value": its streams hand off through stream memory
-    # operations (DOPT_LAGGED_SYNC=value) instead of events
+    # "1-noside": the lagged schedule on one stream; "1-pg": the exchange through the process group's
+    # all-to-all-v instead of the engine's own RCCL communicator (dopt_lagged_exchange, the default)
     opts = lagged.split("-")
     side = "0" if "noside" in opts else "1"
-    sync = "value" if "value" in opts else "event"
-    a2a = "current" if "current" in opts else "nccl"  # "1-current": the all-to-all on the side stream itself
-    # "1-pg": the exchange through the process group's all-to-all-v instead of the engine's own RCCL
-    # communicator (dopt_lagged_exchange, the default)
     transport = "pg" if "pg" in opts else "rccl"
     lagged = opts[0]
-    os.environ.update(DOPT_LAGGED=lagged, DOPT_LAGGED_SIDE=side,
-                      DOPT_LAGGED_SYNC=sync, DOPT_A2A_STREAM=a2a, DOPT_TRANSPORT=transport,
+    os.environ.update(DOPT_LAGGED=lagged, DOPT_LAGGED_SIDE=side, DOPT_TRANSPORT=transport,
                       DOPT_FORCE_COLLECTIVES="1" if backend == "nccl" else "0")
     if backend == "nccl":
         torch.cuda.set_device(0)
@@ -108,10 +103,9 @@ def _rank_main(rank, world, rdv, dtype, out, mean=False, T=T, lagged="1", N=N, D
                                                       ("float64/x32", True, T, "1", 2),
                                                       ("float64/x32", "csr", T, "1", 2),
                                                       ("float64/x32", False, T, "1-noside", 2),
-                                                      ("float64/x32", False, T, "1-value", 2),
-                                                      ("float64", "torus", T, "1-value", 3),
-                                                      ("float32", "torus", T, "1-event", 3),
-                                                      ("float64/x32", "torus", T, "1-current", 2),
+                                                      ("float64", "torus", T, "1", 3),
+                                                      ("float32", "torus", T, "1-noside", 3),
+                                                      ("float64/x32", "torus", T, "1", 2),
                                                       ("float32", "csr", T, "0", 2)])
 def test_ranks_match_single_context(tmp_path, dtype, mean, T, lagged, world):
     import torch.multiprocessing as mp
@@ -493,10 +487,9 @@ def _rccl_self_exchange(rank, world, rdv, out):
 
 
 @pytest.mark.parametrize("dtype,lagged", [("float64", "1"), ("float64/x32", "1"), ("float64", "1-noside"),
-                                          ("float32", "1"), ("float64", "1-value"), ("float64/x32", "1-value"),
-                                          ("float64", "1-pg"), ("float64/x32", "1-pg"), ("float64", "1-pg-value"),
-                                          ("float64", "1-pg-current"), ("float64/x32", "1-pg-current"),
-                                          ("float64", "1-noside-pg-current")])
+                                          ("float32", "1"), ("float64/x32", "1-noside"),
+                                          ("float64", "1-pg"), ("float64/x32", "1-pg"), ("float32", "1-pg"),
+                                          ("float64", "1-noside-pg")])
 def test_rccl_one_rank_self_exchange_matches_single_context(tmp_path, monkeypatch, dtype, lagged):
     """the RCCL path at world 1 (collectives forced) with an exchange that moves data -- a
     third of the workers' rows and the rank's own column sums go through the all-to-all to itself (a
