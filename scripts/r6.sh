@@ -70,6 +70,22 @@ for step in "$@"; do
         || { tail -n 20 gpurun_out/r6_rp_$r.err; die rank_proxy 1; }
       python3 -c "import json; d=json.loads(open('gpurun_out/r6_rp_$r.json').read().strip().splitlines()[-1]); p=d['plan']; [print('strong rank', $r, g['leg'], g['workers'], 'halo', p['halo_rows_in'], 'interior', p['interior'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]"
     done ;;
+  transport_ab)  # rank 0 of the 8-rank strong leg, the engine's non-blocking RCCL communicator vs the process group's
+    # all-to-all (DOPT_TRANSPORT=pg), interleaved twice, one process each -> profiles/r6_rank_proxy.txt
+    for rep in 1 2; do
+      for t in rccl pg; do
+        DOPT_TRANSPORT=$t timeout -k 10 300 python3 tools/rank_proxy.py --world 8 --rank 0 --scaling strong --legs proxy \
+          --reps 1 --steps ${STEPS:-2000} --warmup 300 > gpurun_out/r6_tab_${t}_$rep.json 2> gpurun_out/r6_tab_${t}_$rep.err \
+          || { tail -n 20 gpurun_out/r6_tab_${t}_$rep.err; die transport_ab 1; }
+        python3 -c "import json; d=json.loads(open('gpurun_out/r6_tab_${t}_$rep.json').read().strip().splitlines()[-1]); [print('transport', '$t', 'rep', $rep, g['leg'], g['workers'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]"
+      done
+    done ;;
+  proxy_trace)  # kernel trace of the strong leg's rank 0 (proxy alone, 600 rounds) -> profiles/r6_rank_proxy.txt
+    timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r6_pt -o run -- \
+      python3 tools/rank_proxy.py --world 8 --rank 0 --scaling strong --legs proxy --reps 1 --steps 600 --warmup 100 \
+      > gpurun_out/r6_pt.log 2>&1 || { tail -n 20 gpurun_out/r6_pt.log; die proxy_trace 1; }
+    python3 tools/trace_rounds.py gpurun_out/r6_pt/run_kernel_trace.csv
+    python3 tools/trace_window.py gpurun_out/r6_pt/run_kernel_trace.csv ;;
   c3_profile)  # the driver's shape under rocprofv3: kernel trace + stats, FETCH_SIZE / WRITE_SIZE passes
     # -> profiles/r6_kernel_stats.csv, r6_pmc.json (scripts/pmc_summary.py)
     OUT=gpurun_out/prof_r6 PSTEPS=20 PWARM=5 bash scripts/profile.sh || die c3_profile 1 ;;
