@@ -613,10 +613,18 @@ int upload_idx_chunk(dopt_ctx* c, const int32_t* idx, int64_t h0, int64_t nr, in
   return DOPT_OK;
 }
 
-// The sampled profiling events release to device scope instead of the system-scope fence (whose L2
-// writeback and invalidate the following kernels pay): only this device reads what they order (round 5,
-// profiles/r5_pe_ab.txt: within the run-to-run noise either way).
-constexpr unsigned kProfEventFlags = hipEventDefault | hipEventReleaseToDevice;
+// Events that only order this device's streams (or only time them) skip the system-scope fence of an event
+// record: the kernels before them release their writes at their own end, exactly as for a consumer later on
+// the same stream.  tools/xq_probe.hip (profiles/r6_xq_probe.txt, one-workgroup kernels on the device clock):
+// a record between two kernels of a stream costs 3.8 us with the fence and 2.4 without (1.0 with no record);
+// a kernel waiting on another stream's event that completes just before it could run starts 11.4 us after
+// that event's kernel with the fence and 8.2 without (4.0 when the event completed long before); a
+// device-scope release (hipEventReleaseToDevice) is no cheaper than the system-scope one.  The lagged
+// schedule's fork (the side stream waits for k_mixcs) and join (the engine stream waits for the exchange)
+// are such events.
+constexpr unsigned kOrderEventFlags = hipEventDisableTiming | hipEventDisableSystemFence;
+// The sampled profiling events (timing only)
+constexpr unsigned kProfEventFlags = hipEventDefault | hipEventDisableSystemFence;
 
 int prof_event(dopt_ctx* c, bool stop) {
   if (!stop) c->prof_skip = (c->prof_seq++ % c->prof_every) != 0;
@@ -2612,7 +2620,7 @@ namespace {
 // An exchange was just enqueued on the side stream: the next mix / tail waits for it.
 int lagged_mark_exchange(dopt_ctx* c) {
   // an event of the context's own (no timing, created once) behind the exchange on the side stream
-  if (!c->lg_xev) HIPOK(hipEventCreateWithFlags(&c->lg_xev, hipEventDisableTiming));
+  if (!c->lg_xev) HIPOK(hipEventCreateWithFlags(&c->lg_xev, kOrderEventFlags));
   HIPOK(hipEventRecord(c->lg_xev, c->lg_side));
   c->lg_xwait = true;
   return DOPT_OK;
@@ -2679,7 +2687,7 @@ int dopt_lagged_side_stream(dopt_ctx* c, void* stream) {
   int rc;
   if ((rc = set_device(c))) return rc;
   if (stream && !c->lg_side_ev)
-    HIPOK(hipEventCreateWithFlags(&c->lg_side_ev, hipEventDisableTiming));
+    HIPOK(hipEventCreateWithFlags(&c->lg_side_ev, kOrderEventFlags));
   c->lg_side = (hipStream_t)stream;
   c->lg_xwait = false;
   return DOPT_OK;

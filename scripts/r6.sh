@@ -86,6 +86,20 @@ for step in "$@"; do
       > gpurun_out/r6_pt.log 2>&1 || { tail -n 20 gpurun_out/r6_pt.log; die proxy_trace 1; }
     python3 tools/trace_rounds.py gpurun_out/r6_pt/run_kernel_trace.csv
     python3 tools/trace_window.py gpurun_out/r6_pt/run_kernel_trace.csv ;;
+  xq_probe)  # what a cross-stream hand-off costs (tools/xq_probe.hip, built in-tree beforehand) -> profiles/r6_xq_probe.txt
+    timeout -k 10 120 tools/xq_probe ${REPS:-50} > gpurun_out/r6_xq_probe.txt 2>&1 || { cat gpurun_out/r6_xq_probe.txt; die xq_probe 1; }
+    cat gpurun_out/r6_xq_probe.txt ;;
+  ev_ab)  # the hand-off events without the system fence (this build) vs with it (tools/ab_prev/libdopt.so: the
+    # previous commit's library), the strong leg's rank 0, proxy alone, interleaved -> profiles/r6_ev_ab.txt
+    for rep in 1 2 3; do
+      for arm in new prev; do
+        lib=""; [ $arm = prev ] && lib="DOPT_LIB=$PWD/tools/ab_prev/libdopt.so"
+        env $lib timeout -k 10 300 python3 tools/rank_proxy.py --world 8 --rank 0 --scaling ${SCALING:-strong} --legs proxy \
+          --reps 1 --steps ${STEPS:-2000} --warmup 300 > gpurun_out/r6_ev_${arm}_$rep.json 2> gpurun_out/r6_ev_${arm}_$rep.err \
+          || { tail -n 20 gpurun_out/r6_ev_${arm}_$rep.err; die ev_ab 1; }
+        python3 -c "import json; d=json.loads(open('gpurun_out/r6_ev_${arm}_$rep.json').read().strip().splitlines()[-1]); [print('events', '$arm', 'rep', $rep, g['leg'], g['workers'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]"
+      done
+    done ;;
   c3_profile)  # the driver's shape under rocprofv3: kernel trace + stats, FETCH_SIZE / WRITE_SIZE passes
     # -> profiles/r6_kernel_stats.csv, r6_pmc.json (scripts/pmc_summary.py)
     OUT=gpurun_out/prof_r6 PSTEPS=20 PWARM=5 bash scripts/profile.sh || die c3_profile 1 ;;
