@@ -530,7 +530,8 @@ def setup_leg(args, config, n_global, world, rank, dev):
                   "halo_rows_in": int(plan.n_halo), "send_rows_out": int(len(plan.send_ids)),
                   "halo_bytes_in_per_round": int(plan.n_halo) * ld * esz_state,
                   "send_bytes_out_per_round": int(len(plan.send_ids)) * ld * esz_state,
-                  "peers": [int(p) for p in runner._peers]}
+                  "peers": [int(p) for p in runner._peers],
+                  "exchange_beside_gradient": runner.side is not None}
         if S.mean is None:  # the lagged schedule: the column sums ride the halo all-to-all
             S.comm.update({"collectives_per_round": 1 if world > 1 else 0,
                            "exchange": ("one RCCL group of per-peer sends / receives per round, issued by the engine "
@@ -585,29 +586,28 @@ def per_rank(world, item):
     return out
 
 
-def serial_exchange_leg(args, S, world, barrier, dev):
-    """N > 1, after the headline leg, on its engine and shards: the same rounds with the exchange serialised on
-    the engine stream (DOPT_LAGGED_SIDE=0: the exchange between the mix and the next
-    gradient kernel instead of beside it).  On one GPU the RCCL kernel beside the gradient kernel cost that
-    kernel up to ~70 us per round on some boxes (tools/rank_proxy.py) while a serial exchange
-    adds the transfer itself; which form wins with real peers over xGMI only a multi-GPU run can tell, so the
-    scaling run reports both (this one is not `value`)."""
+def alt_exchange_leg(args, S, world, barrier, dev):
+    """N > 1, after the headline leg, on its engine and shards: the same rounds with the exchange in the other
+    form -- serialised on the engine stream (between the mix and the next gradient kernel) where the headline
+    ran it on the side stream beside the gradient kernel, and the reverse.  distributed.side_stream_wanted
+    picks the form from one-GPU rank proxies, where the exchange is an RCCL self-copy; with real peers over
+    xGMI a serial exchange also exposes the transfer, which only a multi-GPU run can price, so the scaling
+    run reports both (this one is not `value`)."""
     import torch
     import torch.distributed as dist
 
     import distributed
 
-    keys = ("DOPT_LAGGED_SIDE",)
-    old = {k: os.environ.get(k) for k in keys}
-    os.environ.update(DOPT_LAGGED_SIDE="0")
+    side = "0" if S.comm.get("exchange_beside_gradient") else "1"
+    old = os.environ.get("DOPT_LAGGED_SIDE")
+    os.environ["DOPT_LAGGED_SIDE"] = side
     try:
         runner = distributed.DistributedDSGD(S.eng, S.plan, S.n_global, S.n_global * S.m, device=dev)
     finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+        if old is None:
+            os.environ.pop("DOPT_LAGGED_SIDE", None)
+        else:
+            os.environ["DOPT_LAGGED_SIDE"] = old
     if not runner._lagged_ok:
         return None
     eta0, b, lam = S.eta0, S.b, S.lam
@@ -618,9 +618,10 @@ def serial_exchange_leg(args, S, world, barrier, dev):
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     dt = float(tt.item())
     return {"value": S.n_global * args.steps / dt, "unit": "worker-iters/s", "ms_per_step": dt / args.steps * 1e3,
-            "kernel_avg_ms": kr_ms / launches if launches else None, "side_stream": runner.side is not None,
-            "final_objective": float(obj[-1]),
-            "form": "the exchange serialised on the engine stream (DOPT_LAGGED_SIDE=0)"}
+            "kernel_avg_ms": kr_ms / launches if launches else None,
+            "exchange_beside_gradient": runner.side is not None, "final_objective": float(obj[-1]),
+            "form": ("the exchange on the side stream beside the gradient kernel (DOPT_LAGGED_SIDE=1)" if side == "1"
+                     else "the exchange serialised on the engine stream (DOPT_LAGGED_SIDE=0)")}
 
 
 def transport_probe(args, world, dev, barrier, shape, reps=20, warm=3):
@@ -879,12 +880,12 @@ def main():
         out["metric"] = f"worker-iters/sec ({args.config.upper()}, secondary config)"
     secondary = rank == 0 and world == 1 and not args.phase and args.config == "c3" and not args.no_secondary
     if world > 1 and args.config == "c3" and S.flush is not None and not args.no_alt_exchange:
-        log("headline leg again with the exchange serialised on the engine stream (A/B with real peers)")
+        log("headline leg again with the exchange in the other form (A/B with real peers)")
         try:  # diagnostic only: a failure here must not cost the line its value
-            out["serial_exchange"] = serial_exchange_leg(args, S, world, barrier, dev)
+            out["alt_exchange"] = alt_exchange_leg(args, S, world, barrier, dev)
         except Exception as e:  # noqa: BLE001
-            log(f"serial_exchange failed: {e!r}")
-            out["serial_exchange"] = {"error": repr(e)[:300]}
+            log(f"alt_exchange failed: {e!r}")
+            out["alt_exchange"] = {"error": repr(e)[:300]}
     if secondary and b == m:
         log("f(x*): device L-BFGS")
         out["suboptimality"] = suboptimality(eng, lam, float(obj[-1]))
@@ -900,7 +901,11 @@ def main():
     eng.close()
     if args.config == "c3" and world > 1 and args.scaling == "both":
         log(f"weak-scaling leg: {args.workers} workers per rank, {args.workers * world} over {world} ranks")
-        out["weak"] = extra_leg(args, world, rank, dev, barrier, "weak")
+        try:  # secondary: a failure here must not cost the line its value (every rank raises alike)
+            out["weak"] = extra_leg(args, world, rank, dev, barrier, "weak")
+        except Exception as e:  # noqa: BLE001
+            log(f"weak leg failed: {e!r}")
+            out["weak"] = {"error": repr(e)[:300]}
     if world > 1 and getattr(S, "exchange_shape", None) is not None:
         log("transport probe: the headline leg's exchange and an 8 MiB all-reduce alone")
         try:  # diagnostic only, as above

@@ -103,9 +103,6 @@ struct RoundArgs {
   const double* xsum;
   double xsum_n;
   void* xbar_out;
-  // multi-GPU phase path's gradient launch: a worker queue ([0] tickets, [1] workgroups done; both zero between
-  // launches) for dynamic persistent workgroups (k_round VAR bit 22), or null (one workgroup per worker)
-  unsigned* wq;
 };
 
 // History fold riding a k_colsum_final launch (one extra block): *out_c = sum sc[0:nc],

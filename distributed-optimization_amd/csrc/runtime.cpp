@@ -205,7 +205,6 @@ struct dopt_ctx {
   hipEvent_t lg_side_ev = nullptr;
   bool lg_xwait = false;  // the next mix / tail waits for the exchange (lg_xev)
   hipEvent_t lg_xev = nullptr;  // recorded on the side stream behind an exchange issued there
-  unsigned* wq = nullptr;       // [2] the phase gradient launch's worker queue (RoundArgs.wq; zero between launches)
   // dopt_lagged_transport: the exchange through an RCCL communicator of the caller's (transport.cpp), one
   // send / receive per non-empty block of the layout, issued by dopt_lagged_exchange
   dopt_comm* xp = nullptr;
@@ -1288,7 +1287,6 @@ int dopt_destroy(dopt_ctx* c) {
   dfree_t(c->rs_flags);
   for (double** p : {&c->lg_own[0], &c->lg_own[1], &c->lg_cons[0], &c->lg_cons[1], &c->lg_part}) dfree_t(*p);
   dfree_t(c->lg_sum_in);
-  dfree_t(c->wq);
   dfree_t(c->lg_sum_out);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->lg_side_ev) (void)hipEventDestroy(c->lg_side_ev);
@@ -2147,11 +2145,6 @@ int dopt_phase_grad(dopt_ctx* c, int64_t batch, const int32_t* idx, double lam_g
     a.eta = c->ph_eta;
   }
   if (a.flags & F_LOSS) c->loss_groups = c->slab_n[0] = c->n;  // per-worker loss slabs
-  if (!c->wq) {  // dynamic persistent workgroups (k_round VAR bit 22): the queue, zeroed once
-    if ((rc = dalloc_t(&c->wq, 2 * sizeof(unsigned)))) return rc;
-    HIPOK(hipMemsetAsync(c->wq, 0, 2 * sizeof(unsigned), c->stream));
-  }
-  a.wq = c->wq;
   if (c->prof && (rc = prof_event(c, false))) return rc;
   HIPOK(launch_round(c->dtype, c->xdtype, c->problem, c->cpl, true, cons || loss || dev, a, (int)c->n, c->stream));
   if (c->prof && (rc = prof_event(c, true))) return rc;

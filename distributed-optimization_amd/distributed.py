@@ -513,6 +513,29 @@ def close_comms(abort=False):
         c.close(abort)
 
 
+GRAD_WG_PER_CU = 2  # resident gradient workgroups per CU (the headline k_round: 191 VGPRs, 4 waves, ~78 KB LDS)
+
+
+def side_stream_wanted(n_local, dev=None, cus=None):
+    """Whether the lagged schedule runs the exchange on a side stream beside the next gradient kernel.
+
+    Only when one generation of workgroups covers the rank's gradient launch (n_local workers <= 2 per CU).
+    A launch of several generations loses one whole generation whenever the exchange's RCCL kernel holds a
+    workgroup slot during it, and the gradient kernel beside RCCL runs slower: rank proxies on the box put
+    the exchange serialised on the engine stream ahead at 4 ranks (0.347 vs 0.411 ms per round), 2 ranks
+    (0.653-0.672 vs 0.702-0.722) and the weak leg at 8 ranks (1.317-1.320 vs 1.351-1.353); a one-generation
+    rank keeps the overlap (0.1753 vs 0.1780 ms), profiles/r6_side_exp.txt.  DOPT_LAGGED_SIDE=1 always
+    takes the side stream, =0 never."""
+    knob = os.environ.get("DOPT_LAGGED_SIDE", "auto")
+    if knob in ("0", "1"):
+        return knob == "1"
+    if cus is None:
+        import torch
+
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    return int(n_local) <= GRAD_WG_PER_CU * int(cus)
+
+
 def _stream(dev, role):
     """The process's stream `role` (0: the engine's rounds, 1: the lagged schedule's side stream) on device
     `dev`, created once and shared by every runner of the process (bench.py's strong leg builds a second
@@ -592,12 +615,12 @@ class DistributedDSGD:
         self.mean = mean
         engine.set_stream(self.stream.cuda_stream)
         # a second stream for each mix's column-sum totals (k_mixcs_final) and the exchange, so the
-        # next gradient kernel does not wait for them -- whenever there is an exchange to order it
-        # (DOPT_LAGGED_SIDE=0: one stream)
+        # next gradient kernel does not wait for them -- whenever there is an exchange to order it and
+        # the rank's gradient launch is one generation of workgroups (side_stream_wanted)
         self.side = None
         self._stream_switch = None
         if (self._lagged_ok and not self._solo() and self.exchange.peers_or_collective()
-                and os.environ.get("DOPT_LAGGED_SIDE", "1") != "0"):
+                and side_stream_wanted(plan.n_local, self.dev)):
             self.side = _stream(self.dev, 1)
         engine.lagged_side_stream(self.side.cuda_stream if self.side is not None else None)
         # the engine's own RCCL communicator for the lagged exchange (dopt_lagged_exchange), RCCL only

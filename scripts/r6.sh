@@ -38,7 +38,7 @@ d = json.loads(sys.stdin.read())
 print('value', d['value'], 'scaling', d['scaling'], 'workers_total', d['config']['workers_total'], 'per_gpu', d['config']['workers_per_gpu'])
 print('per_rank', [(r['rank'], r['workers']) for r in d.get('per_rank', [])])
 w = d.get('weak'); print('weak', None if w is None else (w['value'], w['n_workers_total'], w['workers_per_gpu']))
-s = d.get('serial_exchange'); print('serial_exchange', None if s is None else (s.get('value'), s.get('ms_per_step')))
+s = d.get('alt_exchange'); print('alt_exchange', None if s is None else (s.get('value'), s.get('ms_per_step'), s.get('exchange_beside_gradient')))
 print('transport_probe', d.get('transport_probe'))"
 }
 
@@ -80,12 +80,13 @@ for step in "$@"; do
         python3 -c "import json; d=json.loads(open('gpurun_out/r6_tab_${t}_$rep.json').read().strip().splitlines()[-1]); [print('transport', '$t', 'rep', $rep, g['leg'], g['workers'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]"
       done
     done ;;
-  proxy_trace)  # kernel trace of the strong leg's rank 0 (proxy alone, 600 rounds) -> profiles/r6_rank_proxy.txt
-    timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r6_pt -o run -- \
-      python3 tools/rank_proxy.py --world 8 --rank 0 --scaling strong --legs proxy --reps 1 --steps 600 --warmup 100 \
-      > gpurun_out/r6_pt.log 2>&1 || { tail -n 20 gpurun_out/r6_pt.log; die proxy_trace 1; }
-    python3 tools/trace_rounds.py gpurun_out/r6_pt/run_kernel_trace.csv
-    python3 tools/trace_window.py gpurun_out/r6_pt/run_kernel_trace.csv ;;
+  proxy_trace)  # kernel trace of the strong leg's rank 0 (proxy alone, WORLD ranks, default 8) -> profiles/r6_rank_proxy.txt
+    W=${WORLD:-8}; D=gpurun_out/r6_pt${WORLD:+_$WORLD}
+    timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv -d $D -o run -- \
+      python3 tools/rank_proxy.py --world $W --rank 0 --scaling strong --legs proxy --reps 1 --steps $((600 * 8 / W)) \
+      --warmup 100 > $D.log 2>&1 || { tail -n 20 $D.log; die proxy_trace 1; }
+    python3 tools/trace_rounds.py $D/run_kernel_trace.csv
+    python3 tools/trace_window.py $D/run_kernel_trace.csv ;;
   scale_proxy)  # rank 0 of the strong leg at 2, 4 and 8 ranks (2048 / 1024 / 512 workers) beside the fused 4096-worker
     # round: the per-rank efficiency the driver's 1/2/4/8-GPU line can reach before xGMI -> profiles/r6_scale_proxy.txt
     for w in 2 4 8; do
@@ -94,48 +95,24 @@ for step in "$@"; do
         || { tail -n 20 gpurun_out/r6_sp_$w.err; die scale_proxy 1; }
       python3 -c "import json; d=json.loads(open('gpurun_out/r6_sp_$w.json').read().strip().splitlines()[-1]); p=d['plan']; [print('world', $w, g['leg'], g['workers'], 'halo', p['halo_rows_in'], 'interior', p['interior'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]; print('proxy / fused', [round(x, 4) for x in d['proxy_over_fused']])"
     done ;;
-  queue_ab)  # the phase path's gradient launch from a worker queue (this build) vs one workgroup per worker
-    # (tools/ab_prev/libdopt.so), rank 0 of the strong leg at 2 / 4 / 8 ranks and of the weak leg at 8, interleaved
-    # -> profiles/r6_queue_ab.txt
+  side_policy)  # the exchange's form as distributed.side_stream_wanted picks it (auto) vs forced side / serial: rank 0 of
+    # the strong leg at 2 / 4 / 8 ranks and of the weak leg at 8, two interleaved reps -> profiles/r6_side_policy.txt
     for rep in 1 2; do
-      for cfg in "strong 2" "strong 4" "strong 8" "weak 8"; do
+      for cfg in "strong 8" "strong 4" "strong 2" "weak 8"; do
         sc=${cfg% *}; w=${cfg#* }
-        for arm in new prev; do
-          lib=""; [ $arm = prev ] && lib="DOPT_LIB=$PWD/tools/ab_prev/libdopt.so"
-          st=$((1000 * 8 / w)); [ $sc = weak ] && st=150
-          env $lib timeout -k 10 300 python3 tools/rank_proxy.py --world $w --rank 0 --scaling $sc --legs proxy --reps 1 \
-            --steps $st --warmup 50 > gpurun_out/r6_q_${sc}${w}_${arm}_$rep.json 2> gpurun_out/r6_q_${sc}${w}_${arm}_$rep.err \
-            || { tail -n 20 gpurun_out/r6_q_${sc}${w}_${arm}_$rep.err; die queue_ab 1; }
-          python3 -c "import json; d=json.loads(open('gpurun_out/r6_q_${sc}${w}_${arm}_$rep.json').read().strip().splitlines()[-1]); [print('$sc', 'world', $w, '$arm', 'rep', $rep, g['workers'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]"
+        st=$((1000 * 8 / w)); [ $sc = weak ] && st=150
+        for arm in auto 1 0; do
+          sd=""; [ $arm = auto ] || sd="DOPT_LAGGED_SIDE=$arm"
+          env $sd timeout -k 10 300 python3 tools/rank_proxy.py --world $w --rank 0 --scaling $sc --legs proxy \
+            --reps 1 --steps $st --warmup 50 > gpurun_out/r6_sp_${sc}${w}_${arm}_$rep.json 2> gpurun_out/r6_sp_${sc}${w}_${arm}_$rep.err \
+            || { tail -n 20 gpurun_out/r6_sp_${sc}${w}_${arm}_$rep.err; die side_policy 1; }
+          python3 -c "import json; d=json.loads(open('gpurun_out/r6_sp_${sc}${w}_${arm}_$rep.json').read().strip().splitlines()[-1]); [print('$sc', 'world', $w, 'side=$arm', 'rep', $rep, g['workers'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]"
         done
-      done
-    done ;;
-  queue_tests)  # the worker-queue launch bitwise vs one context, and the multi-rank tests that run it
-    echo "=== queue tests"; tests r6_queue_tests tests/test_gpu_distributed.py -k "worker_queue or strong_split or eight_ranks or torus" ;;
-  queue_solo)  # (A/B) the queue launch without any exchange: bench.py --phase at world 1, 512 / 1024 / 4096 workers
-    for w in 512 1024 4096; do
-      for arm in new prev; do
-        lib=""; [ $arm = prev ] && lib="DOPT_LIB=$PWD/tools/ab_prev/libdopt.so"
-        st=$((400 * 4096 / w)); [ $st -gt 3000 ] && st=3000
-        env $lib timeout -k 10 200 python3 bench.py --no-cpu-baseline --no-secondary --phase --scaling weak --workers $w --steps $st --warmup 50 \
-          > gpurun_out/r6_qs_${w}_$arm.json 2> gpurun_out/r6_qs_${w}_$arm.err || { tail -n 20 gpurun_out/r6_qs_${w}_$arm.err; die queue_solo 1; }
-        echo -n "phase world 1, $w workers, $arm: "; json_line gpurun_out/r6_qs_${w}_$arm.json
       done
     done ;;
   xq_probe)  # what a cross-stream hand-off costs (tools/xq_probe.hip, built in-tree beforehand) -> profiles/r6_xq_probe.txt
     timeout -k 10 120 tools/xq_probe ${REPS:-50} > gpurun_out/r6_xq_probe.txt 2>&1 || { cat gpurun_out/r6_xq_probe.txt; die xq_probe 1; }
     cat gpurun_out/r6_xq_probe.txt ;;
-  ev_ab)  # the hand-off events without the system fence (this build) vs with it (tools/ab_prev/libdopt.so: the
-    # previous commit's library), the strong leg's rank 0, proxy alone, interleaved -> profiles/r6_ev_ab.txt
-    for rep in 1 2 3; do
-      for arm in new prev; do
-        lib=""; [ $arm = prev ] && lib="DOPT_LIB=$PWD/tools/ab_prev/libdopt.so"
-        env $lib timeout -k 10 300 python3 tools/rank_proxy.py --world 8 --rank 0 --scaling ${SCALING:-strong} --legs proxy \
-          --reps 1 --steps ${STEPS:-2000} --warmup 300 > gpurun_out/r6_ev_${arm}_$rep.json 2> gpurun_out/r6_ev_${arm}_$rep.err \
-          || { tail -n 20 gpurun_out/r6_ev_${arm}_$rep.err; die ev_ab 1; }
-        python3 -c "import json; d=json.loads(open('gpurun_out/r6_ev_${arm}_$rep.json').read().strip().splitlines()[-1]); [print('events', '$arm', 'rep', $rep, g['leg'], g['workers'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]"
-      done
-    done ;;
   c3_profile)  # the driver's shape under rocprofv3: kernel trace + stats, FETCH_SIZE / WRITE_SIZE passes
     # -> profiles/r6_kernel_stats.csv, r6_pmc.json (scripts/pmc_summary.py)
     OUT=gpurun_out/prof_r6 PSTEPS=20 PWARM=5 bash scripts/profile.sh || die c3_profile 1 ;;

@@ -214,23 +214,6 @@ def test_torus_strips_ranks_match_single_context(tmp_path, monkeypatch, world, d
     _compare_single(got, dtype, "torus", t, n, d, m)
 
 
-@pytest.mark.parametrize("n", [1200, 2100])
-def test_worker_queue_launch_matches_single_context(tmp_path, n):
-    """The phase path's gradient launch takes its workers from a queue (k_round VAR bit 22: as many persistent
-    workgroups as are resident, 512 here, each taking workers until none are left): with 1200 / 2100 workers
-    every workgroup runs 2-5 workers in an order only the queue decides -- the iterates are still bitwise one
-    context's one-workgroup-per-worker rounds, the history rtol 1e-12 (the headline's float64-over-float32
-    kernel at d = 1024)."""
-    import torch.multiprocessing as mp
-
-    d, m, t = 1024, 16, 6
-    mp.start_processes(_rank_main, args=(1, _rdv(tmp_path), "float64/x32", str(tmp_path), False, t, "1", n, d, m),
-                       nprocs=1, join=True, start_method="spawn")
-    got = np.load(tmp_path / "dist.npz")
-    assert len(got["obj"]) == len(got["cons"]) == t
-    _compare_single(got, "float64/x32", False, t, n, d, m)
-
-
 def _trainer_rank(rank, world, rdv, out):
     import json
 
