@@ -118,9 +118,11 @@ _SIGS = {
     "dopt_comm_library": ([], ctypes.c_char_p),
     "dopt_lagged_transport": ([_P, _P, _P, _P], ctypes.c_int),
     "dopt_lagged_exchange": ([_P], ctypes.c_int),
+    "dopt_lagged_ipc_export": ([_P, _P, _P, _P], ctypes.c_int),
+    "dopt_lagged_ipc_import": ([_P, _I32, _I32, _P, _P, _P, _P, _P, _P, ctypes.c_double], ctypes.c_int),
 }
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 8  # DOPT_ABI_VERSION of include/dopt.h
+ABI_VERSION = 9  # DOPT_ABI_VERSION of include/dopt.h
 
 
 def lib():
@@ -605,6 +607,35 @@ class Engine:
             old.users.discard(self)
         comm.users.add(self)
         self._comm = comm
+
+    IPC_HANDLE_BYTES = 64  # DOPT_IPC_HANDLE_BYTES
+
+    def lagged_ipc_export(self):
+        """dopt_lagged_ipc_export: (memory handle bytes, event handle bytes, slot bytes) of this context's
+        send slots for the pull transport."""
+        mh = (ctypes.c_uint8 * self.IPC_HANDLE_BYTES)()
+        eh = (ctypes.c_uint8 * self.IPC_HANDLE_BYTES)()
+        slot = ctypes.c_int64(0)
+        check(lib().dopt_lagged_ipc_export(self._h, mh, eh, ctypes.byref(slot)))
+        self.lagged_transport(None)  # (the engine detached any RCCL transport as well)
+        return bytes(mh), bytes(eh), int(slot.value)
+
+    def lagged_ipc_import(self, world, rank, mem_handles, event_handles, slot_bytes, src_off, recv_rows,
+                          counters_addr, timeout_s):
+        """dopt_lagged_ipc_import: the peers' exported handles (bytes each, rank order), their slot bytes, the
+        byte offset of this rank's block in each peer's slot, recv_rows per peer, the address of `world`
+        shared int64 counters (kept alive by the caller while the context uses them) and the host wait bound."""
+        n = self.IPC_HANDLE_BYTES
+        if len(mem_handles) != world or len(event_handles) != world or any(
+                len(h) != n for h in list(mem_handles) + list(event_handles)):
+            raise ValueError(f"{world} handles of {n} bytes per kind expected")
+        mh = (ctypes.c_uint8 * (n * world)).from_buffer_copy(b"".join(mem_handles))
+        eh = (ctypes.c_uint8 * (n * world)).from_buffer_copy(b"".join(event_handles))
+        arrs = [np.ascontiguousarray(a, dtype=np.int64) for a in (slot_bytes, src_off, recv_rows)]
+        if any(a.shape != (world,) for a in arrs):
+            raise ValueError(f"{world} entries per array expected")
+        check(lib().dopt_lagged_ipc_import(self._h, int(world), int(rank), mh, eh, *[_ptr(a) for a in arrs],
+                                           ctypes.c_void_p(int(counters_addr)), float(timeout_s)))
 
     def lagged_exchange(self):
         """dopt_lagged_exchange: the round's exchange through the attached communicator."""

@@ -303,6 +303,18 @@ void mixcs_shape(int dtype, int64_t n, int32_t nch, int32_t* ncb, int32_t* r, in
 hipError_t launch_xbar_ranks(int dtype, const McsArgs& m, const void* halo, int64_t ld, int32_t nch,
                              void* xbar_out, void* send, hipStream_t s);
 // dst[k] = x[ids[k]] rows (halo send buffer); ids[k] < 0: row k left alone.
+// The pull transport's copies (kernels.hip k_pull): nb peer blocks; block b's source in send slot k is
+// src[2 b + k] (device array of pointers into the peers' allocations), its destination dst + dst_off[b] (bytes,
+// device array), n16[b] 16-byte chunks (device array); max16 the largest block (host value, grid size).
+struct PullArgs {
+  const void* const* src;
+  char* dst;
+  const int64_t* dst_off;
+  const int64_t* n16;
+  int32_t nb;
+  int64_t max16;
+};
+hipError_t launch_pull(const PullArgs& a, int slot, hipStream_t s);
 hipError_t launch_gather_rows(int dtype, const void* x, const int32_t* ids, int64_t n, int64_t ld,
                               int32_t nchunks, void* dst, hipStream_t s);
 // Synthetic shards (rows_per_worker rows per worker), X ~ N(0,1) + bias column; xrows > 0: X in

@@ -1570,6 +1570,28 @@ hipError_t launch_gather_rows(int dtype, const void* x, const int32_t* ids, int6
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------- the pull transport
+// One launch pulls every peer's block of this round (DOPT_TRANSPORT=ipc, runtime.cpp "pull transport"): block b
+// of the grid's y dimension copies the 16-byte chunks of peer block b from the peer's send slot (a pointer into
+// the peer's allocation, opened through its IPC handle) into this rank's halo.  Plain vector loads and stores;
+// the ordering against the peer's writes is the peer's interprocess event, waited for before the launch.
+__global__ __launch_bounds__(NT) void k_pull(const PullArgs a, int slot) {
+  const int b = blockIdx.y;
+  const uint4* __restrict__ src = (const uint4*)a.src[2 * b + slot];
+  uint4* __restrict__ dst = (uint4*)(a.dst + a.dst_off[b]);
+  const int64_t n = a.n16[b];
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) dst[i] = src[i];
+}
+
+hipError_t launch_pull(const PullArgs& a, int slot, hipStream_t s) {
+  if (a.nb <= 0) return hipSuccess;
+  // enough workgroups for the largest block at 4 chunks per thread, at most 64 per block (a few MB per
+  // peer per round: the copy is latency-bound over xGMI, not a full-chip stream)
+  const int64_t gx = std::min<int64_t>(64, std::max<int64_t>(1, (a.max16 + 4 * NT - 1) / (4 * NT)));
+  hipLaunchKernelGGL(k_pull, dim3((unsigned)gx, (unsigned)a.nb), dim3(NT), 0, s, a, slot);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------- synthetic data
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;

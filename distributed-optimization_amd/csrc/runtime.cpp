@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -209,6 +210,24 @@ struct dopt_ctx {
   // send / receive per non-empty block of the layout, issued by dopt_lagged_exchange
   dopt_comm* xp = nullptr;
   std::vector<XpOp> xp_ops;
+  // dopt_lagged_ipc_*: the pull transport (DOPT_TRANSPORT=ipc).  The send rows live in two slots (round
+  // parity) of this rank's own allocation, exported through an IPC handle; each round every rank pulls its
+  // blocks out of the peers' slots with one k_pull launch, after the peers' interprocess events (section
+  // "pull transport" below)
+  bool ipc = false;
+  char* ipc_send = nullptr;             // [2 x ipc_slot bytes]
+  int64_t ipc_slot = 0;
+  hipEvent_t ipc_ev = nullptr;          // interprocess: recorded behind each slot's rows and sums
+  std::vector<void*> ipc_open;          // the peers' allocations opened here
+  std::vector<hipEvent_t> ipc_pev;      // the peers' events, opened here
+  std::vector<int32_t> ipc_peers;       // ranks pulled from (not this one)
+  int64_t* ipc_cnt = nullptr;           // [world] host shared memory of the caller's: events recorded per rank
+  int64_t ipc_rec = 0;                  // events this rank recorded
+  double ipc_timeout = 0.0;
+  PullArgs ipc_pa{};
+  void** ipc_src_d = nullptr;           // device copies of the pull's arrays
+  int64_t* ipc_off_d = nullptr;
+  int64_t* ipc_n16_d = nullptr;
   int64_t* lg_sum_in = nullptr;            // [world] halo row of peer p's sums
   int64_t* lg_sum_out = nullptr;           // [world] send row of the sums for peer p
   double* lg_own[2] = {nullptr, nullptr};  // [ld] this rank's column sums of x_g (g parity)
@@ -302,6 +321,26 @@ int dalloc(void** p, size_t bytes) {
   }
   return DOPT_OK;
 }
+int ipc_publish(dopt_ctx* c);
+int ipc_pull(dopt_ctx* c);
+
+// The pull transport's peer side: handles opened by dopt_lagged_ipc_import closed, its arrays freed.
+void ipc_close(dopt_ctx* c) {
+  for (void* q : c->ipc_open)
+    if (q) (void)hipIpcCloseMemHandle(q);
+  for (hipEvent_t e : c->ipc_pev)
+    if (e) (void)hipEventDestroy(e);
+  c->ipc_open.clear();
+  c->ipc_pev.clear();
+  c->ipc_peers.clear();
+  dfree_t(c->ipc_src_d);
+  dfree_t(c->ipc_off_d);
+  dfree_t(c->ipc_n16_d);
+  c->ipc_pa = PullArgs{};
+  c->ipc_cnt = nullptr;
+  c->ipc = false;
+}
+
 template <typename P>
 int dalloc_t(P** p, size_t bytes) {
   void* v = (void*)*p;
@@ -1152,6 +1191,7 @@ int run_dsgd_rs(dopt_ctx* c, int64_t t0, int64_t T, double eta0, int64_t batch, 
 // Minibatch rounds whose metrics need a pass over every shard row anyway take the gradient
 // inside that pass (k_round F_BIP).  DOPT_BIP=0: a separate metrics pass (A/B runs).
 static_assert(kMaxBipRows == DOPT_MAX_BIP_ROWS, "dopt.h and engine.h disagree");
+static_assert(HIP_IPC_HANDLE_SIZE == DOPT_IPC_HANDLE_BYTES, "dopt.h and HIP disagree on IPC handle bytes");
 bool bip_possible(dopt_ctx* c, int64_t batch, const int32_t* idx) {
   const char* v = getenv("DOPT_BIP");
   if (v && v[0] == '0') return false;
@@ -1288,6 +1328,9 @@ int dopt_destroy(dopt_ctx* c) {
   for (double** p : {&c->lg_own[0], &c->lg_own[1], &c->lg_cons[0], &c->lg_cons[1], &c->lg_part}) dfree_t(*p);
   dfree_t(c->lg_sum_in);
   dfree_t(c->lg_sum_out);
+  ipc_close(c);
+  if (c->ipc_send) (void)hipFree(c->ipc_send);
+  if (c->ipc_ev) (void)hipEventDestroy(c->ipc_ev);
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   if (c->lg_side_ev) (void)hipEventDestroy(c->lg_side_ev);
   if (c->lg_xev) (void)hipEventDestroy(c->lg_xev);
@@ -2025,6 +2068,7 @@ int dopt_set_halo(dopt_ctx* c, int64_t n_halo, void* halo_dev, int64_t n_send, v
   c->halo = halo_dev;
   c->n_send = n_send;
   c->send = send_dev;
+  c->ipc = false;  // (a pull transport is set up again after the buffers: dopt_lagged_ipc_export)
   c->send_fresh = false;
   // inverse map for dopt_phase_mix: worker -> the send rows that carry it (one row per peer)
   std::vector<int64_t> sp((size_t)c->n + 1, 0);
@@ -2599,6 +2643,10 @@ int dopt_lagged_begin(dopt_ctx* c, int64_t batch) {
   int rc;
   if ((rc = dopt_phase_begin(c, batch))) return rc;
   if ((rc = lagged_ready(c))) return rc;
+  if (c->ipc) {  // slot 0 holds x_0's rows and sums (round g's in slot g % 2)
+    c->send = c->ipc_send;
+    c->ipc_rec = 0;
+  }
   if ((rc = dopt_phase_gather(c))) return rc;  // send rows of x_0 (later rounds: k_mixcs writes them)
   // this rank's column sums of x_0 -> lg_own[0] and the send buffer's sum rows
   HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur], c->n, c->ld, (int32_t)c->nchs, kRowsPerGroup, c->part, nullptr,
@@ -2613,7 +2661,7 @@ int dopt_lagged_begin(dopt_ctx* c, int64_t batch) {
   }
   c->lg = 0;
   c->lg_xwait = false;
-  return DOPT_OK;
+  return ipc_publish(c);
 }
 
 namespace {
@@ -2623,6 +2671,51 @@ int lagged_mark_exchange(dopt_ctx* c) {
   if (!c->lg_xev) HIPOK(hipEventCreateWithFlags(&c->lg_xev, kOrderEventFlags));
   HIPOK(hipEventRecord(c->lg_xev, c->lg_side));
   c->lg_xwait = true;
+  return DOPT_OK;
+}
+}  // namespace
+
+// ---- the pull transport (DOPT_TRANSPORT=ipc; round 6).  RCCL's kernel beside the gradient kernel slows it
+// by 4-16 % on the rank proxies while a plain copy kernel there costs ~1 % (profiles/r6_xcopy_ab.txt), so
+// this transport moves the rows with a copy kernel of the engine's own:
+//  * every rank writes round g's send rows and sums into slot g % 2 of its own allocation (exported once
+//    through an IPC handle) and then records an interprocess event on the stream that wrote them, and
+//    publishes "g + 1 events recorded" in host shared memory (ipc_publish);
+//  * the exchange of round g waits on the host until every peer has published g + 1 (so that the stream wait
+//    below refers to that record, not an older one), makes the exchange stream wait for the peers' events, and
+//    pulls every block with one k_pull launch from the peers' slot g % 2 into this rank's halo (ipc_pull).
+// No slot is overwritten while a peer may still read it, by the round structure itself: rank r writes slot
+// g % 2 again in its mix of round g + 1, which waited for the pulls of its own exchange of round g + 1, which
+// waited for every peer's event of round g + 1 -- recorded after that peer's mix of round g, which waited for
+// the peer's pulls of round g.  The host wait is bounded (timeout_s, the job's collective bound).
+namespace {
+int ipc_publish(dopt_ctx* c) {
+  if (!c->ipc) return DOPT_OK;
+  HIPOK(hipEventRecord(c->ipc_ev, c->lg_side ? c->lg_side : c->stream));
+  c->ipc_rec += 1;
+  __atomic_store_n(c->ipc_cnt + c->lg_rank, c->ipc_rec, __ATOMIC_RELEASE);
+  return DOPT_OK;
+}
+
+int ipc_pull(dopt_ctx* c) {
+  const int64_t need = c->ipc_rec;  // this round's data: every peer's event number `need`
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int32_t p : c->ipc_peers) {
+    int spins = 0;
+    while (__atomic_load_n(c->ipc_cnt + p, __ATOMIC_ACQUIRE) < need) {
+      if (++spins > 256) {
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (c->ipc_timeout > 0 && el > c->ipc_timeout)
+          return fail(DOPT_ERR_COMM, "rank %d: peer %d published %lld of %lld rounds in %.0f s (a peer stopped?)",
+                      c->lg_rank, p, (long long)__atomic_load_n(c->ipc_cnt + p, __ATOMIC_ACQUIRE), (long long)need,
+                      c->ipc_timeout);
+        std::this_thread::sleep_for(std::chrono::microseconds(spins > 4096 ? 200 : 2));
+      }
+    }
+  }
+  hipStream_t xs = c->lg_side ? c->lg_side : c->stream;
+  for (hipEvent_t e : c->ipc_pev) HIPOK(hipStreamWaitEvent(xs, e, 0));
+  HIPOK(launch_pull(c->ipc_pa, (int)((need - 1) & 1), xs));
   return DOPT_OK;
 }
 }  // namespace
@@ -2665,13 +2758,128 @@ int dopt_lagged_transport(dopt_ctx* c, dopt_comm* comm, const int64_t* send_rows
   CHECK_ARG((so == 0 || c->send) && (ro == 0 || c->halo), "send / halo buffer missing");
   c->xp = comm;
   c->xp_ops = std::move(ops);
+  ipc_close(c);
+  return DOPT_OK;
+}
+
+int dopt_lagged_ipc_export(dopt_ctx* c, uint8_t* mem_handle, uint8_t* event_handle, int64_t* slot_bytes) {
+  CHECK_ARG(c && mem_handle && event_handle && slot_bytes, "NULL argument");
+  if (!c->have_data) return fail(DOPT_ERR_STATE, "load the shards first");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  ipc_close(c);
+  const int64_t row = c->ld * (int64_t)c->esz;
+  const int64_t slot = (std::max<int64_t>(1, c->n_send) * row + 255) / 256 * 256;
+  if (c->ipc_send) {
+    HIPOK(hipDeviceSynchronize());  // (a previous chain's pulls by peers finished with their runner)
+    HIPOK(hipFree(c->ipc_send));
+    c->ipc_send = nullptr;
+  }
+  HIPOK(hipMalloc((void**)&c->ipc_send, (size_t)(2 * slot)));
+  HIPOK(hipMemset(c->ipc_send, 0, (size_t)(2 * slot)));
+  if (!c->ipc_ev) HIPOK(hipEventCreateWithFlags(&c->ipc_ev, hipEventInterprocess | hipEventDisableTiming));
+  HIPOK(hipIpcGetMemHandle((hipIpcMemHandle_t*)mem_handle, c->ipc_send));
+  HIPOK(hipIpcGetEventHandle((hipIpcEventHandle_t*)event_handle, c->ipc_ev));
+  c->ipc_slot = slot;
+  *slot_bytes = slot;
+  return DOPT_OK;
+}
+
+int dopt_lagged_ipc_import(dopt_ctx* c, int32_t world, int32_t rank, const uint8_t* mem_handles,
+                           const uint8_t* event_handles, const int64_t* slot_bytes, const int64_t* src_off,
+                           const int64_t* recv_rows, int64_t* counters, double timeout_s) {
+  CHECK_ARG(c && mem_handles && event_handles && slot_bytes && src_off && recv_rows && counters, "NULL argument");
+  CHECK_ARG(c->ipc_send, "dopt_lagged_ipc_export first");
+  CHECK_ARG(c->lg_world == world && c->lg_rank == rank,
+            "pull transport of rank %d of %d, exchange layout of rank %d of %d (dopt_lagged_exchange_layout first)",
+            rank, world, c->lg_rank, c->lg_world);
+  CHECK_ARG(timeout_s >= 0, "timeout_s must be >= 0 (0: unbounded)");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  ipc_close(c);
+  c->xp = nullptr;
+  c->xp_ops.clear();
+  const int64_t row = c->ld * (int64_t)c->esz;
+  CHECK_ARG(row % 16 == 0, "rows of %lld bytes: the pull copies 16-byte chunks", (long long)row);
+  std::vector<const void*> src;
+  std::vector<int64_t> off, n16;
+  int64_t ro = 0, max16 = 0;
+  for (int32_t p = 0; p < world; ++p) {
+    CHECK_ARG(recv_rows[p] >= 0 && src_off[p] >= 0 && src_off[p] % 16 == 0, "peer %d: bad block", p);
+    if (recv_rows[p] == 0) continue;
+    const int64_t bytes = recv_rows[p] * row;
+    CHECK_ARG(src_off[p] + bytes <= slot_bytes[p], "peer %d: block past its send slot (%lld + %lld > %lld bytes)", p,
+              (long long)src_off[p], (long long)bytes, (long long)slot_bytes[p]);
+    const char* base = c->ipc_send;
+    if (p != rank) {
+      void* q = nullptr;
+      hipError_t e = hipIpcOpenMemHandle(&q, *(const hipIpcMemHandle_t*)(mem_handles + (size_t)p * DOPT_IPC_HANDLE_BYTES),
+                                         hipIpcMemLazyEnablePeerAccess);
+      if (e != hipSuccess) {
+        ipc_close(c);
+        return fail(DOPT_ERR_HIP, "rank %d: hipIpcOpenMemHandle of peer %d: %s", rank, p, hipGetErrorString(e));
+      }
+      c->ipc_open.push_back(q);
+      hipEvent_t ev = nullptr;
+      e = hipIpcOpenEventHandle(&ev, *(const hipIpcEventHandle_t*)(event_handles + (size_t)p * DOPT_IPC_HANDLE_BYTES));
+      if (e != hipSuccess) {
+        ipc_close(c);
+        return fail(DOPT_ERR_HIP, "rank %d: hipIpcOpenEventHandle of peer %d: %s", rank, p, hipGetErrorString(e));
+      }
+      c->ipc_pev.push_back(ev);
+      c->ipc_peers.push_back(p);
+      base = (const char*)q;
+    }
+    src.push_back(base + src_off[p]);
+    src.push_back(base + slot_bytes[p] + src_off[p]);
+    off.push_back(ro * row);
+    n16.push_back(bytes / 16);
+    max16 = std::max(max16, bytes / 16);
+    ro += recv_rows[p];
+  }
+  if (ro > c->n_halo) {
+    ipc_close(c);
+    return fail(DOPT_ERR_INVALID, "%lld halo rows pulled, the halo holds %lld (dopt_set_halo first)", (long long)ro,
+                (long long)c->n_halo);
+  }
+  const int nb = (int)off.size();
+  if (nb > 65535) {
+    ipc_close(c);
+    return fail(DOPT_ERR_INVALID, "%d peer blocks: at most 65535", nb);
+  }
+  if ((rc = dalloc_t(&c->ipc_src_d, std::max<size_t>(1, src.size()) * sizeof(void*))) ||
+      (rc = dalloc_t(&c->ipc_off_d, std::max<size_t>(1, off.size()) * sizeof(int64_t))) ||
+      (rc = dalloc_t(&c->ipc_n16_d, std::max<size_t>(1, n16.size()) * sizeof(int64_t)))) {
+    ipc_close(c);
+    return rc;
+  }
+  if (nb > 0) {
+    HIPOK(hipMemcpy(c->ipc_src_d, src.data(), src.size() * sizeof(void*), hipMemcpyHostToDevice));
+    HIPOK(hipMemcpy(c->ipc_off_d, off.data(), off.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+    HIPOK(hipMemcpy(c->ipc_n16_d, n16.data(), n16.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  }
+  c->ipc_pa.src = (const void* const*)c->ipc_src_d;
+  c->ipc_pa.dst = (char*)c->halo;
+  c->ipc_pa.dst_off = c->ipc_off_d;
+  c->ipc_pa.n16 = c->ipc_n16_d;
+  c->ipc_pa.nb = nb;
+  c->ipc_pa.max16 = max16;
+  c->ipc_cnt = counters;
+  c->ipc_rec = 0;
+  c->ipc_timeout = timeout_s;
+  c->ipc = true;
+  c->send = c->ipc_send;
   return DOPT_OK;
 }
 
 int dopt_lagged_exchange(dopt_ctx* c) {
   CHECK_ARG(c, "ctx is NULL");
-  if (!c->xp) return fail(DOPT_ERR_STATE, "no transport (dopt_lagged_transport first)");
   int rc;
+  if (c->ipc) {
+    if ((rc = ipc_pull(c))) return rc;
+    return c->lg_side ? lagged_mark_exchange(c) : DOPT_OK;
+  }
+  if (!c->xp) return fail(DOPT_ERR_STATE, "no transport (dopt_lagged_transport first)");
   {
     if ((rc = comm_exchange(c->xp, c->xp_ops.data(), c->xp_ops.size(), c->send, c->halo,
                             c->lg_side ? c->lg_side : c->stream)))
@@ -2706,6 +2914,7 @@ int dopt_lagged_mix(dopt_ctx* c, int64_t t, double eta0, int consensus, double* 
   int rc;
   if ((rc = lagged_ready(c))) return rc;
   if (!c->G) return fail(DOPT_ERR_STATE, "gradient phase missing");
+  if (c->ipc) c->send = c->ipc_send + ((c->lg + 1) & 1) * c->ipc_slot;  // x_{g+1}'s rows and sums
   RoundArgs a = base_args(c);
   a.x_old = c->xs[c->cur];
   a.x_new = c->xs[c->cur ^ 1];
@@ -2741,7 +2950,7 @@ int dopt_lagged_mix(dopt_ctx* c, int64_t t, double eta0, int consensus, double* 
   c->lg += 1;
   c->S_ext = nullptr;
   c->send_fresh = c->n_send > 0;
-  return DOPT_OK;
+  return ipc_publish(c);
 }
 
 int dopt_lagged_tail(dopt_ctx* c, int consensus, int objective, double* cons1, double* xnorm1, double* loss1,

@@ -447,12 +447,68 @@ _COMMS = {}
 def transport_kind():
     """The lagged schedule's exchange over RCCL: "rccl" -- the engine's own communicator, RCCL sends and
     receives issued by dopt_lagged_exchange on the side stream (ABI 7, csrc/transport.cpp: 4.5-6 us of host
-    time per round against 22 us for the process group's alltoall_base, profiles/r5_rccl_probe.txt) -- or
-    "pg": torch's process group all-to-all-v (rounds 3-4).  DOPT_TRANSPORT overrides."""
+    time per round against 22 us for the process group's alltoall_base, profiles/r5_rccl_probe.txt) --,
+    "pg": torch's process group all-to-all-v (rounds 3-4), or "ipc": the engine's pull transport (ABI 9, ranks
+    of one node: a copy kernel reads the peers' send slots through IPC handles, no RCCL kernel beside the
+    gradient kernel; IpcTransport).  DOPT_TRANSPORT overrides."""
     v = os.environ.get("DOPT_TRANSPORT", "rccl").strip().lower()
-    if v not in ("rccl", "pg"):
-        raise ValueError(f"DOPT_TRANSPORT={v!r}: 'rccl' or 'pg'")
+    if v not in ("rccl", "pg", "ipc"):
+        raise ValueError(f"DOPT_TRANSPORT={v!r}: 'rccl', 'pg' or 'ipc'")
     return v
+
+
+class IpcTransport:
+    """The pull transport's setup for one runner (dopt_lagged_ipc_*; DESIGN.md section 6, "A transport
+    without RCCL's kernel").  Every rank exports its context's send slots and event, the handles and each
+    rank's send-block offsets travel over the job's process group (any backend: gloo in the one-GPU
+    multi-process tests), rank 0 creates the shared counters (POSIX shared memory, one int64 per rank) the
+    others attach to, and every rank opens its peers' handles.  The ranks must share one node."""
+
+    def __init__(self, engine, plan, layout, group, row_bytes, timeout_s):
+        import torch.distributed as dist
+        from multiprocessing import resource_tracker, shared_memory
+
+        world, rank = plan.world, plan.rank
+        self._shm = self._cnt = None
+        self._creator = rank == 0
+        mh, eh, slot = engine.lagged_ipc_export()
+        send_off = np.concatenate([[0], np.cumsum(layout.send_sizes)]).astype(np.int64) * int(row_bytes)
+        mine = (mh, eh, slot, [int(v) for v in send_off[:-1]])
+        name = None
+        if world == 1:
+            infos = [mine]
+        else:
+            infos = [None] * world
+            dist.all_gather_object(infos, mine, group=group)
+        if self._creator:
+            shm = shared_memory.SharedMemory(create=True, size=max(4096, 8 * world))
+            shm.buf[:8 * world] = bytes(8 * world)
+            name = shm.name
+        if world > 1:
+            box = [name]
+            dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                       group=group)
+            name = box[0]
+        if not self._creator:
+            shm = shared_memory.SharedMemory(name=name)
+            resource_tracker.unregister(shm._name, "shared_memory")  # rank 0 owns the segment
+        self._shm = shm
+        self._cnt = np.ndarray((world,), dtype=np.int64, buffer=shm.buf)
+        engine.lagged_ipc_import(world, rank, [i[0] for i in infos], [i[1] for i in infos], [i[2] for i in infos],
+                                 [infos[p][3][rank] for p in range(world)], list(layout.recv_sizes),
+                                 self._cnt.ctypes.data, timeout_s)
+        if world > 1:  # every rank has opened its peers' handles before any rank's first round publishes
+            dist.barrier(group=group)
+
+    def close(self):
+        """Unmap the counters (rank 0 removes the segment); the context must no longer run lagged rounds
+        with this transport (a new runner exports and imports again)."""
+        self._cnt = None
+        if self._shm is not None:
+            self._shm.close()
+            if self._creator:
+                self._shm.unlink()
+            self._shm = None
 
 
 def _comm(group, dev):
@@ -511,29 +567,6 @@ def close_comms(abort=False):
     while _COMMS:
         _, c = _COMMS.popitem()
         c.close(abort)
-
-
-GRAD_WG_PER_CU = 2  # resident gradient workgroups per CU (the headline k_round: 191 VGPRs, 4 waves, ~78 KB LDS)
-
-
-def side_stream_wanted(n_local, dev=None, cus=None):
-    """Whether the lagged schedule runs the exchange on a side stream beside the next gradient kernel.
-
-    Only when one generation of workgroups covers the rank's gradient launch (n_local workers <= 2 per CU).
-    A launch of several generations loses one whole generation whenever the exchange's RCCL kernel holds a
-    workgroup slot during it, and the gradient kernel beside RCCL runs slower: rank proxies on the box put
-    the exchange serialised on the engine stream ahead at 4 ranks (0.347 vs 0.411 ms per round), 2 ranks
-    (0.653-0.672 vs 0.702-0.722) and the weak leg at 8 ranks (1.317-1.320 vs 1.351-1.353); a one-generation
-    rank keeps the overlap (0.1753 vs 0.1780 ms), profiles/r6_side_exp.txt.  DOPT_LAGGED_SIDE=1 always
-    takes the side stream, =0 never."""
-    knob = os.environ.get("DOPT_LAGGED_SIDE", "auto")
-    if knob in ("0", "1"):
-        return knob == "1"
-    if cus is None:
-        import torch
-
-        cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    return int(n_local) <= GRAD_WG_PER_CU * int(cus)
 
 
 def _stream(dev, role):
@@ -615,18 +648,25 @@ class DistributedDSGD:
         self.mean = mean
         engine.set_stream(self.stream.cuda_stream)
         # a second stream for each mix's column-sum totals (k_mixcs_final) and the exchange, so the
-        # next gradient kernel does not wait for them -- whenever there is an exchange to order it and
-        # the rank's gradient launch is one generation of workgroups (side_stream_wanted)
+        # next gradient kernel does not wait for them -- whenever there is an exchange to order it
+        # (DOPT_LAGGED_SIDE=0: one stream, the exchange serialised between the mix and the next gradient
+        # kernel; DESIGN.md section 6, "Which form of the exchange")
         self.side = None
         self._stream_switch = None
         if (self._lagged_ok and not self._solo() and self.exchange.peers_or_collective()
-                and side_stream_wanted(plan.n_local, self.dev)):
+                and os.environ.get("DOPT_LAGGED_SIDE", "1") != "0"):
             self.side = _stream(self.dev, 1)
         engine.lagged_side_stream(self.side.cuda_stream if self.side is not None else None)
-        # the engine's own RCCL communicator for the lagged exchange (dopt_lagged_exchange), RCCL only
+        # the engine's own RCCL communicator for the lagged exchange (dopt_lagged_exchange), RCCL only; or
+        # the engine's pull transport (DOPT_TRANSPORT=ipc), over any process group
         self.comm = None
-        if (self.device_comm and self._lagged_ok and mean is None and self.exchange.collective
-                and transport_kind() == "rccl"):
+        self.ipc = None
+        kind = transport_kind()
+        if self._lagged_ok and mean is None and kind == "ipc" and (plan.world > 1 or forced) and lay.ks > 0:
+            engine.lagged_transport(None)
+            self.ipc = IpcTransport(engine, plan, lay, group, ld * esz, timeout_seconds())
+        elif (self.device_comm and self._lagged_ok and mean is None and self.exchange.collective
+                and kind == "rccl"):
             self.comm = _comm(group, self.dev)
             engine.lagged_transport(self.comm, lay.send_sizes, lay.recv_sizes)
         else:
@@ -645,10 +685,16 @@ class DistributedDSGD:
         k_mixcs_final), with the engine stream current again afterwards.  The current stream is switched
         through torch._C._cuda_setStream with the two streams' cached ids (what torch.cuda.stream's
         context manager does, without its per-call Python: VERDICT r4 item 4, host cost per round)."""
-        if self.comm is not None:  # the engine issues it on the side stream and orders the engine stream after it
-            if self.comm.closed:
+        if self.comm is not None or self.ipc is not None:  # the engine issues it on the side stream and orders
+            if self.comm is not None and self.comm.closed:  # the engine stream after it
                 raise CollectiveError(f"rank {self.plan.rank}: the engine's RCCL communicator was aborted")
-            self.eng.lagged_exchange()
+            if self.ipc is None:
+                self.eng.lagged_exchange()
+                return None
+            try:  # (a peer that stopped publishing its rounds: the engine's bounded host wait)
+                self.eng.lagged_exchange()
+            except RuntimeError as e:
+                raise CollectiveError(f"rank {self.plan.rank}: {e}") from e
             return None
         side = self.side
         if side is None:

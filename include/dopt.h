@@ -53,8 +53,10 @@ extern "C" {
  *      dopt_lagged_exchange): the lagged schedule's exchange as RCCL sends / receives issued by the
  *      engine on its side stream, without the process group's per-call cost.
  *   8  round 6: dopt_comm_create takes timeout_s -- the communicator is created non-blocking and its
- *      setup, a peer's first connection and its destroy are each bounded by that time. */
-#define DOPT_ABI_VERSION 8
+ *      setup, a peer's first connection and its destroy are each bounded by that time.
+ *   9  round 6: the pull transport (dopt_lagged_ipc_export / _import): the lagged exchange as a copy
+ *      kernel of the engine's reading the peers' send slots through IPC handles, no RCCL kernel. */
+#define DOPT_ABI_VERSION 9
 
 typedef struct dopt_ctx dopt_ctx;
 typedef struct dopt_comm dopt_comm; /* an RCCL communicator the engine drives itself (ABI 7) */
@@ -454,6 +456,24 @@ int dopt_comm_destroy(dopt_comm *comm, int32_t abort);
 const char *dopt_comm_library(void);
 int dopt_lagged_transport(dopt_ctx *ctx, dopt_comm *comm, const int64_t *send_rows, const int64_t *recv_rows);
 int dopt_lagged_exchange(dopt_ctx *ctx);
+/* Pull transport (ABI 9): the same exchange without RCCL, for ranks of one node.  Replaces, like
+ * dopt_lagged_transport, the neighbour reads of the reference's mix (trainer.py:173) across ranks.
+ * dopt_lagged_ipc_export: after dopt_set_halo -- the context keeps its send rows in two slots (round
+ *   parity) of an allocation of its own instead of the caller's send buffer; returns that allocation's IPC
+ *   handle, an interprocess event's handle (DOPT_IPC_HANDLE_BYTES each) and the bytes of one slot.
+ * dopt_lagged_ipc_import: after every rank exported and dopt_lagged_exchange_layout: per rank p (rank order,
+ *   world entries of each array), p's two handles and slot bytes, the byte offset in p's slot of the block
+ *   p sends to this rank and recv_rows[p] rows that block holds (this rank's own entry: its self block,
+ *   if any).  counters: world int64 in host memory shared by the ranks (zeroed), where each rank publishes
+ *   how many rounds of send rows it has recorded; a rank waits at most timeout_s (0: unbounded) for a peer's
+ *   round before DOPT_ERR_COMM.  Detaches an RCCL transport; dopt_lagged_transport with a communicator or
+ *   dopt_set_halo detaches this one.  dopt_lagged_exchange then pulls every block with one copy kernel on
+ *   the side stream (the engine stream without one), ordered before the next dopt_lagged_mix / _tail. */
+#define DOPT_IPC_HANDLE_BYTES 64
+int dopt_lagged_ipc_export(dopt_ctx *ctx, uint8_t *mem_handle, uint8_t *event_handle, int64_t *slot_bytes);
+int dopt_lagged_ipc_import(dopt_ctx *ctx, int32_t world, int32_t rank, const uint8_t *mem_handles,
+                           const uint8_t *event_handles, const int64_t *slot_bytes, const int64_t *src_off,
+                           const int64_t *recv_rows, int64_t *counters, double timeout_s);
 /* Centralized trainer across ranks (trainer.py:41-71): gradients of the local
  * workers at the shared iterate (fuse_loss: the objective partial of the shared
  * iterate over the same rows, full shards only), local column sums of the

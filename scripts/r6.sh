@@ -95,21 +95,33 @@ for step in "$@"; do
         || { tail -n 20 gpurun_out/r6_sp_$w.err; die scale_proxy 1; }
       python3 -c "import json; d=json.loads(open('gpurun_out/r6_sp_$w.json').read().strip().splitlines()[-1]); p=d['plan']; [print('world', $w, g['leg'], g['workers'], 'halo', p['halo_rows_in'], 'interior', p['interior'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]; print('proxy / fused', [round(x, 4) for x in d['proxy_over_fused']])"
     done ;;
-  side_policy)  # the exchange's form as distributed.side_stream_wanted picks it (auto) vs forced side / serial: rank 0 of
-    # the strong leg at 2 / 4 / 8 ranks and of the weak leg at 8, two interleaved reps -> profiles/r6_side_policy.txt
+  ipc_ab)  # the pull transport (DOPT_TRANSPORT=ipc: k_pull reads the send slots, no RCCL kernel) vs the engine's RCCL
+    # transport, side stream (s1) / serial (s0): rank 0 of the strong leg at 4 / 2 / 8 ranks and of the weak leg at 8
+    # (world 1, the rank's blocks pulled from its own slot), two interleaved reps; then kernel traces at 4 and 8
+    # ranks -> profiles/r6_ipc_ab.txt
     for rep in 1 2; do
-      for cfg in "strong 8" "strong 4" "strong 2" "weak 8"; do
+      for cfg in "strong 4" "strong 2" "strong 8" "weak 8"; do
         sc=${cfg% *}; w=${cfg#* }
         st=$((1000 * 8 / w)); [ $sc = weak ] && st=150
-        for arm in auto 1 0; do
-          sd=""; [ $arm = auto ] || sd="DOPT_LAGGED_SIDE=$arm"
-          env $sd timeout -k 10 300 python3 tools/rank_proxy.py --world $w --rank 0 --scaling $sc --legs proxy \
-            --reps 1 --steps $st --warmup 50 > gpurun_out/r6_sp_${sc}${w}_${arm}_$rep.json 2> gpurun_out/r6_sp_${sc}${w}_${arm}_$rep.err \
-            || { tail -n 20 gpurun_out/r6_sp_${sc}${w}_${arm}_$rep.err; die side_policy 1; }
-          python3 -c "import json; d=json.loads(open('gpurun_out/r6_sp_${sc}${w}_${arm}_$rep.json').read().strip().splitlines()[-1]); [print('$sc', 'world', $w, 'side=$arm', 'rep', $rep, g['workers'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]"
+        for arm in rccl_s1 ipc_s1 ipc_s0 rccl_s0; do
+          tr=${arm%_*}; sd=${arm#*_s}
+          env DOPT_TRANSPORT=$tr DOPT_LAGGED_SIDE=$sd timeout -k 10 300 python3 tools/rank_proxy.py --world $w --rank 0 --scaling $sc --legs proxy \
+            --reps 1 --steps $st --warmup 50 > gpurun_out/r6_ia_${sc}${w}_${arm}_$rep.json 2> gpurun_out/r6_ia_${sc}${w}_${arm}_$rep.err \
+            || { tail -n 20 gpurun_out/r6_ia_${sc}${w}_${arm}_$rep.err; die ipc_ab 1; }
+          python3 -c "import json; d=json.loads(open('gpurun_out/r6_ia_${sc}${w}_${arm}_$rep.json').read().strip().splitlines()[-1]); [print('$sc', 'world', $w, '$arm', 'rep', $rep, g['workers'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]"
         done
       done
+    done
+    for w in 4 8; do
+      D=gpurun_out/r6_ia_tr$w
+      DOPT_TRANSPORT=ipc timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv -d $D -o run -- \
+        python3 tools/rank_proxy.py --world $w --rank 0 --scaling strong --legs proxy --reps 1 --steps $((300 * 8 / w)) \
+        --warmup 100 > $D.log 2>&1 || { tail -n 20 $D.log; die ipc_ab 1; }
+      python3 tools/trace_rounds.py $D/run_kernel_trace.csv
+      python3 tools/trace_window.py $D/run_kernel_trace.csv
     done ;;
+  pull_tests)  # the pull transport's multi-process tests (2-8 processes on the one GPU) -> profiles/r6_pull_tests.txt
+    echo "=== pull transport tests"; tests r6_pull_tests tests/test_gpu_distributed.py -k pull ;;
   xq_probe)  # what a cross-stream hand-off costs (tools/xq_probe.hip, built in-tree beforehand) -> profiles/r6_xq_probe.txt
     timeout -k 10 120 tools/xq_probe ${REPS:-50} > gpurun_out/r6_xq_probe.txt 2>&1 || { cat gpurun_out/r6_xq_probe.txt; die xq_probe 1; }
     cat gpurun_out/r6_xq_probe.txt ;;

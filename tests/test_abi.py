@@ -26,7 +26,7 @@ def test_library_exports_everything():
     L = _dopt.lib()
     for name in declared_symbols():
         assert hasattr(L, name), name
-    assert L.dopt_abi_version() == 8 == _dopt.ABI_VERSION
+    assert L.dopt_abi_version() == 9 == _dopt.ABI_VERSION
 
 
 def test_no_silent_fallback_without_gpu():

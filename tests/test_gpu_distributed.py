@@ -43,10 +43,11 @@ def _rank_main(rank, world, rdv, dtype, out, mean=False, T=T, lagged="1", N=N, D
     import topology as TP
 
     # "1-noside": the lagged schedule on one stream; "1-pg": the exchange through the process group's
-    # all-to-all-v instead of the engine's own RCCL communicator (dopt_lagged_exchange, the default)
+    # all-to-all-v instead of the engine's own RCCL communicator (dopt_lagged_exchange, the default);
+    # "1-ipc": the engine's pull transport (dopt_lagged_ipc_*: peers' send slots read through IPC handles)
     opts = lagged.split("-")
     side = "0" if "noside" in opts else "1"
-    transport = "pg" if "pg" in opts else "rccl"
+    transport = "pg" if "pg" in opts else "ipc" if "ipc" in opts else "rccl"
     lagged = opts[0]
     os.environ.update(DOPT_LAGGED=lagged, DOPT_LAGGED_SIDE=side, DOPT_TRANSPORT=transport,
                       DOPT_FORCE_COLLECTIVES="1" if backend == "nccl" else "0")
@@ -68,7 +69,7 @@ def _rank_main(rank, world, rdv, dtype, out, mean=False, T=T, lagged="1", N=N, D
     info = {"interior": eng.phase_interior_count(), "n_local": plan.n_local, "n_halo": plan.n_halo,
             "send_sizes": list(run.layout.send_sizes), "recv_sizes": list(run.layout.recv_sizes),
             "ks": run.layout.ks, "side": run.side is not None, "collective": bool(run.exchange.collective),
-            "native": run.comm is not None}
+            "native": run.comm is not None, "ipc": run.ipc is not None}
     np.save(os.path.join(out, f"info{rank}.npy"), np.array([repr(info)]))
     which = os.environ.get("DOPT_TEST_METRICS", "both")
     if os.environ.get("DOPT_TEST_PIPE") == "1":  # a chain of pipelined calls covering T rounds, then the tail
@@ -514,6 +515,106 @@ def test_rccl_one_rank_self_exchange_matches_single_context(tmp_path, monkeypatc
     assert it["native"] == ("pg" not in lagged), it
     assert it["interior"] < N - len(range(0, N, 3)), it  # readers of the halo copies are not interior
     _compare_single(got, dtype, False, 9)
+
+
+@pytest.mark.parametrize("dtype,mean,world,lagged,pipe", [("float64/x32", False, 2, "1-ipc", False),
+                                                         ("float64", False, 3, "1-ipc", True),
+                                                         ("float32", False, 2, "1-ipc-noside", True),
+                                                         ("float64", False, 2, "1-ipc", False),
+                                                         ("float64/x32", "torus", 4, "1-ipc", True)])
+def test_pull_transport_matches_single_context(tmp_path, monkeypatch, dtype, mean, world, lagged, pipe):
+    """DOPT_TRANSPORT=ipc (ABI 9): 2-4 processes on the one GPU, each pulling its halo rows and the peers'
+    column sums out of the peers' send slots through IPC handles (k_pull after the peers' interprocess
+    events, the slots alternating by round parity) -- real cross-process device traffic, no RCCL.  Side
+    stream or one stream, single calls and pipelined chains (T = 1 included): iterates bitwise one
+    context's, history rtol 1e-12.  A pull that ran before the peer's rows were written, or a slot reused
+    while a peer still read it, would mix stale rows."""
+    import torch.multiprocessing as mp
+
+    if pipe:
+        monkeypatch.setenv("DOPT_TEST_PIPE", "1")
+    for T_ in ((1, 7) if not pipe and world == 2 and dtype == "float64" else (7,)):
+        sub = tmp_path / f"T{T_}"
+        sub.mkdir()
+        mp.start_processes(_rank_main, args=(world, _rdv(sub), dtype, str(sub), mean, T_, lagged), nprocs=world,
+                           join=True, start_method="spawn")
+        got = np.load(sub / "dist.npz")
+        assert len(got["obj"]) == len(got["cons"]) == T_
+        for r, it in enumerate(_info(sub, world)):
+            assert it["ipc"] and not it["native"] and it["side"] == ("noside" not in lagged), it
+        _compare_single(got, dtype, mean, T_)
+
+
+def test_pull_transport_eight_ranks_match_single_context(tmp_path, monkeypatch):
+    """The pull transport at the SCALE run's rank count: 8 processes x 256 workers of the spectrally
+    partitioned random 4-regular graph, every rank pulling from all 7 peers each round, pipelined chain."""
+    import torch.multiprocessing as mp
+
+    n, d, m, t = 2048, 100, 32, 6
+    monkeypatch.setenv("DOPT_TEST_PARTITION", "1")
+    monkeypatch.setenv("DOPT_TEST_PIPE", "1")
+    mp.start_processes(_rank_main, args=(8, _rdv(tmp_path), "float64/x32", str(tmp_path), False, t, "1-ipc", n, d, m),
+                       nprocs=8, join=True, start_method="spawn")
+    got = np.load(tmp_path / "dist.npz")
+    assert len(got["obj"]) == len(got["cons"]) == t
+    assert all(it["ipc"] for it in _info(tmp_path, 8))
+    _compare_single(got, "float64/x32", False, t, n, d, m, parts=8)
+
+
+@pytest.mark.parametrize("dtype,lagged", [("float64/x32", "1-ipc"), ("float64", "1-ipc-noside")])
+def test_pull_transport_one_rank_self_block(tmp_path, monkeypatch, dtype, lagged):
+    """The pull transport at world 1 with a self block (collectives forced, as tools/rank_proxy.py runs a
+    rank): a third of the rows and the rank's own sums pulled from its own slot into its halo."""
+    import torch.multiprocessing as mp
+
+    monkeypatch.setenv("DOPT_TEST_SELF_HALO", "1")
+    monkeypatch.setenv("DOPT_TEST_PIPE", "1")
+    mp.start_processes(_rank_main, args=(1, _rdv(tmp_path), dtype, str(tmp_path), False, 9, lagged, N, D, M, "nccl"),
+                       nprocs=1, join=True, start_method="spawn")
+    got = np.load(tmp_path / "dist.npz")
+    it = _info(tmp_path, 1)[0]
+    assert it["ipc"] and it["ks"] > 0, it
+    _compare_single(got, dtype, False, 9)
+
+
+def _pull_stalled(rank, world, rdv, out):
+    """Rank 1 sets the pull transport up and then never runs a round: rank 0's first exchange must fail
+    with CollectiveError once DOPT_PG_TIMEOUT has passed."""
+    import time
+
+    import torch  # noqa: F401
+    import torch.distributed as dist
+
+    import distributed as Dm
+
+    os.environ.update(DOPT_TRANSPORT="ipc", DOPT_PG_TIMEOUT="5")
+    dist.init_process_group("gloo", init_method=rdv, rank=rank, world_size=world)
+    top = _topo(False, N)
+    plan = Dm.build_plan(top, world, rank)
+    eng = _engine("float64")
+    eng.generate_shards("logistic", plan.n_local, D, M, seed=9, first_worker=plan.lo)
+    run = Dm.DistributedDSGD(eng, plan, N, N * M, device=0)
+    msg = ""
+    if rank == 0:
+        t0 = time.monotonic()
+        try:
+            run.run(3, 0.05, M, 1e-3, 1e-3, 0.25)
+        except Dm.CollectiveError as e:
+            msg = f"{time.monotonic() - t0:.1f} {e}"
+        np.save(os.path.join(out, "stalled.npy"), np.array([msg]))
+    dist.barrier()  # (gloo: rank 1 waits here the whole time, its context idle)
+    eng.close()
+    dist.destroy_process_group()
+
+
+def test_pull_transport_stalled_peer_is_bounded(tmp_path):
+    import torch.multiprocessing as mp
+
+    mp.start_processes(_pull_stalled, args=(2, _rdv(tmp_path), str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    msg = str(np.load(tmp_path / "stalled.npy")[0])
+    assert "published" in msg and "peer 1" in msg, msg
+    assert float(msg.split()[0]) < 30.0, msg
 
 
 def test_rccl_alltoall_halo_exchange_one_rank(tmp_path):
