@@ -586,42 +586,45 @@ def per_rank(world, item):
     return out
 
 
-def alt_exchange_leg(args, S, world, barrier, dev):
-    """N > 1, after the headline leg, on its engine and shards: the same rounds with the exchange in the other
-    form -- serialised on the engine stream (between the mix and the next gradient kernel) where the headline
-    ran it on the side stream beside the gradient kernel, and the reverse.  distributed.side_stream_wanted
-    picks the form from one-GPU rank proxies, where the exchange is an RCCL self-copy; with real peers over
-    xGMI a serial exchange also exposes the transfer, which only a multi-GPU run can price, so the scaling
-    run reports both (this one is not `value`)."""
+def exchange_leg(args, S, world, barrier, dev, env, form):
+    """N > 1, after the headline leg, on its engine and shards: the same rounds with the exchange in another
+    form (`env`: the switches that select it, restored afterwards) -- not `value`.  The scaling run prices
+    with real peers over xGMI what the one-GPU rank proxies cannot: the exchange serialised on the engine
+    stream where the headline ran it beside the gradient kernel (or the reverse), and the pull transport
+    (DOPT_TRANSPORT=ipc, a copy kernel instead of RCCL's)."""
     import torch
     import torch.distributed as dist
 
     import distributed
 
-    side = "0" if S.comm.get("exchange_beside_gradient") else "1"
-    old = os.environ.get("DOPT_LAGGED_SIDE")
-    os.environ["DOPT_LAGGED_SIDE"] = side
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         runner = distributed.DistributedDSGD(S.eng, S.plan, S.n_global, S.n_global * S.m, device=dev)
     finally:
-        if old is None:
-            os.environ.pop("DOPT_LAGGED_SIDE", None)
-        else:
-            os.environ["DOPT_LAGGED_SIDE"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     if not runner._lagged_ok:
         return None
     eta0, b, lam = S.eta0, S.b, S.lam
-    dt, launches, kr_ms, every, obj, cons = timed_leg(
-        S.eng, lambda k: runner.run_pipelined(k, eta0, b, lam, lam, 0.0), args.steps, args.warmup, S.plan.n_local,
-        S.d, barrier, args.event_every, lambda: runner.run_pipelined(0, eta0, b, lam, lam, 0.0))
+    try:
+        dt, launches, kr_ms, every, obj, cons = timed_leg(
+            S.eng, lambda k: runner.run_pipelined(k, eta0, b, lam, lam, 0.0), args.steps, args.warmup,
+            S.plan.n_local, S.d, barrier, args.event_every, lambda: runner.run_pipelined(0, eta0, b, lam, lam, 0.0))
+    finally:
+        if runner.ipc is not None:
+            runner.ipc.close()
     tt = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}" if args.backend == "nccl" else "cpu")
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     dt = float(tt.item())
     return {"value": S.n_global * args.steps / dt, "unit": "worker-iters/s", "ms_per_step": dt / args.steps * 1e3,
             "kernel_avg_ms": kr_ms / launches if launches else None,
-            "exchange_beside_gradient": runner.side is not None, "final_objective": float(obj[-1]),
-            "form": ("the exchange on the side stream beside the gradient kernel (DOPT_LAGGED_SIDE=1)" if side == "1"
-                     else "the exchange serialised on the engine stream (DOPT_LAGGED_SIDE=0)")}
+            "exchange_beside_gradient": runner.side is not None,
+            "transport": "ipc" if runner.ipc is not None else "rccl" if runner.comm is not None else "process group",
+            "final_objective": float(obj[-1]), "form": form}
 
 
 def transport_probe(args, world, dev, barrier, shape, reps=20, warm=3):
@@ -724,7 +727,8 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=0, help="CPU baseline processes (0: the box's CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-alt-exchange", action="store_true",
-                    help="N > 1: skip the headline leg's second timing with the exchange serialised on the engine stream")
+                    help="N > 1: skip the headline leg's timings with the exchange in the other form and over the "
+                         "pull transport")
     ap.add_argument("--no-secondary", action="store_true",
                     help="N=1: skip the f64-storage / f32 legs, the f(x*) solver and the drop-in trainer leg")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (gloo: 1-GPU rehearsal)")
@@ -880,12 +884,22 @@ def main():
         out["metric"] = f"worker-iters/sec ({args.config.upper()}, secondary config)"
     secondary = rank == 0 and world == 1 and not args.phase and args.config == "c3" and not args.no_secondary
     if world > 1 and args.config == "c3" and S.flush is not None and not args.no_alt_exchange:
-        log("headline leg again with the exchange in the other form (A/B with real peers)")
-        try:  # diagnostic only: a failure here must not cost the line its value
-            out["alt_exchange"] = alt_exchange_leg(args, S, world, barrier, dev)
-        except Exception as e:  # noqa: BLE001
-            log(f"alt_exchange failed: {e!r}")
-            out["alt_exchange"] = {"error": repr(e)[:300]}
+        side = "0" if S.comm.get("exchange_beside_gradient") else "1"
+        legs = [("alt_exchange", {"DOPT_LAGGED_SIDE": side},
+                 "the exchange on the side stream beside the gradient kernel (DOPT_LAGGED_SIDE=1)" if side == "1"
+                 else "the exchange serialised on the engine stream (DOPT_LAGGED_SIDE=0)")]
+        # (over gloo too: the one-GPU rehearsal's ranks share the card, as the pull tests do)
+        legs.append(("ipc_transport", {"DOPT_TRANSPORT": "ipc"},
+                     "the pull transport: k_pull reads the peers' send slots through IPC handles (DOPT_TRANSPORT=ipc)"))
+        for key, env, form in legs:
+            log(f"headline leg again, {form} (A/B with real peers)")
+            try:  # diagnostic only: a failure here must not cost the line its value
+                out[key] = r = exchange_leg(args, S, world, barrier, dev, env, form)
+                if r is not None:  # every leg starts from zero iterates: the same bits whatever the transport
+                    r["final_objective_matches_value"] = r["final_objective"] == out["final_objective"]
+            except Exception as e:  # noqa: BLE001
+                log(f"{key} failed: {e!r}")
+                out[key] = {"error": repr(e)[:300]}
     if secondary and b == m:
         log("f(x*): device L-BFGS")
         out["suboptimality"] = suboptimality(eng, lam, float(obj[-1]))

@@ -616,8 +616,8 @@ class Engine:
         mh = (ctypes.c_uint8 * self.IPC_HANDLE_BYTES)()
         eh = (ctypes.c_uint8 * self.IPC_HANDLE_BYTES)()
         slot = ctypes.c_int64(0)
+        self.lagged_transport(None)  # (detaches any RCCL transport: the engine's exchange is this one's next)
         check(lib().dopt_lagged_ipc_export(self._h, mh, eh, ctypes.byref(slot)))
-        self.lagged_transport(None)  # (the engine detached any RCCL transport as well)
         return bytes(mh), bytes(eh), int(slot.value)
 
     def lagged_ipc_import(self, world, rank, mem_handles, event_handles, slot_bytes, src_off, recv_rows,

@@ -1573,14 +1573,21 @@ hipError_t launch_gather_rows(int dtype, const void* x, const int32_t* ids, int6
 // ---------------------------------------------------------------------------- the pull transport
 // One launch pulls every peer's block of this round (DOPT_TRANSPORT=ipc, runtime.cpp "pull transport"): block b
 // of the grid's y dimension copies the 16-byte chunks of peer block b from the peer's send slot (a pointer into
-// the peer's allocation, opened through its IPC handle) into this rank's halo.  Plain vector loads and stores;
-// the ordering against the peer's writes is the peer's interprocess event, waited for before the launch.
+// the peer's allocation, opened through its IPC handle) into this rank's halo.  The ordering against the peer's
+// writes is the peer's interprocess event, waited for before the launch; the slots are uncached allocations
+// (written through to memory by the peer's kernels) and the loads are system-scope (sc0 sc1: no L2 line of an
+// earlier round of the same slot can answer them), so the copy sees the peer's round on another GPU too.
+// Vector loads and stores only.
 __global__ __launch_bounds__(NT) void k_pull(const PullArgs a, int slot) {
   const int b = blockIdx.y;
-  const uint4* __restrict__ src = (const uint4*)a.src[2 * b + slot];
+  const uint64_t* __restrict__ src = (const uint64_t*)a.src[2 * b + slot];
   uint4* __restrict__ dst = (uint4*)(a.dst + a.dst_off[b]);
   const int64_t n = a.n16[b];
-  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) dst[i] = src[i];
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    const uint64_t lo = __hip_atomic_load(src + 2 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t hi = __hip_atomic_load(src + 2 * i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    dst[i] = make_uint4((unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32));
+  }
 }
 
 hipError_t launch_pull(const PullArgs& a, int slot, hipStream_t s) {

@@ -2734,7 +2734,10 @@ int dopt_lagged_transport(dopt_ctx* c, dopt_comm* comm, const int64_t* send_rows
   CHECK_ARG(c, "ctx is NULL");
   c->xp = nullptr;
   c->xp_ops.clear();
-  if (!comm) return DOPT_OK;
+  if (!comm) {  // detach either transport
+    ipc_close(c);
+    return DOPT_OK;
+  }
   CHECK_ARG(send_rows && recv_rows, "NULL argument");
   CHECK_ARG(comm_device(comm) == c->device, "communicator on device %d, context on device %d", comm_device(comm),
             c->device);
@@ -2775,7 +2778,9 @@ int dopt_lagged_ipc_export(dopt_ctx* c, uint8_t* mem_handle, uint8_t* event_hand
     HIPOK(hipFree(c->ipc_send));
     c->ipc_send = nullptr;
   }
-  HIPOK(hipMalloc((void**)&c->ipc_send, (size_t)(2 * slot)));
+  // uncached: the mix kernels' writes of the send rows go through to memory, where a peer's pull (on another
+  // GPU: over xGMI) reads them after the interprocess event, with no dirty line left in this GPU's L2
+  HIPOK(hipExtMallocWithFlags((void**)&c->ipc_send, (size_t)(2 * slot), hipDeviceMallocUncached));
   HIPOK(hipMemset(c->ipc_send, 0, (size_t)(2 * slot)));
   if (!c->ipc_ev) HIPOK(hipEventCreateWithFlags(&c->ipc_ev, hipEventInterprocess | hipEventDisableTiming));
   HIPOK(hipIpcGetMemHandle((hipIpcMemHandle_t*)mem_handle, c->ipc_send));

@@ -471,15 +471,35 @@ class IpcTransport:
         world, rank = plan.world, plan.rank
         self._shm = self._cnt = None
         self._creator = rank == 0
-        mh, eh, slot = engine.lagged_ipc_export()
+
+        def agree(err):  # every rank learns every rank's failure: all raise together, none waits for a peer
+            if world == 1:
+                errs = [err]
+            else:
+                errs = [None] * world
+                dist.all_gather_object(errs, err, group=group)
+            bad = [e for e in errs if e]
+            if bad:
+                engine.lagged_transport(None)  # (no context keeps the counters about to be unmapped)
+                self.close()
+                raise CollectiveError("pull transport setup failed: " + "; ".join(bad))
+
+        err, mh, eh, slot = None, b"", b"", 0
+        try:
+            mh, eh, slot = engine.lagged_ipc_export()
+        except Exception as e:  # noqa: BLE001  (reported to every rank below)
+            err = f"rank {rank}: {e}"
         send_off = np.concatenate([[0], np.cumsum(layout.send_sizes)]).astype(np.int64) * int(row_bytes)
-        mine = (mh, eh, slot, [int(v) for v in send_off[:-1]])
+        mine = (err, mh, eh, slot, [int(v) for v in send_off[:-1]])
         name = None
         if world == 1:
             infos = [mine]
         else:
             infos = [None] * world
             dist.all_gather_object(infos, mine, group=group)
+        bad = [i[0] for i in infos if i[0]]
+        if bad:
+            raise CollectiveError("pull transport setup failed: " + "; ".join(bad))
         if self._creator:
             shm = shared_memory.SharedMemory(create=True, size=max(4096, 8 * world))
             shm.buf[:8 * world] = bytes(8 * world)
@@ -494,11 +514,15 @@ class IpcTransport:
             resource_tracker.unregister(shm._name, "shared_memory")  # rank 0 owns the segment
         self._shm = shm
         self._cnt = np.ndarray((world,), dtype=np.int64, buffer=shm.buf)
-        engine.lagged_ipc_import(world, rank, [i[0] for i in infos], [i[1] for i in infos], [i[2] for i in infos],
-                                 [infos[p][3][rank] for p in range(world)], list(layout.recv_sizes),
-                                 self._cnt.ctypes.data, timeout_s)
-        if world > 1:  # every rank has opened its peers' handles before any rank's first round publishes
-            dist.barrier(group=group)
+        err = None
+        try:
+            engine.lagged_ipc_import(world, rank, [i[1] for i in infos], [i[2] for i in infos],
+                                     [i[3] for i in infos], [infos[p][4][rank] for p in range(world)],
+                                     list(layout.recv_sizes), self._cnt.ctypes.data, timeout_s)
+        except Exception as e:  # noqa: BLE001
+            err = f"rank {rank}: {e}"
+        # (also the barrier: every rank has opened its peers' handles before any rank's first round publishes)
+        agree(err)
 
     def close(self):
         """Unmap the counters (rank 0 removes the segment); the context must no longer run lagged rounds

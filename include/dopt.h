@@ -438,7 +438,8 @@ int dopt_lagged_exchange_issued(dopt_ctx *ctx, int *ordered);
  *   dopt_comm_destroy (abort = 1: without waiting for pending work, after a peer failed);
  *   dopt_comm_check: DOPT_ERR_COMM if RCCL reported an asynchronous error.
  * dopt_comm_library: the path of the RCCL library in use (the process's copy when one is loaded).
- * dopt_lagged_transport: route the context's exchange through comm (NULL: detach): per peer p in rank
+ * dopt_lagged_transport: route the context's exchange through comm (NULL: detach, the pull transport's
+ *   too): per peer p in rank
  *   order, send_rows[p] rows of the send buffer go to p and recv_rows[p] rows of the halo buffer come
  *   from p (the blocks of the all-to-all-v layout; the rank's own block at world 1 with a self block);
  *   after dopt_set_halo and dopt_lagged_exchange_layout, whose rank and world must match comm's.

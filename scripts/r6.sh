@@ -38,7 +38,8 @@ d = json.loads(sys.stdin.read())
 print('value', d['value'], 'scaling', d['scaling'], 'workers_total', d['config']['workers_total'], 'per_gpu', d['config']['workers_per_gpu'])
 print('per_rank', [(r['rank'], r['workers']) for r in d.get('per_rank', [])])
 w = d.get('weak'); print('weak', None if w is None else (w['value'], w['n_workers_total'], w['workers_per_gpu']))
-s = d.get('alt_exchange'); print('alt_exchange', None if s is None else (s.get('value'), s.get('ms_per_step'), s.get('exchange_beside_gradient')))
+for k in ('alt_exchange', 'ipc_transport'):
+    s = d.get(k); print(k, None if s is None else (s.get('value'), s.get('ms_per_step'), s.get('exchange_beside_gradient'), s.get('transport'), s.get('final_objective_matches_value')))
 print('transport_probe', d.get('transport_probe'))"
 }
 
@@ -87,13 +88,18 @@ for step in "$@"; do
       --warmup 100 > $D.log 2>&1 || { tail -n 20 $D.log; die proxy_trace 1; }
     python3 tools/trace_rounds.py $D/run_kernel_trace.csv
     python3 tools/trace_window.py $D/run_kernel_trace.csv ;;
-  scale_proxy)  # rank 0 of the strong leg at 2, 4 and 8 ranks (2048 / 1024 / 512 workers) beside the fused 4096-worker
-    # round: the per-rank efficiency the driver's 1/2/4/8-GPU line can reach before xGMI -> profiles/r6_scale_proxy.txt
-    for w in 2 4 8; do
-      timeout -k 10 300 python3 tools/rank_proxy.py --world $w --rank 0 --scaling strong --legs fused,proxy --reps 1 \
-        --steps $((1000 * 8 / w)) --warmup 200 > gpurun_out/r6_sp_$w.json 2> gpurun_out/r6_sp_$w.err \
-        || { tail -n 20 gpurun_out/r6_sp_$w.err; die scale_proxy 1; }
-      python3 -c "import json; d=json.loads(open('gpurun_out/r6_sp_$w.json').read().strip().splitlines()[-1]); p=d['plan']; [print('world', $w, g['leg'], g['workers'], 'halo', p['halo_rows_in'], 'interior', p['interior'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]; print('proxy / fused', [round(x, 4) for x in d['proxy_over_fused']])"
+  scale_proxy)  # rank 0 of the strong leg at 2, 4 and 8 ranks (2048 / 1024 / 512 workers) and of the weak leg at 8 beside
+    # the fused round of the same workers, over the engine's RCCL transport and the pull transport: the per-rank
+    # efficiency the driver's 1/2/4/8-GPU line can reach before xGMI -> profiles/r6_scale_proxy.txt
+    for tr in ${TRANSPORTS:-rccl ipc}; do
+      for cfg in "strong 2" "strong 4" "strong 8" "weak 8"; do
+        sc=${cfg% *}; w=${cfg#* }
+        st=$((1000 * 8 / w)); [ $sc = weak ] && st=150
+        DOPT_TRANSPORT=$tr timeout -k 10 300 python3 tools/rank_proxy.py --world $w --rank 0 --scaling $sc --legs fused,proxy --reps 1 \
+          --steps $st --warmup 200 > gpurun_out/r6_sp_${tr}_$sc$w.json 2> gpurun_out/r6_sp_${tr}_$sc$w.err \
+          || { tail -n 20 gpurun_out/r6_sp_${tr}_$sc$w.err; die scale_proxy 1; }
+        python3 -c "import json; d=json.loads(open('gpurun_out/r6_sp_${tr}_$sc$w.json').read().strip().splitlines()[-1]); p=d['plan']; [print('$tr', '$sc', 'world', $w, g['leg'], g['workers'], 'halo', p['halo_rows_in'], 'interior', p['interior'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]; print('$tr', '$sc', 'world', $w, 'proxy / fused', [round(x, 4) for x in d['proxy_over_fused']])"
+      done
     done ;;
   ipc_ab)  # the pull transport (DOPT_TRANSPORT=ipc: k_pull reads the send slots, no RCCL kernel) vs the engine's RCCL
     # transport, side stream (s1) / serial (s0): rank 0 of the strong leg at 4 / 2 / 8 ranks and of the weak leg at 8
