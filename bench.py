@@ -531,10 +531,14 @@ def setup_leg(args, config, n_global, world, rank, dev):
                   "halo_bytes_in_per_round": int(plan.n_halo) * ld * esz_state,
                   "send_bytes_out_per_round": int(len(plan.send_ids)) * ld * esz_state,
                   "peers": [int(p) for p in runner._peers],
-                  "exchange_beside_gradient": runner.side is not None}
+                  "exchange_beside_gradient": runner.side is not None,
+                  "transport": ("ipc" if runner.ipc is not None else "rccl" if runner.comm is not None
+                                else "process group")}
         if S.mean is None:  # the lagged schedule: the column sums ride the halo all-to-all
             S.comm.update({"collectives_per_round": 1 if world > 1 else 0,
-                           "exchange": ("one RCCL group of per-peer sends / receives per round, issued by the engine "
+                           "exchange": ("one k_pull launch per round reading the peers' send slots through IPC "
+                                        "handles (the pull transport, dopt_lagged_ipc_*)" if runner.ipc is not None else
+                                        "one RCCL group of per-peer sends / receives per round, issued by the engine "
                                         "(dopt_lagged_exchange)" if runner.comm is not None else
                                         "one all_to_all_single per round") + ": halo rows + every rank's column sums",
                            "colsum_bytes_per_peer_per_round": lay.ks * ld * esz_state,
@@ -590,8 +594,8 @@ def exchange_leg(args, S, world, barrier, dev, env, form):
     """N > 1, after the headline leg, on its engine and shards: the same rounds with the exchange in another
     form (`env`: the switches that select it, restored afterwards) -- not `value`.  The scaling run prices
     with real peers over xGMI what the one-GPU rank proxies cannot: the exchange serialised on the engine
-    stream where the headline ran it beside the gradient kernel (or the reverse), and the pull transport
-    (DOPT_TRANSPORT=ipc, a copy kernel instead of RCCL's)."""
+    stream where the headline ran it beside the gradient kernel (or the reverse), and the other transport (the
+    engine's RCCL sends / receives or its pull transport, DOPT_TRANSPORT)."""
     import torch
     import torch.distributed as dist
 
@@ -727,8 +731,8 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=0, help="CPU baseline processes (0: the box's CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-alt-exchange", action="store_true",
-                    help="N > 1: skip the headline leg's timings with the exchange in the other form and over the "
-                         "pull transport")
+                    help="N > 1: skip the headline leg's timings with the exchange in the other stream form and "
+                         "over the other transport")
     ap.add_argument("--no-secondary", action="store_true",
                     help="N=1: skip the f64-storage / f32 legs, the f(x*) solver and the drop-in trainer leg")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (gloo: 1-GPU rehearsal)")
@@ -888,9 +892,15 @@ def main():
         legs = [("alt_exchange", {"DOPT_LAGGED_SIDE": side},
                  "the exchange on the side stream beside the gradient kernel (DOPT_LAGGED_SIDE=1)" if side == "1"
                  else "the exchange serialised on the engine stream (DOPT_LAGGED_SIDE=0)")]
-        # (over gloo too: the one-GPU rehearsal's ranks share the card, as the pull tests do)
-        legs.append(("ipc_transport", {"DOPT_TRANSPORT": "ipc"},
-                     "the pull transport: k_pull reads the peers' send slots through IPC handles (DOPT_TRANSPORT=ipc)"))
+        # the other transport: RCCL where the headline pulled, the pull transport where it used RCCL or the
+        # process group (over gloo too: the one-GPU rehearsal's ranks share the card, as the pull tests do)
+        if S.comm.get("transport") == "ipc":
+            legs.append(("alt_transport", {"DOPT_TRANSPORT": "rccl"},
+                         "the engine's RCCL transport: grouped ncclSend / ncclRecv (DOPT_TRANSPORT=rccl)"))
+        else:
+            legs.append(("alt_transport", {"DOPT_TRANSPORT": "ipc"},
+                         "the pull transport: k_pull reads the peers' send slots through IPC handles "
+                         "(DOPT_TRANSPORT=ipc)"))
         for key, env, form in legs:
             log(f"headline leg again, {form} (A/B with real peers)")
             try:  # diagnostic only: a failure here must not cost the line its value

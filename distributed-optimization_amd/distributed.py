@@ -445,16 +445,29 @@ _COMMS = {}
 
 
 def transport_kind():
-    """The lagged schedule's exchange over RCCL: "rccl" -- the engine's own communicator, RCCL sends and
-    receives issued by dopt_lagged_exchange on the side stream (ABI 7, csrc/transport.cpp: 4.5-6 us of host
-    time per round against 22 us for the process group's alltoall_base, profiles/r5_rccl_probe.txt) --,
-    "pg": torch's process group all-to-all-v (rounds 3-4), or "ipc": the engine's pull transport (ABI 9, ranks
-    of one node: a copy kernel reads the peers' send slots through IPC handles, no RCCL kernel beside the
-    gradient kernel; IpcTransport).  DOPT_TRANSPORT overrides."""
-    v = os.environ.get("DOPT_TRANSPORT", "rccl").strip().lower()
-    if v not in ("rccl", "pg", "ipc"):
-        raise ValueError(f"DOPT_TRANSPORT={v!r}: 'rccl', 'pg' or 'ipc'")
+    """The lagged schedule's exchange: "ipc" -- the engine's pull transport (ABI 9, ranks of one node: a copy
+    kernel reads the peers' send slots through IPC handles, no RCCL kernel beside the gradient kernel;
+    IpcTransport), "rccl" -- the engine's own communicator, RCCL sends and receives issued by
+    dopt_lagged_exchange on the side stream (ABI 7, csrc/transport.cpp: 4.5-6 us of host time per round against
+    22 us for the process group's alltoall_base, profiles/r5_rccl_probe.txt) --, or "pg": torch's process group
+    all-to-all-v (rounds 3-4).  "auto" (the default): the pull transport over RCCL jobs whose ranks share one
+    node, RCCL otherwise and whenever the pull transport cannot be set up (every rank falls back together);
+    DOPT_TRANSPORT overrides."""
+    v = os.environ.get("DOPT_TRANSPORT", "auto").strip().lower()
+    if v not in ("auto", "rccl", "pg", "ipc"):
+        raise ValueError(f"DOPT_TRANSPORT={v!r}: 'auto', 'ipc', 'rccl' or 'pg'")
     return v
+
+
+def _one_node(group):
+    """Whether every rank of `group` runs on this host (hostnames all-gathered once per call)."""
+    import socket
+
+    import torch.distributed as dist
+
+    names = [None] * dist.get_world_size(group)
+    dist.all_gather_object(names, socket.gethostname(), group=group)
+    return len(set(names)) == 1
 
 
 class IpcTransport:
@@ -473,11 +486,8 @@ class IpcTransport:
         self._creator = rank == 0
 
         def agree(err):  # every rank learns every rank's failure: all raise together, none waits for a peer
-            if world == 1:
-                errs = [err]
-            else:
-                errs = [None] * world
-                dist.all_gather_object(errs, err, group=group)
+            errs = [None] * world
+            dist.all_gather_object(errs, err, group=group)
             bad = [e for e in errs if e]
             if bad:
                 engine.lagged_transport(None)  # (no context keeps the counters about to be unmapped)
@@ -492,30 +502,30 @@ class IpcTransport:
         send_off = np.concatenate([[0], np.cumsum(layout.send_sizes)]).astype(np.int64) * int(row_bytes)
         mine = (err, mh, eh, slot, [int(v) for v in send_off[:-1]])
         name = None
-        if world == 1:
-            infos = [mine]
-        else:
-            infos = [None] * world
-            dist.all_gather_object(infos, mine, group=group)
+        infos = [None] * world  # (world 1 too: the same object collectives as a job's, over its backend)
+        dist.all_gather_object(infos, mine, group=group)
         bad = [i[0] for i in infos if i[0]]
         if bad:
             raise CollectiveError("pull transport setup failed: " + "; ".join(bad))
         if self._creator:
-            shm = shared_memory.SharedMemory(create=True, size=max(4096, 8 * world))
-            shm.buf[:8 * world] = bytes(8 * world)
-            name = shm.name
-        if world > 1:
-            box = [name]
-            dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0,
-                                       group=group)
-            name = box[0]
-        if not self._creator:
-            shm = shared_memory.SharedMemory(name=name)
-            resource_tracker.unregister(shm._name, "shared_memory")  # rank 0 owns the segment
-        self._shm = shm
-        self._cnt = np.ndarray((world,), dtype=np.int64, buffer=shm.buf)
+            try:
+                shm = shared_memory.SharedMemory(create=True, size=max(4096, 8 * world))
+                shm.buf[:8 * world] = bytes(8 * world)
+                name = shm.name
+            except Exception as e:  # noqa: BLE001  (sent to every rank instead of the segment's name)
+                name = "ERR:" + repr(e)[:200]
+        box = [name]
+        dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        name = box[0]
+        if name.startswith("ERR:"):
+            raise CollectiveError(f"pull transport setup failed: rank 0's shared counters: {name[4:]}")
         err = None
         try:
+            if not self._creator:
+                shm = shared_memory.SharedMemory(name=name)
+                resource_tracker.unregister(shm._name, "shared_memory")  # rank 0 owns the segment
+            self._shm = shm
+            self._cnt = np.ndarray((world,), dtype=np.int64, buffer=shm.buf)
             engine.lagged_ipc_import(world, rank, [i[1] for i in infos], [i[2] for i in infos],
                                      [i[3] for i in infos], [infos[p][4][rank] for p in range(world)],
                                      list(layout.recv_sizes), self._cnt.ctypes.data, timeout_s)
@@ -681,20 +691,34 @@ class DistributedDSGD:
                 and os.environ.get("DOPT_LAGGED_SIDE", "1") != "0"):
             self.side = _stream(self.dev, 1)
         engine.lagged_side_stream(self.side.cuda_stream if self.side is not None else None)
-        # the engine's own RCCL communicator for the lagged exchange (dopt_lagged_exchange), RCCL only; or
-        # the engine's pull transport (DOPT_TRANSPORT=ipc), over any process group
+        # the lagged exchange's transport (transport_kind): the engine's pull transport (ranks of one node) or
+        # its own RCCL communicator (dopt_lagged_exchange); otherwise the process group / host transfers
         self.comm = None
         self.ipc = None
         kind = transport_kind()
-        if self._lagged_ok and mean is None and kind == "ipc" and (plan.world > 1 or forced) and lay.ks > 0:
+        lagged_x = self._lagged_ok and mean is None and (plan.world > 1 or forced) and lay.ks > 0
+        if kind == "auto":  # (every rank computes the same answer: the inputs are the job's, the test collective)
+            kind = "ipc" if (lagged_x and self.device_comm and plan.world > 1 and _one_node(group)) else "rccl"
+            if kind == "ipc":
+                try:
+                    engine.lagged_transport(None)
+                    self.ipc = IpcTransport(engine, plan, lay, group, ld * esz, timeout_seconds())
+                except CollectiveError as e:  # raised on every rank together: all fall back to RCCL
+                    import sys
+
+                    print(f"[distributed] rank {plan.rank}: {e}; the exchange goes over RCCL", file=sys.stderr)
+                    self.ipc = None
+                    kind = "rccl"
+        elif kind == "ipc" and lagged_x:
             engine.lagged_transport(None)
             self.ipc = IpcTransport(engine, plan, lay, group, ld * esz, timeout_seconds())
-        elif (self.device_comm and self._lagged_ok and mean is None and self.exchange.collective
-                and kind == "rccl"):
-            self.comm = _comm(group, self.dev)
-            engine.lagged_transport(self.comm, lay.send_sizes, lay.recv_sizes)
-        else:
-            engine.lagged_transport(None)
+        if self.ipc is None:
+            if (self.device_comm and self._lagged_ok and mean is None and self.exchange.collective
+                    and kind == "rccl"):
+                self.comm = _comm(group, self.dev)
+                engine.lagged_transport(self.comm, lay.send_sizes, lay.recv_sizes)
+            else:
+                engine.lagged_transport(None)
         # the communicator is created by one small collective here, not inside the first round
         # (the halo all-to-all and the all-reduces of the rounds then find it ready)
         if self.device_comm and dist.get_world_size(group) > 1:

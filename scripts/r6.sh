@@ -38,7 +38,8 @@ d = json.loads(sys.stdin.read())
 print('value', d['value'], 'scaling', d['scaling'], 'workers_total', d['config']['workers_total'], 'per_gpu', d['config']['workers_per_gpu'])
 print('per_rank', [(r['rank'], r['workers']) for r in d.get('per_rank', [])])
 w = d.get('weak'); print('weak', None if w is None else (w['value'], w['n_workers_total'], w['workers_per_gpu']))
-for k in ('alt_exchange', 'ipc_transport'):
+print('transport', d.get('comm', {}).get('transport'))
+for k in ('alt_exchange', 'alt_transport'):
     s = d.get(k); print(k, None if s is None else (s.get('value'), s.get('ms_per_step'), s.get('exchange_beside_gradient'), s.get('transport'), s.get('final_objective_matches_value')))
 print('transport_probe', d.get('transport_probe'))"
 }

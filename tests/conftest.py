@@ -27,7 +27,7 @@ def pytest_configure(config):
 # Files whose every test starts rank processes (their harness, not the kernels, is the fragile part):
 # run after the single-process oracle-parity files, so a rendezvous failure under -x cannot hide the
 # parity signal (a port race in test_gpu_distributed stopped the run before test_gpu_parity).
-MULTIPROC_FILES = {"test_gpu_distributed.py", "test_distributed_cpu.py", "test_bench_launch.py"}
+MULTIPROC_FILES = {"test_ipc_setup_cpu.py", "test_gpu_distributed.py", "test_distributed_cpu.py", "test_bench_launch.py"}
 
 
 def _multiproc(item):

@@ -482,7 +482,9 @@ def test_engine_transport_wait_is_bounded(monkeypatch):
 
 def test_transport_kind(monkeypatch):
     monkeypatch.delenv("DOPT_TRANSPORT", raising=False)
-    assert D.transport_kind() == "rccl"
+    assert D.transport_kind() == "auto"
+    monkeypatch.setenv("DOPT_TRANSPORT", "ipc")
+    assert D.transport_kind() == "ipc"
     monkeypatch.setenv("DOPT_TRANSPORT", "PG")
     assert D.transport_kind() == "pg"
     monkeypatch.setenv("DOPT_TRANSPORT", "mpi")

@@ -69,7 +69,7 @@ def _rank_main(rank, world, rdv, dtype, out, mean=False, T=T, lagged="1", N=N, D
     info = {"interior": eng.phase_interior_count(), "n_local": plan.n_local, "n_halo": plan.n_halo,
             "send_sizes": list(run.layout.send_sizes), "recv_sizes": list(run.layout.recv_sizes),
             "ks": run.layout.ks, "side": run.side is not None, "collective": bool(run.exchange.collective),
-            "native": run.comm is not None, "ipc": run.ipc is not None}
+            "native": run.comm is not None, "ipc": run.ipc is not None, "one_node": Dm._one_node(None)}
     np.save(os.path.join(out, f"info{rank}.npy"), np.array([repr(info)]))
     which = os.environ.get("DOPT_TEST_METRICS", "both")
     if os.environ.get("DOPT_TEST_PIPE") == "1":  # a chain of pipelined calls covering T rounds, then the tail
@@ -573,7 +573,7 @@ def test_pull_transport_one_rank_self_block(tmp_path, monkeypatch, dtype, lagged
                        nprocs=1, join=True, start_method="spawn")
     got = np.load(tmp_path / "dist.npz")
     it = _info(tmp_path, 1)[0]
-    assert it["ipc"] and it["ks"] > 0, it
+    assert it["ipc"] and it["ks"] > 0 and it["one_node"], it  # (the setup's object collectives over RCCL)
     _compare_single(got, dtype, False, 9)
 
 
