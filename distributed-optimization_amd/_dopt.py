@@ -589,6 +589,7 @@ class Engine:
         """dopt_lagged_transport: route the exchange through `comm` (a Comm; None: detach), blocks of
         send_rows[p] / recv_rows[p] rows per peer p in rank order."""
         old = getattr(self, "_comm", None)
+        self._ipc_owner = None  # (a pull transport set up later marks itself again: distributed.IpcTransport)
         if comm is None:
             if self._h:  # (a closed context holds no transport)
                 check(lib().dopt_lagged_transport(self._h, None, None, None))

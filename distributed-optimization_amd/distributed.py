@@ -481,9 +481,12 @@ class IpcTransport:
         import torch.distributed as dist
         from multiprocessing import resource_tracker, shared_memory
 
+        import weakref
+
         world, rank = plan.world, plan.rank
         self._shm = self._cnt = None
         self._creator = rank == 0
+        self._eng = weakref.ref(engine)
 
         def agree(err):  # every rank learns every rank's failure: all raise together, none waits for a peer
             errs = [None] * world
@@ -533,10 +536,14 @@ class IpcTransport:
             err = f"rank {rank}: {e}"
         # (also the barrier: every rank has opened its peers' handles before any rank's first round publishes)
         agree(err)
+        engine._ipc_owner = self  # (Engine.lagged_transport clears it: another transport took over)
 
     def close(self):
-        """Unmap the counters (rank 0 removes the segment); the context must no longer run lagged rounds
-        with this transport (a new runner exports and imports again)."""
+        """Detach the context if this transport is still its exchange, then unmap the counters (rank 0
+        removes the segment).  A new runner exports and imports again."""
+        eng = self._eng() if getattr(self, "_eng", None) is not None else None
+        if eng is not None and getattr(eng, "_ipc_owner", None) is self:
+            eng.lagged_transport(None)  # (no context keeps the counters about to be unmapped)
         self._cnt = None
         if self._shm is not None:
             self._shm.close()
@@ -712,6 +719,10 @@ class DistributedDSGD:
         elif kind == "ipc" and lagged_x:
             engine.lagged_transport(None)
             self.ipc = IpcTransport(engine, plan, lay, group, ld * esz, timeout_seconds())
+        if self.ipc is not None:  # the shared counters go with the runner (rank 0 removes the segment)
+            import weakref
+
+            weakref.finalize(self, self.ipc.close)
         if self.ipc is None:
             if (self.device_comm and self._lagged_ok and mean is None and self.exchange.collective
                     and kind == "rccl"):

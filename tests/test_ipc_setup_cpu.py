@@ -3,7 +3,7 @@ stand-in engine that records what the library would be given: every rank receive
 slot size in rank order, the byte offset of ITS block in each peer's send slot (the peer's send offsets, not
 its own), its own receive block sizes, and the address of counters every rank sees (one shared segment);
 a failure on any rank fails every rank's setup (no rank left waiting in a collective), and the segment is
-removed when rank 0 closes."""
+removed when rank 0 closes, which also detaches the context if the transport is still its exchange."""
 import os
 
 import numpy as np
@@ -63,7 +63,12 @@ def _rank(rank, world, rdv, out, fail_rank, fail_at):
         res["counters"] = [int(v) for v in t._cnt]  # ... and reads every rank's
         res["segment"] = t._shm.name
         dist.barrier()
+        n = len(eng.calls)
         t.close()
+        res["detached_on_close"] = eng.calls[n:] == [("detach",)]
+        eng._ipc_owner = None  # another transport took over: a second close leaves the context alone
+        t.close()
+        res["second_close_quiet"] = len(eng.calls) == n + 1
         dist.barrier()
     np.save(os.path.join(out, f"r{rank}.npy"), np.array([repr(res)]))
     dist.destroy_process_group()
@@ -91,6 +96,7 @@ def test_handles_offsets_and_shared_counters(tmp_path, world):
         assert src_off == want, (r, src_off, want)
         assert recv_rows == [10 * (r + 1) + p if p != r else 0 for p in range(world)]
         assert got["counters"] == [1000 + p for p in range(world)]  # one segment, seen by every rank
+        assert got["detached_on_close"] and got["second_close_quiet"], got
     assert len({g["segment"] for g in res}) == 1
     assert not os.path.exists("/dev/shm/" + res[0]["segment"].lstrip("/"))  # removed by rank 0's close
 
