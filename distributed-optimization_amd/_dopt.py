@@ -120,6 +120,7 @@ _SIGS = {
     "dopt_lagged_exchange": ([_P], ctypes.c_int),
     "dopt_lagged_ipc_export": ([_P, _P, _P, _P], ctypes.c_int),
     "dopt_lagged_ipc_import": ([_P, _I32, _I32, _P, _P, _P, _P, _P, _P, ctypes.c_double], ctypes.c_int),
+    "dopt_lagged_ipc_check": ([_P, _I32], ctypes.c_int),
 }
 EXPORTED = tuple(_SIGS)
 ABI_VERSION = 9  # DOPT_ABI_VERSION of include/dopt.h
@@ -637,6 +638,10 @@ class Engine:
             raise ValueError(f"{world} entries per array expected")
         check(lib().dopt_lagged_ipc_import(self._h, int(world), int(rank), mh, eh, *[_ptr(a) for a in arrs],
                                            ctypes.c_void_p(int(counters_addr)), float(timeout_s)))
+
+    def lagged_ipc_check(self, step):
+        """dopt_lagged_ipc_check: step 0 publishes a record, step 1 pulls every peer's (each synchronous)."""
+        check(lib().dopt_lagged_ipc_check(self._h, int(step)))
 
     def lagged_exchange(self):
         """dopt_lagged_exchange: the round's exchange through the attached communicator."""

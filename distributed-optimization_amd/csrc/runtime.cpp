@@ -2643,10 +2643,9 @@ int dopt_lagged_begin(dopt_ctx* c, int64_t batch) {
   int rc;
   if ((rc = dopt_phase_begin(c, batch))) return rc;
   if ((rc = lagged_ready(c))) return rc;
-  if (c->ipc) {  // slot 0 holds x_0's rows and sums (round g's in slot g % 2)
-    c->send = c->ipc_send;
-    c->ipc_rec = 0;
-  }
+  // the pull transport: the slot of the next record (records are numbered across chains, so a peer's
+  // counter never names an older chain's round)
+  if (c->ipc) c->send = c->ipc_send + (c->ipc_rec & 1) * c->ipc_slot;
   if ((rc = dopt_phase_gather(c))) return rc;  // send rows of x_0 (later rounds: k_mixcs writes them)
   // this rank's column sums of x_0 -> lg_own[0] and the send buffer's sum rows
   HIPOK(launch_colsum_partial(c->dtype, c->xs[c->cur], c->n, c->ld, (int32_t)c->nchs, kRowsPerGroup, c->part, nullptr,
@@ -2678,16 +2677,17 @@ int lagged_mark_exchange(dopt_ctx* c) {
 // ---- the pull transport (DOPT_TRANSPORT=ipc; round 6).  RCCL's kernel beside the gradient kernel slows it
 // by 4-16 % on the rank proxies while a plain copy kernel there costs ~1 % (profiles/r6_xcopy_ab.txt), so
 // this transport moves the rows with a copy kernel of the engine's own:
-//  * every rank writes round g's send rows and sums into slot g % 2 of its own allocation (exported once
-//    through an IPC handle) and then records an interprocess event on the stream that wrote them, and
-//    publishes "g + 1 events recorded" in host shared memory (ipc_publish);
-//  * the exchange of round g waits on the host until every peer has published g + 1 (so that the stream wait
-//    below refers to that record, not an older one), makes the exchange stream wait for the peers' events, and
-//    pulls every block with one k_pull launch from the peers' slot g % 2 into this rank's halo (ipc_pull).
-// No slot is overwritten while a peer may still read it, by the round structure itself: rank r writes slot
-// g % 2 again in its mix of round g + 1, which waited for the pulls of its own exchange of round g + 1, which
-// waited for every peer's event of round g + 1 -- recorded after that peer's mix of round g, which waited for
-// the peer's pulls of round g.  The host wait is bounded (timeout_s, the job's collective bound).
+//  * every rank writes the send rows and sums of its record r (r = 1, 2, ...: the chains' begins and mixes,
+//    numbered across chains and identical on every rank) into slot (r - 1) % 2 of its own allocation (exported
+//    once through an IPC handle), records an interprocess event on the stream that wrote them, and publishes
+//    "r events recorded" in host shared memory (ipc_publish);
+//  * an exchange for record r waits on the host until every peer has published r (so that the stream wait below
+//    refers to that record, not an older one), makes the exchange stream wait for the peers' events, and pulls
+//    every block with one k_pull launch from the peers' slot (r - 1) % 2 into this rank's halo (ipc_pull).
+// No slot is overwritten while a peer may still read it, by the schedule itself: a rank writes slot (r - 1) % 2
+// again for record r + 2, in a mix that waited for its own pulls of record r + 1, which waited for every
+// peer's event r + 1 -- recorded after that peer's mix that followed its pulls of record r.  The host wait is
+// bounded (timeout_s, the job's collective bound).
 namespace {
 int ipc_publish(dopt_ctx* c) {
   if (!c->ipc) return DOPT_OK;
@@ -2877,6 +2877,17 @@ int dopt_lagged_ipc_import(dopt_ctx* c, int32_t world, int32_t rank, const uint8
   return DOPT_OK;
 }
 
+int dopt_lagged_ipc_check(dopt_ctx* c, int32_t step) {
+  CHECK_ARG(c, "ctx is NULL");
+  CHECK_ARG(step == 0 || step == 1, "step 0 (publish) or 1 (pull)");
+  if (!c->ipc) return fail(DOPT_ERR_STATE, "no pull transport (dopt_lagged_ipc_import first)");
+  int rc;
+  if ((rc = set_device(c))) return rc;
+  if ((rc = step == 0 ? ipc_publish(c) : ipc_pull(c))) return rc;
+  HIPOK(hipStreamSynchronize(c->lg_side ? c->lg_side : c->stream));
+  return DOPT_OK;
+}
+
 int dopt_lagged_exchange(dopt_ctx* c) {
   CHECK_ARG(c, "ctx is NULL");
   int rc;
@@ -2919,7 +2930,7 @@ int dopt_lagged_mix(dopt_ctx* c, int64_t t, double eta0, int consensus, double* 
   int rc;
   if ((rc = lagged_ready(c))) return rc;
   if (!c->G) return fail(DOPT_ERR_STATE, "gradient phase missing");
-  if (c->ipc) c->send = c->ipc_send + ((c->lg + 1) & 1) * c->ipc_slot;  // x_{g+1}'s rows and sums
+  if (c->ipc) c->send = c->ipc_send + (c->ipc_rec & 1) * c->ipc_slot;  // x_{g+1}'s rows and sums: the next record
   RoundArgs a = base_args(c);
   a.x_old = c->xs[c->cur];
   a.x_new = c->xs[c->cur ^ 1];

@@ -536,6 +536,15 @@ class IpcTransport:
             err = f"rank {rank}: {e}"
         # (also the barrier: every rank has opened its peers' handles before any rank's first round publishes)
         agree(err)
+        # one trial exchange before any round, every step agreed: a runtime that cannot wait on a peer's
+        # interprocess event or read its memory fails here, on every rank, instead of in a round
+        for step in (0, 1):
+            err = None
+            try:
+                engine.lagged_ipc_check(step)
+            except Exception as e:  # noqa: BLE001
+                err = f"rank {rank}: trial {'publish' if step == 0 else 'pull'}: {e}"
+            agree(err)
         engine._ipc_owner = self  # (Engine.lagged_transport clears it: another transport took over)
 
     def close(self):

@@ -467,14 +467,19 @@ int dopt_lagged_exchange(dopt_ctx *ctx);
  *   p sends to this rank and recv_rows[p] rows that block holds (this rank's own entry: its self block,
  *   if any).  counters: world int64 in host memory shared by the ranks (zeroed), where each rank publishes
  *   how many rounds of send rows it has recorded; a rank waits at most timeout_s (0: unbounded) for a peer's
- *   round before DOPT_ERR_COMM.  Detaches an RCCL transport; dopt_lagged_transport with a communicator or
- *   dopt_set_halo detaches this one.  dopt_lagged_exchange then pulls every block with one copy kernel on
- *   the side stream (the engine stream without one), ordered before the next dopt_lagged_mix / _tail. */
+ *   round before DOPT_ERR_COMM.  Detaches an RCCL transport; dopt_lagged_transport or dopt_set_halo
+ *   detaches this one.  dopt_lagged_exchange then pulls every block with one copy kernel on the side stream
+ *   (the engine stream without one), ordered before the next dopt_lagged_mix / _tail.
+ * dopt_lagged_ipc_check: the transport tried once before any round, in two collective steps with the
+ *   caller's agreement between them -- step 0 publishes a record (the slots' current content), step 1 pulls
+ *   every peer's; each waits for its stream.  A failure in either (an IPC event the runtime cannot wait on,
+ *   a peer's memory it cannot read) lets every rank choose another transport before the first round. */
 #define DOPT_IPC_HANDLE_BYTES 64
 int dopt_lagged_ipc_export(dopt_ctx *ctx, uint8_t *mem_handle, uint8_t *event_handle, int64_t *slot_bytes);
 int dopt_lagged_ipc_import(dopt_ctx *ctx, int32_t world, int32_t rank, const uint8_t *mem_handles,
                            const uint8_t *event_handles, const int64_t *slot_bytes, const int64_t *src_off,
                            const int64_t *recv_rows, int64_t *counters, double timeout_s);
+int dopt_lagged_ipc_check(dopt_ctx *ctx, int32_t step);
 /* Centralized trainer across ranks (trainer.py:41-71): gradients of the local
  * workers at the shared iterate (fuse_loss: the objective partial of the shared
  * iterate over the same rows, full shards only), local column sums of the

@@ -83,6 +83,9 @@ def _rank_main(rank, world, rdv, dtype, out, mean=False, T=T, lagged="1", N=N, D
                                        consensus=which != "obj"))
         obj = None if which == "cons" else np.concatenate([p[0] for p in parts])
         cons = None if which == "obj" else np.concatenate([p[1] for p in parts])
+    elif os.environ.get("DOPT_TEST_CHAINS"):  # several closed chains in a row on one runner (T rounds each)
+        parts = [run.run(T, 0.05, B, 1e-3, 1e-3, 0.25) for _ in range(int(os.environ["DOPT_TEST_CHAINS"]))]
+        obj, cons = np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts])
     else:
         obj, cons = run.run(T, 0.05, B, 1e-3, 1e-3, 0.25, objective=which != "cons", consensus=which != "obj")
     obj = np.zeros(0) if obj is None else obj
@@ -543,6 +546,28 @@ def test_pull_transport_matches_single_context(tmp_path, monkeypatch, dtype, mea
         for r, it in enumerate(_info(sub, world)):
             assert it["ipc"] and not it["native"] and it["side"] == ("noside" not in lagged), it
         _compare_single(got, dtype, mean, T_)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_pull_transport_successive_chains(tmp_path, monkeypatch, world):
+    """Three closed chains in a row on one runner (bench.py's warmup, then timed rounds): the pull transport's
+    records are numbered across chains, so a rank entering the next chain never takes a peer's counter of the
+    previous one for the new round.  Iterates and history bitwise those of the same schedule over the host
+    transport."""
+    import torch.multiprocessing as mp
+
+    monkeypatch.setenv("DOPT_TEST_CHAINS", "3")
+    got = {}
+    for lagged in ("1", "1-ipc"):
+        sub = tmp_path / lagged
+        sub.mkdir()
+        mp.start_processes(_rank_main, args=(world, _rdv(sub), "float64/x32", str(sub), False, 4, lagged), nprocs=world,
+                           join=True, start_method="spawn")
+        got[lagged] = np.load(sub / "dist.npz")
+        assert all(it["ipc"] == (lagged == "1-ipc") for it in _info(sub, world))
+    assert len(got["1"]["obj"]) == 12
+    for k in ("x", "obj", "cons"):
+        assert np.array_equal(got["1"][k], got["1-ipc"][k]), k
 
 
 def test_pull_transport_eight_ranks_match_single_context(tmp_path, monkeypatch):

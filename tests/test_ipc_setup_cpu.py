@@ -25,6 +25,11 @@ class _Eng:
             raise RuntimeError("hipExtMallocWithFlags: out of memory")
         return bytes([self.rank]) * 64, bytes([100 + self.rank]) * 64, 4096 * (self.rank + 1)
 
+    def lagged_ipc_check(self, step):
+        if self.fail_at == f"check{step}":
+            raise RuntimeError("hipStreamWaitEvent: invalid argument")
+        self.calls.append(("check", step))
+
     def lagged_ipc_import(self, world, rank, mh, eh, slots, src_off, recv_rows, addr, timeout_s):
         if self.fail_at == "import":
             raise RuntimeError("hipIpcOpenMemHandle of peer 0: invalid argument")
@@ -56,6 +61,7 @@ def _rank(rank, world, rdv, out, fail_rank, fail_at):
     except D.CollectiveError as e:
         res["error"] = str(e)
     else:
+        assert [c for c in eng.calls if c[0] == "check"] == [("check", 0), ("check", 1)]
         imp = [c for c in eng.calls if c[0] == "import"][0]
         res["import"] = imp[1:8] + (imp[9],)
         t._cnt[rank] = 1000 + rank  # every rank writes its own counter ...
@@ -101,7 +107,8 @@ def test_handles_offsets_and_shared_counters(tmp_path, world):
     assert not os.path.exists("/dev/shm/" + res[0]["segment"].lstrip("/"))  # removed by rank 0's close
 
 
-@pytest.mark.parametrize("fail_rank,fail_at", [(1, "export"), (0, "import"), (1, "import")])
+@pytest.mark.parametrize("fail_rank,fail_at", [(1, "export"), (0, "import"), (1, "import"), (0, "check0"),
+                                               (1, "check1")])
 def test_a_failure_fails_every_rank(tmp_path, fail_rank, fail_at):
     res = _run(tmp_path, 2, fail_rank, fail_at)
     for got in res:
