@@ -63,14 +63,14 @@ for step in "$@"; do
     # 'weak' -> profiles/r6_rehearsal8.json
     rehearsal8 r6_rehearsal8 900 ;;
   rank_proxy)  # every rank of the 8-rank strong leg on one GPU (tools/rank_proxy.py: the real plan, the exchange
-    # through RCCL to itself) beside the fused 4096-worker round -> profiles/r6_rank_proxy.txt
+    # to itself over TRANSPORT, default rccl) beside the fused 4096-worker round -> profiles/r6_rank_proxy.txt
     for r in ${RANKS:-0 1 2 3 4 5 6 7}; do
       legs=proxy
       [ $r = 0 ] && legs=fused,proxy
-      timeout -k 10 300 python3 tools/rank_proxy.py --world 8 --rank $r --scaling strong --legs $legs --reps 1 \
-        --steps ${STEPS:-2000} --warmup 300 > gpurun_out/r6_rp_$r.json 2> gpurun_out/r6_rp_$r.err \
+      DOPT_TRANSPORT=${TRANSPORT:-rccl} timeout -k 10 300 python3 tools/rank_proxy.py --world 8 --rank $r --scaling strong \
+        --legs $legs --reps 1 --steps ${STEPS:-2000} --warmup 300 > gpurun_out/r6_rp_$r.json 2> gpurun_out/r6_rp_$r.err \
         || { tail -n 20 gpurun_out/r6_rp_$r.err; die rank_proxy 1; }
-      python3 -c "import json; d=json.loads(open('gpurun_out/r6_rp_$r.json').read().strip().splitlines()[-1]); p=d['plan']; [print('strong rank', $r, g['leg'], g['workers'], 'halo', p['halo_rows_in'], 'interior', p['interior'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]"
+      python3 -c "import json; d=json.loads(open('gpurun_out/r6_rp_$r.json').read().strip().splitlines()[-1]); p=d['plan']; [print('${TRANSPORT:-rccl}', 'strong rank', $r, g['leg'], g['workers'], 'halo', p['halo_rows_in'], 'interior', p['interior'], round(g['value']), round(g['ms_per_round'], 4), round(g['kernel_avg_ms'], 4)) for g in d['legs']]"
     done ;;
   transport_ab)  # rank 0 of the 8-rank strong leg, the engine's non-blocking RCCL communicator vs the process group's
     # all-to-all (DOPT_TRANSPORT=pg), interleaved twice, one process each -> profiles/r6_rank_proxy.txt
