@@ -191,24 +191,27 @@ def _info(tmp_path, world):
     return [ast.literal_eval(str(np.load(tmp_path / f"info{r}.npy")[0])) for r in range(world)]
 
 
-@pytest.mark.parametrize("world,dtype,d,m", [(2, "float64", 100, 32), (8, "float64", 100, 32),
-                                             (8, "float64/x32", 1024, 16)])
-def test_torus_strips_ranks_match_single_context(tmp_path, monkeypatch, world, dtype, d, m):
+@pytest.mark.parametrize("world,dtype,d,m,lagged", [(2, "float64", 100, 32, "1"), (8, "float64", 100, 32, "1"),
+                                                    (8, "float64/x32", 1024, 16, "1"),
+                                                    (8, "float64/x32", 1024, 16, "1-ipc")])
+def test_torus_strips_ranks_match_single_context(tmp_path, monkeypatch, world, dtype, d, m, lagged):
     """config C4's split -- a torus (trainer.py:99-108) in strips of torus rows, one
     strip per rank (64 x 64 torus: strips of 32 rows at 2 ranks, 8 at 8 ranks, >= 256 workers per rank so
     every context launches the headline's kernel instance) -- as a chain of pipelined calls through the
     device kernels: the strip interiors stepped inside the gradient kernel (dopt_phase_interior_count =
     64 x (rows - 2)), the two boundary rows mixed in k_mixcs from the halo rows, the column sums riding
-    the all-to-all to all 7 peers.  Iterates bitwise one context's, history rtol 1e-12."""
+    the all-to-all to all 7 peers (or, "1-ipc", pulled by the pull transport).  Iterates bitwise one
+    context's, history rtol 1e-12."""
     import torch.multiprocessing as mp
 
     n, t = 4096, 7
     monkeypatch.setenv("DOPT_TEST_PIPE", "1")
-    mp.start_processes(_rank_main, args=(world, _rdv(tmp_path), dtype, str(tmp_path), "torus", t, "1", n, d, m),
+    mp.start_processes(_rank_main, args=(world, _rdv(tmp_path), dtype, str(tmp_path), "torus", t, lagged, n, d, m),
                        nprocs=world, join=True, start_method="spawn")
     got = np.load(tmp_path / "dist.npz")
     assert len(got["obj"]) == len(got["cons"]) == t
     info = _info(tmp_path, world)
+    assert all(it["ipc"] == ("ipc" in lagged) for it in info)
     rows = 64 // world
     for r, it in enumerate(info):
         assert it["n_local"] == 64 * rows and it["n_halo"] == 2 * 64, it
@@ -340,7 +343,7 @@ def test_strong_split_bench_shape_matches_single_context(tmp_path, monkeypatch, 
     _compare_single(got, "float64/x32", False, t, n, d, m, parts=world)
 
 
-@pytest.mark.parametrize("lagged", ["1", "0"])
+@pytest.mark.parametrize("lagged", ["1", "0", "1-ipc"])
 def test_device_sampler_ranks_match_single_context(tmp_path, monkeypatch, lagged):
     """sampling='device' across ranks: worker i's minibatch of round t depends only on
     (seed, t, global id), so 3 ranks (phase path, lagged or serial) reproduce one context's
