@@ -326,6 +326,8 @@ int ipc_pull(dopt_ctx* c);
 
 // The pull transport's peer side: handles opened by dopt_lagged_ipc_import closed, its arrays freed.
 void ipc_close(dopt_ctx* c) {
+  // (no pull of this context may still read a peer's allocation when its mapping goes: teardown and setup only)
+  if (!c->ipc_open.empty()) (void)hipDeviceSynchronize();
   for (void* q : c->ipc_open)
     if (q) (void)hipIpcCloseMemHandle(q);
   for (hipEvent_t e : c->ipc_pev)
