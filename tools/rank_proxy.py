@@ -12,8 +12,10 @@ copy (a local row stands in for the remote one: the values differ, the schedule,
 bytes and the exchange's kernel do not).  So one GPU runs the lagged schedule exactly as rank R would:
 the gradient kernel with the interior workers stepped inside it, `k_mixcs` over the real boundary
 workers, `k_mixcs_final` and an all-to-all that moves |send set| rows plus the sum rows, with the
-collectives forced (DOPT_FORCE_COLLECTIVES=1).  What it cannot show: xGMI itself (the self copy is a
-local device copy), RCCL's latency with 7 peers, and rank imbalance.
+collectives forced (DOPT_FORCE_COLLECTIVES=1).  The exchange goes over the transport DOPT_TRANSPORT names:
+at world 1 the default is the engine's RCCL communicator; DOPT_TRANSPORT=ipc pulls the rank's blocks from
+its own send slot with k_pull (the pull transport, the default of a multi-GPU job on one node).  What it
+cannot show: xGMI itself (the self copy is a local device copy), the peers' latency, and rank imbalance.
 
   python3 tools/rank_proxy.py --world 8 --rank 0 --scaling weak --reps 2 --steps 400 --warmup 50
   python3 tools/rank_proxy.py --world 8 --plan-only          # plan statistics only (CPU)
